@@ -1,0 +1,123 @@
+"""Drop-in for spec_denoising/pipeline_data.py (the reference's STFT front-end API).
+
+Same names, arguments, return types and exceptions as the reference, so the
+reference's scripts and notebooks call it unchanged:
+
+    from specenh.pipeline_data import specgr, norm, rescale, quantfilt, meansub
+    s, f, t = specgr(fname, chn + 1, spec_params, 2)        # pipeline_data.py:97
+
+``specgr`` runs the whole spectrogram -> log -> min-max -> drop-Nyquist chain as
+one HIP launch pair on the GPU (csrc/stft_psd.hip) and returns float64 numpy
+arrays like the reference (computed in fp32 on the device; tolerance in
+DESIGN.md). ``specgr_batch`` is the tensor-in/tensor-out fast path that keeps
+data on the device.
+
+The image-filter helpers ``norm/rescale/quantfilt/meansub`` (:38-61) are the
+label-generator chain; they are SURVEY §8(f1) ("next") and currently accept
+numpy (exact reference arithmetic) or device tensors (torch ops on the device).
+``gaussblr``/``morph`` need OpenCV semantics (cv2 is absent here): not yet built.
+"""
+from __future__ import annotations
+
+import pickle
+
+import numpy as np
+import torch
+
+from . import stft as _stft
+
+
+def _device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("specenh requires a ROCm GPU (HIP); there is no CPU fallback")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _params(spec_params):
+    return dict(nperseg=int(spec_params["nperseg"]), noverlap=int(spec_params["noverlap"]),
+                fs=spec_params["fs"], window=spec_params["window"],
+                scaling=spec_params.get("scaling", "density"),
+                detrend=spec_params.get("detrend", "linear"),
+                eps=float(spec_params.get("eps", 1e-11)))
+
+
+def specgr_batch(x: torch.Tensor, spec_params: dict, cut_shot: float | None = None,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """Batched specgr on device tensors: ``x[B, L]`` -> ``Sxx[B, nperseg//2, T]`` fp32.
+
+    Normalisation is per spectrogram (pipeline_data.py:34 applied to each row of x).
+    """
+    p = _params(spec_params)
+    if cut_shot is not None:
+        x = x[..., : np.int_(cut_shot * p["fs"])]
+    return _stft.stft_psd(x, p["nperseg"], p["noverlap"], p["window"], p["fs"], p["scaling"],
+                          p["detrend"], p["eps"], log=True, normalize=True, drop_nyquist=True,
+                          out=out)
+
+
+def specgr_array(sig_in, spec_params: dict):
+    """specgr on an in-memory 1-D signal: returns (Sxx float64, f, t) like the reference."""
+    p = _params(spec_params)
+    x = torch.as_tensor(np.ascontiguousarray(sig_in), dtype=torch.float32, device=_device())
+    S = specgr_batch(x.unsqueeze(0), spec_params)[0]
+    f = _stft.frequencies(p["nperseg"], p["fs"])[:-1]
+    t = _stft.times(x.shape[-1], p["nperseg"], p["noverlap"], p["fs"])
+    return S.double().cpu().numpy(), f, t
+
+
+def specgr(fname, ecen, spec_params, cut_shot=2, key_format="\\tecef%.2i", field=None):
+    """pipeline_data.py:28-36. ``key_format``/``field`` select the BES variant of
+    denoising_by_svd.ipynb cell 1 (``'besfu%02d'``, ``'data.BES'``)."""
+    with open(fname, "rb") as fh:
+        ece_data = pickle.load(fh)  # pickle.UnpicklingError propagates (caller catches it)
+    rec = ece_data[key_format % (ecen)]  # KeyError for a missing channel
+    if field is not None:
+        rec = rec[field]
+    sig_in = np.asarray(rec)[: np.int_(cut_shot * spec_params["fs"])]
+    return specgr_array(sig_in, spec_params)
+
+
+# ------------------------------------------------------------- filter helpers
+def _is_tensor(a):
+    return isinstance(a, torch.Tensor)
+
+
+def norm(data):
+    """pipeline_data.py:38-41."""
+    if _is_tensor(data):
+        return (data - data.mean()) / data.std(unbiased=False)
+    mn = data.mean()
+    std = data.std()
+    return (data - mn) / std
+
+
+def rescale(data):
+    """pipeline_data.py:43-44."""
+    return (data - data.min()) / (data.max() - data.min())
+
+
+def quantfilt(src, thr=0.9):
+    """pipeline_data.py:46-49: zero entries below their column's thr-quantile."""
+    if _is_tensor(src):
+        filt = torch.quantile(src, thr, dim=0, interpolation="linear")
+        return torch.where(src < filt, torch.zeros_like(src), src)
+    filt = np.quantile(src, thr, axis=0)
+    return np.where(src < filt, 0, src)
+
+
+def meansub(src):
+    """pipeline_data.py:58-61."""
+    if _is_tensor(src):
+        return rescale((src - src.mean(dim=1, keepdim=True)).abs())
+    mn = np.mean(src, axis=1)[:, np.newaxis]
+    return rescale(np.absolute(src - mn))
+
+
+def gaussblr(src, filt=(31, 3)):
+    """pipeline_data.py:52-55 (cv2.GaussianBlur on uint8). Not built yet: SURVEY §8(f1)."""
+    raise NotImplementedError("gaussblr needs OpenCV semantics; GPU port is a §8(f1) item")
+
+
+def morph(src):
+    """pipeline_data.py:64-72 (cv2 close/open on uint8). Not built yet: SURVEY §8(f1)."""
+    raise NotImplementedError("morph needs OpenCV semantics; GPU port is a §8(f1) item")

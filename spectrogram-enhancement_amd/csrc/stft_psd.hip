@@ -65,6 +65,7 @@ struct StftArgs {
   unsigned* minmax;  // [batch][2] order-preserving keys
   const float* window;
   const float2* twiddle;  // W_N^m, m in [0, N)
+  const double* dc_coef;  // c_n: DC bin of the detrended, windowed frame = <x, c> (fp64)
 };
 
 // Per-N decomposition: G lanes per FFT, WAVES per workgroup, Stockham radices.
@@ -170,10 +171,22 @@ __global__ __launch_bounds__(Layout<N>::THREADS) void stft_psd_kernel(StftArgs a
   const float* xa = xs + (long long)(va ? fa : 0) * a.hop;
   const float* xb = xs + (long long)(vb ? fa + 1 : 0) * a.hop;
 
-  // ---- pass 1: load, detrend sums, detrend + window, radix-R1 DIF, store to LDS ----
+  // ---- pass 1: load, detrend, window, radix-R1 DIF, store to LDS ----
+  // Detrend in two sweeps over the register-resident samples: a rough mean m1
+  // (division by N = 2^k is exact), then mean/slope of the residuals x - m1. The
+  // rounding of m1 then never enters y coherently: the post-detrend DC bin (tiny by
+  // construction, and the usual argmin of the spectrogram) keeps fp32-rounding
+  // accuracy instead of inheriting |mean| * eps * sum(w).
   float2 v[BPL1][R1];
-  float s0a = 0.f, s1a = 0.f, s0b = 0.f, s1b = 0.f;
   constexpr float kmid = 0.5f * float(N - 1);
+  constexpr float invN = 1.0f / float(N);
+  float s0a = 0.f, s0b = 0.f;
+  // DC bin in fp64: X_0 = sum_n w_n y_n = <x, c> with c = w - mean(w) - kc * sum(w kc)/sum(kc^2)
+  // (c is orthogonal to constants and ramps, so the detrend cancellation happens exactly
+  // in the coefficients, not in the data). After detrending X_0 is tiny by construction;
+  // in fp32 it would sit at the rounding floor eps*||w y|| and, being the usual
+  // spectrogram minimum under 'spectrum' scaling, would shift every normalised value.
+  double dca = 0.0, dcb = 0.0;
 #pragma unroll
   for (int i = 0; i < BPL1; ++i) {
     const int b = gl + i * G;
@@ -184,27 +197,53 @@ __global__ __launch_bounds__(Layout<N>::THREADS) void stft_psd_kernel(StftArgs a
       const float xa_n = va ? la : 0.f;
       const float xb_n = vb ? lb : 0.f;
       v[i][r] = make_float2(xa_n, xb_n);
-      const float kc = float(n) - kmid;
       s0a += xa_n;
       s0b += xb_n;
-      s1a = fmaf(kc, xa_n, s1a);
-      s1b = fmaf(kc, xb_n, s1b);
+      const double c = a.dc_coef[n];
+      dca = fma((double)xa_n, c, dca);
+      dcb = fma((double)xb_n, c, dcb);
     }
   }
 #pragma unroll
   for (int m = G / 2; m >= 1; m >>= 1) {
-    s0a += __shfl_xor(s0a, m);
-    s0b += __shfl_xor(s0b, m);
-    s1a += __shfl_xor(s1a, m);
-    s1b += __shfl_xor(s1b, m);
+    dca += __shfl_xor(dca, m);
+    dcb += __shfl_xor(dcb, m);
   }
-  float mean_a = 0.f, mean_b = 0.f, slope_a = 0.f, slope_b = 0.f;
+  float lo_a = 0.f, lo_b = 0.f, slope_a = 0.f, slope_b = 0.f;
   if (a.detrend != SPECENH_DETREND_NONE) {
-    mean_a = s0a * (1.0f / float(N));
-    mean_b = s0b * (1.0f / float(N));
+#pragma unroll
+    for (int m = G / 2; m >= 1; m >>= 1) {
+      s0a += __shfl_xor(s0a, m);
+      s0b += __shfl_xor(s0b, m);
+    }
+    const float m1a = s0a * invN, m1b = s0b * invN;
+    float r0a = 0.f, r0b = 0.f, r1a = 0.f, r1b = 0.f;
+#pragma unroll
+    for (int i = 0; i < BPL1; ++i) {
+      const int b = gl + i * G;
+#pragma unroll
+      for (int r = 0; r < R1; ++r) {
+        const float kc = float(b + r * NB1) - kmid;
+        const float ra = v[i][r].x - m1a, rb = v[i][r].y - m1b;
+        v[i][r] = make_float2(ra, rb);
+        r0a += ra;
+        r0b += rb;
+        r1a = fmaf(kc, ra, r1a);
+        r1b = fmaf(kc, rb, r1b);
+      }
+    }
+#pragma unroll
+    for (int m = G / 2; m >= 1; m >>= 1) {
+      r0a += __shfl_xor(r0a, m);
+      r0b += __shfl_xor(r0b, m);
+      r1a += __shfl_xor(r1a, m);
+      r1b += __shfl_xor(r1b, m);
+    }
+    lo_a = r0a * invN;
+    lo_b = r0b * invN;
     if (a.detrend == SPECENH_DETREND_LINEAR) {
-      slope_a = s1a * a.inv_kk;
-      slope_b = s1b * a.inv_kk;
+      slope_a = r1a * a.inv_kk;
+      slope_b = r1b * a.inv_kk;
     }
   }
 #pragma unroll
@@ -215,8 +254,8 @@ __global__ __launch_bounds__(Layout<N>::THREADS) void stft_psd_kernel(StftArgs a
       const int n = b + r * NB1;
       const float kc = float(n) - kmid;
       const float w = s_win[n];
-      const float ya = fmaf(-slope_a, kc, v[i][r].x - mean_a);
-      const float yb = fmaf(-slope_b, kc, v[i][r].y - mean_b);
+      const float ya = fmaf(-slope_a, kc, v[i][r].x - lo_a);
+      const float yb = fmaf(-slope_b, kc, v[i][r].y - lo_b);
       v[i][r] = make_float2(w * ya, w * yb);
     }
     fft_dif<R1>(v[i]);
@@ -246,6 +285,10 @@ __global__ __launch_bounds__(Layout<N>::THREADS) void stft_psd_kernel(StftArgs a
       const float s = (k == 0 || k == N / 2) ? 0.25f * a.scale : 0.5f * a.scale;
       float pa = fmaf(ar, ar, ai * ai) * s;
       float pb = fmaf(br, br, bi * bi) * s;
+      if (k == 0) {
+        pa = (float)(dca * dca * (double)a.scale);
+        pb = (float)(dcb * dcb * (double)a.scale);
+      }
       if (want_log) {
         pa = __log2f(pa + a.eps);
         pb = __log2f(pb + a.eps);
@@ -342,6 +385,7 @@ struct specenh_stft_plan {
   int device;
   float* d_window;
   float2* d_twiddle;
+  double* d_dc;
 };
 
 extern "C" {
@@ -379,6 +423,23 @@ int specenh_stft_plan_create(specenh_stft_plan** plan, int nperseg, int noverlap
     s2 += window_host[i] * window_host[i];
     win[i] = float(window_host[i]);
   }
+  // DC coefficients c_n (fp64): the detrend folded into the window (see kernel).
+  std::vector<double> dc(N);
+  {
+    const double kmid = 0.5 * (N - 1);
+    double sk2 = 0, swk = 0;
+    for (int i = 0; i < N; ++i) {
+      sk2 += (i - kmid) * (i - kmid);
+      swk += window_host[i] * (i - kmid);
+    }
+    const double wbar = s1 / N;
+    for (int i = 0; i < N; ++i) {
+      double c = window_host[i];
+      if (detrend != SPECENH_DETREND_NONE) c -= wbar;
+      if (detrend == SPECENH_DETREND_LINEAR) c -= (i - kmid) * (swk / sk2);
+      dc[i] = c;
+    }
+  }
   std::vector<float2> tw(N);
   for (int m = 0; m < N; ++m) {
     ct::CS cs = ct::cossin_frac(m, N);
@@ -396,11 +457,14 @@ int specenh_stft_plan_create(specenh_stft_plan** plan, int nperseg, int noverlap
   hipError_t e = hipGetDevice(&p->device);
   if (e == hipSuccess) e = hipMalloc(&p->d_window, N * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&p->d_twiddle, N * sizeof(float2));
+  if (e == hipSuccess) e = hipMalloc(&p->d_dc, N * sizeof(double));
+  if (e == hipSuccess) e = hipMemcpy(p->d_dc, dc.data(), N * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_window, win.data(), N * sizeof(float), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_twiddle, tw.data(), N * sizeof(float2), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     (void)hipFree(p->d_window);
     (void)hipFree(p->d_twiddle);
+    (void)hipFree(p->d_dc);
     delete p;
     return set_error(SPECENH_EHIP, std::string("plan allocation: ") + hipGetErrorString(e));
   }
@@ -412,6 +476,7 @@ int specenh_stft_plan_destroy(specenh_stft_plan* plan) {
   if (!plan) return SPECENH_OK;
   (void)hipFree(plan->d_window);
   (void)hipFree(plan->d_twiddle);
+  (void)hipFree(plan->d_dc);
   delete plan;
   return SPECENH_OK;
 }
@@ -452,6 +517,7 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
   a.minmax = (unsigned*)workspace;
   a.window = plan->d_window;
   a.twiddle = plan->d_twiddle;
+  a.dc_coef = plan->d_dc;
   const long long F_out = a.F_out;
   for (long long b0 = 0; b0 < batch; b0 += 65535) {
     const long long nb = std::min<long long>(65535, batch - b0);

@@ -26,6 +26,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <algorithm>
 #include <string>
@@ -33,6 +34,10 @@
 
 #include "fft_common.hpp"
 #include "specenh.h"
+
+// Development-only flag bit (not part of the public header): skip the output store,
+// to separate compute from store cost when profiling.
+#define SPECENH_STFT_DEV_NOSTORE (1 << 16)
 
 namespace specenh {
 
@@ -62,50 +67,105 @@ struct StftArgs {
   int flags;
   float* out;
   int F_out;
-  unsigned* minmax;  // [batch][2] order-preserving keys
   const float* window;
-  const float2* twiddle;  // W_N^m, m in [0, N)
+  const float2* twiddle;  // per-pass [r-1][k] tables (TwOff<N>)
   const double* dc_coef;  // c_n: DC bin of the detrended, windowed frame = <x, c> (fp64)
 };
 
 // Per-N decomposition: G lanes per FFT, WAVES per workgroup, Stockham radices.
 template <int N>
 struct Cfg;
-template <> struct Cfg<64>   { static constexpr int G = 8,  WAVES = 4, R1 = 8,  R2 = 8,  R3 = 1; };
-template <> struct Cfg<128>  { static constexpr int G = 8,  WAVES = 4, R1 = 16, R2 = 8,  R3 = 1; };
-template <> struct Cfg<256>  { static constexpr int G = 16, WAVES = 4, R1 = 16, R2 = 16, R3 = 1; };
-template <> struct Cfg<512>  { static constexpr int G = 16, WAVES = 4, R1 = 32, R2 = 16, R3 = 1; };
-template <> struct Cfg<1024> { static constexpr int G = 32, WAVES = 4, R1 = 32, R2 = 32, R3 = 1; };
-template <> struct Cfg<2048> { static constexpr int G = 64, WAVES = 4, R1 = 32, R2 = 8,  R3 = 8; };
-template <> struct Cfg<4096> { static constexpr int G = 64, WAVES = 2, R1 = 32, R2 = 16, R3 = 8; };
+// G lanes own one FFT (two frames); WAVES per workgroup (one workgroup per CU: the
+// LDS footprint is sized for that); R1 x R2 (x R3) Stockham radices; PF = prefetch the
+// next tile's samples into registers while the current tile computes.
+template <> struct Cfg<64>   { static constexpr int G = 8,  WAVES = 8, R1 = 8,  R2 = 8,  R3 = 1, PF = 1; };
+template <> struct Cfg<128>  { static constexpr int G = 8,  WAVES = 8, R1 = 16, R2 = 8,  R3 = 1, PF = 1; };
+template <> struct Cfg<256>  { static constexpr int G = 16, WAVES = 8, R1 = 16, R2 = 16, R3 = 1, PF = 1; };
+template <> struct Cfg<512>  { static constexpr int G = 16, WAVES = 8, R1 = 32, R2 = 16, R3 = 1, PF = 1; };
+template <> struct Cfg<1024> { static constexpr int G = 32, WAVES = 8, R1 = 32, R2 = 32, R3 = 1, PF = 1; };
+template <> struct Cfg<2048> { static constexpr int G = 64, WAVES = 4, R1 = 32, R2 = 8,  R3 = 8, PF = 1; };
+template <> struct Cfg<4096> { static constexpr int G = 64, WAVES = 2, R1 = 32, R2 = 16, R3 = 8, PF = 0; };
+
+// Stockham pass p >= 2 of radix R at stride NS uses twiddles W_N^{r k N/(NS R)} for
+// r in [1, R), k in [0, NS); stored as a [r-1][k] table so the lanes of a group read
+// consecutive k (conflict-free). TwOff<N>::P2 / P3 are the per-pass table offsets.
+template <int N>
+struct TwOff {
+  using C = Cfg<N>;
+  static constexpr int P2 = 0;
+  static constexpr int P3 = P2 + (C::R2 - 1) * C::R1;
+  static constexpr int TOTAL = P3 + (C::R3 > 1 ? (C::R3 - 1) * C::R1 * C::R2 : 0);
+};
 
 template <int N>
 struct Layout {
   using C = Cfg<N>;
   static constexpr int G = C::G;
   static constexpr int THREADS = 64 * C::WAVES;
+  static constexpr int WPE = C::WAVES >= 8 ? C::WAVES / 4 : 1;  // waves per SIMD
   static constexpr int FFTS = C::WAVES * (64 / G);  // concurrent FFTs per workgroup
-  static constexpr int TF = 2 * FFTS;                // frames per workgroup tile
+  static constexpr int TF = 2 * FFTS;                // frames per tile (power of two)
+  static constexpr int LOG_TF = ilog2(TF);
   static constexpr int TS = TF + 1;                  // tile row stride (odd: conflict-free)
   static constexpr int NBINS = N / 2 + 1;
+  static constexpr int IB = (NBINS + G - 1) / G;     // bins per lane in the epilogue
   static constexpr int BUF = N + N / 32;             // padded complex entries per FFT
+  static constexpr int BUF_BYTES = FFTS * BUF * 8;
+  static constexpr int TILE_BYTES = NBINS * TS * 4;  // aliases the FFT buffers
+  static constexpr int TWN = TwOff<N>::TOTAL;
   // byte offsets into dynamic LDS (all multiples of 16)
-  static constexpr int OFF_TW = 0;
-  static constexpr int OFF_WIN = OFF_TW + N * 8;
+  static constexpr int OFF_DC = 0;
+  static constexpr int OFF_TW = OFF_DC + N * 8;
+  static constexpr int OFF_WIN = OFF_TW + ((TWN * 8 + 15) / 16) * 16;
   static constexpr int OFF_BUF = OFF_WIN + N * 4;
-  static constexpr int OFF_TILE = OFF_BUF + FFTS * BUF * 8;
-  static constexpr int OFF_RED = OFF_TILE + ((NBINS * TS * 4 + 15) / 16) * 16;
-  static constexpr int BYTES = OFF_RED + 2 * C::WAVES * 4 + 16;
+  static constexpr int OFF_RED = OFF_BUF + (BUF_BYTES > TILE_BYTES ? BUF_BYTES : TILE_BYTES);
+  static constexpr int BYTES = OFF_RED + 4 * C::WAVES * 4;
   static_assert(BYTES <= 160 * 1024, "LDS budget");
   static_assert(C::R1 * C::R2 * C::R3 == N, "radix product");
+  static_assert((TF & (TF - 1)) == 0, "tile width must be a power of two");
 };
 
 __device__ __forceinline__ int pad(int e) { return e + (e >> 5); }
 
+// ---------------------------------------------------------------- lane-group sums
+// Sum over aligned groups of G lanes, result in every lane of the group. DPP
+// (quad_perm, row half-mirror, row mirror) inside a 16-lane row; ds_swizzle / a
+// 32-lane shuffle above that.
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int G, typename T>
+__device__ __forceinline__ T group_sum(T v) {
+  static_assert(G >= 4 && G <= 64, "group size");
+  if constexpr (sizeof(T) == 4) {
+    v += dppf<0xB1>(v);  // quad_perm [1,0,3,2]
+    v += dppf<0x4E>(v);  // quad_perm [2,3,0,1]
+    if constexpr (G >= 8) v += dppf<0x141>(v);   // row_half_mirror
+    if constexpr (G >= 16) v += dppf<0x140>(v);  // row_mirror
+  } else {
+    v += dppd<0xB1>(v);
+    v += dppd<0x4E>(v);
+    if constexpr (G >= 8) v += dppd<0x141>(v);
+    if constexpr (G >= 16) v += dppd<0x140>(v);
+  }
+  if constexpr (G >= 32) v += __shfl_xor(v, 16);
+  if constexpr (G >= 64) v += __shfl_xor(v, 32);
+  return v;
+}
+
 // Stockham pass NS>1 through the LDS buffer (all butterflies of the lane read first,
 // then written back in place: legal because the whole FFT lives in one wave).
 template <int N, int G, int R, int NS>
-__device__ __forceinline__ void stockham_pass(float2* buf, const float2* tw, int gl) {
+__device__ __forceinline__ void stockham_pass(float2* buf, const float2* tw /* [R-1][NS] */,
+                                              int gl) {
   constexpr int NB = N / R;
   constexpr int BPL = NB / G;
   constexpr int LOGR = ilog2(R);
@@ -123,7 +183,7 @@ __device__ __forceinline__ void stockham_pass(float2* buf, const float2* tw, int
     const int b = gl + i * G;
     const int k = b % NS;
 #pragma unroll
-    for (int r = 1; r < R; ++r) v[i][r] = cmul(v[i][r], tw[r * k * (N / (NS * R))]);
+    for (int r = 1; r < R; ++r) v[i][r] = cmul(v[i][r], tw[(r - 1) * NS + k]);
     fft_dif<R>(v[i]);
     const int base = (b / NS) * NS * R + k;
 #pragma unroll
@@ -132,130 +192,135 @@ __device__ __forceinline__ void stockham_pass(float2* buf, const float2* tw, int
   wave_lds_sync();
 }
 
+// acc += (double)x * c, as one opaque statement: hipcc otherwise converts all N/G
+// samples to fp64 up front (2 VGPRs each) before running the FMA chain.
+// v_cvt_f64_f32 -> v_fma_f64 is an ordinary VALU RAW dependency (interlocked).
+__device__ __forceinline__ void dc_fma(double& acc, float x, double c) {
+  double t;
+  asm volatile("v_cvt_f64_f32 %1, %2\n\tv_fma_f64 %0, %1, %3, %0"
+               : "+v"(acc), "=&v"(t)
+               : "v"(x), "v"(c));
+}
+
+// Raw samples of one FFT pair as this lane holds them: x[.][r] = (frame a, frame b)
+// at n = gl + i*G + r*NB1.
 template <int N>
-__global__ __launch_bounds__(Layout<N>::THREADS) void stft_psd_kernel(StftArgs a) {
+struct PairSamples {
+  static constexpr int R1 = Cfg<N>::R1;
+  static constexpr int BPL1 = (N / R1) / Cfg<N>::G;
+  float2 x[BPL1][R1];
+};
+
+template <int N>
+__device__ __forceinline__ void load_pair(PairSamples<N>& s, const float* xs, long long hop,
+                                          int fa, int T, int gl) {
+  constexpr int G = Cfg<N>::G;
+  constexpr int NB1 = N / Cfg<N>::R1;
+  // Frames past the end read frame 0 of the same shot (always in bounds); they are
+  // zeroed at use: loads stay unconditional (no per-element branch / wait).
+  const float* xa = xs + (long long)(fa < T ? fa : 0) * hop + gl;
+  const float* xb = xs + (long long)(fa + 1 < T ? fa + 1 : 0) * hop + gl;
+#pragma unroll
+  for (int i = 0; i < PairSamples<N>::BPL1; ++i)
+#pragma unroll
+    for (int r = 0; r < PairSamples<N>::R1; ++r) {
+      const int o = i * G + r * NB1;
+      s.x[i][r] = make_float2(xa[o], xb[o]);
+    }
+}
+
+// Detrend + window + all FFT passes for one pair; leaves Z (natural order) in `buf`
+// and returns the fp64 DC bins of both frames.
+template <int N>
+__device__ __forceinline__ void fft_pair(const StftArgs& a, const PairSamples<N>& in, bool va,
+                                         bool vb, const float2* s_tw, const float* s_win,
+                                         const double* s_dc, float2* buf, int gl, double& dca,
+                                         double& dcb) {
   using C = Cfg<N>;
-  using Lo = Layout<N>;
   constexpr int G = C::G;
   constexpr int R1 = C::R1;
   constexpr int NB1 = N / R1;
   constexpr int BPL1 = NB1 / G;
   constexpr int LOGR1 = ilog2(R1);
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float2* s_tw = reinterpret_cast<float2*>(smem + Lo::OFF_TW);
-  float* s_win = reinterpret_cast<float*>(smem + Lo::OFF_WIN);
-  float* s_tile = reinterpret_cast<float*>(smem + Lo::OFF_TILE);
-  float* s_red = reinterpret_cast<float*>(smem + Lo::OFF_RED);
-
-  const int tid = threadIdx.x;
-  const int shot = blockIdx.y;
-  const int t0 = blockIdx.x * Lo::TF;
-
-  for (int i = tid; i < N; i += Lo::THREADS) {
-    s_tw[i] = a.twiddle[i];
-    s_win[i] = a.window[i];
-  }
-  __syncthreads();
-
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int gl = lane % G;                          // lane within the FFT group
-  const int fi = wave * (64 / G) + lane / G;        // FFT index within the tile
-  float2* buf = reinterpret_cast<float2*>(smem + Lo::OFF_BUF) + fi * Lo::BUF;
-  const int fa = t0 + 2 * fi;                       // frame index of the real part
-  const bool va = fa < a.T;
-  const bool vb = fa + 1 < a.T;
-  // Invalid frames (tail of the last tile) read frame 0 of the same shot and are
-  // zeroed after the load: loads stay unconditional (no per-element branch/wait).
-  const float* xs = a.x + (long long)shot * a.x_stride;
-  const float* xa = xs + (long long)(va ? fa : 0) * a.hop;
-  const float* xb = xs + (long long)(vb ? fa + 1 : 0) * a.hop;
-
-  // ---- pass 1: load, detrend, window, radix-R1 DIF, store to LDS ----
-  // Detrend in two sweeps over the register-resident samples: a rough mean m1
-  // (division by N = 2^k is exact), then mean/slope of the residuals x - m1. The
-  // rounding of m1 then never enters y coherently: the post-detrend DC bin (tiny by
-  // construction, and the usual argmin of the spectrogram) keeps fp32-rounding
-  // accuracy instead of inheriting |mean| * eps * sum(w).
-  float2 v[BPL1][R1];
   constexpr float kmid = 0.5f * float(N - 1);
   constexpr float invN = 1.0f / float(N);
-  float s0a = 0.f, s0b = 0.f;
-  // DC bin in fp64: X_0 = sum_n w_n y_n = <x, c> with c = w - mean(w) - kc * sum(w kc)/sum(kc^2)
+
+  // DC bin in fp64: X_0 = sum_n w_n y_n = <x, c> with c = w - mean(w) - kc*sum(w kc)/sum(kc^2)
   // (c is orthogonal to constants and ramps, so the detrend cancellation happens exactly
   // in the coefficients, not in the data). After detrending X_0 is tiny by construction;
   // in fp32 it would sit at the rounding floor eps*||w y|| and, being the usual
   // spectrogram minimum under 'spectrum' scaling, would shift every normalised value.
-  double dca = 0.0, dcb = 0.0;
+  float2 v[BPL1][R1];
+  float s0a = 0.f, s0b = 0.f;
+  dca = 0.0;
+  dcb = 0.0;
+  const double* dcp = s_dc + gl;
 #pragma unroll
-  for (int i = 0; i < BPL1; ++i) {
-    const int b = gl + i * G;
+  for (int i = 0; i < BPL1; ++i)
 #pragma unroll
     for (int r = 0; r < R1; ++r) {
-      const int n = b + r * NB1;
-      const float la = xa[n], lb = xb[n];
-      const float xa_n = va ? la : 0.f;
-      const float xb_n = vb ? lb : 0.f;
+      const float xa_n = va ? in.x[i][r].x : 0.f;
+      const float xb_n = vb ? in.x[i][r].y : 0.f;
       v[i][r] = make_float2(xa_n, xb_n);
       s0a += xa_n;
       s0b += xb_n;
-      const double c = a.dc_coef[n];
-      dca = fma((double)xa_n, c, dca);
-      dcb = fma((double)xb_n, c, dcb);
+      const double c = dcp[i * G + r * NB1];
+      dc_fma(dca, xa_n, c);
+      dc_fma(dcb, xb_n, c);
     }
-  }
-#pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1) {
-    dca += __shfl_xor(dca, m);
-    dcb += __shfl_xor(dcb, m);
-  }
-  float lo_a = 0.f, lo_b = 0.f, slope_a = 0.f, slope_b = 0.f;
+  dca = group_sum<G>(dca);
+  dcb = group_sum<G>(dcb);
+
+  // Detrend in two sweeps over the register-resident samples: a rough mean m1
+  // (division by N = 2^k is exact), then mean/slope of the residuals x - m1, so the
+  // rounding of m1 never enters y coherently. With kc_n = n - (N-1)/2 and
+  // n = gl + j (j = i*G + r*NB1 a compile-time offset): kc = kc0 + j, so every
+  // per-register factor is an immediate (no per-lane kc registers).
+  const float kc0 = float(gl) - kmid;
+  float A_a = 0.f, A_b = 0.f, B_a = 0.f, B_b = 0.f;  // y = r - A - B*j
   if (a.detrend != SPECENH_DETREND_NONE) {
-#pragma unroll
-    for (int m = G / 2; m >= 1; m >>= 1) {
-      s0a += __shfl_xor(s0a, m);
-      s0b += __shfl_xor(s0b, m);
-    }
+    s0a = group_sum<G>(s0a);
+    s0b = group_sum<G>(s0b);
     const float m1a = s0a * invN, m1b = s0b * invN;
     float r0a = 0.f, r0b = 0.f, r1a = 0.f, r1b = 0.f;
 #pragma unroll
-    for (int i = 0; i < BPL1; ++i) {
-      const int b = gl + i * G;
+    for (int i = 0; i < BPL1; ++i)
 #pragma unroll
       for (int r = 0; r < R1; ++r) {
-        const float kc = float(b + r * NB1) - kmid;
+        const float j = float(i * G + r * NB1);
         const float ra = v[i][r].x - m1a, rb = v[i][r].y - m1b;
         v[i][r] = make_float2(ra, rb);
         r0a += ra;
         r0b += rb;
-        r1a = fmaf(kc, ra, r1a);
-        r1b = fmaf(kc, rb, r1b);
+        r1a = fmaf(j, ra, r1a);
+        r1b = fmaf(j, rb, r1b);
       }
-    }
-#pragma unroll
-    for (int m = G / 2; m >= 1; m >>= 1) {
-      r0a += __shfl_xor(r0a, m);
-      r0b += __shfl_xor(r0b, m);
-      r1a += __shfl_xor(r1a, m);
-      r1b += __shfl_xor(r1b, m);
-    }
-    lo_a = r0a * invN;
-    lo_b = r0b * invN;
+    r1a = fmaf(kc0, r0a, r1a);  // lane sums of kc*r = kc0*sum(r) + sum(j*r)
+    r1b = fmaf(kc0, r0b, r1b);
+    r0a = group_sum<G>(r0a);
+    r0b = group_sum<G>(r0b);
+    r1a = group_sum<G>(r1a);
+    r1b = group_sum<G>(r1b);
+    A_a = r0a * invN;
+    A_b = r0b * invN;
     if (a.detrend == SPECENH_DETREND_LINEAR) {
-      slope_a = r1a * a.inv_kk;
-      slope_b = r1b * a.inv_kk;
+      const float sa = r1a * a.inv_kk, sb = r1b * a.inv_kk;
+      A_a = fmaf(sa, kc0, A_a);
+      A_b = fmaf(sb, kc0, A_b);
+      B_a = sa;
+      B_b = sb;
     }
   }
+  const float* win = s_win + gl;
 #pragma unroll
   for (int i = 0; i < BPL1; ++i) {
     const int b = gl + i * G;
 #pragma unroll
     for (int r = 0; r < R1; ++r) {
-      const int n = b + r * NB1;
-      const float kc = float(n) - kmid;
-      const float w = s_win[n];
-      const float ya = fmaf(-slope_a, kc, v[i][r].x - lo_a);
-      const float yb = fmaf(-slope_b, kc, v[i][r].y - lo_b);
+      const int j = i * G + r * NB1;
+      const float w = win[j];
+      const float ya = fmaf(-B_a, float(j), v[i][r].x - A_a);
+      const float yb = fmaf(-B_b, float(j), v[i][r].y - A_b);
       v[i][r] = make_float2(w * ya, w * yb);
     }
     fft_dif<R1>(v[i]);
@@ -263,29 +328,86 @@ __global__ __launch_bounds__(Layout<N>::THREADS) void stft_psd_kernel(StftArgs a
     for (int r = 0; r < R1; ++r) buf[pad(b * R1 + bitrev(r, LOGR1))] = v[i][r];
   }
   wave_lds_sync();
+  stockham_pass<N, G, C::R2, R1>(buf, s_tw + TwOff<N>::P2, gl);
+  if constexpr (C::R3 > 1) stockham_pass<N, G, C::R3, R1 * C::R2>(buf, s_tw + TwOff<N>::P3, gl);
+}
 
-  // ---- remaining Stockham passes in LDS ----
-  stockham_pass<N, G, C::R2, R1>(buf, s_tw, gl);
-  if constexpr (C::R3 > 1) stockham_pass<N, G, C::R3, R1 * C::R2>(buf, s_tw, gl);
+// One workgroup per spectrogram (shot): loops over tiles of TF frames. Tables are
+// staged in LDS once per shot; each lane group's next-tile samples are prefetched
+// into registers while the current tile computes. Per tile every lane group runs one
+// FFT pair and keeps its PSD / log2-PSD values (IB bins x 2 frames) in registers;
+// the FFT buffers are then reused as the (bins x frames) tile so the store writes
+// frequency-row segments of TF frames. With NORMALIZE the workgroup knows the whole
+// spectrogram's min/max at the end and rescales its own output in a final sweep
+// (the rows were written moments ago and are re-read from the on-die caches).
+template <int N>
+__global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_kernel(
+    StftArgs a) {
+  using C = Cfg<N>;
+  using Lo = Layout<N>;
+  constexpr int G = C::G;
+  constexpr int IB = Lo::IB;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* s_dc = reinterpret_cast<double*>(smem + Lo::OFF_DC);
+  float2* s_tw = reinterpret_cast<float2*>(smem + Lo::OFF_TW);
+  float* s_win = reinterpret_cast<float*>(smem + Lo::OFF_WIN);
+  float* s_tile = reinterpret_cast<float*>(smem + Lo::OFF_BUF);
+  float* s_red = reinterpret_cast<float*>(smem + Lo::OFF_RED);
 
-  // ---- epilogue: separate the two frames, PSD, log, min/max, stage the tile ----
+  const int tid = threadIdx.x;
+  const long long shot = blockIdx.x;
+  for (int i = tid; i < Lo::TWN; i += Lo::THREADS) s_tw[i] = a.twiddle[i];
+  for (int i = tid; i < N; i += Lo::THREADS) {
+    s_win[i] = a.window[i];
+    s_dc[i] = a.dc_coef[i];
+  }
+
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int gl = lane % G;                          // lane within the FFT group
+  const int fi = wave * (64 / G) + lane / G;        // FFT index within the tile
+  float2* buf = reinterpret_cast<float2*>(smem + Lo::OFF_BUF) + fi * Lo::BUF;
+  const float* xs = a.x + shot * a.x_stride;
   const bool want_log = (a.flags & (SPECENH_STFT_LOG | SPECENH_STFT_NORMALIZE)) != 0;
   const bool log2_out = (a.flags & SPECENH_STFT_NORMALIZE) != 0;
+  const float scale_mid = 0.5f * a.scale, scale_end = 0.25f * a.scale;
+  const int ntiles = (a.T + Lo::TF - 1) / Lo::TF;
+  float* o_shot = a.out + shot * (long long)a.F_out * a.T;
   float lmin = INFINITY, lmax = -INFINITY;
-  const int fl = 2 * fi;
-  constexpr int IB = (Lo::NBINS + G - 1) / G;
-#pragma unroll 4
-  for (int i = 0; i < IB; ++i) {
-    const int k = gl + i * G;
-    if (k < Lo::NBINS) {
-      const float2 zk = buf[pad(k)];
-      const float2 zm = buf[pad((N - k) & (N - 1))];
+
+  PairSamples<N> nxt;
+  if constexpr (C::PF) load_pair<N>(nxt, xs, a.hop, 2 * fi, a.T, gl);
+  __syncthreads();
+
+  for (int tile = 0; tile < ntiles; ++tile) {
+    const int t0 = tile * Lo::TF;
+    const int fa = t0 + 2 * fi;
+    const bool va = fa < a.T;
+    const bool vb = fa + 1 < a.T;
+    PairSamples<N> cur;
+    if constexpr (C::PF) {
+      cur = nxt;
+      if (tile + 1 < ntiles) load_pair<N>(nxt, xs, a.hop, fa + Lo::TF, a.T, gl);
+    } else {
+      load_pair<N>(cur, xs, a.hop, fa, a.T, gl);
+    }
+    double dca, dcb;
+    fft_pair<N>(a, cur, va, vb, s_tw, s_win, s_dc, buf, gl, dca, dcb);
+
+    // ---- separate the two frames, PSD (+log2/ln), running min/max; values in registers ----
+    float pv[IB][2];
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int k = gl + i * G;
+      const int kk = k < Lo::NBINS ? k : 0;
+      const float2 zk = buf[pad(kk)];
+      const float2 zm = buf[pad((N - kk) & (N - 1))];
       const float ar = zk.x + zm.x, ai = zk.y - zm.y;
       const float br = zk.x - zm.x, bi = zk.y + zm.y;
-      const float s = (k == 0 || k == N / 2) ? 0.25f * a.scale : 0.5f * a.scale;
-      float pa = fmaf(ar, ar, ai * ai) * s;
-      float pb = fmaf(br, br, bi * bi) * s;
-      if (k == 0) {
+      const float sc = (kk == 0 || kk == N / 2) ? scale_end : scale_mid;
+      float pa = fmaf(ar, ar, ai * ai) * sc;
+      float pb = fmaf(br, br, bi * bi) * sc;
+      if (kk == 0) {
         pa = (float)(dca * dca * (double)a.scale);
         pb = (float)(dcb * dcb * (double)a.scale);
       }
@@ -297,16 +419,38 @@ __global__ __launch_bounds__(Layout<N>::THREADS) void stft_psd_kernel(StftArgs a
           pb *= 0.69314718055994530942f;
         }
       }
-      if (va) { lmin = fminf(lmin, pa); lmax = fmaxf(lmax, pa); }
-      if (vb) { lmin = fminf(lmin, pb); lmax = fmaxf(lmax, pb); }
-      s_tile[k * Lo::TS + fl] = pa;
-      s_tile[k * Lo::TS + fl + 1] = pb;
+      const bool vk = k < Lo::NBINS;
+      if (vk && va) { lmin = fminf(lmin, pa); lmax = fmaxf(lmax, pa); }
+      if (vk && vb) { lmin = fminf(lmin, pb); lmax = fmaxf(lmax, pb); }
+      pv[i][0] = pa;
+      pv[i][1] = pb;
     }
+    __syncthreads();  // every group is done with its FFT buffer: reuse as the tile
+    const int fl = 2 * fi;
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int k = gl + i * G;
+      if (k < Lo::NBINS) {
+        s_tile[k * Lo::TS + fl] = pv[i][0];
+        s_tile[k * Lo::TS + fl + 1] = pv[i][1];
+      }
+    }
+    __syncthreads();
+    // ---- store frequency-row segments: out[shot][k][t0 : t0+tfv] ----
+    const int tfv = min(Lo::TF, a.T - t0);
+    if (!(a.flags & SPECENH_STFT_DEV_NOSTORE)) {
+      float* o = o_shot + t0;
+      for (int e = tid; e < a.F_out * Lo::TF; e += Lo::THREADS) {
+        const int k = e >> Lo::LOG_TF;
+        const int f = e & (Lo::TF - 1);
+        if (f < tfv) o[(long long)k * a.T + f] = s_tile[k * Lo::TS + f];
+      }
+    }
+    __syncthreads();  // tile (= FFT buffers) free for the next tile's FFTs
   }
-  __syncthreads();
 
-  // ---- per-spectrogram min/max (one atomic pair per workgroup) ----
   if (a.flags & SPECENH_STFT_NORMALIZE) {
+    // ---- whole-spectrogram min/max, then rescale this shot's rows in place ----
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
       lmin = fminf(lmin, __shfl_xor(lmin, m));
@@ -316,47 +460,31 @@ __global__ __launch_bounds__(Layout<N>::THREADS) void stft_psd_kernel(StftArgs a
       s_red[wave] = lmin;
       s_red[C::WAVES + wave] = lmax;
     }
-    __syncthreads();
-    if (tid == 0) {
-      float mn = s_red[0], mx = s_red[C::WAVES];
-      for (int w = 1; w < C::WAVES; ++w) {
-        mn = fminf(mn, s_red[w]);
-        mx = fmaxf(mx, s_red[C::WAVES + w]);
-      }
-      atomicMin(&a.minmax[2 * shot], f2key(mn));
-      atomicMax(&a.minmax[2 * shot + 1], f2key(mx));
+    __syncthreads();  // also orders this workgroup's row stores before the re-reads
+    float mn = s_red[0], mx = s_red[C::WAVES];
+#pragma unroll
+    for (int w = 1; w < C::WAVES; ++w) {
+      mn = fminf(mn, s_red[w]);
+      mx = fmaxf(mx, s_red[C::WAVES + w]);
     }
+    const float inv = 1.0f / (mx - mn);  // max == min -> NaN, as the reference's 0/0
+    const long long total = (long long)a.F_out * a.T;
+    const long long head = ((16 - ((size_t)o_shot & 15)) & 15) / 4;  // to 16-B alignment
+    const long long h = head < total ? head : total;
+    for (long long e = tid; e < h; e += Lo::THREADS) o_shot[e] = (o_shot[e] - mn) * inv;
+    float4* o4 = reinterpret_cast<float4*>(o_shot + h);
+    const long long n4 = (total - h) / 4;
+    for (long long e = tid; e < n4; e += Lo::THREADS) {
+      float4 q = o4[e];
+      q.x = (q.x - mn) * inv;
+      q.y = (q.y - mn) * inv;
+      q.z = (q.z - mn) * inv;
+      q.w = (q.w - mn) * inv;
+      o4[e] = q;
+    }
+    for (long long e = h + 4 * n4 + tid; e < total; e += Lo::THREADS)
+      o_shot[e] = (o_shot[e] - mn) * inv;
   }
-
-  // ---- store whole frequency rows of the tile: out[shot][k][t0 : t0+TFv] ----
-  const int tfv = min(Lo::TF, a.T - t0);
-  float* o = a.out + (long long)shot * a.F_out * a.T + t0;
-  const int total = a.F_out * tfv;
-  for (int e = tid; e < total; e += Lo::THREADS) {
-    const int k = e / tfv;
-    const int f = e - k * tfv;
-    o[(long long)k * a.T + f] = s_tile[k * Lo::TS + f];
-  }
-}
-
-__global__ void minmax_init_kernel(unsigned* mm, long long batch) {
-  long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  if (i < batch) {
-    mm[2 * i] = 0xffffffffu;
-    mm[2 * i + 1] = 0u;
-  }
-}
-
-// out[b] = (L - min_b) / (max_b - min_b) over one spectrogram's F*T values.
-__global__ __launch_bounds__(256) void normalize_kernel(float* out, const unsigned* mm,
-                                                        long long per_shot) {
-  const long long shot = blockIdx.y;
-  const float mn = key2f(mm[2 * shot]);
-  const float mx = key2f(mm[2 * shot + 1]);
-  const float inv = 1.0f / (mx - mn);
-  float* o = out + shot * per_shot;
-  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < per_shot; e += 256ll * gridDim.x)
-    o[e] = (o[e] - mn) * inv;
 }
 
 template <int N>
@@ -369,8 +497,8 @@ hipError_t launch_stft(const StftArgs& a, long long batch, hipStream_t stream) {
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  dim3 grid((a.T + Lo::TF - 1) / Lo::TF, (unsigned)batch);
-  hipLaunchKernelGGL(stft_psd_kernel<N>, grid, dim3(Lo::THREADS), Lo::BYTES, stream, a);
+  hipLaunchKernelGGL(stft_psd_kernel<N>, dim3((unsigned)batch), dim3(Lo::THREADS), Lo::BYTES,
+                     stream, a);
   return hipGetLastError();
 }
 
@@ -440,10 +568,23 @@ int specenh_stft_plan_create(specenh_stft_plan** plan, int nperseg, int noverlap
       dc[i] = c;
     }
   }
-  std::vector<float2> tw(N);
-  for (int m = 0; m < N; ++m) {
-    ct::CS cs = ct::cossin_frac(m, N);
-    tw[m] = make_float2(float(cs.c), float(-cs.s));
+  std::vector<float2> tw;
+  auto add_pass = [&](int R, int NS) {  // [r-1][k] = W_N^{r k N/(NS R)}
+    for (int r = 1; r < R; ++r)
+      for (int k = 0; k < NS; ++k) {
+        ct::CS cs = ct::cossin_frac((long long)r * k * (N / (NS * R)), N);
+        tw.push_back(make_float2(float(cs.c), float(-cs.s)));
+      }
+  };
+  switch (N) {
+#define SPECENH_TW_CASE(NN)                                                              \
+  case NN:                                                                               \
+    add_pass(Cfg<NN>::R2, Cfg<NN>::R1);                                                  \
+    if (Cfg<NN>::R3 > 1) add_pass(Cfg<NN>::R3, Cfg<NN>::R1 * Cfg<NN>::R2);               \
+    break;
+    SPECENH_TW_CASE(64) SPECENH_TW_CASE(128) SPECENH_TW_CASE(256) SPECENH_TW_CASE(512)
+    SPECENH_TW_CASE(1024) SPECENH_TW_CASE(2048) SPECENH_TW_CASE(4096)
+#undef SPECENH_TW_CASE
   }
   auto* p = new specenh_stft_plan{};
   p->nperseg = N;
@@ -456,11 +597,11 @@ int specenh_stft_plan_create(specenh_stft_plan** plan, int nperseg, int noverlap
   p->scale = scaling == SPECENH_SCALING_DENSITY ? 1.0 / (fs * s2) : 1.0 / (s1 * s1);
   hipError_t e = hipGetDevice(&p->device);
   if (e == hipSuccess) e = hipMalloc(&p->d_window, N * sizeof(float));
-  if (e == hipSuccess) e = hipMalloc(&p->d_twiddle, N * sizeof(float2));
+  if (e == hipSuccess) e = hipMalloc(&p->d_twiddle, tw.size() * sizeof(float2));
   if (e == hipSuccess) e = hipMalloc(&p->d_dc, N * sizeof(double));
   if (e == hipSuccess) e = hipMemcpy(p->d_dc, dc.data(), N * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_window, win.data(), N * sizeof(float), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(p->d_twiddle, tw.data(), N * sizeof(float2), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(p->d_twiddle, tw.data(), tw.size() * sizeof(float2), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     (void)hipFree(p->d_window);
     (void)hipFree(p->d_twiddle);
@@ -483,7 +624,8 @@ int specenh_stft_plan_destroy(specenh_stft_plan* plan) {
 
 size_t specenh_stft_workspace_bytes(const specenh_stft_plan* plan, long long batch) {
   (void)plan;
-  return (size_t)(batch > 0 ? batch : 0) * 2 * sizeof(unsigned);
+  (void)batch;
+  return 0;
 }
 
 int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long batch,
@@ -498,9 +640,7 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
   if (T < 0) return (int)T;
   if (x_stride < length) return set_error(SPECENH_EINVAL, "x_stride < length");
   if (T > (1ll << 30)) return set_error(SPECENH_EINVAL, "too many frames");
-  if (flags & SPECENH_STFT_NORMALIZE) {
-    if (!workspace) return set_error(SPECENH_EINVAL, "NORMALIZE needs a workspace");
-  }
+  (void)workspace;  // no workspace needed (min/max is workgroup-local); kept for ABI stability
   hipStream_t st = (hipStream_t)stream;
   StftArgs a{};
   a.x = x;
@@ -514,22 +654,15 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
   a.flags = flags;
   a.out = out;
   a.F_out = (flags & SPECENH_STFT_DROP_NYQUIST) ? N / 2 : N / 2 + 1;
-  a.minmax = (unsigned*)workspace;
   a.window = plan->d_window;
   a.twiddle = plan->d_twiddle;
   a.dc_coef = plan->d_dc;
   const long long F_out = a.F_out;
-  for (long long b0 = 0; b0 < batch; b0 += 65535) {
-    const long long nb = std::min<long long>(65535, batch - b0);
+  for (long long b0 = 0; b0 < batch; b0 += 1 << 30) {
+    const long long nb = std::min<long long>(1 << 30, batch - b0);
     StftArgs c = a;
     c.x = x + b0 * x_stride;
     c.out = out + b0 * F_out * T;
-    c.minmax = a.minmax ? a.minmax + 2 * b0 : nullptr;
-    if (flags & SPECENH_STFT_NORMALIZE) {
-      hipLaunchKernelGGL(minmax_init_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0,
-                         st, c.minmax, nb);
-      SPECENH_HIP_CHECK(hipGetLastError());
-    }
     hipError_t e;
     switch (N) {
       case 64: e = launch_stft<64>(c, nb, st); break;
@@ -543,13 +676,6 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
     }
     if (e != hipSuccess)
       return set_error(SPECENH_EHIP, std::string("stft launch: ") + hipGetErrorString(e));
-    if (flags & SPECENH_STFT_NORMALIZE) {
-      const long long per_shot = F_out * T;
-      unsigned gx = (unsigned)std::min<long long>((per_shot + 255) / 256, 64);
-      hipLaunchKernelGGL(normalize_kernel, dim3(gx, (unsigned)nb), dim3(256), 0, st, c.out,
-                         c.minmax, per_shot);
-      SPECENH_HIP_CHECK(hipGetLastError());
-    }
   }
   return SPECENH_OK;
 }

@@ -23,8 +23,12 @@ OBJ = os.path.join(HERE, "build", "obj")
 LIB = os.path.join(HERE, "specenh", "libspecenh.so")
 ARCH = os.environ.get("SPECENH_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# -packed-fp32-ops: on CDNA4 a v_pk_*_f32 costs the issue slots of two scalar ops, and
+# VOP3P cannot take literal operands, so packed codegen only adds SGPR-held constants
+# (spills) and register-pair moves to the FFT kernels.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I" + os.path.join(REPO, "include"),
-          "-I" + CSRC, "-Wall", "-Wno-unused-function"]
+          "-I" + CSRC, "-Wall", "-Wno-unused-function",
+          "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 
 
 def _mtime(p):

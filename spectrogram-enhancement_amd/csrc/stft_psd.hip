@@ -127,6 +127,29 @@ struct Layout {
 
 __device__ __forceinline__ int pad(int e) { return e + (e >> 5); }
 
+// min/max of three floats as one instruction each (plain fminf/fmaxf get NaN-quieting
+// canonicalisation v_max ops on every operand). Operands are finite here or NaN only
+// when the input itself is NaN.
+__device__ __forceinline__ float fmin3(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float fmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// Workgroup barrier that orders LDS only: waits for this wave's LDS ops (lgkmcnt) and
+// meets the other waves, but leaves global loads (the register prefetch) and global
+// stores in flight. __syncthreads() would add s_waitcnt vmcnt(0) and serialise both.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // ---------------------------------------------------------------- lane-group sums
 // Sum over aligned groups of G lanes, result in every lane of the group. DPP
 // (quad_perm, row half-mirror, row mirror) inside a 16-lane row; ds_swizzle / a
@@ -211,31 +234,42 @@ struct PairSamples {
   float2 x[BPL1][R1];
 };
 
+// Shot-local buffer descriptor (wave-uniform base, 32-bit offsets): every sample load
+// and row store is then one VGPR offset + an immediate, not a 64-bit address pair.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
+                                           (int)(bytes < 0x7fffffffll ? bytes : 0x7fffffffll),
+                                           0x00020000);
+}
+
 template <int N>
-__device__ __forceinline__ void load_pair(PairSamples<N>& s, const float* xs, long long hop,
+__device__ __forceinline__ void load_pair(PairSamples<N>& s, __amdgpu_buffer_rsrc_t xr, int hop,
                                           int fa, int T, int gl) {
   constexpr int G = Cfg<N>::G;
   constexpr int NB1 = N / Cfg<N>::R1;
-  // Frames past the end read frame 0 of the same shot (always in bounds); they are
-  // zeroed at use: loads stay unconditional (no per-element branch / wait).
-  const float* xa = xs + (long long)(fa < T ? fa : 0) * hop + gl;
-  const float* xb = xs + (long long)(fa + 1 < T ? fa + 1 : 0) * hop + gl;
+  // Frames past the end duplicate the last frame: their spectra equal a valid one, so
+  // they cannot move the min/max and need no masking; they are never stored.
+  const int oa = ((fa < T ? fa : T - 1) * hop + gl) * 4;
+  const int ob = ((fa + 1 < T ? fa + 1 : T - 1) * hop + gl) * 4;
 #pragma unroll
   for (int i = 0; i < PairSamples<N>::BPL1; ++i)
 #pragma unroll
     for (int r = 0; r < PairSamples<N>::R1; ++r) {
-      const int o = i * G + r * NB1;
-      s.x[i][r] = make_float2(xa[o], xb[o]);
+      const int o = (i * G + r * NB1) * 4;
+      s.x[i][r] = make_float2(
+          __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, oa + o, 0, 0)),
+          __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ob + o, 0, 0)));
     }
 }
 
 // Detrend + window + all FFT passes for one pair; leaves Z (natural order) in `buf`
 // and returns the fp64 DC bins of both frames.
 template <int N>
-__device__ __forceinline__ void fft_pair(const StftArgs& a, const PairSamples<N>& in, bool va,
+__device__ __forceinline__ void fft_pair(const StftArgs& a, PairSamples<N>& in, bool va,
                                          bool vb, const float2* s_tw, const float* s_win,
                                          const double* s_dc, float2* buf, int gl, double& dca,
-                                         double& dcb) {
+                                         double& dcb, __amdgpu_buffer_rsrc_t xr, int fa_next,
+                                         bool prefetch) {
   using C = Cfg<N>;
   constexpr int G = C::G;
   constexpr int R1 = C::R1;
@@ -251,60 +285,55 @@ __device__ __forceinline__ void fft_pair(const StftArgs& a, const PairSamples<N>
   // in fp32 it would sit at the rounding floor eps*||w y|| and, being the usual
   // spectrogram minimum under 'spectrum' scaling, would shift every normalised value.
   float2 v[BPL1][R1];
-  float s0a = 0.f, s0b = 0.f;
-  dca = 0.0;
-  dcb = 0.0;
+  float s0a = 0.f, s0b = 0.f, s1a = 0.f, s1b = 0.f;
+  // 4 independent fp64 partial sums per frame: a single chain of R1 dependent
+  // v_fma_f64 would be latency-bound.
+  constexpr int NDC = 4;
+  double pda[NDC] = {}, pdb[NDC] = {};
   const double* dcp = s_dc + gl;
 #pragma unroll
   for (int i = 0; i < BPL1; ++i)
 #pragma unroll
     for (int r = 0; r < R1; ++r) {
-      const float xa_n = va ? in.x[i][r].x : 0.f;
-      const float xb_n = vb ? in.x[i][r].y : 0.f;
-      v[i][r] = make_float2(xa_n, xb_n);
+      const int j = i * G + r * NB1;
+      const float xa_n = in.x[i][r].x, xb_n = in.x[i][r].y;
+      v[i][r] = in.x[i][r];
       s0a += xa_n;
       s0b += xb_n;
-      const double c = dcp[i * G + r * NB1];
-      dc_fma(dca, xa_n, c);
-      dc_fma(dcb, xb_n, c);
+      s1a = fmaf(float(j), xa_n, s1a);
+      s1b = fmaf(float(j), xb_n, s1b);
+      const double c = dcp[j];
+      dc_fma(pda[(i * R1 + r) % NDC], xa_n, c);
+      dc_fma(pdb[(i * R1 + r) % NDC], xb_n, c);
     }
+  dca = (pda[0] + pda[1]) + (pda[2] + pda[3]);
+  dcb = (pdb[0] + pdb[1]) + (pdb[2] + pdb[3]);
+  // `in` is consumed: refill it with the next tile's samples now, so their HBM latency
+  // hides under this pair's FFT (the fences keep the loads after the reads above).
+  __builtin_amdgcn_sched_barrier(0);
+  if (prefetch) load_pair<N>(in, xr, a.hop, fa_next, a.T, gl);
+  __builtin_amdgcn_sched_barrier(0);
   dca = group_sum<G>(dca);
   dcb = group_sum<G>(dcb);
 
-  // Detrend in two sweeps over the register-resident samples: a rough mean m1
-  // (division by N = 2^k is exact), then mean/slope of the residuals x - m1, so the
-  // rounding of m1 never enters y coherently. With kc_n = n - (N-1)/2 and
-  // n = gl + j (j = i*G + r*NB1 a compile-time offset): kc = kc0 + j, so every
-  // per-register factor is an immediate (no per-lane kc registers).
+  // Linear detrend in one sweep: mean and least-squares slope from the lane sums
+  // S0 = sum x, S1 = sum j x (kc_n = kc0 + j with the lane base kc0 = gl - (N-1)/2 and
+  // j = i*G + r*NB1 a compile-time offset, so per-register factors are immediates).
+  // Only the DC bin is sensitive to the fp32 rounding of the fitted line (a coherent
+  // error times sum(w)); it is taken from the fp64 path above instead.
   const float kc0 = float(gl) - kmid;
-  float A_a = 0.f, A_b = 0.f, B_a = 0.f, B_b = 0.f;  // y = r - A - B*j
+  float A_a = 0.f, A_b = 0.f, B_a = 0.f, B_b = 0.f;  // y = x - A - B*j
   if (a.detrend != SPECENH_DETREND_NONE) {
+    s1a = fmaf(kc0, s0a, s1a);  // lane sums of kc*x
+    s1b = fmaf(kc0, s0b, s1b);
     s0a = group_sum<G>(s0a);
     s0b = group_sum<G>(s0b);
-    const float m1a = s0a * invN, m1b = s0b * invN;
-    float r0a = 0.f, r0b = 0.f, r1a = 0.f, r1b = 0.f;
-#pragma unroll
-    for (int i = 0; i < BPL1; ++i)
-#pragma unroll
-      for (int r = 0; r < R1; ++r) {
-        const float j = float(i * G + r * NB1);
-        const float ra = v[i][r].x - m1a, rb = v[i][r].y - m1b;
-        v[i][r] = make_float2(ra, rb);
-        r0a += ra;
-        r0b += rb;
-        r1a = fmaf(j, ra, r1a);
-        r1b = fmaf(j, rb, r1b);
-      }
-    r1a = fmaf(kc0, r0a, r1a);  // lane sums of kc*r = kc0*sum(r) + sum(j*r)
-    r1b = fmaf(kc0, r0b, r1b);
-    r0a = group_sum<G>(r0a);
-    r0b = group_sum<G>(r0b);
-    r1a = group_sum<G>(r1a);
-    r1b = group_sum<G>(r1b);
-    A_a = r0a * invN;
-    A_b = r0b * invN;
+    A_a = s0a * invN;
+    A_b = s0b * invN;
     if (a.detrend == SPECENH_DETREND_LINEAR) {
-      const float sa = r1a * a.inv_kk, sb = r1b * a.inv_kk;
+      s1a = group_sum<G>(s1a);
+      s1b = group_sum<G>(s1b);
+      const float sa = s1a * a.inv_kk, sb = s1b * a.inv_kk;
       A_a = fmaf(sa, kc0, A_a);
       A_b = fmaf(sb, kc0, A_b);
       B_a = sa;
@@ -367,7 +396,7 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
   const int gl = lane % G;                          // lane within the FFT group
   const int fi = wave * (64 / G) + lane / G;        // FFT index within the tile
   float2* buf = reinterpret_cast<float2*>(smem + Lo::OFF_BUF) + fi * Lo::BUF;
-  const float* xs = a.x + shot * a.x_stride;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + shot * a.x_stride, a.x_stride * 4);
   const bool want_log = (a.flags & (SPECENH_STFT_LOG | SPECENH_STFT_NORMALIZE)) != 0;
   const bool log2_out = (a.flags & SPECENH_STFT_NORMALIZE) != 0;
   const float scale_mid = 0.5f * a.scale, scale_end = 0.25f * a.scale;
@@ -375,57 +404,62 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
   float* o_shot = a.out + shot * (long long)a.F_out * a.T;
   float lmin = INFINITY, lmax = -INFINITY;
 
+  const __amdgpu_buffer_rsrc_t orr = make_rsrc(o_shot, (long long)a.F_out * a.T * 4);
   PairSamples<N> nxt;
-  if constexpr (C::PF) load_pair<N>(nxt, xs, a.hop, 2 * fi, a.T, gl);
+  if constexpr (C::PF) load_pair<N>(nxt, xr, a.hop, 2 * fi, a.T, gl);
   __syncthreads();
 
   for (int tile = 0; tile < ntiles; ++tile) {
     const int t0 = tile * Lo::TF;
     const int fa = t0 + 2 * fi;
-    const bool va = fa < a.T;
-    const bool vb = fa + 1 < a.T;
-    PairSamples<N> cur;
-    if constexpr (C::PF) {
-      cur = nxt;
-      if (tile + 1 < ntiles) load_pair<N>(nxt, xs, a.hop, fa + Lo::TF, a.T, gl);
-    } else {
-      load_pair<N>(cur, xs, a.hop, fa, a.T, gl);
-    }
+    const bool va = true, vb = true;  // tail frames are clamped duplicates (load_pair)
+    if constexpr (!C::PF) load_pair<N>(nxt, xr, a.hop, fa, a.T, gl);
     double dca, dcb;
-    fft_pair<N>(a, cur, va, vb, s_tw, s_win, s_dc, buf, gl, dca, dcb);
+    fft_pair<N>(a, nxt, va, vb, s_tw, s_win, s_dc, buf, gl, dca, dcb, xr, fa + Lo::TF,
+                C::PF && tile + 1 < ntiles);
 
     // ---- separate the two frames, PSD (+log2/ln), running min/max; values in registers ----
     float pv[IB][2];
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
+      // bins k = gl + i*G: only i == 0 holds k = 0 (gl == 0), only i == IB-1 can hold
+      // k = N/2 and k > N/2 (clamped to a duplicate of bin gl), all compile-time known.
       const int k = gl + i * G;
-      const int kk = k < Lo::NBINS ? k : 0;
+      const int kk = (i == IB - 1 && k >= Lo::NBINS) ? gl : k;
       const float2 zk = buf[pad(kk)];
       const float2 zm = buf[pad((N - kk) & (N - 1))];
       const float ar = zk.x + zm.x, ai = zk.y - zm.y;
       const float br = zk.x - zm.x, bi = zk.y + zm.y;
-      const float sc = (kk == 0 || kk == N / 2) ? scale_end : scale_mid;
-      float pa = fmaf(ar, ar, ai * ai) * sc;
-      float pb = fmaf(br, br, bi * bi) * sc;
-      if (kk == 0) {
-        pa = (float)(dca * dca * (double)a.scale);
-        pb = (float)(dcb * dcb * (double)a.scale);
-      }
+      float qa = fmaf(ar, ar, ai * ai);
+      float qb = fmaf(br, br, bi * bi);
+      float sc = scale_mid;
+      if (i == IB - 1 && (N / 2) % G == 0) sc = (kk == N / 2) ? scale_end : scale_mid;
+      float pa, pb;
       if (want_log) {
-        pa = __log2f(pa + a.eps);
-        pb = __log2f(pb + a.eps);
-        if (!log2_out) {
-          pa *= 0.69314718055994530942f;
-          pb *= 0.69314718055994530942f;
+        pa = __log2f(fmaf(qa, sc, a.eps));
+        pb = __log2f(fmaf(qb, sc, a.eps));
+      } else {
+        pa = qa * sc;
+        pb = qb * sc;
+      }
+      if (i == 0) {  // DC of both frames from the fp64 path (lane gl == 0 only)
+        const float da = (float)(dca * dca * (double)a.scale);
+        const float db = (float)(dcb * dcb * (double)a.scale);
+        if (gl == 0) {
+          pa = want_log ? __log2f(da + a.eps) : da;
+          pb = want_log ? __log2f(db + a.eps) : db;
         }
       }
-      const bool vk = k < Lo::NBINS;
-      if (vk && va) { lmin = fminf(lmin, pa); lmax = fmaxf(lmax, pa); }
-      if (vk && vb) { lmin = fminf(lmin, pb); lmax = fmaxf(lmax, pb); }
+      if (want_log && !log2_out) {
+        pa *= 0.69314718055994530942f;
+        pb *= 0.69314718055994530942f;
+      }
+      lmin = fmin3(lmin, pa, pb);
+      lmax = fmax3(lmax, pa, pb);
       pv[i][0] = pa;
       pv[i][1] = pb;
     }
-    __syncthreads();  // every group is done with its FFT buffer: reuse as the tile
+    lds_barrier();  // every group is done with its FFT buffer: reuse as the tile
     const int fl = 2 * fi;
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
@@ -435,18 +469,32 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
         s_tile[k * Lo::TS + fl + 1] = pv[i][1];
       }
     }
-    __syncthreads();
+    lds_barrier();
     // ---- store frequency-row segments: out[shot][k][t0 : t0+tfv] ----
+    // Compile-time trip count: the compiler can then count these stores in its partial
+    // vmcnt waits for the prefetched samples instead of draining everything.
     const int tfv = min(Lo::TF, a.T - t0);
     if (!(a.flags & SPECENH_STFT_DEV_NOSTORE)) {
-      float* o = o_shot + t0;
-      for (int e = tid; e < a.F_out * Lo::TF; e += Lo::THREADS) {
-        const int k = e >> Lo::LOG_TF;
-        const int f = e & (Lo::TF - 1);
-        if (f < tfv) o[(long long)k * a.T + f] = s_tile[k * Lo::TS + f];
+      constexpr int ST = (Lo::NBINS * Lo::TF + Lo::THREADS - 1) / Lo::THREADS;
+      constexpr int ROWS_PER_IT = Lo::THREADS >> Lo::LOG_TF;
+      const int k0 = tid >> Lo::LOG_TF;
+      const int f = tid & (Lo::TF - 1);
+      // one VGPR offset for all stores of this tile; the row step is a scalar soffset
+      const int voff = (k0 * a.T + t0 + f) * 4;
+      const int sstep = ROWS_PER_IT * a.T * 4;
+      int soff = 0;
+      asm volatile("" : "+s"(soff));  // opaque: keeps the 33 offsets from being hoisted
+                                      // out of the tile loop into (spilled) SGPRs
+#pragma unroll
+      for (int it = 0; it < ST; ++it) {
+        const int k = k0 + it * ROWS_PER_IT;
+        if (k < a.F_out && f < tfv)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s_tile[k * Lo::TS + f]), orr,
+                                                voff, soff, 0);
+        soff += sstep;
       }
     }
-    __syncthreads();  // tile (= FFT buffers) free for the next tile's FFTs
+    lds_barrier();  // tile (= FFT buffers) free for the next tile's FFTs
   }
 
   if (a.flags & SPECENH_STFT_NORMALIZE) {

@@ -12,9 +12,10 @@ Each rank owns its own 4096 shots (shot-sharded, no collective in the data path;
 weak scaling); value = all ranks' spectrograms / max-over-ranks wall time.
 
 Rank 0 prints ONE JSON line (contract in the task statement) with:
-  roofline      the dominant kernel (stft_psd_kernel) timed alone with HIP events on
-                the stream it runs on; achieved = 780,288 algorithmic bytes per
-                spectrogram x 4096 / its average launch time.
+  roofline      the dominant (and only) kernel of a step, stft_psd_kernel<1024>, timed
+                with HIP events on the stream it runs on; achieved = 780,288
+                algorithmic bytes per spectrogram x 4096 / its average launch time
+                (SURVEY.md §8(d) C2).
   cpu_baseline  the reference's CPU chain (scipy.signal.spectrogram -> log -> min-max
                 -> drop row, oracle.spectrogram.specgr_scipy) on a bounded sample of
                 the same workload, timed on this host's cores before the GPU is
@@ -99,7 +100,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from specenh import pipeline_data, stft
+    from specenh import pipeline_data
     from specenh.synthetic import plasma_chirps_torch
 
     torch.cuda.set_device(local_rank)
@@ -134,19 +135,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # ---- dominant kernel alone (stft_psd_kernel; log + drop-Nyquist, no min-max pass) ----
+    # ---- dominant kernel: the step IS one launch of stft_psd_kernel<1024> (log, min-max
+    # and drop-Nyquist fused); time that launch with HIP events on the stream it runs on ----
     stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     kreps = max(5, args.steps)
-    for _ in range(2):
-        stft.stft_psd(x, **{k: SPEC[k] for k in ("nperseg", "noverlap", "window", "fs",
-                                                 "scaling", "detrend", "eps")},
-                      log=True, drop_nyquist=True, out=out)
     ev0.record(stream)
     for _ in range(kreps):
-        stft.stft_psd(x, **{k: SPEC[k] for k in ("nperseg", "noverlap", "window", "fs",
-                                                 "scaling", "detrend", "eps")},
-                      log=True, drop_nyquist=True, out=out)
+        step()
     ev1.record(stream)
     ev1.synchronize()
     kernel_ms = ev0.elapsed_time(ev1) / kreps

@@ -82,6 +82,20 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
                      long long length, long long x_stride, float* out, int flags,
                      void* workspace, void* stream);
 
+/* ---------------------------------------------------------------- SVD denoiser
+ * Batched replacement for denoiseSignal(matrix, start, stop, use_optimal=False)
+ * (spec_denoising/denoising_by_svd.ipynb:188-229):
+ *   u, s, vh = np.linalg.svd(A, full_matrices=False)
+ *   out = u[:, start:stop] @ diag(s[start:stop]) @ vh[start:stop, :]
+ * with the notebook's clamping (start < 0 -> 0, stop > r -> r, r = min(m, n)) and
+ * start >= stop -> zeros. A: device fp32, matrix b at A + b*a_stride, row-major m x n.
+ * out: device fp32 [batch][m][n]. The top-K singular subspace it needs (K = stop, or
+ * start when stop == r) must satisfy K <= 40 (SPECENH_EUNSUPPORTED otherwise).
+ * workspace: >= specenh_svd_workspace_bytes(batch, m, n, K) bytes. */
+size_t specenh_svd_workspace_bytes(long long batch, int m, int n, int kmax);
+int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long a_stride,
+                        int start, int stop, float* out, void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,553 @@
+// svd_denoise.hip — batched SVD low-rank denoiser for gfx950.
+//
+// Replaces spec_denoising/denoising_by_svd.ipynb:188-229 (denoiseSignal):
+//   u, s, vh = np.linalg.svd(A, full_matrices=False)
+//   out = u[:, start:stop] @ diag(s[start:stop]) @ vh[start:stop, :]
+// for a batch of matrices. Identity used: s_i u_i v_i^T = A v_i v_i^T, so
+//   out = A * (V_sel V_sel^T)                       (m >= n, V right singular vectors)
+//   out = (U_sel U_sel^T) * A                       (m <  n, U left singular vectors)
+// and with V_K = the top-K vectors:
+//   [start, stop) with stop <  r : out = A V_stop V_stop^T - A V_start V_start^T
+//   [start, stop) with stop == r : out = A - A V_start V_start^T      (e.g. the default 1..r)
+// so only a top-K subspace of the Gram matrix is ever needed (K = stop or start).
+//
+// Pipeline (all HIP, one stream):
+//   1. gram_kernel     G = X^T X per matrix, X = A (m>=n) or A^T (m<n); fp32 MFMA
+//                      v_mfma_f32_32x32x2_f32 (bit-exact fp32 FMA chains), 32x32 tile per wave.
+//   2. subspace_kernel one workgroup per matrix: Y = G*Omega, then q rounds of
+//                      {CholeskyQR2 in fp64, Y = G*Z}; Rayleigh-Ritz H = Z^T G Z;
+//                      cyclic Jacobi on H (one wave); V = Z*Q sorted by Ritz value.
+//   3. recon_kernel    out = X P or X - X P with P = V_K V_K^T restricted to the selected
+//                      columns (written back in A's orientation).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+
+#include "fft_common.hpp"
+#include "specenh.h"
+
+namespace specenh {
+int set_error(int code, const std::string& msg);  // stft_psd.hip
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Element (k, i) of X for matrix b: X = A (k = row, i = col) or X = A^T.
+struct XView {
+  const float* base;
+  long long batch_stride;
+  long long sk, si;  // strides of k and i
+};
+
+// ---------------------------------------------------------------- 1. Gram
+// Each wave computes one 32x32 tile (ti <= tj) of G = X^T X over K rows of X.
+// MFMA 32x32x2 f32: lane l supplies A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31];
+// D[row][col] with col = l&31, row = (reg&3) + 8*(reg>>2) + 4*(l>>5).
+__global__ __launch_bounds__(256) void gram_kernel(XView x, int K, int r, float* G,
+                                                   int ntiles_side) {
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int ntri = ntiles_side * (ntiles_side + 1) / 2;
+  const int t = blockIdx.x * 4 + wave;
+  if (t >= ntri) return;  // wave-uniform
+  // t -> (ti, tj), ti <= tj, row-major over the upper triangle
+  int ti = 0, rem = t;
+  while (rem >= ntiles_side - ti) {
+    rem -= ntiles_side - ti;
+    ++ti;
+  }
+  const int tj = ti + rem;
+  const long long b = blockIdx.y;
+  const float* X = x.base + b * x.batch_stride;
+  const int ci = ti * 32 + (lane & 31), cj = tj * 32 + (lane & 31);
+  const int kh = lane >> 5;
+  const bool vi = ci < r, vj = cj < r;
+  const float* pi = X + (vi ? ci : 0) * x.si + kh * x.sk;
+  const float* pj = X + (vj ? cj : 0) * x.si + kh * x.sk;
+  f32x16 acc = {};
+  int k = 0;
+  for (; k + 2 <= K; k += 2) {
+    const float a = vi ? pi[(long long)k * x.sk] : 0.f;
+    const float bb = vj ? pj[(long long)k * x.sk] : 0.f;
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb, acc, 0, 0, 0);
+  }
+  if (k < K) {  // odd K: last row paired with a zero row
+    const float a = (vi && kh == 0) ? pi[(long long)k * x.sk] : 0.f;
+    const float bb = (vj && kh == 0) ? pj[(long long)k * x.sk] : 0.f;
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb, acc, 0, 0, 0);
+  }
+  float* Gb = G + b * (long long)r * r;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = ti * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+    const int col = tj * 32 + (lane & 31);
+    if (row < r && col < r) {
+      Gb[(long long)row * r + col] = acc[reg];
+      Gb[(long long)col * r + row] = acc[reg];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- 2. subspace
+constexpr int SS_THREADS = 256;
+constexpr int PMAX = 48;  // max subspace width (LDS: r=256 -> 2 x 48 KB + tables)
+
+// deterministic pseudo-random start vectors
+__device__ __forceinline__ float hash_unit(unsigned i, unsigned j) {
+  unsigned h = i * 0x9E3779B1u ^ (j + 0x7F4A7C15u) * 0x85EBCA77u;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return (float)(h & 0xFFFFFF) * (1.0f / 16777216.0f) - 0.5f;
+}
+
+// Y = G Z for symmetric G (global, r x r) and Z (LDS, r x P): Y[i][:] = sum_j G[j][i] Z[j][:].
+// One row i per thread; at each j the threads read row j of G coalesced and Z[j][:] is an
+// LDS broadcast.
+template <int P>
+__device__ void gemm_GZ(const float* G, int r, const float* sZ, float* sY) {
+  for (int i = threadIdx.x; i < r; i += SS_THREADS) {
+    float acc[P];
+#pragma unroll
+    for (int c = 0; c < P; ++c) acc[c] = 0.f;
+    for (int j = 0; j < r; ++j) {
+      const float g = G[(long long)j * r + i];
+      const float4* zj = reinterpret_cast<const float4*>(sZ + j * P);
+#pragma unroll
+      for (int c4 = 0; c4 < P / 4; ++c4) {
+        const float4 z = zj[c4];
+        acc[4 * c4 + 0] = fmaf(g, z.x, acc[4 * c4 + 0]);
+        acc[4 * c4 + 1] = fmaf(g, z.y, acc[4 * c4 + 1]);
+        acc[4 * c4 + 2] = fmaf(g, z.z, acc[4 * c4 + 2]);
+        acc[4 * c4 + 3] = fmaf(g, z.w, acc[4 * c4 + 3]);
+      }
+    }
+    float4* yi = reinterpret_cast<float4*>(sY + i * P);
+#pragma unroll
+    for (int c4 = 0; c4 < P / 4; ++c4)
+      yi[c4] = make_float4(acc[4 * c4], acc[4 * c4 + 1], acc[4 * c4 + 2], acc[4 * c4 + 3]);
+  }
+}
+
+// Orthonormalise the columns of Y (r x P, LDS) into Z with CholeskyQR in fp64:
+// S = Y^T Y, S = R^T R, Z = Y R^-1. fp64 keeps the Gram of Y (condition up to ~1e12
+// here) factorisable; callers run it twice (CholeskyQR2) for fp32-level orthogonality.
+template <int P>
+__device__ void cholqr(const float* sY, float* sZ, int r, double* sS, double* sRi) {
+  const int tid = threadIdx.x;
+  constexpr int NPAIRS = P * (P + 1) / 2;
+  for (int q = tid; q < NPAIRS; q += SS_THREADS) {
+    int a = 0, rem = q;
+    while (rem >= P - a) {
+      rem -= P - a;
+      ++a;
+    }
+    const int bcol = a + rem;
+    double s = 0.0;
+    for (int i = 0; i < r; ++i) s += (double)sY[i * P + a] * (double)sY[i * P + bcol];
+    sS[a * P + bcol] = s;
+  }
+  __syncthreads();
+  if (tid < 64) {  // Cholesky S = R^T R (R upper, in place), one wave
+    for (int k = 0; k < P; ++k) {
+      double d = sS[k * P + k];
+      d = d > 0.0 ? sqrt(d) : 1e-300;  // rank-deficient: keep going, column ~ 0
+      wave_lds_sync();
+      if (tid == 0) sS[k * P + k] = d;
+      for (int j = k + 1 + tid; j < P; j += 64) sS[k * P + j] /= d;
+      wave_lds_sync();
+      constexpr int W = P;  // trailing block <= P x P
+      for (int idx = tid; idx < W * W; idx += 64) {
+        const int i2 = idx / W, j2 = idx % W;
+        if (i2 > k && j2 >= i2) sS[i2 * P + j2] -= sS[k * P + i2] * sS[k * P + j2];
+      }
+      wave_lds_sync();
+    }
+  }
+  // R^-1 (upper) into sRi, one wave, one column per lane:
+  //   Rinv[j][j] = 1/R[j][j];  Rinv[i][j] = -(sum_{k=i+1..j} R[i][k] Rinv[k][j]) / R[i][i]
+  // (lane j reads only R and its own column of Rinv).
+  if (tid < 64) {
+    for (int idx = tid; idx < P * P; idx += 64) sRi[idx] = 0.0;
+    wave_lds_sync();
+    for (int j = tid; j < P; j += 64) {
+      sRi[j * P + j] = 1.0 / sS[j * P + j];
+      for (int i = j - 1; i >= 0; --i) {
+        double acc = 0.0;
+        for (int k = i + 1; k <= j; ++k) acc += sS[i * P + k] * sRi[k * P + j];
+        sRi[i * P + j] = -acc / sS[i * P + i];
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < r; i += SS_THREADS) {  // z = y R^-1 (row times upper triangle)
+    double z[P];
+#pragma unroll
+    for (int c = 0; c < P; ++c) z[c] = 0.0;
+#pragma unroll 1
+    for (int d = 0; d < P; ++d) {
+      const double yd = sY[i * P + d];
+      const double* rd = sRi + d * P;
+#pragma unroll
+      for (int c = 0; c < P; ++c) z[c] = fma(yd, rd[c], z[c]);  // rd[c] = 0 for c < d
+    }
+#pragma unroll
+    for (int c = 0; c < P; ++c) sZ[i * P + c] = (float)z[c];
+  }
+  __syncthreads();
+}
+
+// Parallel (round-robin / Brent-Luk) cyclic Jacobi on the symmetric P x P matrix H in
+// LDS, one wave: each round rotates P/2 disjoint (a, b) pairs at once; Q accumulates
+// the eigenvectors. Angles in fp64.
+template <int P>
+__device__ void jacobi(float* sH, float* sQ, float* sCS, int* sPair) {
+  const int lane = threadIdx.x;  // wave 0
+  for (int idx = lane; idx < P * P; idx += 64) sQ[idx] = (idx / P == idx % P) ? 1.f : 0.f;
+  wave_lds_sync();
+  for (int sweep = 0; sweep < 15; ++sweep) {
+    double off = 0.0, diag = 0.0;
+    for (int idx = lane; idx < P * P; idx += 64) {
+      const double h = sH[idx];
+      if (idx / P != idx % P) off += h * h; else diag += h * h;
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+      off += __shfl_xor(off, m);
+      diag += __shfl_xor(diag, m);
+    }
+    if (off <= 1e-28 * diag) break;  // uniform
+    for (int round = 0; round < P - 1; ++round) {
+      if (lane < P / 2) {  // tournament pairing: player 0 fixed, others rotate
+        auto player = [&](int k) { return k == 0 ? 0 : 1 + (k - 1 + round) % (P - 1); };
+        int a = player(lane), b = player(P - 1 - lane);
+        if (a > b) { const int t = a; a = b; b = t; }
+        const double hab = sH[a * P + b];
+        double c = 1.0, s = 0.0;
+        if (fabs(hab) > 1e-37) {
+          const double haa = sH[a * P + a], hbb = sH[b * P + b];
+          const double tau = (hbb - haa) / (2.0 * hab);
+          const double tt = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+          c = 1.0 / sqrt(1.0 + tt * tt);
+          s = tt * c;
+        }
+        sCS[2 * lane] = (float)c;
+        sCS[2 * lane + 1] = (float)s;
+        sPair[2 * lane] = a;
+        sPair[2 * lane + 1] = b;
+      }
+      wave_lds_sync();
+      for (int idx = lane; idx < (P / 2) * P; idx += 64) {  // rows a, b of every pair
+        const int j = idx / P, k = idx % P;
+        const int a = sPair[2 * j], b = sPair[2 * j + 1];
+        const float c = sCS[2 * j], s = sCS[2 * j + 1];
+        const float xa = sH[a * P + k], xb = sH[b * P + k];
+        sH[a * P + k] = c * xa - s * xb;
+        sH[b * P + k] = s * xa + c * xb;
+      }
+      wave_lds_sync();
+      for (int idx = lane; idx < (P / 2) * P; idx += 64) {  // columns a, b; Q columns
+        const int j = idx / P, k = idx % P;
+        const int a = sPair[2 * j], b = sPair[2 * j + 1];
+        const float c = sCS[2 * j], s = sCS[2 * j + 1];
+        const float xa = sH[k * P + a], xb = sH[k * P + b];
+        sH[k * P + a] = c * xa - s * xb;
+        sH[k * P + b] = s * xa + c * xb;
+        const float qa = sQ[k * P + a], qb = sQ[k * P + b];
+        sQ[k * P + a] = c * qa - s * qb;
+        sQ[k * P + b] = s * qa + c * qb;
+      }
+      wave_lds_sync();
+    }
+  }
+}
+
+template <int P>
+struct SsLayout {
+  static size_t bytes(int r) {
+    return (size_t)2 * r * P * 4 + (size_t)2 * P * P * 8 + (size_t)2 * P * P * 4 + P * 4 + P * 8 +
+           64;
+  }
+};
+
+// One workgroup per matrix: top-K eigenpairs of G (r x r) -> V[b] (r x K), theta[b] (K).
+template <int P>
+__global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, int r, int K,
+                                                              int iters, float* V,
+                                                              float* theta) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* sS = reinterpret_cast<double*>(smem);            // P x P
+  double* sRi = sS + P * P;                                  // P x P
+  float* sZ = reinterpret_cast<float*>(sRi + P * P);        // r x P
+  float* sY = sZ + r * P;                                    // r x P
+  float* sH = sY + r * P;                                    // P x P
+  float* sQ = sH + P * P;                                    // P x P
+  float* sCS = sQ + P * P;                                   // P (c, s per pair)
+  int* sPair = reinterpret_cast<int*>(sCS + P);              // P
+  int* sOrd = sPair + P;                                     // P
+  const long long b = blockIdx.x;
+  const float* Gb = G + b * (long long)r * r;
+  const int tid = threadIdx.x;
+
+  for (int idx = tid; idx < r * P; idx += SS_THREADS) sZ[idx] = hash_unit(idx / P, idx % P);
+  __syncthreads();
+  gemm_GZ<P>(Gb, r, sZ, sY);
+  __syncthreads();
+  for (int it = 0; it < iters; ++it) {
+    cholqr<P>(sY, sZ, r, sS, sRi);  // Z = orth(Y)
+    cholqr<P>(sZ, sY, r, sS, sRi);  // second pass into Y ...
+    gemm_GZ<P>(Gb, r, sY, sZ); // ... Z = G * orth(Y)
+    __syncthreads();
+    // swap names: basis in sY, product in sZ -> keep (Y := product, Z := basis)
+    float* t = sY;
+    sY = sZ;
+    sZ = t;
+  }
+  // Rayleigh-Ritz: H = Z^T (G Z) = Z^T Y
+  for (int q = tid; q < P * P; q += SS_THREADS) {
+    const int a = q / P, c = q % P;
+    double s = 0.0;
+    for (int i = 0; i < r; ++i) s += (double)sZ[i * P + a] * (double)sY[i * P + c];
+    sH[q] = (float)s;
+  }
+  __syncthreads();
+  for (int q = tid; q < P * P; q += SS_THREADS) {  // symmetrise
+    const int a = q / P, c = q % P;
+    if (a < c) {
+      const float m = 0.5f * (sH[a * P + c] + sH[c * P + a]);
+      sH[a * P + c] = m;
+      sH[c * P + a] = m;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    jacobi<P>(sH, sQ, sCS, sPair);
+    if (tid == 0) {  // sort Ritz values descending (insertion sort, P <= 64)
+      for (int c = 0; c < P; ++c) sOrd[c] = c;
+      for (int c = 1; c < P; ++c) {
+        const int key = sOrd[c];
+        int d = c - 1;
+        while (d >= 0 && sH[sOrd[d] * P + sOrd[d]] < sH[key * P + key]) {
+          sOrd[d + 1] = sOrd[d];
+          --d;
+        }
+        sOrd[d + 1] = key;
+      }
+    }
+  }
+  __syncthreads();
+  float* Vb = V + b * (long long)r * K;  // V[:, c] = Z Q[:, ord[c]], c < K
+  for (int idx = tid; idx < r * K; idx += SS_THREADS) {
+    const int i = idx / K, c = idx % K;
+    const int col = sOrd[c];
+    double s = 0.0;
+#pragma unroll
+    for (int d = 0; d < P; ++d) s += (double)sZ[i * P + d] * sQ[d * P + col];
+    Vb[(long long)i * K + c] = (float)s;
+  }
+  if (tid < K) theta[b * K + tid] = sH[sOrd[tid] * P + sOrd[tid]];
+}
+
+// ---------------------------------------------------------------- 3. reconstruction
+// Workgroup = (matrix, block of RB X-rows). With X_blk (RB x r), V (r x K):
+//   Y = X_blk V_K                       (RB x K)      phase 1
+//   out = Y[:, lo:hi] V[:, lo:hi]^T     (RB x r)      phase 2 (complement: X_blk - ...)
+constexpr int RB = 32;
+
+template <int KP>
+__global__ __launch_bounds__(256) void recon_kernel(XView x, int Kr, int r, const float* V,
+                                                    int K, int lo, int hi, int complement,
+                                                    float* out, long long out_bstride,
+                                                    long long osk, long long osi) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* sV = reinterpret_cast<float*>(smem);  // r x KP (zero-padded columns)
+  float* sX = sV + r * KP;                      // RB x (r + 1)
+  float* sY = sX + RB * (r + 1);                // RB x KP
+  const long long b = blockIdx.y;
+  const int k0 = blockIdx.x * RB;
+  const int tid = threadIdx.x;
+  const float* X = x.base + b * x.batch_stride;
+  const float* Vb = V + b * (long long)r * K;
+  for (int idx = tid; idx < r * KP; idx += 256) {
+    const int i = idx / KP, c = idx % KP;
+    sV[idx] = (c >= lo && c < hi) ? Vb[(long long)i * K + c] : 0.f;  // only used columns
+  }
+  const int rows = min(RB, Kr - k0);
+  if (x.si == 1) {
+    for (int idx = tid; idx < RB * r; idx += 256) {
+      const int kk = idx / r, i = idx % r;
+      sX[kk * (r + 1) + i] = kk < rows ? X[(long long)(k0 + kk) * x.sk + i] : 0.f;
+    }
+  } else {  // transposed view: read along the contiguous k direction
+    for (int idx = tid; idx < RB * r; idx += 256) {
+      const int i = idx / RB, kk = idx % RB;
+      sX[kk * (r + 1) + i] = kk < rows ? X[(long long)(k0 + kk) * x.sk + (long long)i * x.si] : 0.f;
+    }
+  }
+  __syncthreads();
+  // phase 1: RB x KP entries of Y, 256 threads
+  for (int e = tid; e < RB * KP; e += 256) {
+    const int kk = e / KP, c = e % KP;
+    float s = 0.f;
+    if (c >= lo && c < hi)
+      for (int i = 0; i < r; ++i) s = fmaf(sX[kk * (r + 1) + i], sV[i * KP + c], s);
+    sY[e] = s;
+  }
+  __syncthreads();
+  // phase 2: out rows, thread per column i (coalesced along i for m >= n)
+  float* Ob = out + b * out_bstride;
+  for (int e = tid; e < RB * r; e += 256) {
+    int kk, i;
+    if (osi == 1) { kk = e / r; i = e % r; } else { i = e / RB; kk = e % RB; }
+    if (kk >= rows) continue;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < KP; ++c) s = fmaf(sY[kk * KP + c], sV[i * KP + c], s);
+    const float v = complement ? sX[kk * (r + 1) + i] - s : s;
+    Ob[(long long)(k0 + kk) * osk + (long long)i * osi] = v;
+  }
+}
+
+}  // namespace specenh
+
+using namespace specenh;
+
+namespace {
+template <int P>
+hipError_t launch_subspace_t(const float* G, int r, int K, float* V, float* theta,
+                             long long batch, hipStream_t st) {
+  const size_t lds = SsLayout<P>::bytes(r);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipError_t e = hipFuncSetAttribute((const void*)subspace_kernel<P>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(subspace_kernel<P>, dim3((unsigned)batch), dim3(SS_THREADS), lds, st, G, r,
+                     K, 3, V, theta);
+  return hipGetLastError();
+}
+
+hipError_t launch_subspace(int p, const float* G, int r, int K, float* V, float* theta,
+                           long long batch, hipStream_t st) {
+  switch (p) {
+    case 8: return launch_subspace_t<8>(G, r, K, V, theta, batch, st);
+    case 16: return launch_subspace_t<16>(G, r, K, V, theta, batch, st);
+    case 24: return launch_subspace_t<24>(G, r, K, V, theta, batch, st);
+    case 32: return launch_subspace_t<32>(G, r, K, V, theta, batch, st);
+    case 40: return launch_subspace_t<40>(G, r, K, V, theta, batch, st);
+    case 48: return launch_subspace_t<48>(G, r, K, V, theta, batch, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int KP>
+hipError_t launch_recon_t(XView xb, int Kr, int r, const float* V, int K, int lo, int hi,
+                          int comp, float* out, long long ob, long long osk, long long osi,
+                          long long nb, hipStream_t st) {
+  const size_t lds = (size_t)r * KP * 4 + (size_t)RB * (r + 1) * 4 + (size_t)RB * KP * 4;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipError_t e = hipFuncSetAttribute((const void*)recon_kernel<KP>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(recon_kernel<KP>, dim3((Kr + RB - 1) / RB, (unsigned)nb), dim3(256), lds,
+                     st, xb, Kr, r, V, K, lo, hi, comp, out, ob, osk, osi);
+  return hipGetLastError();
+}
+
+hipError_t launch_recon(int KP, XView xb, int Kr, int r, const float* V, int K, int lo, int hi,
+                        int comp, float* out, long long ob, long long osk, long long osi,
+                        long long nb, hipStream_t st) {
+  switch (KP) {
+#define SPECENH_RC(n) \
+  case n: return launch_recon_t<n>(xb, Kr, r, V, K, lo, hi, comp, out, ob, osk, osi, nb, st);
+    SPECENH_RC(8) SPECENH_RC(16) SPECENH_RC(24) SPECENH_RC(32) SPECENH_RC(40) SPECENH_RC(48)
+#undef SPECENH_RC
+    default: return hipErrorInvalidValue;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+size_t specenh_svd_workspace_bytes(long long batch, int m, int n, int kmax) {
+  const long long r = std::min(m, n);
+  return (size_t)(batch * r * r + batch * r * kmax + batch * kmax) * sizeof(float);
+}
+
+int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long a_stride,
+                        int start, int stop, float* out, void* workspace, void* stream) {
+  if (batch < 0 || m <= 0 || n <= 0) return set_error(SPECENH_EINVAL, "bad matrix shape");
+  if (batch == 0) return SPECENH_OK;
+  if (!A || !out || !workspace) return set_error(SPECENH_EINVAL, "null pointer");
+  if (a_stride < (long long)m * n) return set_error(SPECENH_EINVAL, "a_stride < m*n");
+  const int r = std::min(m, n);
+  // denoising_by_svd.ipynb:224-227 clamping
+  if (start < 0) start = 0;
+  if (stop > r) stop = r;
+  hipStream_t st = (hipStream_t)stream;
+  const long long ob = (long long)m * n;
+  if (stop <= start) {  // empty range: zeros (u[:, s:s] @ ... = 0)
+    if (hipMemsetAsync(out, 0, (size_t)batch * ob * sizeof(float), st) != hipSuccess)
+      return set_error(SPECENH_EHIP, "memset");
+    return SPECENH_OK;
+  }
+  // Needed top-K subspace: complement form when stop == r.
+  const bool complement = (stop == r);
+  const int K = complement ? start : stop;
+  if (complement && start == 0) {  // whole range: out = A (u s vh reproduces A)
+    if (hipMemcpy2DAsync(out, ob * sizeof(float), A, a_stride * sizeof(float),
+                         ob * sizeof(float), batch, hipMemcpyDeviceToDevice, st) != hipSuccess)
+      return set_error(SPECENH_EHIP, "copy");
+    return SPECENH_OK;
+  }
+  if (K > PMAX - 8 || K > r)
+    return set_error(SPECENH_EUNSUPPORTED,
+                     "GPU SVD denoiser needs a top-K subspace with K <= 40 (K = stop, or start "
+                     "when stop == r)");
+  // subspace width: K + 8 oversampling, multiple of 8, <= r (rounded down to 8)
+  int p = std::max(8, ((K + 8 + 7) / 8) * 8);
+  if (p > r) p = (r / 8) * 8;
+  if (p < K || p < 8)
+    return set_error(SPECENH_EUNSUPPORTED, "matrix too small for the GPU subspace solver");
+  // X orientation: Gram over the smaller dimension
+  XView xv;
+  xv.base = A;
+  xv.batch_stride = a_stride;
+  int Kr;  // rows of X
+  long long osk, osi;
+  if (m >= n) {
+    xv.sk = n; xv.si = 1; Kr = m; osk = n; osi = 1;
+  } else {
+    xv.sk = 1; xv.si = n; Kr = n; osk = 1; osi = n;
+  }
+  const int lo = complement ? 0 : start, hi = complement ? start : stop;
+  float* G = (float*)workspace;
+  float* V = G + batch * (long long)r * r;
+  float* theta = V + batch * (long long)r * K;
+  const int nts = (r + 31) / 32;
+  const int ntri = nts * (nts + 1) / 2;
+  for (long long b0 = 0; b0 < batch; b0 += 65535) {
+    const long long nb = std::min<long long>(65535, batch - b0);
+    XView xb = xv;
+    xb.base = A + b0 * a_stride;
+    hipLaunchKernelGGL(gram_kernel, dim3((ntri + 3) / 4, (unsigned)nb), dim3(256), 0, st, xb,
+                       Kr, r, G + b0 * (long long)r * r, nts);
+  }
+  if (hipGetLastError() != hipSuccess) return set_error(SPECENH_EHIP, "gram launch");
+  const int KP = ((hi - lo > 0 ? K : 1) + 7) / 8 * 8;
+  hipError_t e = launch_subspace(p, G, r, K, V, theta, batch, st);
+  if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("subspace: ") + hipGetErrorString(e));
+  for (long long b0 = 0; b0 < batch; b0 += 65535) {
+    const long long nb = std::min<long long>(65535, batch - b0);
+    XView xb = xv;
+    xb.base = A + b0 * a_stride;
+    e = launch_recon(KP, xb, Kr, r, V + b0 * (long long)r * K, K, lo, hi, complement ? 1 : 0,
+                     out + b0 * ob, ob, osk, osi, nb, st);
+    if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("recon: ") + hipGetErrorString(e));
+  }
+  if (hipGetLastError() != hipSuccess) return set_error(SPECENH_EHIP, "recon launch");
+  return SPECENH_OK;
+}
+
+}  // extern "C"

@@ -52,6 +52,10 @@ SIGNATURES = {
     "specenh_stft_psd": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_longlong, _c.c_longlong,
                                     _c.c_longlong, _c.c_void_p, _c.c_int, _c.c_void_p,
                                     _c.c_void_p]),
+    "specenh_svd_workspace_bytes": (_c.c_size_t, [_c.c_longlong, _c.c_int, _c.c_int, _c.c_int]),
+    "specenh_svd_denoise": (_c.c_int, [_c.c_void_p, _c.c_longlong, _c.c_int, _c.c_int,
+                                       _c.c_longlong, _c.c_int, _c.c_int, _c.c_void_p,
+                                       _c.c_void_p, _c.c_void_p]),
 }
 
 

@@ -1,0 +1,101 @@
+"""Drop-in for the SVD denoiser of spec_denoising/denoising_by_svd.ipynb (cell 1).
+
+    from specenh.svd import omega, denoiseSignal, computeSignal
+    svd = denoiseSignal(s)                       # denoising_by_svd.ipynb:263
+
+Same names, arguments and semantics as the notebook (:155-229):
+  * ``omega(beta)``          Gavish-Donoho polynomial (host scalar, as in the notebook)
+  * ``denoiseSignal(matrix, start=None, stop=None, use_optimal=False)``
+        keep singular components [start, stop) — defaults start=1, stop=r; clamps
+        start<0 -> 0 and stop>r -> r; start>=stop gives zeros.
+  * ``denoise_batch(A[B, m, n], start, stop)`` — device tensors in/out (fast path).
+
+The arithmetic runs on the GPU (csrc/svd_denoise.hip through the C-ABI
+``specenh_svd_denoise``): fp32-MFMA Gram matrix, top-K subspace iteration with fp64
+CholeskyQR2 + Rayleigh-Ritz, reconstruction ``A V V^T``. numpy inputs come back as
+float64 numpy arrays like the reference. ``use_optimal`` / ``computeSignal`` need
+every singular value (the median); they are not on the GPU path yet and raise
+NotImplementedError.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def omega(beta):
+    """denoising_by_svd.ipynb:155-159 (http://www.pyrunner.com/weblog/2016/08/01/optimal-svht/)."""
+    coef = [0.56, -0.95, 1.82, 1.43]
+    poly = [beta ** (3 - n) for n in range(4)]
+    return sum(c * p for c, p in zip(coef, poly))
+
+
+def _resolve(r: int, start, stop):
+    """denoising_by_svd.ipynb:219-227 (non-optimal branch)."""
+    if start is None:
+        start = 1
+    if stop is None:
+        stop = r
+    start = int(start)
+    stop = int(stop)
+    if start < 0:
+        start = 0
+    if stop > r:
+        stop = r
+    return start, stop
+
+
+def denoise_batch(A: torch.Tensor, start=None, stop=None,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+    """Batched denoiseSignal on device tensors: ``A[B, m, n]`` (or ``[m, n]``) fp32."""
+    if not isinstance(A, torch.Tensor) or A.device.type != "cuda":
+        raise RuntimeError("specenh.svd.denoise_batch runs on the GPU only (no CPU fallback)")
+    squeeze = A.dim() == 2
+    if squeeze:
+        A = A.unsqueeze(0)
+    if A.dim() != 3:
+        raise ValueError("A must be [batch, m, n]")
+    if A.dtype != torch.float32:
+        A = A.float()
+    if not (A.stride(2) == 1 and A.stride(1) == A.shape[2]):
+        A = A.contiguous()
+    B, m, n = A.shape
+    r = min(m, n)
+    start, stop = _resolve(r, start, stop)
+    if out is None:
+        out = torch.empty((B, m, n), dtype=torch.float32, device=A.device)
+    K = max(start, stop) if stop < r else start
+    L = _lib.lib()
+    ws = torch.empty(max(16, int(L.specenh_svd_workspace_bytes(B, m, n, max(K, 1)))),
+                     dtype=torch.uint8, device=A.device)
+    _lib.check(L.specenh_svd_denoise(ctypes.c_void_p(A.data_ptr()), B, m, n, A.stride(0),
+                                     start, stop, ctypes.c_void_p(out.data_ptr()),
+                                     ctypes.c_void_p(ws.data_ptr()),
+                                     ctypes.c_void_p(_lib.current_stream_handle(A.device))),
+               "svd_denoise")
+    return out[0] if squeeze else out
+
+
+def denoiseSignal(matrix, start=None, stop=None, use_optimal=False):
+    """denoising_by_svd.ipynb:188-229."""
+    if use_optimal:
+        raise NotImplementedError("use_optimal needs every singular value (median); not on the "
+                                  "GPU path yet")
+    if isinstance(matrix, torch.Tensor):
+        return denoise_batch(matrix, start, stop)
+    a = np.asarray(matrix)
+    if not torch.cuda.is_available():
+        raise RuntimeError("specenh requires a ROCm GPU (HIP); there is no CPU fallback")
+    t = torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device="cuda")
+    return denoise_batch(t, start, stop).double().cpu().numpy()
+
+
+def computeSignal(matrix):
+    """denoising_by_svd.ipynb:161-186 (components [1, 2*num_sing) with the optimal
+    threshold): needs the median singular value — not on the GPU path yet."""
+    raise NotImplementedError("computeSignal needs every singular value (median); not on the "
+                              "GPU path yet")

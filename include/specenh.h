@@ -96,6 +96,68 @@ size_t specenh_svd_workspace_bytes(long long batch, int m, int n, int kmax);
 int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long a_stride,
                         int start, int stop, float* out, void* workspace, void* stream);
 
+/* ---------------------------------------------------------------- conv autoencoder
+ * Primitives under the Keras-shaped facade (specenh.keras) that replaces the model of
+ * VAE/manual_scan_3layers.py:186-212 (Conv2D / MaxPooling2D / Conv2DTranspose,
+ * padding "same", Adam + binary_crossentropy). Tensors are NHWC, device resident.
+ * dtype codes: SPECENH_DTYPE_F32 / SPECENH_DTYPE_BF16 (MFMA operands; accumulation,
+ * biases, master weights, gradients of weights and the loss stay fp32). */
+#define SPECENH_DTYPE_F32 0
+#define SPECENH_DTYPE_BF16 1
+#define SPECENH_ACT_NONE 0
+#define SPECENH_ACT_RELU 1
+#define SPECENH_ACT_SIGMOID 2
+
+/* Implicit-GEMM convolution: out[m][co] = act(sum_k A[m][k] * w_gemm[k][co] + bias[co]),
+ * m = (n, oy, ox) over [N][OH][OW], k = (ky, kx, ci) over [KH][KW][C],
+ * A[m][k] = in[n][iy][ix][ci] with vy = oy*stride - pad_t + ky, iy = vy / in_dil when
+ * vy >= 0, vy % in_dil == 0 and iy < IH (else 0); likewise x with pad_l.
+ *   Conv2D(k, "same") forward       stride 1, pad (k-1)/2, in_dil 1, w_gemm = HWIO kernel
+ *   Conv2DTranspose(k, 2, "same")   stride 1, pad k-1-(k-2)/2, in_dil 2, w_gemm = flipped
+ *   their input gradients           (see specenh_weight_flip_transpose)
+ * logits (optional, fp32 [M][CO]) receives the pre-activation; mask (optional, dtype
+ * [M][CO]) zeroes outputs where mask <= 0 (backward through a ReLU); out is fp32 when
+ * out_f32 != 0, else dtype. bias may be NULL. */
+int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, const void* w_gemm,
+                   int KH, int KW, int CO, const float* bias, int stride, int pad_t, int pad_l,
+                   int in_dil, int OH, int OW, int act, const void* mask, float* logits,
+                   void* out, int out_f32, void* stream);
+/* Weight gradient of the same convolution: dw[k][co] += sum_m A[m][k] * dout[m][co]
+ * (fp32, accumulated), dbias[co] += sum_m dout[m][co] (optional). Deterministic: pixel
+ * chunks are reduced in a fixed order through `workspace`, which must hold
+ * specenh_conv2d_wgrad_workspace_bytes(N, OH, OW, KH, KW, C, CO) bytes. */
+size_t specenh_conv2d_wgrad_workspace_bytes(int N, int OH, int OW, int KH, int KW, int C,
+                                            int CO);
+int specenh_conv2d_wgrad(int dtype, const void* in, int N, int IH, int IW, int C,
+                         const void* dout, int KH, int KW, int CO, int stride, int pad_t,
+                         int pad_l, int in_dil, int OH, int OW, float* dw, float* dbias,
+                         void* workspace, void* stream);
+/* MaxPooling2D((2,2), padding="same") on even H, W: out [N][H/2][W/2][C] + argmax (0..3). */
+int specenh_maxpool2_fwd(int dtype, const void* in, int N, int H, int W, int C, void* out,
+                         unsigned char* argmax, void* stream);
+/* din [N][H][W][C] = dout routed to the argmax, times (relu_in > 0) when relu_in != NULL. */
+int specenh_maxpool2_bwd(int dtype, const void* dout, const unsigned char* argmax,
+                         const void* relu_in, int N, int H, int W, int C, void* din,
+                         void* stream);
+/* binary_crossentropy after a sigmoid, from the fp32 logits z (Keras graph mode):
+ * *loss_sum += sum_i max(z,0) - z t + log1p(exp(-|z|)) (fp64, zero it first);
+ * grad (optional) = (sigmoid(z) - t) / n in grad_dtype. */
+int specenh_bce_logits(const float* z, const void* target, int target_dtype, long long n,
+                       void* grad, int grad_dtype, double* loss_sum, void* stream);
+/* Keras Adam on fp32 master weights, with g = grad_scale * grad (1/world_size after a
+ * summing all-reduce): m = b1 m + (1-b1) g, v = b2 v + (1-b2) g^2,
+ * w -= lr_t m / (sqrt(v) + eps); w_bf16 (optional) receives bf16(w). */
+int specenh_adam_step(float* w, const float* g, float* m, float* v, long long n, float lr_t,
+                      float b1, float b2, float eps, float grad_scale, void* w_bf16,
+                      void* stream);
+/* bd[((a*k + b)*co + o)*ci + i] = bf[(((k-1-a)*k + (k-1-b))*ci + i)*co + o]:
+ * the GEMM weights of a convolution's input gradient from its forward GEMM weights. */
+int specenh_weight_flip_transpose(int dtype, const void* bf, int k, int ci, int co, void* bd,
+                                  void* stream);
+/* Element conversion f32 <-> bf16 (round to nearest even). */
+int specenh_cast(int src_dtype, const void* src, int dst_dtype, void* dst, long long n,
+                 void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -56,6 +56,31 @@ SIGNATURES = {
     "specenh_svd_denoise": (_c.c_int, [_c.c_void_p, _c.c_longlong, _c.c_int, _c.c_int,
                                        _c.c_longlong, _c.c_int, _c.c_int, _c.c_void_p,
                                        _c.c_void_p, _c.c_void_p]),
+    "specenh_conv2d": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
+                                  _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_void_p,
+                                  _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
+                                  _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int,
+                                  _c.c_void_p]),
+    "specenh_conv2d_wgrad": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                        _c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                        _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
+                                        _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                        _c.c_void_p]),
+    "specenh_conv2d_wgrad_workspace_bytes": (_c.c_size_t, [_c.c_int] * 7),
+    "specenh_maxpool2_fwd": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                        _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p]),
+    "specenh_maxpool2_bwd": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                        _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_void_p,
+                                        _c.c_void_p]),
+    "specenh_bce_logits": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_longlong,
+                                      _c.c_void_p, _c.c_int, _c.c_void_p, _c.c_void_p]),
+    "specenh_adam_step": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                     _c.c_longlong, _c.c_float, _c.c_float, _c.c_float,
+                                     _c.c_float, _c.c_float, _c.c_void_p, _c.c_void_p]),
+    "specenh_weight_flip_transpose": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int,
+                                                 _c.c_int, _c.c_void_p, _c.c_void_p]),
+    "specenh_cast": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_void_p, _c.c_longlong,
+                                _c.c_void_p]),
 }
 
 

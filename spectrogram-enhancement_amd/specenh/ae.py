@@ -1,0 +1,415 @@
+"""Device engine of the convolutional autoencoder (VAE/manual_scan_3layers.py:186-212).
+
+The Keras facade (specenh.keras) builds a chain of layers and hands it to
+:class:`AutoencoderEngine`, which owns every device buffer and sequences the C-ABI
+kernels of csrc/conv_ae.hip:
+
+* forward   Conv2D / Conv2DTranspose = implicit-GEMM conv (+bias, relu/sigmoid fused),
+            MaxPooling2D = maxpool2 with argmax;
+* loss      binary_crossentropy from the last layer's fp32 logits (Keras graph mode);
+* backward  per conv layer: wgrad (+bias grad) and, except for the first layer, the
+            input gradient as another implicit-GEMM conv over flipped/transposed weights
+            whose epilogue applies the previous ReLU's mask; pools route through argmax
+            with the ReLU mask fused;
+* update    one Keras-Adam launch over ONE flat fp32 parameter buffer (GEMM layout), which
+            also refreshes the bf16 copy the MFMA kernels read; a data-parallel run
+            all-reduces the ONE flat gradient buffer (RCCL) before it.
+
+Weights live in "GEMM layout": Bf[(ky, kx, ci)][co] such that the forward pass is
+out[m][co] = sum_k A[m][k] Bf[k][co]. For Conv2D this is the Keras HWIO kernel itself;
+for Conv2DTranspose (Keras kernel [k, k, Cout, Cin]) Bf = kernel[::-1, ::-1] with the
+channel axes swapped. Adam is elementwise, so it runs on this layout directly.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+
+F32, BF16 = 0, 1
+ACT = {None: 0, "linear": 0, "relu": 1, "sigmoid": 2}
+_ALIGN = 64  # elements; keeps every layer's GEMM weights 16-byte aligned for bf16 x8 loads
+
+
+def _vp(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+@dataclass
+class ConvOp:
+    """One Conv2D (kind "conv") or Conv2DTranspose ("convT") in GEMM form."""
+    kind: str
+    cin: int
+    cout: int
+    k: int
+    act: str | None
+    stride: int = 1          # Conv2DTranspose stride (upsampling factor)
+    padding: str = "same"    # Conv2D: "same" | "valid"
+    off_w: int = 0           # offsets into the flat parameter buffer (elements)
+    off_b: int = 0
+
+    @property
+    def n_w(self):
+        return self.k * self.k * self.cin * self.cout
+
+    def out_hw(self, h, w):
+        if self.kind == "convT":
+            return h * self.stride, w * self.stride
+        if self.padding == "valid":
+            return h - self.k + 1, w - self.k + 1
+        return h, w
+
+    def fwd_geom(self):
+        """(stride, pad_t, pad_l, in_dil) of the forward implicit GEMM."""
+        k = self.k
+        if self.kind == "conv":
+            p = 0 if self.padding == "valid" else (k - 1) // 2
+            return 1, p, p, 1
+        pt = max(k - self.stride, 0) // 2              # TF SAME for the transposed conv
+        return 1, k - 1 - pt, k - 1 - pt, self.stride  # conv over the dilated input
+
+    def dgrad_geom(self):
+        """(stride, pad_t, pad_l, in_dil) of the input gradient as a conv over dOut."""
+        k = self.k
+        if self.kind == "conv":
+            p = 0 if self.padding == "valid" else (k - 1) // 2
+            return 1, k - 1 - p, k - 1 - p, 1
+        pt = max(k - self.stride, 0) // 2
+        return self.stride, pt, pt, 1
+
+
+@dataclass
+class PoolOp:
+    kind: str = "pool"
+
+
+def keras_to_gemm(op: ConvOp, kernel: np.ndarray) -> np.ndarray:
+    """Keras kernel -> Bf[(ky,kx,ci)][co] (flattened fp32)."""
+    kernel = np.asarray(kernel, dtype=np.float32)
+    if op.kind == "conv":
+        assert kernel.shape == (op.k, op.k, op.cin, op.cout), kernel.shape
+        return np.ascontiguousarray(kernel).reshape(-1)
+    assert kernel.shape == (op.k, op.k, op.cout, op.cin), kernel.shape
+    return np.ascontiguousarray(kernel[::-1, ::-1].transpose(0, 1, 3, 2)).reshape(-1)
+
+
+def gemm_to_keras(op: ConvOp, flat: np.ndarray) -> np.ndarray:
+    bf = np.asarray(flat, dtype=np.float32).reshape(op.k, op.k, op.cin, op.cout)
+    if op.kind == "conv":
+        return bf.copy()
+    return np.ascontiguousarray(bf[::-1, ::-1].transpose(0, 1, 3, 2))
+
+
+class AutoencoderEngine:
+    """Device state + kernel sequencing for a chain of Conv/Pool/ConvT layers."""
+
+    def __init__(self, ops, input_shape, compute_dtype="float32", device=None):
+        if device is None:
+            if not torch.cuda.is_available():
+                raise RuntimeError("specenh requires a ROCm GPU (HIP); there is no CPU fallback")
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("specenh.ae runs on the GPU only (no CPU fallback)")
+        self.L = _lib.lib()
+        self.ops = list(ops)
+        self.input_shape = tuple(input_shape)  # (H, W, C)
+        self.dt = BF16 if compute_dtype in ("bfloat16", "bf16", "mixed_bfloat16") else F32
+        self.tdt = torch.bfloat16 if self.dt == BF16 else torch.float32
+        self._validate()
+        off = 0
+        for op in self.ops:
+            if isinstance(op, ConvOp):
+                op.off_w = off
+                off += -(-op.n_w // _ALIGN) * _ALIGN
+                op.off_b = off
+                off += -(-op.cout // _ALIGN) * _ALIGN
+        self.n_flat = off
+        dev = self.device
+        self.w = torch.zeros(off, dtype=torch.float32, device=dev)   # fp32 master weights
+        self.g = torch.zeros(off, dtype=torch.float32, device=dev)   # gradients
+        self.m = torch.zeros(off, dtype=torch.float32, device=dev)   # Adam moments
+        self.v = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.w_lp = torch.zeros(off, dtype=self.tdt, device=dev) if self.dt == BF16 else None
+        # flipped/transposed copies for the input gradients (compute dtype)
+        self.w_d = {i: torch.zeros(op.n_w, dtype=self.tdt, device=dev)
+                    for i, op in enumerate(self.ops) if isinstance(op, ConvOp) and i > 0}
+        self.t = 0  # Adam iterations
+        self._bufs = {}
+        self._loss = torch.zeros(1, dtype=torch.float64, device=dev)
+
+    # ------------------------------------------------------------------ shapes
+    def _validate(self):
+        convs = [op for op in self.ops if isinstance(op, ConvOp)]
+        if not convs:
+            raise ValueError("model has no convolution layers")
+        h, w, c = self.input_shape
+        for i, op in enumerate(self.ops):
+            if isinstance(op, PoolOp):
+                if h % 2 or w % 2:
+                    raise NotImplementedError("MaxPooling2D on odd spatial sizes")
+                h, w = h // 2, w // 2
+                continue
+            if op.cin != c:
+                raise ValueError(f"layer {i}: expects {op.cin} channels, gets {c}")
+            if op.act not in ACT:
+                raise NotImplementedError(f"activation {op.act!r}")
+            if op.kind == "convT" and op.k < op.stride:
+                raise NotImplementedError("Conv2DTranspose with kernel_size < strides")
+            h, w = op.out_hw(h, w)
+            if h <= 0 or w <= 0:
+                raise ValueError(f"layer {i}: output size {h}x{w}")
+            c = op.cout
+        self.output_shape = (h, w, c)
+
+    def shapes(self):
+        """Per-op input shapes (H, W, C) plus the final output shape."""
+        out = []
+        h, w, c = self.input_shape
+        for op in self.ops:
+            out.append((h, w, c))
+            if isinstance(op, PoolOp):
+                h, w = h // 2, w // 2
+            else:
+                h, w = op.out_hw(h, w)
+                c = op.cout
+        out.append((h, w, c))
+        return out
+
+    def _buffers(self, N, train):
+        key = (N, train)
+        b = self._bufs.get(key)
+        if b is not None:
+            return b
+        dev, shp = self.device, self.shapes()
+        b = {"h": [None] * (len(self.ops) + 1), "am": [None] * len(self.ops),
+             "d": [None] * (len(self.ops) + 1)}
+        for i in range(1, len(self.ops) + 1):
+            H, W, C = shp[i]
+            last = i == len(self.ops)
+            dtype = torch.float32 if (last and not train) else self.tdt
+            b["h"][i] = torch.empty((N, H, W, C), dtype=dtype, device=dev)
+            if train:
+                b["d"][i] = torch.empty((N, H, W, C), dtype=self.tdt, device=dev)
+        for i, op in enumerate(self.ops):
+            if isinstance(op, PoolOp) and train:
+                H, W, C = shp[i + 1]
+                b["am"][i] = torch.empty((N, H, W, C), dtype=torch.uint8, device=dev)
+        if train:
+            H, W, C = shp[-1]
+            b["z"] = torch.empty((N, H, W, C), dtype=torch.float32, device=dev)
+            ws = 16
+            for i, op in enumerate(self.ops):
+                if isinstance(op, ConvOp):
+                    OH, OW, _ = shp[i + 1]
+                    ws = max(ws, int(self.L.specenh_conv2d_wgrad_workspace_bytes(
+                        N, OH, OW, op.k, op.k, op.cin, op.cout)))
+            b["ws"] = torch.empty(ws, dtype=torch.uint8, device=dev)
+        if len(self._bufs) >= 4:  # e.g. full + partial batch for train and inference
+            self._bufs.pop(next(iter(self._bufs)))
+        self._bufs[key] = b
+        return b
+
+    # ------------------------------------------------------------------ weights
+    def set_keras_weights(self, weights):
+        """weights: [kernel0, bias0, kernel1, bias1, ...] in Keras shapes."""
+        convs = [op for op in self.ops if isinstance(op, ConvOp)]
+        if len(weights) != 2 * len(convs):
+            raise ValueError(f"expected {2 * len(convs)} arrays, got {len(weights)}")
+        host = np.zeros(self.n_flat, dtype=np.float32)
+        for j, op in enumerate(convs):
+            host[op.off_w:op.off_w + op.n_w] = keras_to_gemm(op, weights[2 * j])
+            b = np.asarray(weights[2 * j + 1], dtype=np.float32).reshape(-1)
+            if b.shape[0] != op.cout:
+                raise ValueError("bias shape")
+            host[op.off_b:op.off_b + op.cout] = b
+        self.w.copy_(torch.from_numpy(host))
+        self._refresh_lowp()
+
+    def get_keras_weights(self):
+        host = self.w.cpu().numpy()
+        out = []
+        for op in self.ops:
+            if isinstance(op, ConvOp):
+                out.append(gemm_to_keras(op, host[op.off_w:op.off_w + op.n_w]))
+                out.append(host[op.off_b:op.off_b + op.cout].copy())
+        return out
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _refresh_lowp(self):
+        st = self._stream()
+        if self.dt == BF16:
+            _lib.check(self.L.specenh_cast(F32, _vp(self.w), BF16, _vp(self.w_lp), self.n_flat,
+                                           st), "cast")
+        src = self.w_lp if self.dt == BF16 else self.w
+        for i, wd in self.w_d.items():
+            op = self.ops[i]
+            _lib.check(self.L.specenh_weight_flip_transpose(
+                self.dt, ctypes.c_void_p(src.data_ptr() + op.off_w * src.element_size()), op.k,
+                op.cin, op.cout, _vp(wd), st), "flip_transpose")
+
+    def _wptr(self, op):
+        src = self.w_lp if self.dt == BF16 else self.w
+        return ctypes.c_void_p(src.data_ptr() + op.off_w * src.element_size())
+
+    def _bptr(self, op, buf=None):
+        buf = self.w if buf is None else buf
+        return ctypes.c_void_p(buf.data_ptr() + op.off_b * 4)
+
+    # ------------------------------------------------------------------ passes
+    def _conv(self, op, x, out, *, weights, geom, act, mask=None, logits=None, bias=True,
+              out_shape=None, cin=None, cout=None):
+        N, IH, IW, C = x.shape
+        OH, OW = out_shape
+        s, pt, pl, dil = geom
+        _lib.check(self.L.specenh_conv2d(
+            self.dt, _vp(x), N, IH, IW, C, weights, op.k, op.k, cout, self._bptr(op) if bias
+            else ctypes.c_void_p(0), s, pt, pl, dil, OH, OW, ACT[act], _vp(mask), _vp(logits),
+            _vp(out), int(out.dtype == torch.float32), self._stream()),
+            "conv2d")
+
+    def forward(self, x, train=False):
+        """x: device [N, H, W, C] in the compute dtype. Returns the output buffer
+        (fp32 for inference, compute dtype for training; reused between calls)."""
+        N = x.shape[0]
+        if x.dtype != self.tdt or not x.is_contiguous() or tuple(x.shape[1:]) != self.input_shape:
+            raise ValueError(f"forward expects a contiguous {self.tdt} [N, *{self.input_shape}]")
+        b = self._buffers(N, train)
+        b["h"][0] = x
+        if train:
+            self._last_train_N = N
+        st = self._stream()
+        n_ops = len(self.ops)
+        for i, op in enumerate(self.ops):
+            hin, hout = b["h"][i], b["h"][i + 1]
+            if isinstance(op, PoolOp):
+                _, H, W, C = hin.shape
+                am = b["am"][i]
+                if am is None:
+                    am = b.setdefault("am_inf", {}).get(hin.shape)
+                    if am is None:
+                        am = torch.empty((N, H // 2, W // 2, C), dtype=torch.uint8,
+                                         device=self.device)
+                        b["am_inf"][hin.shape] = am
+                _lib.check(self.L.specenh_maxpool2_fwd(self.dt, _vp(hin), N, H, W, C, _vp(hout),
+                                                       _vp(am), st), "maxpool2_fwd")
+                continue
+            last = i == n_ops - 1
+            self._conv(op, hin, hout, weights=self._wptr(op), geom=op.fwd_geom(), act=op.act,
+                       logits=b["z"] if (train and last) else None,
+                       out_shape=hout.shape[1:3], cout=op.cout)
+        return b["h"][n_ops]
+
+    def loss_and_grad(self, y, want_grad=True, accumulate=None):
+        """BCE of the last forward(train=True) against y (device, same shape).
+
+        The fp64 sum over elements is added to ``accumulate`` (a device fp64 [1] tensor)
+        when given, else to self._loss after zeroing it; the tensor is returned (the
+        mean is sum / y.numel()). Fills the last layer's gradient when want_grad."""
+        if tuple(y.shape) != (self._last_train_N,) + self.output_shape:
+            raise ValueError(f"targets must have shape (N, *{self.output_shape})")
+        if y.dtype not in (torch.bfloat16, torch.float32) or not y.is_contiguous():
+            raise TypeError("targets must be contiguous float32 or bfloat16")
+        b = self._buffers(self._last_train_N, True)
+        z = b["z"]
+        if accumulate is None:
+            accumulate = self._loss
+            accumulate.zero_()
+        ydt = BF16 if y.dtype == torch.bfloat16 else F32
+        _lib.check(self.L.specenh_bce_logits(
+            _vp(z), _vp(y), ydt, z.numel(), _vp(b["d"][-1]) if want_grad else ctypes.c_void_p(0),
+            self.dt, _vp(accumulate), self._stream()), "bce_logits")
+        return accumulate
+
+    def backward(self):
+        """Gradients of the last loss_and_grad() into self.g (overwritten)."""
+        N = self._last_train_N
+        b = self._buffers(N, True)
+        st = self._stream()
+        self.g.zero_()
+        n_ops = len(self.ops)
+        for i in range(n_ops - 1, -1, -1):
+            op = self.ops[i]
+            d_out = b["d"][i + 1]
+            hin = b["h"][i]
+            prev = self.ops[i - 1] if i > 0 else None
+            relu_mask = hin if (isinstance(prev, ConvOp) and prev.act == "relu") else None
+            if isinstance(op, PoolOp):
+                if i == 0:
+                    continue  # nothing upstream needs the gradient
+                _, H, W, C = hin.shape
+                _lib.check(self.L.specenh_maxpool2_bwd(self.dt, _vp(d_out), _vp(b["am"][i]),
+                                                       _vp(relu_mask), N, H, W, C,
+                                                       _vp(b["d"][i]), st), "maxpool2_bwd")
+                continue
+            if op.act == "sigmoid" and i != n_ops - 1:
+                raise NotImplementedError("sigmoid activation before the last layer")
+            _, IH, IW, C = hin.shape
+            OH, OW = d_out.shape[1:3]
+            s, pt, pl, dil = op.fwd_geom()
+            _lib.check(self.L.specenh_conv2d_wgrad(
+                self.dt, _vp(hin), N, IH, IW, C, _vp(d_out), op.k, op.k, op.cout, s, pt, pl, dil,
+                OH, OW, ctypes.c_void_p(self.g.data_ptr() + op.off_w * 4),
+                self._bptr(op, self.g), _vp(b["ws"]), st), "conv2d_wgrad")
+            if i == 0:
+                continue
+            self._conv(op, d_out, b["d"][i], weights=_vp(self.w_d[i]), geom=op.dgrad_geom(),
+                       act=None, mask=relu_mask, bias=False, out_shape=(IH, IW), cout=op.cin)
+
+    def adam(self, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7, grad_scale=1.0):
+        self.t += 1
+        lr_t = lr * math.sqrt(1.0 - beta_2 ** self.t) / (1.0 - beta_1 ** self.t)
+        _lib.check(self.L.specenh_adam_step(
+            _vp(self.w), _vp(self.g), _vp(self.m), _vp(self.v), self.n_flat, lr_t, beta_1, beta_2,
+            epsilon, grad_scale, _vp(self.w_lp), self._stream()), "adam_step")
+        if self.w_d:
+            src = self.w_lp if self.dt == BF16 else self.w
+            st = self._stream()
+            for i, wd in self.w_d.items():
+                op = self.ops[i]
+                _lib.check(self.L.specenh_weight_flip_transpose(
+                    self.dt, ctypes.c_void_p(src.data_ptr() + op.off_w * src.element_size()),
+                    op.k, op.cin, op.cout, _vp(wd), st), "flip_transpose")
+
+    def train_step(self, x, y, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7,
+                   process_group=None):
+        """One fit() step: forward, BCE, backward, [gradient all-reduce], Adam. Returns the
+        device fp64 loss sum of this rank (divide by y.numel() for the mean).
+
+        With ``process_group`` (an initialised torch.distributed group, RCCL on the GPU)
+        the flat gradient buffer is SUM-all-reduced in one call and Adam scales it by
+        1/world_size: every rank then applies the identical update."""
+        self.forward(x, train=True)
+        loss = self.loss_and_grad(y)
+        self.backward()
+        scale = 1.0
+        if process_group is not None:
+            import torch.distributed as dist
+            dist.all_reduce(self.g, op=dist.ReduceOp.SUM, group=process_group)
+            scale = 1.0 / dist.get_world_size(process_group)
+        self.adam(lr, beta_1, beta_2, epsilon, grad_scale=scale)
+        return loss
+
+    def to_compute(self, x):
+        """Host/device array -> contiguous device tensor in the compute dtype."""
+        t = torch.as_tensor(x)
+        if t.device != self.device:
+            if t.dtype != torch.float32:
+                t = t.float()
+            t = t.contiguous().to(self.device, non_blocking=False)
+        t = t.contiguous()
+        if t.dtype == self.tdt:
+            return t
+        if t.dtype != torch.float32:
+            raise TypeError(f"unsupported input dtype {t.dtype}")
+        out = torch.empty(t.shape, dtype=self.tdt, device=self.device)
+        _lib.check(self.L.specenh_cast(F32, _vp(t), self.dt, _vp(out), t.numel(),
+                                       self._stream()), "cast")
+        return out

@@ -1,0 +1,395 @@
+"""GPU parity of the conv autoencoder (csrc/conv_ae.hip via the C-ABI) against the
+oracle (oracle/autoencoder.py, a PyTorch-CPU restatement of the Keras model — parity
+vs Keras itself is unpinned: TensorFlow is absent, SURVEY.md §8 c).
+
+Tolerances (SURVEY.md §8 d):
+  * fp32 compute: outputs ||d||_inf / ||ref||_inf <= 1e-5; gradients per tensor
+    ||d||_2 / ||ref||_2 <= 1e-5 (fp32 accumulation over up to 10^6 terms).
+  * bf16 compute (mixed_bfloat16): output PSNR >= 40 dB vs the fp32 oracle (peak 1, the
+    sigmoid range); gradient cosine similarity >= 0.99.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import autoencoder as ora
+
+pytestmark = pytest.mark.gpu
+
+TOL_OUT = 1e-5
+TOL_GRAD = 1e-5
+PSNR_MIN = 40.0
+
+
+def _ae():
+    from specenh import ae
+    return ae
+
+
+def oracle_spec(ops):
+    spec = []
+    for op in ops:
+        if op.kind == "pool":
+            spec.append(("pool",))
+        else:
+            spec.append((op.kind, op.cin, op.cout, op.k, op.act))
+    return spec
+
+
+def make(ops, hwc, dtype="float32", seed=0, device="cuda:0"):
+    ae = _ae()
+    eng = ae.AutoencoderEngine(ops, hwc, compute_dtype=dtype, device=device)
+    params = ora.glorot_params(oracle_spec(ops), seed=seed)
+    rng = np.random.default_rng(seed + 100)
+    for p in params:  # non-zero biases exercise the bias path
+        if p is not None:
+            p["b"] = (0.05 * rng.standard_normal(p["b"].shape)).astype(np.float32)
+    ws = []
+    for p in params:
+        if p is not None:
+            ws += [p["W"], p["b"]]
+    eng.set_keras_weights(ws)
+    return eng, params
+
+
+def ref_forward(ops, params, x, grads=False, y=None):
+    tp = [None if p is None else {"W": torch.tensor(p["W"], dtype=torch.float64,
+                                                    requires_grad=grads),
+                                  "b": torch.tensor(p["b"], dtype=torch.float64,
+                                                    requires_grad=grads)} for p in params]
+    xt = torch.tensor(x, dtype=torch.float64)
+    out, z = ora.forward(oracle_spec(ops), tp, xt, return_logits=True)
+    if not grads:
+        return out.numpy(), z.numpy()
+    loss = ora.bce_from_logits(z, torch.tensor(y, dtype=torch.float64))
+    loss.backward()
+    g = []
+    for p in tp:
+        if p is not None:
+            g += [p["W"].grad.numpy(), p["b"].grad.numpy()]
+    return out.detach().numpy(), float(loss), g
+
+
+def engine_grads(eng):
+    ae = _ae()
+    host = eng.g.cpu().numpy()
+    out = []
+    for op in eng.ops:
+        if isinstance(op, ae.ConvOp):
+            out.append(ae.gemm_to_keras(op, host[op.off_w:op.off_w + op.n_w]))
+            out.append(host[op.off_b:op.off_b + op.cout])
+    return out
+
+
+def normwise(a, b):
+    return float(np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-30))
+
+
+def psnr(a, b):
+    mse = float(np.mean((a.astype(np.float64) - b) ** 2))
+    return math.inf if mse == 0 else 10 * math.log10(1.0 / mse)
+
+
+def ref_model_ops(c1=16, c2=32, c3=64, k=5):
+    ae = _ae()
+    C = ae.ConvOp
+    P = ae.PoolOp
+    return [C("conv", 1, c1, k, "relu"), P(), C("conv", c1, c2, k, "relu"), P(),
+            C("conv", c2, c3, k, "relu"), P(), C("convT", c3, c3, k, "relu", stride=2),
+            C("convT", c3, c2, k, "relu", stride=2), C("convT", c2, c1, k, "relu", stride=2),
+            C("conv", c1, 1, k, "sigmoid")]
+
+
+def upload(eng, a):
+    return eng.to_compute(torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)))
+
+
+# ----------------------------------------------------------------------------- single ops
+SINGLE = [("conv", 1, 16, 5, 20, 12), ("conv", 16, 32, 5, 16, 16), ("conv", 24, 1, 3, 9, 7),
+          ("conv", 8, 40, 5, 8, 8), ("convT", 64, 64, 5, 8, 8), ("convT", 32, 16, 5, 10, 6),
+          ("convT", 3, 5, 3, 5, 7), ("convT", 4, 8, 4, 6, 6)]
+
+
+@pytest.mark.parametrize("kind,cin,cout,k,H,W", SINGLE)
+def test_single_layer_forward_and_wgrad_fp32(gpu_device, kind, cin, cout, k, H, W):
+    ae = _ae()
+    ops = [ae.ConvOp(kind, cin, cout, k, "sigmoid", stride=2 if kind == "convT" else 1)]
+    eng, params = make(ops, (H, W, cin), seed=cin * 7 + cout)
+    rng = np.random.default_rng(1)
+    x = rng.uniform(0, 1, (3, H, W, cin)).astype(np.float32)
+    out_shape = (3,) + eng.output_shape
+    y = rng.uniform(0, 1, out_shape).astype(np.float32)
+    ref, ref_loss, ref_g = ref_forward(ops, params, x, grads=True, y=y)
+    got = eng.forward(upload(eng, x), train=False).cpu().numpy()
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() / np.abs(ref).max() <= TOL_OUT
+    eng.forward(upload(eng, x), train=True)
+    loss = eng.loss_and_grad(upload(eng, y))
+    eng.backward()
+    assert abs(float(loss.item()) / y.size - ref_loss) <= 1e-6 * abs(ref_loss)
+    for a, b in zip(engine_grads(eng), ref_g):
+        assert normwise(a, b) <= TOL_GRAD
+
+
+@pytest.mark.parametrize("first,second", [("conv", "conv"), ("conv", "convT"),
+                                          ("convT", "conv"), ("convT", "convT")])
+def test_two_layer_dgrad_through_relu_fp32(gpu_device, first, second):
+    """Input gradients (dgrad conv + fused ReLU mask) of both layer kinds."""
+    ae = _ae()
+    ops = [ae.ConvOp(first, 8, 16, 5, "relu", stride=2),
+           ae.ConvOp(second, 16, 1, 5, "sigmoid", stride=2)]
+    eng, params = make(ops, (8, 6, 8), seed=5)
+    rng = np.random.default_rng(2)
+    x = rng.uniform(0, 1, (2, 8, 6, 8)).astype(np.float32)
+    y = rng.uniform(0, 1, (2,) + eng.output_shape).astype(np.float32)
+    _, ref_loss, ref_g = ref_forward(ops, params, x, grads=True, y=y)
+    eng.forward(upload(eng, x), train=True)
+    eng.loss_and_grad(upload(eng, y))
+    eng.backward()
+    for a, b in zip(engine_grads(eng), ref_g):
+        assert normwise(a, b) <= TOL_GRAD
+
+
+def test_pool_backward_routes_to_argmax_with_relu_mask(gpu_device):
+    ae = _ae()
+    ops = [ae.ConvOp("conv", 1, 8, 3, "relu"), ae.PoolOp(), ae.ConvOp("conv", 8, 1, 3, "sigmoid")]
+    eng, params = make(ops, (16, 12, 1), seed=9)
+    rng = np.random.default_rng(3)
+    x = rng.uniform(0, 1, (4, 16, 12, 1)).astype(np.float32)
+    y = rng.uniform(0, 1, (4, 8, 6, 1)).astype(np.float32)
+    _, _, ref_g = ref_forward(ops, params, x, grads=True, y=y)
+    eng.forward(upload(eng, x), train=True)
+    eng.loss_and_grad(upload(eng, y))
+    eng.backward()
+    for a, b in zip(engine_grads(eng), ref_g):
+        assert normwise(a, b) <= TOL_GRAD
+
+
+# ----------------------------------------------------------------------------- full model
+def test_reference_model_forward_fp32(gpu_device):
+    ops = ref_model_ops()
+    eng, params = make(ops, (128, 128, 1), seed=11)
+    x = np.random.default_rng(4).uniform(0, 1, (4, 128, 128, 1)).astype(np.float32)
+    ref, _ = ref_forward(ops, params, x)
+    got = eng.forward(upload(eng, x), train=False).cpu().numpy()
+    assert np.abs(got - ref).max() / np.abs(ref).max() <= TOL_OUT
+
+
+def test_reference_model_gradients_fp32(gpu_device):
+    ops = ref_model_ops()
+    eng, params = make(ops, (128, 128, 1), seed=12)
+    rng = np.random.default_rng(5)
+    x = rng.uniform(0, 1, (4, 128, 128, 1)).astype(np.float32)
+    y = rng.uniform(0, 1, (4, 128, 128, 1)).astype(np.float32)
+    _, ref_loss, ref_g = ref_forward(ops, params, x, grads=True, y=y)
+    eng.forward(upload(eng, x), train=True)
+    loss = eng.loss_and_grad(upload(eng, y))
+    eng.backward()
+    assert abs(float(loss.item()) / y.size - ref_loss) <= 1e-6 * ref_loss
+    errs = [normwise(a, b) for a, b in zip(engine_grads(eng), ref_g)]
+    assert max(errs) <= TOL_GRAD, errs
+
+
+def test_reference_model_bf16_forward_psnr_and_gradients(gpu_device):
+    ops = ref_model_ops()
+    eng, params = make(ops, (128, 128, 1), dtype="mixed_bfloat16", seed=13)
+    rng = np.random.default_rng(6)
+    x = rng.uniform(0, 1, (4, 128, 128, 1)).astype(np.float32)
+    y = rng.uniform(0, 1, (4, 128, 128, 1)).astype(np.float32)
+    ref, ref_loss, ref_g = ref_forward(ops, params, x, grads=True, y=y)
+    got = eng.forward(upload(eng, x), train=False).cpu().numpy()
+    assert psnr(got, ref) >= PSNR_MIN
+    eng.forward(upload(eng, x), train=True)
+    loss = eng.loss_and_grad(upload(eng, y))
+    eng.backward()
+    assert abs(float(loss.item()) / y.size - ref_loss) <= 1e-3 * ref_loss
+    for a, b in zip(engine_grads(eng), ref_g):
+        cos = float(np.dot(a.ravel(), b.ravel()) /
+                    (np.linalg.norm(a) * np.linalg.norm(b) + 1e-30))
+        if np.linalg.norm(b) > 0:
+            assert cos >= 0.99
+
+
+def test_adam_trajectory_fp32_matches_keras_adam(gpu_device):
+    """10 fit() steps (forward, BCE, backward, Keras Adam) vs oracle.train_step."""
+    ops = ref_model_ops(4, 8, 8, 5)
+    eng, params = make(ops, (32, 32, 1), seed=21)
+    rng = np.random.default_rng(7)
+    x = rng.uniform(0, 1, (8, 32, 32, 1)).astype(np.float32)
+    y = (x > 0.5).astype(np.float32)
+    spec = oracle_spec(ops)
+    tp = [None if p is None else {"W": torch.tensor(p["W"], dtype=torch.float64,
+                                                    requires_grad=True),
+                                  "b": torch.tensor(p["b"], dtype=torch.float64,
+                                                    requires_grad=True)} for p in params]
+    opt = ora.KerasAdam()
+    xt, yt = torch.tensor(x, dtype=torch.float64), torch.tensor(y, dtype=torch.float64)
+    xd, yd = upload(eng, x), upload(eng, y)
+    w0 = [w.copy() for w in eng.get_keras_weights()]
+    for step in range(10):
+        ref_loss = ora.train_step(spec, tp, xt, yt, opt)
+        loss = float(eng.train_step(xd, yd).item()) / y.size
+        assert abs(loss - ref_loss) <= 1e-4 * ref_loss, (step, loss, ref_loss)
+    ref_w = []
+    for p in tp:
+        if p is not None:
+            ref_w += [p["W"].detach().numpy(), p["b"].detach().numpy()]
+    got_w = eng.get_keras_weights()
+    moved = np.sqrt(sum(np.sum((r - a) ** 2) for r, a in zip(ref_w, w0)))
+    diff = np.sqrt(sum(np.sum((r - g) ** 2) for r, g in zip(ref_w, got_w)))
+    assert diff <= 1e-2 * moved
+
+
+def test_adam_kernel_formula(gpu_device):
+    from specenh import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(8)
+    n = 10_000
+    w, g, m, v = (rng.standard_normal(n).astype(np.float32) for _ in range(4))
+    v = np.abs(v)
+    d = [torch.from_numpy(a.copy()).to(gpu_device) for a in (w, g, m, v)]
+    wb = torch.empty(n, dtype=torch.bfloat16, device=gpu_device)
+    lr_t, b1, b2, eps, sc = 1e-3 * math.sqrt(1 - 0.999 ** 3) / (1 - 0.9 ** 3), 0.9, 0.999, 1e-7, 0.5
+    import ctypes
+    _lib.check(L.specenh_adam_step(*(ctypes.c_void_p(t.data_ptr()) for t in d), n, lr_t, b1, b2,
+                                   eps, sc, ctypes.c_void_p(wb.data_ptr()), None))
+    torch.cuda.synchronize()
+    g2 = g.astype(np.float64) * sc
+    m2 = b1 * m + (1 - b1) * g2
+    v2 = b2 * v + (1 - b2) * g2 * g2
+    w2 = w - lr_t * m2 / (np.sqrt(v2) + eps)
+    np.testing.assert_allclose(d[0].cpu().numpy(), w2, rtol=1e-6, atol=1e-8)
+    np.testing.assert_allclose(d[2].cpu().numpy(), m2, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(d[3].cpu().numpy(), v2, rtol=1e-6, atol=1e-7)
+    assert torch.equal(wb, d[0].to(torch.bfloat16))
+
+
+# ----------------------------------------------------------------------------- facade
+def _small_model(policy="float32"):
+    from specenh.keras import layers, mixed_precision
+    from specenh.keras.models import Model
+    mixed_precision.set_global_policy(policy)
+    try:
+        inp = layers.Input(shape=(32, 32, 1))
+        x = layers.Conv2D(8, 5, activation="relu", padding="same")(inp)
+        x = layers.MaxPooling2D((2, 2), padding="same")(x)
+        x = layers.Conv2D(16, 5, activation="relu", padding="same")(x)
+        x = layers.MaxPooling2D((2, 2), padding="same")(x)
+        x = layers.Conv2DTranspose(16, 5, strides=2, activation="relu", padding="same")(x)
+        x = layers.Conv2DTranspose(8, 5, strides=2, activation="relu", padding="same")(x)
+        x = layers.Conv2D(1, 5, activation="sigmoid", padding="same")(x)
+        m = Model(inp, x)
+    finally:
+        mixed_precision.set_global_policy("float32")
+    m.compile(optimizer="adam", loss="binary_crossentropy")
+    return m
+
+
+def _toy_data(n, seed=0):
+    rng = np.random.default_rng(seed)
+    clean = np.zeros((n, 32, 32, 1), np.float32)
+    for i in range(n):
+        r = rng.integers(4, 28)
+        clean[i, r - 2:r + 2, :, 0] = 1.0
+    noisy = np.clip(clean + 0.3 * rng.standard_normal(clean.shape), 0, 1).astype(np.float32)
+    return noisy, clean
+
+
+@pytest.mark.parametrize("policy", ["float32", "mixed_bfloat16"])
+def test_fit_predict_evaluate_history(gpu_device, policy):
+    from specenh.keras import callbacks, utils
+    utils.set_random_seed(0)
+    m = _small_model(policy)
+    x, y = _toy_data(96)
+    xv, yv = _toy_data(32, seed=1)
+    es = callbacks.EarlyStopping(monitor="val_loss", mode="min", patience=50)
+    hist = m.fit(x=x, y=y, epochs=6, batch_size=16, shuffle=True, validation_data=(xv, yv),
+                 verbose=0, callbacks=[es])
+    assert set(hist.history) == {"loss", "val_loss"}
+    assert len(hist.history["val_loss"]) == 6
+    assert hist.history["loss"][-1] < hist.history["loss"][0]
+    assert all(np.isfinite(hist.history["val_loss"]))
+    p = m.predict(xv)
+    assert p.shape == (32, 32, 32, 1) and p.dtype == np.float32
+    assert np.all((p >= 0) & (p <= 1))
+    # predict is independent of batch composition (per-sample computation)
+    np.testing.assert_array_equal(m.predict(xv[:5]), p[:5])
+    ev = m.evaluate(xv, yv, batch_size=8)
+    assert abs(ev - hist.history["val_loss"][-1]) <= 1e-6 * ev
+
+
+def test_fit_loss_matches_oracle_fp32(gpu_device):
+    """One epoch without shuffling: history['loss'] is the batch-weighted mean of the
+    per-step losses of oracle.train_step on the same batches (last batch partial)."""
+    from specenh.keras import utils
+    utils.set_random_seed(0)
+    m = _small_model()
+    x, y = _toy_data(40)
+    spec = oracle_spec(m._ops)
+    ws = m.get_weights()
+    tp, j = [], 0
+    for s in spec:
+        if s[0] == "pool":
+            tp.append(None)
+        else:
+            tp.append({"W": torch.tensor(ws[j], dtype=torch.float64, requires_grad=True),
+                       "b": torch.tensor(ws[j + 1], dtype=torch.float64, requires_grad=True)})
+            j += 2
+    opt = ora.KerasAdam()
+    tot = 0.0
+    for s in range(0, 40, 16):
+        xb = torch.tensor(x[s:s + 16], dtype=torch.float64)
+        yb = torch.tensor(y[s:s + 16], dtype=torch.float64)
+        tot += ora.train_step(spec, tp, xb, yb, opt) * xb.shape[0]
+    hist = m.fit(x, y, epochs=1, batch_size=16, shuffle=False, verbose=0)
+    assert abs(hist.history["loss"][0] - tot / 40) <= 1e-5 * (tot / 40)
+
+
+def test_save_load_predict_identical(gpu_device, tmp_path):
+    from specenh.keras.models import load_model
+    m = _small_model()
+    x, y = _toy_data(32)
+    m.fit(x, y, epochs=1, batch_size=16, verbose=0)
+    m.save(str(tmp_path / "m"))
+    m2 = load_model(str(tmp_path / "m"))
+    np.testing.assert_array_equal(m2.predict(x), m.predict(x))
+    # optimizer state travels: one more identical step on both
+    m.fit(x, y, epochs=1, batch_size=32, shuffle=False, verbose=0)
+    m2.fit(x, y, epochs=1, batch_size=32, shuffle=False, verbose=0)
+    for a, b in zip(m.get_weights(), m2.get_weights()):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_errors(gpu_device):
+    m = _small_model()
+    with pytest.raises(ValueError):
+        m.predict(np.zeros((2, 32, 16, 1), np.float32))
+    with pytest.raises(ValueError):
+        m.fit(np.zeros((2, 32, 32, 1)), np.zeros((3, 32, 32, 1)))
+    ae = _ae()
+    with pytest.raises(RuntimeError, match="GPU only"):
+        ae.AutoencoderEngine(m._ops, (32, 32, 1), device="cpu")
+    from specenh import _lib
+    L = _lib.lib()
+    with pytest.raises(ValueError):
+        _lib.check(L.specenh_maxpool2_fwd(0, None, 1, 3, 4, 1, None, None, None))
+    with pytest.raises(ValueError):
+        _lib.check(L.specenh_conv2d(0, None, 1, 4, 4, 1, None, 3, 3, 1, None, 1, 1, 1, 1, 4, 4,
+                                    0, None, None, None, 1, None))
+
+
+def test_backward_is_bitwise_deterministic(gpu_device):
+    ops = ref_model_ops()
+    eng, _ = make(ops, (64, 64, 1), dtype="mixed_bfloat16", seed=31)
+    rng = np.random.default_rng(9)
+    x = upload(eng, rng.uniform(0, 1, (16, 64, 64, 1)))
+    y = upload(eng, rng.uniform(0, 1, (16, 64, 64, 1)))
+    grads = []
+    for _ in range(2):
+        eng.forward(x, train=True)
+        eng.loss_and_grad(y)
+        eng.backward()
+        grads.append(eng.g.clone())
+    assert torch.equal(grads[0], grads[1])

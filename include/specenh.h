@@ -108,13 +108,18 @@ int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long
 #define SPECENH_ACT_RELU 1
 #define SPECENH_ACT_SIGMOID 2
 
-/* Implicit-GEMM convolution: out[m][co] = act(sum_k A[m][k] * w_gemm[k][co] + bias[co]),
- * m = (n, oy, ox) over [N][OH][OW], k = (ky, kx, ci) over [KH][KW][C],
+/* Implicit-GEMM convolution: out[m][co] = act(sum_k A[m][k] * w_gemm[co][k] + bias[co]),
+ * m = (n, oy, ox) over [N][OH][OW], k = (ky, kx, ci) over [KH][KW][C]; w_gemm is the
+ * N-major GEMM operand [CO][KH][KW][C] ("OHWI"),
  * A[m][k] = in[n][iy][ix][ci] with vy = oy*stride - pad_t + ky, iy = vy / in_dil when
  * vy >= 0, vy % in_dil == 0 and iy < IH (else 0); likewise x with pad_l.
- *   Conv2D(k, "same") forward       stride 1, pad (k-1)/2, in_dil 1, w_gemm = HWIO kernel
- *   Conv2DTranspose(k, 2, "same")   stride 1, pad k-1-(k-2)/2, in_dil 2, w_gemm = flipped
+ *   Conv2D(k, "same") forward       stride 1, pad (k-1)/2, in_dil 1,
+ *                                   w_gemm[co][ky][kx][ci] = kernel[ky][kx][ci][co]
+ *   Conv2DTranspose(k, 2, "same")   stride 1, pad k-1-(k-2)/2, in_dil 2,
+ *                                   w_gemm[co][ky][kx][ci] = kernel[k-1-ky][k-1-kx][co][ci]
  *   their input gradients           (see specenh_weight_flip_transpose)
+ * A dilated input (in_dil 2, stride 1) is computed as in_dil^2 dense output phases; the
+ * zero holes are never gathered or multiplied.
  * logits (optional, fp32 [M][CO]) receives the pre-activation; mask (optional, dtype
  * [M][CO]) zeroes outputs where mask <= 0 (backward through a ReLU); out is fp32 when
  * out_f32 != 0, else dtype. bias may be NULL. */
@@ -122,8 +127,8 @@ int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, cons
                    int KH, int KW, int CO, const float* bias, int stride, int pad_t, int pad_l,
                    int in_dil, int OH, int OW, int act, const void* mask, float* logits,
                    void* out, int out_f32, void* stream);
-/* Weight gradient of the same convolution: dw[k][co] += sum_m A[m][k] * dout[m][co]
- * (fp32, accumulated), dbias[co] += sum_m dout[m][co] (optional). Deterministic: pixel
+/* Weight gradient of the same convolution: dw[co][k] += sum_m dout[m][co] * A[m][k]
+ * (fp32, w_gemm layout, accumulated), dbias[co] += sum_m dout[m][co] (optional). Deterministic: pixel
  * chunks are reduced in a fixed order through `workspace`, which must hold
  * specenh_conv2d_wgrad_workspace_bytes(N, OH, OW, KH, KW, C, CO) bytes. */
 size_t specenh_conv2d_wgrad_workspace_bytes(int N, int OH, int OW, int KH, int KW, int C,
@@ -150,13 +155,26 @@ int specenh_bce_logits(const float* z, const void* target, int target_dtype, lon
 int specenh_adam_step(float* w, const float* g, float* m, float* v, long long n, float lr_t,
                       float b1, float b2, float eps, float grad_scale, void* w_bf16,
                       void* stream);
-/* bd[((a*k + b)*co + o)*ci + i] = bf[(((k-1-a)*k + (k-1-b))*ci + i)*co + o]:
+/* bd[i][a][b][o] = bt[o][k-1-a][k-1-b][i] (bt: [co][k][k][ci], bd: [ci][k][k][co]):
  * the GEMM weights of a convolution's input gradient from its forward GEMM weights. */
-int specenh_weight_flip_transpose(int dtype, const void* bf, int k, int ci, int co, void* bd,
+int specenh_weight_flip_transpose(int dtype, const void* bt, int k, int ci, int co, void* bd,
                                   void* stream);
 /* Element conversion f32 <-> bf16 (round to nearest even). */
 int specenh_cast(int src_dtype, const void* src, int dst_dtype, void* dst, long long n,
                  void* stream);
+
+/* ---------------------------------------------------------------- strip glue
+ * patch / unpatch / reshape of VAE/manual_scan_3layers.py:28-54:
+ *   pack:   out[(b*n_strips + x)][r][c] = S[b][r][x*width + c], r < rows, c < width
+ *           (S: fp32 [batch][F][T] at S + b*s_stride; out: dst_dtype, i.e. the AE's NHWC
+ *           input with C = 1). Reference values: rows 256, width 128, n_strips 30.
+ *   unpack: out[b][r][x*width + c] = strips[(b*n_strips + x)][r][c] (fp32 out).
+ * width must be a multiple of 4. */
+int specenh_strips_pack(int dst_dtype, const float* S, long long batch, int F, int T,
+                        long long s_stride, int rows, int width, int n_strips, void* out,
+                        void* stream);
+int specenh_strips_unpack(int src_dtype, const void* strips, long long batch, int rows, int width,
+                          int n_strips, float* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -2,28 +2,38 @@
 //
 // Replaces the Keras/TensorFlow layers of VAE/manual_scan_3layers.py:186-212
 // (Conv2D / MaxPooling2D / Conv2DTranspose, padding="same", relu/sigmoid, Adam +
-// binary_crossentropy) with:
-//   * conv_igemm_kernel   ONE implicit-GEMM convolution: out[m][co] = sum_k A[m][k] B[k][co]
-//                         with A gathered from the NHWC input (k = (ky, kx, ci)):
-//                           vy = oy*stride - pad_t + ky, iy = vy / in_dil (valid if exact)
-//                         Conv2D fwd (stride 1), Conv2D dgrad (flipped/transposed B),
-//                         Conv2DTranspose fwd (in_dil = 2 over a flipped B) and
-//                         Conv2DTranspose dgrad (stride 2) are all this kernel.
-//                         Epilogue: + bias, optional pre-activation store, optional ReLU
-//                         mask of another tensor (the backward ReLU), relu / sigmoid.
-//                         MFMA 16x16x32 bf16 (fp32 accumulate) or 16x16x4 f32.
-//   * conv_wgrad_kernel   dB[k][co] += sum_m A[m][k] dOut[m][co] (same gather), split over
-//                         pixel chunks, fp32 atomics into the gradient.
-//   * maxpool2 fwd/bwd    2x2/2 with argmax; backward fuses the ReLU mask of its input.
-//   * bce_logits_kernel   Keras graph-mode BCE after a sigmoid = sigmoid_cross_entropy
-//                         _with_logits, mean over elements; grad = (sigmoid(z) - t) / n.
-//   * adam_kernel         Keras Adam (w -= lr_t m / (sqrt(v) + eps)), refreshes the bf16
-//                         GEMM copy of the weights.
-//   * flip_transpose      Bd[(a,b,co)][ci] = Bf[(k-1-a, k-1-b, ci)][co] (dgrad weights).
+// binary_crossentropy).
+//
+// One implicit GEMM serves every convolution of the model:
+//   out[m][co] = sum_k A[m][k] * Bt[co][k],   m = output pixel, k = (ky, kx, ci)
+// with A gathered from the NHWC input (include/specenh.h, specenh_conv2d). Conv2D
+// forward is a stride-1 conv, the input gradient of Conv2DTranspose is a stride-2 conv,
+// and Conv2DTranspose forward / Conv2D input gradient are convs over a zero-dilated
+// input. The dilated case is never materialised: it is split into in_dil^2 output
+// phases, each a dense stride-1 conv over the undilated input with the sub-kernel of the
+// taps that hit real samples (no MFMA work or gather spent on the holes). One launch
+// carries every phase (blockIdx.z).
+//
+// Weights are N-major ("OHWI"): Bt[co][(ky, kx, ci)], so a B fragment row is contiguous.
+//
+//   conv_fwd_kernel     MFMA 16x16x32 bf16 (fp32 accumulate) or 16x16x4 f32. Workgroup =
+//                       4 waves, 16*MT output pixels x 16*NT channels per wave; the next
+//                       slab's gathers are in flight during the current slab's MFMAs (LDS-
+//                       only barriers); 160-byte LDS rows make every ds_read_b128 fragment
+//                       read bank-conflict free. Epilogue: + bias, optional fp32 pre-
+//                       activation store, optional ReLU mask of another tensor (backward
+//                       through a ReLU), relu / sigmoid.
+//   conv_wgrad_kernel   dBt[co][k] = sum_m dOut[m][co] A[m][k]: the same gather, 64 pixels
+//                       per step staged transposed in LDS (pixel pairs packed per 32-bit
+//                       write), split over pixel chunks into a workspace and reduced in a
+//                       fixed order (bit-reproducible); the bias gradient rides along.
+//   maxpool2 fwd/bwd, bce_logits (Keras graph-mode BCE from logits), adam (Keras form),
+//   flip_transpose (dgrad weights), cast.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <string>
 
 #include "specenh.h"
@@ -34,13 +44,6 @@ int set_error(int code, const std::string& msg);  // stft_psd.hip
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-struct ConvGeom {
-  int N, IH, IW, C;  // input NHWC
-  int OH, OW, CO;    // output NHWC
-  int KH, KW;
-  int stride, pad_t, pad_l, in_dil;
-};
-
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(__bf16 x) { return (float)x; }
 template <typename T>
@@ -50,303 +53,436 @@ __device__ __forceinline__ float from_f<float>(float x) { return x; }
 template <>
 __device__ __forceinline__ __bf16 from_f<__bf16>(float x) { return (__bf16)x; }
 
-// Input coordinate of a (output pixel, tap) pair; -1 if the tap reads padding or a hole
-// of the dilated input.
-__device__ __forceinline__ int in_coord(int base, int kk, int dil, int extent) {
-  const int v = base + kk;
-  if (v < 0) return -1;
-  int i = v;
-  if (dil > 1) {
-    if (v % dil) return -1;
-    i = v / dil;
-  }
-  return i < extent ? i : -1;
+// Barrier for LDS hand-off only: does not drain outstanding global loads (the prefetch).
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
-// Load 8 consecutive GEMM-K elements of row (n, base_y, base_x) starting at k.
+// ------------------------------------------------------------------ geometry
+// One dense implicit GEMM (one output phase):
+//   A[m][(jy, jx, ci)] = in[n][oy*stride - pad_t + jy][ox*stride - pad_l + jx][ci]
+//   weight column of (jy, jx, ci) = ((ky0 + kstep*jy)*KWf + kx0 + kstep*jx)*C + ci
+//   result stored at pixel (oy*oys + oy0, ox*oxs + ox0) of an OHs x OWs image.
+struct Geo {
+  int N, IH, IW, C;
+  int OH, OW, CO;
+  int KH, KW;
+  int stride, pad_t, pad_l;
+  int ky0, kx0, kstep, KWf, Kf;
+  int oys, oy0, oxs, ox0, OHs, OWs;
+};
+constexpr int MAXPH = 4;
+
+__device__ __forceinline__ int wcol(const Geo& g, int tap, int ci) {
+  const int jy = tap / g.KW, jx = tap - (tap / g.KW) * g.KW;
+  return ((g.ky0 + g.kstep * jy) * g.KWf + g.kx0 + g.kstep * jx) * g.C + ci;
+}
+
 template <typename T>
-__device__ __forceinline__ void gather8(const T* __restrict__ in, const ConvGeom& g, int K,
-                                        int n, int by, int bx, int k, bool vm, T (&v)[8]) {
-  if ((g.C & 7) == 0) {  // one tap, 8 contiguous channels
-    bool ok = vm && k < K;
-    int iy = -1, ix = -1, ci = 0;
-    if (ok) {
-      const int tap = k / g.C;
-      ci = k - tap * g.C;
-      const int ky = tap / g.KW, kx = tap - ky * g.KW;
-      iy = in_coord(by, ky, g.in_dil, g.IH);
-      ix = in_coord(bx, kx, g.in_dil, g.IW);
-      ok = iy >= 0 && ix >= 0;
-    }
-    if (ok) {
-      const T* p = in + (((long long)n * g.IH + iy) * g.IW + ix) * g.C + ci;
-      if constexpr (sizeof(T) == 2) {
-        const uint4 q = *reinterpret_cast<const uint4*>(p);
-        const T* e = reinterpret_cast<const T*>(&q);
+struct Tile;
+template <>
+struct Tile<__bf16> {
+  static constexpr int BK = 64, LD = 80;  // 160-byte LDS rows
+};
+template <>
+struct Tile<float> {
+  static constexpr int BK = 32, LD = 40;
+};
+
+// 8 consecutive elements of T as raw 32-bit words.
+template <typename T>
+struct V8 {
+  uint32_t w[sizeof(T) * 2];
+};
+
+template <typename T>
+__device__ __forceinline__ V8<T> ld8(const T* p) {
+  V8<T> v;
+  const uint4 a = reinterpret_cast<const uint4*>(p)[0];
+  v.w[0] = a.x; v.w[1] = a.y; v.w[2] = a.z; v.w[3] = a.w;
+  if constexpr (sizeof(T) == 4) {
+    const uint4 b = reinterpret_cast<const uint4*>(p)[1];
+    v.w[4] = b.x; v.w[5] = b.y; v.w[6] = b.z; v.w[7] = b.w;
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const V8<T>& v) {
+  reinterpret_cast<uint4*>(p)[0] = uint4{v.w[0], v.w[1], v.w[2], v.w[3]};
+  if constexpr (sizeof(T) == 4)
+    reinterpret_cast<uint4*>(p)[1] = uint4{v.w[4], v.w[5], v.w[6], v.w[7]};
+}
+
+template <typename T>
+__device__ __forceinline__ void zero8(V8<T>& v) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = e[j];
-      } else {
-        const float4 q0 = reinterpret_cast<const float4*>(p)[0];
-        const float4 q1 = reinterpret_cast<const float4*>(p)[1];
-        v[0] = q0.x; v[1] = q0.y; v[2] = q0.z; v[3] = q0.w;
-        v[4] = q1.x; v[5] = q1.y; v[6] = q1.z; v[7] = q1.w;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = from_f<T>(0.f);
-    }
-  } else {  // generic (e.g. the 1-channel first layer)
+  for (int i = 0; i < (int)(sizeof(T) * 2); ++i) v.w[i] = 0u;
+}
+
+__device__ __forceinline__ uint32_t bits(float x) { return __float_as_uint(x); }
+__device__ __forceinline__ uint32_t bits(__bf16 x) {
+  return (uint32_t)__builtin_bit_cast(unsigned short, x);
+}
+
+// element j of a V8 (as raw bits)
+template <typename T>
+__device__ __forceinline__ uint32_t elem_bits(const V8<T>& v, int j) {
+  if constexpr (sizeof(T) == 4) return v.w[j];
+  else return (v.w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+}
+
+template <typename T>
+__device__ __forceinline__ void set_elem(V8<T>& v, int j, T x) {
+  if constexpr (sizeof(T) == 4) {
+    v.w[j] = bits(x);
+  } else {
+    const uint32_t b = bits(x) << (16 * (j & 1));
+    v.w[j >> 1] = (v.w[j >> 1] & (0xffff0000u >> (16 * (j & 1)))) | b;
+  }
+}
+
+// 8 GEMM-K elements k .. k+7 of one output pixel (by, bx = top-left of its window, nb =
+// n*IH). Out-of-range rows have by far below zero.
+template <typename T>
+__device__ __forceinline__ V8<T> gather_a8(const T* __restrict__ in, const Geo& g, int K, int k,
+                                           int by, int bx, int nb) {
+  V8<T> v;
+  if ((g.C & 7) == 0) {
+    const int tap = k / g.C, ci = k - (k / g.C) * g.C;
+    const int jy = tap / g.KW, jx = tap - (tap / g.KW) * g.KW;
+    const int iy = by + jy, ix = bx + jx;
+    const bool ok = k < K && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW;
+    v = ld8(in + (ok ? ((nb + iy) * g.IW + ix) * g.C + ci : 0));
+    if (!ok) zero8(v);
+  } else {
+    zero8(v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int kk = k + j;
-      T x = from_f<T>(0.f);
-      if (vm && kk < K) {
-        const int tap = kk / g.C, ci = kk - (kk / g.C) * g.C;
-        const int ky = tap / g.KW, kx = tap - ky * g.KW;
-        const int iy = in_coord(by, ky, g.in_dil, g.IH), ix = in_coord(bx, kx, g.in_dil, g.IW);
-        if (iy >= 0 && ix >= 0) x = in[(((long long)n * g.IH + iy) * g.IW + ix) * g.C + ci];
-      }
-      v[j] = x;
+      const int tap = kk / g.C, ci = kk - (kk / g.C) * g.C;
+      const int jy = tap / g.KW, jx = tap - (tap / g.KW) * g.KW;
+      const int iy = by + jy, ix = bx + jx;
+      const bool ok = kk < K && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW;
+      const T x = in[ok ? ((nb + iy) * g.IW + ix) * g.C + ci : 0];
+      if (ok) set_elem(v, j, x);
     }
   }
+  return v;
 }
 
-// Load 8 consecutive output channels [co, co+8) of GEMM row r of a [rows][CO] matrix.
+// 8 GEMM-K elements k .. k+7 of weight row co (Bt[co][Kf]).
 template <typename T>
-__device__ __forceinline__ void load_row8(const T* __restrict__ p, int rows, int CO, int r, int co,
-                                          T (&v)[8]) {
-  if (r < rows && (CO & 7) == 0 && co + 8 <= CO) {
-    const T* q = p + (long long)r * CO + co;
-    if constexpr (sizeof(T) == 2) {
-      const uint4 u = *reinterpret_cast<const uint4*>(q);
-      const T* e = reinterpret_cast<const T*>(&u);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = e[j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = q[j];
-    }
+__device__ __forceinline__ V8<T> gather_b8(const T* __restrict__ W, const Geo& g, int K, int k,
+                                           int co) {
+  V8<T> v;
+  if ((g.C & 7) == 0) {
+    const bool ok = co < g.CO && k < K;
+    const int tap = k / g.C, ci = k - (k / g.C) * g.C;
+    v = ld8(W + (ok ? co * g.Kf + wcol(g, tap, ci) : 0));
+    if (!ok) zero8(v);
   } else {
+    zero8(v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      v[j] = (r < rows && co + j < CO) ? p[(long long)r * CO + co + j] : from_f<T>(0.f);
+    for (int j = 0; j < 8; ++j) {
+      const int kk = k + j;
+      const bool ok = co < g.CO && kk < K;
+      const int tap = kk / g.C, ci = kk - (kk / g.C) * g.C;
+      const T x = W[ok ? co * g.Kf + wcol(g, tap, ci) : 0];
+      if (ok) set_elem(v, j, x);
+    }
   }
+  return v;
 }
 
-constexpr int BM = 64, BK = 32, KPAD = 8, LDK = BK + KPAD;
-
-// MFMA over one BK=32 slice: a/b rows (16 x 32 each) from LDS with row stride LDK.
+// acc += A_tile(16 rows at sa) x B_tile(16 rows at sb)^T over one BK slab.
 template <typename T>
-__device__ __forceinline__ f32x4 mfma_slice(const T* sa, const T* sb, f32x4 acc, int lane) {
+__device__ __forceinline__ f32x4 mfma_slab(const T* sa, const T* sb, f32x4 acc, int lane) {
+  constexpr int BK = Tile<T>::BK, LD = Tile<T>::LD;
   if constexpr (sizeof(T) == 2) {
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(sa + (lane & 15) * LDK + 8 * (lane >> 4));
-    const bf16x8 b = *reinterpret_cast<const bf16x8*>(sb + (lane & 15) * LDK + 8 * (lane >> 4));
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < BK / 32; ++s) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(sa + (lane & 15) * LD + 32 * s + 8 * (lane >> 4));
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(sb + (lane & 15) * LD + 32 * s + 8 * (lane >> 4));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+    }
   } else {
 #pragma unroll
     for (int s = 0; s < BK / 4; ++s) {
-      const float a = sa[(lane & 15) * LDK + 4 * s + (lane >> 4)];
-      const float b = sb[(lane & 15) * LDK + 4 * s + (lane >> 4)];
+      const float a = sa[(lane & 15) * LD + 4 * s + (lane >> 4)];
+      const float b = sb[(lane & 15) * LD + 4 * s + (lane >> 4)];
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
     }
-    return acc;
   }
+  return acc;
 }
 
-struct ConvFwdArgs {
-  ConvGeom g;
+struct ConvArgs {
+  Geo g[MAXPH];
   const void* in;
-  const void* w;        // GEMM B [K][CO]
-  const float* bias;    // [CO] or null
-  void* out;            // [M][CO], float if out_f32 else T
+  const void* w;      // Bt [CO][Kf]
+  const float* bias;  // [CO] or null
+  void* out;          // [N][OHs][OWs][CO], float if out_f32 else T
+  const void* mask;   // same shape, T, or null: v *= (mask > 0)
+  float* logits;      // same shape, fp32 pre-activation, or null
   int out_f32;
-  const void* mask;     // [M][CO] T or null: v *= (mask > 0)
-  int act;              // 0 none, 1 relu, 2 sigmoid
-  float* logits;        // [M][CO] fp32 pre-activation store or null
+  int act;            // 0 none, 1 relu, 2 sigmoid
 };
 
-// Workgroup: 64 output pixels x (16*NT) output channels; wave w owns rows 16w..16w+15.
-template <typename T, int NT>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvFwdArgs a) {
-  constexpr int BN = 16 * NT;
-  __shared__ __attribute__((aligned(16))) T sA[BM * LDK];
-  __shared__ __attribute__((aligned(16))) T sB[BN * LDK];
-  const ConvGeom& g = a.g;
+// ------------------------------------------------------------------ forward / dgrad
+template <typename T, int MT, int NT>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
+  constexpr int BK = Tile<T>::BK, LD = Tile<T>::LD;
+  constexpr int BM = 64 * MT, BN = 16 * NT;
+  constexpr int KG = BK / 8;          // 8-element groups per k-slab
+  constexpr int RSTEP = 256 / KG;     // rows between a thread's gather rows
+  constexpr int ROWS = BM / RSTEP;    // gather rows per thread
+  constexpr int BG = BN * KG;         // B groups per slab
+  constexpr int BPER = (BG + 255) / 256;
+  __shared__ __attribute__((aligned(16))) T sA[BM * LD];
+  __shared__ __attribute__((aligned(16))) T sB[BN * LD];
+
+  const Geo& g = a.g[blockIdx.z];
+  const int M = g.N * g.OH * g.OW;
+  const int m0 = blockIdx.x * BM;
+  if (m0 >= M) return;
+  const int n0 = blockIdx.y * BN;
+  const int K = g.KH * g.KW * g.C;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
   const T* __restrict__ W = reinterpret_cast<const T*>(a.w);
-  const int K = g.KH * g.KW * g.C;
-  const long long M = (long long)g.N * g.OH * g.OW;
-  const long long m0 = (long long)blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-  // this thread's gather row (tid>>2) and k-group (tid&3)
-  const int ml = tid >> 2, kg = tid & 3;
-  const long long m = m0 + ml;
-  const bool vm = m < M;
-  int n = 0, by = 0, bx = 0;
-  if (vm) {
-    const int hw = g.OH * g.OW;
-    n = (int)(m / hw);
-    const int rem = (int)(m - (long long)n * hw);
-    const int oy = rem / g.OW, ox = rem - (rem / g.OW) * g.OW;
-    by = oy * g.stride - g.pad_t;
-    bx = ox * g.stride - g.pad_l;
-  }
-  f32x4 acc[NT];
+  const int kg = tid % KG, r0 = tid / KG;
+  const int hw = g.OH * g.OW;
+  int by[ROWS], bx[ROWS], nb[ROWS];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int k0 = 0; k0 < K; k0 += BK) {
-    T va[8];
-    gather8<T>(in, g, K, n, by, bx, k0 + 8 * kg, vm, va);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sA[ml * LDK + 8 * kg + j] = va[j];
-    // B tile [BK][BN] -> sB[co][k]
-    constexpr int GROUPS = BN / 8;
-    if (tid < BK * GROUPS) {
-      const int kk = tid / GROUPS, cg = tid - kk * GROUPS;
-      T vb[8];
-      load_row8<T>(W, K, g.CO, k0 + kk, n0 + 8 * cg, vb);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sB[(8 * cg + j) * LDK + kk] = vb[j];
+  for (int i = 0; i < ROWS; ++i) {
+    const int m = m0 + r0 + RSTEP * i;
+    if (m < M) {
+      const int n = m / hw, rem = m - (m / hw) * hw;
+      const int oy = rem / g.OW, ox = rem - (rem / g.OW) * g.OW;
+      by[i] = oy * g.stride - g.pad_t;
+      bx[i] = ox * g.stride - g.pad_l;
+      nb[i] = n * g.IH;
+    } else {
+      by[i] = -(1 << 29);
+      bx[i] = 0;
+      nb[i] = 0;
     }
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-      acc[t] = mfma_slice<T>(sA + 16 * wave * LDK, sB + 16 * t * LDK, acc[t], lane);
-    __syncthreads();
   }
 
-  // epilogue: D[row][col], col = lane&15, row = 4*(lane>>4) + reg
+  f32x4 acc[MT][NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int col = n0 + 16 * t + (lane & 15);
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  V8<T> ra[ROWS], rb[BPER];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < ROWS; ++i) ra[i] = gather_a8<T>(in, g, K, k0 + 8 * kg, by[i], bx[i], nb[i]);
+#pragma unroll
+    for (int j = 0; j < BPER; ++j) {
+      const int idx = tid + 256 * j;
+      const int co_l = idx / KG, kgb = idx - (idx / KG) * KG;
+      if (idx < BG) rb[j] = gather_b8<T>(W, g, K, k0 + 8 * kgb, n0 + co_l);
+    }
+  };
+
+  if (K > 0) fetch(0);
+  for (int k0 = 0; k0 < K; k0 += BK) {
+#pragma unroll
+    for (int i = 0; i < ROWS; ++i) st8(sA + (r0 + RSTEP * i) * LD + 8 * kg, ra[i]);
+#pragma unroll
+    for (int j = 0; j < BPER; ++j) {
+      const int idx = tid + 256 * j;
+      const int co_l = idx / KG, kgb = idx - (idx / KG) * KG;
+      if (idx < BG) st8(sB + co_l * LD + 8 * kgb, rb[j]);
+    }
+    lds_sync();
+    if (k0 + BK < K) fetch(k0 + BK);  // in flight during the MFMAs below
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        acc[i][j] = mfma_slab<T>(sA + 16 * (wave * MT + i) * LD, sB + 16 * j * LD, acc[i][j], lane);
+    lds_sync();
+  }
+
+  // epilogue: D[row][col], col = lane & 15, row = 4*(lane >> 4) + reg
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
-      const long long mm = m0 + 16 * wave + 4 * (lane >> 4) + reg;
-      if (mm >= M || col >= g.CO) continue;
-      const long long idx = mm * g.CO + col;
-      float v = acc[t][reg] + (a.bias ? a.bias[col] : 0.f);
-      if (a.logits) a.logits[idx] = v;
-      if (a.mask && !(to_f(reinterpret_cast<const T*>(a.mask)[idx]) > 0.f)) v = 0.f;
-      if (a.act == 1) v = fmaxf(v, 0.f);
-      else if (a.act == 2) v = 1.f / (1.f + __expf(-v));
-      if (a.out_f32) reinterpret_cast<float*>(a.out)[idx] = v;
-      else reinterpret_cast<T*>(a.out)[idx] = from_f<T>(v);
+      const int m = m0 + 16 * (wave * MT + i) + 4 * (lane >> 4) + reg;
+      if (m >= M) continue;
+      const int n = m / hw, rem = m - (m / hw) * hw;
+      const int oy = rem / g.OW, ox = rem - (rem / g.OW) * g.OW;
+      const long long pix =
+          ((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int col = n0 + 16 * j + (lane & 15);
+        if (col >= g.CO) continue;
+        const long long idx = pix * g.CO + col;
+        float v = acc[i][j][reg] + (a.bias ? a.bias[col] : 0.f);
+        if (a.logits) a.logits[idx] = v;
+        if (a.mask && !(to_f(reinterpret_cast<const T*>(a.mask)[idx]) > 0.f)) v = 0.f;
+        if (a.act == 1) v = fmaxf(v, 0.f);
+        else if (a.act == 2) v = 1.f / (1.f + __expf(-v));
+        if (a.out_f32) reinterpret_cast<float*>(a.out)[idx] = v;
+        else reinterpret_cast<T*>(a.out)[idx] = from_f<T>(v);
+      }
     }
   }
 }
 
-// part[z][k][co] = sum over pixel chunk z of A[m][k] * dOut[m][co] (deterministic split-K:
-// the chunks are summed in order by wgrad_reduce_kernel).
-// Workgroup: 64 GEMM-K rows x (16*NT) channels x `chunk` pixels (multiple of 32).
+// ------------------------------------------------------------------ weight gradient
+struct WgradArgs {
+  Geo g[MAXPH];
+  int chunk[MAXPH];  // pixels per z-slice of each phase (multiple of the pixel step)
+  int Z;             // z-slices per phase
+  const void* in;
+  const void* dout;  // [N][OHs][OWs][CO]
+  float* part;       // [Z][CO][Kf]
+  float* bpart;      // [nphase][Z][CO] (bias) or null
+};
+
+// Workgroup: 64 GEMM-K columns (blockIdx.x) x 16*NT channels (blockIdx.y) x one pixel
+// chunk (blockIdx.z = phase*Z + z). Wave w owns k-columns 16w .. 16w+15.
 template <typename T, int NT>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvGeom g, const T* __restrict__ in,
-                                                          const T* __restrict__ dout,
-                                                          float* __restrict__ part, int chunk) {
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
+  constexpr int BP = Tile<T>::BK;  // pixels per step
+  constexpr int LD = Tile<T>::LD;
   constexpr int BN = 16 * NT;
-  constexpr int BMK = 64, BP = 32, LDP = BP + KPAD;
-  __shared__ __attribute__((aligned(16))) T sA[BMK * LDP];  // [k][m]
-  __shared__ __attribute__((aligned(16))) T sG[BN * LDP];   // [co][m]
+  __shared__ __attribute__((aligned(16))) T sA[64 * LD];  // [k][pixel]
+  __shared__ __attribute__((aligned(16))) T sG[BN * LD];  // [co][pixel]
+  const int ph = blockIdx.z / a.Z, z = blockIdx.z - (blockIdx.z / a.Z) * a.Z;
+  const Geo& g = a.g[ph];
   const int K = g.KH * g.KW * g.C;
-  const long long M = (long long)g.N * g.OH * g.OW;
-  const int k0 = blockIdx.x * BMK;
+  const int k0 = blockIdx.x * 64;
+  if (k0 >= K) return;
   const int n0 = blockIdx.y * BN;
-  const long long p0 = (long long)blockIdx.z * chunk;
+  const int M = g.N * g.OH * g.OW;
+  const int p_begin = z * a.chunk[ph];
+  const int p_end = min(M, p_begin + a.chunk[ph]);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hw = g.OH * g.OW;
-  f32x4 acc[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
+  const T* __restrict__ dout = reinterpret_cast<const T*>(a.dout);
 
-  for (int pc = 0; pc < chunk; pc += BP) {
-    // gather: thread -> pixel (tid & 31), k-group (tid >> 5): 8 k of one pixel
-    {
-      const int ml = tid & 31, kgp = tid >> 5;
-      const long long m = p0 + pc + ml;
-      const bool vm = m < M;
-      int n = 0, by = 0, bx = 0;
-      if (vm) {
-        n = (int)(m / hw);
-        const int rem = (int)(m - (long long)n * hw);
-        const int oy = rem / g.OW, ox = rem - (rem / g.OW) * g.OW;
-        by = oy * g.stride - g.pad_t;
-        bx = ox * g.stride - g.pad_l;
-      }
-      T va[8];
-      gather8<T>(in, g, K, n, by, bx, k0 + 8 * kgp, vm, va);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sA[(8 * kgp + j) * LDP + ml] = va[j];
+  // bf16: thread = (pixel pair, 8-group); f32: thread = (pixel, 8-group)
+  constexpr int PP = sizeof(T) == 2 ? 2 : 1;
+  const int grp = tid & 7, pslot = (tid >> 3) * PP;  // pslot < BP
+  const bool g_on = 8 * grp < BN;
+
+  auto pix_geom = [&](int m, int& by, int& bx, int& nb, long long& orow) {
+    if (m < p_end) {
+      const int n = m / hw, rem = m - (m / hw) * hw;
+      const int oy = rem / g.OW, ox = rem - (rem / g.OW) * g.OW;
+      by = oy * g.stride - g.pad_t;
+      bx = ox * g.stride - g.pad_l;
+      nb = n * g.IH;
+      orow = (((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0) * g.CO;
+    } else {
+      by = -(1 << 29); bx = 0; nb = 0; orow = -1;
     }
-    {  // dOut tile [32 pixels][BN] -> sG[co][m]
-      constexpr int GROUPS = BN / 8;
-      if (tid < BP * GROUPS) {
-        const int ml = tid / GROUPS, cg = tid - ml * GROUPS;
-        const long long m = p0 + pc + ml;
-        T vg[8];
-        if (m < M) {
-          load_row8<T>(dout + m * g.CO, 1, g.CO, 0, n0 + 8 * cg, vg);
+  };
+  V8<T> va[PP], vg[PP];
+  auto fetch = [&](int p0) {
+#pragma unroll
+    for (int q = 0; q < PP; ++q) {
+      int by, bx, nb;
+      long long orow;
+      pix_geom(p0 + pslot + q, by, bx, nb, orow);
+      va[q] = gather_a8<T>(in, g, K, k0 + 8 * grp, by, bx, nb);
+      zero8(vg[q]);
+      if (g_on && orow >= 0) {
+        const int co = n0 + 8 * grp;
+        if ((g.CO & 7) == 0 && co + 8 <= g.CO) {
+          vg[q] = ld8(dout + orow + co);
         } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) vg[j] = from_f<T>(0.f);
+          for (int j = 0; j < 8; ++j)
+            if (co + j < g.CO) set_elem(vg[q], j, dout[orow + co + j]);
         }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sG[(8 * cg + j) * LDP + ml] = vg[j];
       }
     }
-    __syncthreads();
+  };
+  auto stage = [&]() {
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-      acc[t] = mfma_slice<T>(sA + 16 * wave * LDP, sG + 16 * t * LDP, acc[t], lane);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int col = n0 + 16 * t + (lane & 15);
-#pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const int kk = k0 + 16 * wave + 4 * (lane >> 4) + reg;
-      if (kk < K && col < g.CO)
-        part[((long long)blockIdx.z * K + kk) * g.CO + col] = acc[t][reg];
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (PP == 2) {
+        *reinterpret_cast<uint32_t*>(sA + (8 * grp + j) * LD + pslot) =
+            elem_bits(va[0], j) | (elem_bits(va[1], j) << 16);
+        if (g_on)
+          *reinterpret_cast<uint32_t*>(sG + (8 * grp + j) * LD + pslot) =
+              elem_bits(vg[0], j) | (elem_bits(vg[1], j) << 16);
+      } else {
+        *reinterpret_cast<uint32_t*>(sA + (8 * grp + j) * LD + pslot) = elem_bits(va[0], j);
+        if (g_on) *reinterpret_cast<uint32_t*>(sG + (8 * grp + j) * LD + pslot) = elem_bits(vg[0], j);
+      }
     }
+  };
+
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc = 0.f;
+  const bool do_bias = a.bpart && blockIdx.x == 0 && tid < BN;
+
+  if (p_begin < p_end) fetch(p_begin);
+  for (int p0 = p_begin; p0 < p_end; p0 += BP) {
+    stage();
+    lds_sync();
+    if (p0 + BP < p_end) fetch(p0 + BP);
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      acc[j] = mfma_slab<T>(sG + 16 * j * LD, sA + 16 * wave * LD, acc[j], lane);
+    if (do_bias) {
+#pragma unroll 8
+      for (int p = 0; p < BP; ++p) bacc += to_f(sG[tid * LD + p]);
+    }
+    lds_sync();
   }
+
+  // D[co][k]: col = lane & 15 -> k, row = 4*(lane >> 4) + reg -> co
+  const int kc = k0 + 16 * wave + (lane & 15);
+  if (kc < K) {
+    const int tap = kc / g.C, ci = kc - (kc / g.C) * g.C;
+    const int col = wcol(g, tap, ci);
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int co = n0 + 16 * j + 4 * (lane >> 4) + reg;
+        if (co < g.CO) a.part[((long long)z * g.CO + co) * g.Kf + col] = acc[j][reg];
+      }
+  }
+  if (do_bias && n0 + tid < g.CO) a.bpart[((long long)ph * a.Z + z) * g.CO + n0 + tid] = bacc;
 }
 
-// part[block][co] = sum over the block's rows of dOut[m][co]
-template <typename T>
-__global__ __launch_bounds__(256) void bias_grad_kernel(const T* __restrict__ dout, long long M,
-                                                         int CO, float* __restrict__ bpart,
-                                                         int rows_per_block) {
-  __shared__ float s[256];
-  const long long r0 = (long long)blockIdx.x * rows_per_block;
-  const int co = threadIdx.x % CO;
-  const int lanes_per_co = 256 / CO;
-  const int part = threadIdx.x / CO;
-  float acc = 0.f;
-  if (part < lanes_per_co)
-    for (long long r = r0 + part; r < std::min<long long>(M, r0 + rows_per_block); r += lanes_per_co)
-      acc += to_f(dout[r * CO + co]);
-  s[threadIdx.x] = (part < lanes_per_co) ? acc : 0.f;
-  __syncthreads();
-  if (threadIdx.x < CO) {
-    float t = 0.f;
-    for (int p = 0; p < lanes_per_co; ++p) t += s[p * CO + threadIdx.x];
-    bpart[(long long)blockIdx.x * CO + threadIdx.x] = t;
-  }
-}
-
-// dst[e] += sum_{z < nz} part[z * n + e], in order (bit-reproducible).
+// dst[e] += sum_{z < nz} part[z * n + e], always in the same order (bit-reproducible).
 __global__ void ordered_sum_kernel(const float* __restrict__ part, int nz, long long n,
                                    float* __restrict__ dst) {
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
        e += (long long)gridDim.x * blockDim.x) {
-    float t = 0.f;
-    for (int z = 0; z < nz; ++z) t += part[(long long)z * n + e];
-    dst[e] += t;
+    float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+    int z = 0;
+    for (; z + 4 <= nz; z += 4) {
+      t0 += part[(long long)z * n + e];
+      t1 += part[(long long)(z + 1) * n + e];
+      t2 += part[(long long)(z + 2) * n + e];
+      t3 += part[(long long)(z + 3) * n + e];
+    }
+    for (; z < nz; ++z) t0 += part[(long long)z * n + e];
+    dst[e] += (t0 + t1) + (t2 + t3);
   }
 }
 
+// ------------------------------------------------------------------ elementwise
 template <typename T>
 __global__ void maxpool2_fwd_kernel(const T* __restrict__ in, int N, int H, int W, int C,
                                     T* __restrict__ out, unsigned char* __restrict__ am) {
@@ -367,11 +503,11 @@ __global__ void maxpool2_fwd_kernel(const T* __restrict__ in, int N, int H, int 
     if (v2 > best) { best = v2; arg = 2; }
     if (v3 > best) { best = v3; arg = 3; }
     out[i] = from_f<T>(best);
-    am[i] = (unsigned char)arg;
+    if (am) am[i] = (unsigned char)arg;
   }
 }
 
-// dIn = scatter(dOut to argmax) * (relu_in > 0), dIn fully written.
+// dIn = dOut routed to the argmax, times (relu_in > 0); dIn fully written.
 template <typename T>
 __global__ void maxpool2_bwd_kernel(const T* __restrict__ dout, const unsigned char* __restrict__ am,
                                     const T* __restrict__ relu_in, int N, int H, int W, int C,
@@ -396,10 +532,14 @@ __global__ void maxpool2_bwd_kernel(const T* __restrict__ dout, const unsigned c
   }
 }
 
-// Keras BCE after a sigmoid (graph mode): sigmoid_cross_entropy_with_logits, mean.
+// Keras BCE after a sigmoid (graph mode): sigmoid_cross_entropy_with_logits; the grad of
+// the mean is (sigmoid(z) - t) / n. One fp64 atomic per workgroup.
 template <typename TT, typename TG>
-__global__ void bce_logits_kernel(const float* __restrict__ z, const TT* __restrict__ t,
-                                  long long n, TG* __restrict__ grad, double* __restrict__ loss) {
+__global__ __launch_bounds__(256) void bce_logits_kernel(const float* __restrict__ z,
+                                                          const TT* __restrict__ t, long long n,
+                                                          TG* __restrict__ grad,
+                                                          double* __restrict__ loss) {
+  __shared__ double red[4];
   double acc = 0.0;
   const float inv = 1.0f / (float)n;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
@@ -409,7 +549,9 @@ __global__ void bce_logits_kernel(const float* __restrict__ z, const TT* __restr
     if (grad) grad[i] = from_f<TG>((1.f / (1.f + __expf(-zi)) - ti) * inv);
   }
   for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
-  if ((threadIdx.x & 63) == 0 && loss) atomicAdd(loss, acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0 && loss) atomicAdd(loss, (red[0] + red[1]) + (red[2] + red[3]));
 }
 
 template <typename T>
@@ -429,19 +571,20 @@ __global__ void adam_kernel(float* __restrict__ w, const float* __restrict__ g, 
   }
 }
 
-// Bd[((a*k + b)*CO + co)*CI + ci] = Bf[(((k-1-a)*k + (k-1-b))*CI + ci)*CO + co]
+// bd[ci][a][b][co] = bt[co][k-1-a][k-1-b][ci]
 template <typename T>
-__global__ void flip_transpose_kernel(const T* __restrict__ bf, int k, int CI, int CO,
+__global__ void flip_transpose_kernel(const T* __restrict__ bt, int k, int CI, int CO,
                                       T* __restrict__ bd) {
   const long long total = (long long)k * k * CI * CO;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int ci = (int)(i % CI);
-    long long r = i / CI;
-    const int co = (int)(r % CO);
-    r /= CO;
-    const int b = (int)(r % k), aa = (int)(r / k);
-    bd[i] = bf[(((long long)(k - 1 - aa) * k + (k - 1 - b)) * CI + ci) * CO + co];
+    const int co = (int)(i % CO);
+    long long r = i / CO;
+    const int b = (int)(r % k);
+    r /= k;
+    const int aa = (int)(r % k);
+    const int ci = (int)(r / k);
+    bd[i] = bt[(((long long)co * k + (k - 1 - aa)) * k + (k - 1 - b)) * CI + ci];
   }
 }
 
@@ -456,77 +599,108 @@ inline unsigned grid1d(long long n) {
   return (unsigned)std::max<long long>(1, std::min<long long>((n + 255) / 256, 65536));
 }
 
-template <typename T>
-int launch_conv(const ConvFwdArgs& a, hipStream_t st) {
-  const long long M = (long long)a.g.N * a.g.OH * a.g.OW;
-  const unsigned gx = (unsigned)((M + BM - 1) / BM);
-  const int nt = std::min(4, (a.g.CO + 15) / 16);
-  const unsigned gy = (unsigned)((a.g.CO + 16 * nt - 1) / (16 * nt));
-  switch (nt) {
-    case 1: hipLaunchKernelGGL((conv_igemm_kernel<T, 1>), dim3(gx, gy), dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((conv_igemm_kernel<T, 2>), dim3(gx, gy), dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((conv_igemm_kernel<T, 3>), dim3(gx, gy), dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((conv_igemm_kernel<T, 4>), dim3(gx, gy), dim3(256), 0, st, a); break;
+// ------------------------------------------------------------------ host planning
+// Split a conv over an in_dil-dilated input (stride 1) into in_dil^2 dense output phases.
+int plan_phases(int N, int IH, int IW, int C, int CO, int KH, int KW, int stride, int pad_t,
+                int pad_l, int in_dil, int OH, int OW, Geo* g, int* nph) {
+  const int Kf = KH * KW * C;
+  if (in_dil == 1) {
+    g[0] = Geo{N, IH, IW, C, OH, OW, CO, KH, KW, stride, pad_t, pad_l,
+               0, 0, 1, KW, Kf, 1, 0, 1, 0, OH, OW};
+    *nph = 1;
+    return SPECENH_OK;
   }
+  if (in_dil != 2 || stride != 1)
+    return set_error(SPECENH_EUNSUPPORTED, "dilated input supports in_dil 2 with stride 1");
+  const int d = in_dil;
+  int n = 0;
+  for (int py = 0; py < d; ++py) {
+    for (int px = 0; px < d; ++px) {
+      const int OHq = OH > py ? (OH - py + d - 1) / d : 0;
+      const int OWq = OW > px ? (OW - px + d - 1) / d : 0;
+      if (OHq == 0 || OWq == 0) continue;
+      const int ky0 = ((pad_t - py) % d + d) % d, kx0 = ((pad_l - px) % d + d) % d;
+      const int ny = ky0 < KH ? (KH - ky0 + d - 1) / d : 0;
+      const int nx = kx0 < KW ? (KW - kx0 + d - 1) / d : 0;
+      const int offy = (py - pad_t + ky0) / d, offx = (px - pad_l + kx0) / d;  // exact
+      g[n++] = Geo{N, IH, IW, C, OHq, OWq, CO, ny, nx, 1, -offy, -offx,
+                   ky0, kx0, d, KW, Kf, d, py, d, px, OH, OW};
+    }
+  }
+  *nph = n;
+  return SPECENH_OK;
+}
+
+int check_sizes(long long N, long long IH, long long IW, long long C, long long OH, long long OW,
+                long long CO) {
+  if (N <= 0 || IH <= 0 || IW <= 0 || C <= 0 || OH <= 0 || OW <= 0 || CO <= 0)
+    return set_error(SPECENH_EINVAL, "bad convolution geometry");
+  if (N * IH * IW * C >= (1LL << 31) || N * OH * OW * CO >= (1LL << 31))
+    return set_error(SPECENH_EUNSUPPORTED, "tensor too large for one launch (split the batch)");
+  return SPECENH_OK;
+}
+
+template <typename T>
+int launch_fwd(const ConvArgs& a, int nph, hipStream_t st) {
+  int maxM = 0;
+  for (int i = 0; i < nph; ++i) maxM = std::max(maxM, a.g[i].N * a.g[i].OH * a.g[i].OW);
+  const int CO = a.g[0].CO;
+  const int nt = std::min(4, (CO + 15) / 16);
+  const int mt = nt >= 3 ? 2 : 4;
+  const unsigned gx = (unsigned)((maxM + 64 * mt - 1) / (64 * mt));
+  const unsigned gy = (unsigned)((CO + 16 * nt - 1) / (16 * nt));
+  const dim3 grid(gx, gy, nph);
+#define SPECENH_FWD(MT, NT) hipLaunchKernelGGL((conv_fwd_kernel<T, MT, NT>), grid, dim3(256), 0, st, a)
+  if (nt == 1) SPECENH_FWD(4, 1);
+  else if (nt == 2) SPECENH_FWD(4, 2);
+  else if (nt == 3) SPECENH_FWD(2, 3);
+  else SPECENH_FWD(2, 4);
+#undef SPECENH_FWD
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "conv launch");
 }
 
 struct WgradPlan {
-  int nt;
-  unsigned gx, gy, gz;
-  long long chunk;
-  unsigned nbias;  // bias-grad blocks
-  size_t part_elems, bias_elems;
+  int Z, nt;
+  unsigned gx, gy;
 };
-constexpr int BIAS_ROWS = 4096;
 
-WgradPlan wgrad_plan(long long M, int K, int CO) {
+WgradPlan wgrad_plan(int Kf, int CO) {
   WgradPlan p{};
   p.nt = std::min(4, (CO + 15) / 16);
-  p.gx = (unsigned)((K + 63) / 64);
+  p.gx = (unsigned)((Kf + 63) / 64);
   p.gy = (unsigned)((CO + 16 * p.nt - 1) / (16 * p.nt));
-  // pixel chunks: ~4 workgroups per CU overall, chunk a multiple of 32 pixels
-  const long long want = std::max<long long>(1, 1024 / (long long)(p.gx * p.gy));
-  long long chunk = (M + want - 1) / want;
-  p.chunk = std::max<long long>(256, ((chunk + 31) / 32) * 32);
-  p.gz = (unsigned)((M + p.chunk - 1) / p.chunk);
-  p.nbias = (unsigned)((M + BIAS_ROWS - 1) / BIAS_ROWS);
-  p.part_elems = (size_t)p.gz * K * CO;
-  p.bias_elems = (size_t)p.nbias * CO;
+  const long long want = 2048 / std::max<long long>(1, (long long)p.gx * p.gy);
+  p.Z = (int)std::min<long long>(256, std::max<long long>(1, want));
   return p;
 }
 
 template <typename T>
-int launch_wgrad(const ConvGeom& g, const T* in, const T* dout, float* dw, float* db,
-                 float* ws, hipStream_t st) {
-  const long long M = (long long)g.N * g.OH * g.OW;
-  const int K = g.KH * g.KW * g.C;
-  const WgradPlan p = wgrad_plan(M, K, g.CO);
-  const dim3 grid(p.gx, p.gy, p.gz);
-  const int ch = (int)p.chunk;
-  switch (p.nt) {
-    case 1: hipLaunchKernelGGL((conv_wgrad_kernel<T, 1>), grid, dim3(256), 0, st, g, in, dout, ws, ch); break;
-    case 2: hipLaunchKernelGGL((conv_wgrad_kernel<T, 2>), grid, dim3(256), 0, st, g, in, dout, ws, ch); break;
-    case 3: hipLaunchKernelGGL((conv_wgrad_kernel<T, 3>), grid, dim3(256), 0, st, g, in, dout, ws, ch); break;
-    default: hipLaunchKernelGGL((conv_wgrad_kernel<T, 4>), grid, dim3(256), 0, st, g, in, dout, ws, ch); break;
+int launch_wgrad(WgradArgs& a, int nph, float* dw, float* db, hipStream_t st) {
+  const Geo& g0 = a.g[0];
+  const WgradPlan p = wgrad_plan(g0.Kf, g0.CO);
+  constexpr int BP = Tile<T>::BK;
+  a.Z = p.Z;
+  for (int i = 0; i < nph; ++i) {
+    const long long M = (long long)a.g[i].N * a.g[i].OH * a.g[i].OW;
+    long long ch = (M + p.Z - 1) / p.Z;
+    a.chunk[i] = (int)(((ch + BP - 1) / BP) * BP);
   }
-  const long long n = (long long)K * g.CO;
-  hipLaunchKernelGGL(ordered_sum_kernel, dim3(grid1d(n)), dim3(256), 0, st, ws, (int)p.gz, n, dw);
-  if (db) {
-    float* bpart = ws + p.part_elems;
-    hipLaunchKernelGGL(bias_grad_kernel<T>, dim3(p.nbias), dim3(256), 0, st, dout, M, g.CO,
-                       bpart, BIAS_ROWS);
-    hipLaunchKernelGGL(ordered_sum_kernel, dim3(1), dim3(256), 0, st, bpart, (int)p.nbias,
-                       (long long)g.CO, db);
-  }
+  unsigned gx = 0;
+  for (int i = 0; i < nph; ++i)
+    gx = std::max(gx, (unsigned)((a.g[i].KH * a.g[i].KW * a.g[i].C + 63) / 64));
+  const dim3 grid(gx, p.gy, (unsigned)(nph * p.Z));
+#define SPECENH_WG(NT) hipLaunchKernelGGL((conv_wgrad_kernel<T, NT>), grid, dim3(256), 0, st, a)
+  if (p.nt == 1) SPECENH_WG(1);
+  else if (p.nt == 2) SPECENH_WG(2);
+  else if (p.nt == 3) SPECENH_WG(3);
+  else SPECENH_WG(4);
+#undef SPECENH_WG
+  const long long n = (long long)g0.CO * g0.Kf;
+  hipLaunchKernelGGL(ordered_sum_kernel, dim3(grid1d(n)), dim3(256), 0, st, a.part, p.Z, n, dw);
+  if (db)
+    hipLaunchKernelGGL(ordered_sum_kernel, dim3(1), dim3(256), 0, st, a.bpart, nph * p.Z,
+                       (long long)g0.CO, db);
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
-}
-
-int check_geom(const ConvGeom& g) {
-  if (g.N <= 0 || g.IH <= 0 || g.IW <= 0 || g.C <= 0 || g.OH <= 0 || g.OW <= 0 || g.CO <= 0 ||
-      g.KH <= 0 || g.KW <= 0 || g.stride <= 0 || g.in_dil <= 0)
-    return set_error(SPECENH_EINVAL, "bad convolution geometry");
-  return SPECENH_OK;
 }
 
 }  // namespace specenh
@@ -539,46 +713,58 @@ int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, cons
                    int KH, int KW, int CO, const float* bias, int stride, int pad_t, int pad_l,
                    int in_dil, int OH, int OW, int act, const void* mask, float* logits,
                    void* out, int out_f32, void* stream) {
-  ConvFwdArgs a{};
-  a.g = ConvGeom{N, IH, IW, C, OH, OW, CO, KH, KW, stride, pad_t, pad_l, in_dil};
-  if (int e = check_geom(a.g)) return e;
+  if (int e = check_sizes(N, IH, IW, C, OH, OW, CO)) return e;
+  if (KH <= 0 || KW <= 0 || stride <= 0 || in_dil <= 0)
+    return set_error(SPECENH_EINVAL, "bad convolution geometry");
   if (!in || !w_gemm || !out) return set_error(SPECENH_EINVAL, "null pointer");
   if (act < 0 || act > 2) return set_error(SPECENH_EINVAL, "bad activation");
+  if (dtype != 0 && dtype != 1) return set_error(SPECENH_EINVAL, "dtype must be 0 (f32) or 1 (bf16)");
+  ConvArgs a{};
+  int nph = 0;
+  if (int e = plan_phases(N, IH, IW, C, CO, KH, KW, stride, pad_t, pad_l, in_dil, OH, OW, a.g, &nph))
+    return e;
   a.in = in; a.w = w_gemm; a.bias = bias; a.out = out; a.out_f32 = out_f32;
   a.mask = mask; a.act = act; a.logits = logits;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == 0) return launch_conv<float>(a, st);
-  if (dtype == 1) return launch_conv<__bf16>(a, st);
-  return set_error(SPECENH_EINVAL, "dtype must be 0 (f32) or 1 (bf16)");
+  return dtype == 0 ? launch_fwd<float>(a, nph, st) : launch_fwd<__bf16>(a, nph, st);
 }
 
 size_t specenh_conv2d_wgrad_workspace_bytes(int N, int OH, int OW, int KH, int KW, int C,
                                             int CO) {
   if (N <= 0 || OH <= 0 || OW <= 0 || KH <= 0 || KW <= 0 || C <= 0 || CO <= 0) return 0;
-  const WgradPlan p = wgrad_plan((long long)N * OH * OW, KH * KW * C, CO);
-  return (p.part_elems + p.bias_elems) * sizeof(float);
+  const WgradPlan p = wgrad_plan(KH * KW * C, CO);
+  return ((size_t)p.Z * CO * KH * KW * C + (size_t)MAXPH * p.Z * CO) * sizeof(float);
 }
 
 int specenh_conv2d_wgrad(int dtype, const void* in, int N, int IH, int IW, int C, const void* dout,
                          int KH, int KW, int CO, int stride, int pad_t, int pad_l, int in_dil,
                          int OH, int OW, float* dw, float* dbias, void* workspace, void* stream) {
-  ConvGeom g{N, IH, IW, C, OH, OW, CO, KH, KW, stride, pad_t, pad_l, in_dil};
-  if (int e = check_geom(g)) return e;
+  if (int e = check_sizes(N, IH, IW, C, OH, OW, CO)) return e;
+  if (KH <= 0 || KW <= 0 || stride <= 0 || in_dil <= 0)
+    return set_error(SPECENH_EINVAL, "bad convolution geometry");
   if (!in || !dout || !dw || !workspace) return set_error(SPECENH_EINVAL, "null pointer");
-  if (dbias && CO > 256) return set_error(SPECENH_EUNSUPPORTED, "bias grad supports CO <= 256");
+  if (in_dil > KH || in_dil > KW)
+    return set_error(SPECENH_EUNSUPPORTED, "wgrad needs kernel_size >= in_dil");
+  if (dtype != 0 && dtype != 1) return set_error(SPECENH_EINVAL, "dtype must be 0 (f32) or 1 (bf16)");
+  WgradArgs a{};
+  int nph = 0;
+  if (int e = plan_phases(N, IH, IW, C, CO, KH, KW, stride, pad_t, pad_l, in_dil, OH, OW, a.g, &nph))
+    return e;
+  const WgradPlan p = wgrad_plan(KH * KW * C, CO);
+  a.in = in;
+  a.dout = dout;
+  a.part = (float*)workspace;
+  a.bpart = dbias ? a.part + (size_t)p.Z * CO * KH * KW * C : nullptr;
   hipStream_t st = (hipStream_t)stream;
-  float* ws = (float*)workspace;
-  if (dtype == 0)
-    return launch_wgrad<float>(g, (const float*)in, (const float*)dout, dw, dbias, ws, st);
-  if (dtype == 1)
-    return launch_wgrad<__bf16>(g, (const __bf16*)in, (const __bf16*)dout, dw, dbias, ws, st);
-  return set_error(SPECENH_EINVAL, "dtype must be 0 (f32) or 1 (bf16)");
+  return dtype == 0 ? launch_wgrad<float>(a, nph, dw, dbias, st)
+                    : launch_wgrad<__bf16>(a, nph, dw, dbias, st);
 }
 
 int specenh_maxpool2_fwd(int dtype, const void* in, int N, int H, int W, int C, void* out,
                          unsigned char* argmax, void* stream) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || (H & 1) || (W & 1))
     return set_error(SPECENH_EINVAL, "maxpool2 needs even H, W");
+  if (!in || !out) return set_error(SPECENH_EINVAL, "null pointer");
   const long long n = (long long)N * (H / 2) * (W / 2) * C;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == 0)
@@ -597,6 +783,7 @@ int specenh_maxpool2_bwd(int dtype, const void* dout, const unsigned char* argma
                          void* stream) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || (H & 1) || (W & 1))
     return set_error(SPECENH_EINVAL, "maxpool2 needs even H, W");
+  if (!dout || !argmax || !din) return set_error(SPECENH_EINVAL, "null pointer");
   const long long n = (long long)N * (H / 2) * (W / 2) * C;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == 0)
@@ -615,7 +802,7 @@ int specenh_bce_logits(const float* z, const void* target, int target_dtype, lon
                        void* grad, int grad_dtype, double* loss_sum, void* stream) {
   if (!z || !target || n <= 0) return set_error(SPECENH_EINVAL, "bce args");
   hipStream_t st = (hipStream_t)stream;
-  const unsigned gx = std::min<unsigned>(grid1d(n), 2048);
+  const unsigned gx = std::min<unsigned>(grid1d(n), 1024);
 #define SPECENH_BCE(TT, TG)                                                                   \
   hipLaunchKernelGGL((bce_logits_kernel<TT, TG>), dim3(gx), dim3(256), 0, st, z,             \
                      (const TT*)target, n, (TG*)grad, loss_sum)
@@ -637,17 +824,17 @@ int specenh_adam_step(float* w, const float* g, float* m, float* v, long long n,
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "adam");
 }
 
-int specenh_weight_flip_transpose(int dtype, const void* bf, int k, int ci, int co, void* bd,
+int specenh_weight_flip_transpose(int dtype, const void* bt, int k, int ci, int co, void* bd,
                                   void* stream) {
   const long long n = (long long)k * k * ci * co;
-  if (!bf || !bd || n <= 0) return set_error(SPECENH_EINVAL, "flip args");
+  if (!bt || !bd || n <= 0) return set_error(SPECENH_EINVAL, "flip args");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == 0)
     hipLaunchKernelGGL(flip_transpose_kernel<float>, dim3(grid1d(n)), dim3(256), 0, st,
-                       (const float*)bf, k, ci, co, (float*)bd);
+                       (const float*)bt, k, ci, co, (float*)bd);
   else if (dtype == 1)
     hipLaunchKernelGGL(flip_transpose_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st,
-                       (const __bf16*)bf, k, ci, co, (__bf16*)bd);
+                       (const __bf16*)bt, k, ci, co, (__bf16*)bd);
   else
     return set_error(SPECENH_EINVAL, "dtype");
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "flip");

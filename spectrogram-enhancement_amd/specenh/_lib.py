@@ -81,6 +81,11 @@ SIGNATURES = {
                                                  _c.c_int, _c.c_void_p, _c.c_void_p]),
     "specenh_cast": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_void_p, _c.c_longlong,
                                 _c.c_void_p]),
+    "specenh_strips_pack": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_longlong, _c.c_int, _c.c_int,
+                                       _c.c_longlong, _c.c_int, _c.c_int, _c.c_int, _c.c_void_p,
+                                       _c.c_void_p]),
+    "specenh_strips_unpack": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_longlong, _c.c_int, _c.c_int,
+                                         _c.c_int, _c.c_void_p, _c.c_void_p]),
 }
 
 

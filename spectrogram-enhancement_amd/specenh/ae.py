@@ -15,10 +15,11 @@ kernels of csrc/conv_ae.hip:
             also refreshes the bf16 copy the MFMA kernels read; a data-parallel run
             all-reduces the ONE flat gradient buffer (RCCL) before it.
 
-Weights live in "GEMM layout": Bf[(ky, kx, ci)][co] such that the forward pass is
-out[m][co] = sum_k A[m][k] Bf[k][co]. For Conv2D this is the Keras HWIO kernel itself;
-for Conv2DTranspose (Keras kernel [k, k, Cout, Cin]) Bf = kernel[::-1, ::-1] with the
-channel axes swapped. Adam is elementwise, so it runs on this layout directly.
+Weights live in "GEMM layout" Bt[co][(ky, kx, ci)] such that the forward pass is
+out[m][co] = sum_k A[m][k] Bt[co][k]. For Conv2D this is the Keras HWIO kernel with the
+output channel moved first; for Conv2DTranspose (Keras kernel [k, k, Cout, Cin]) it is
+kernel[::-1, ::-1] with Cout moved first. Adam is elementwise, so it runs on this
+layout directly.
 """
 from __future__ import annotations
 
@@ -89,20 +90,20 @@ class PoolOp:
 
 
 def keras_to_gemm(op: ConvOp, kernel: np.ndarray) -> np.ndarray:
-    """Keras kernel -> Bf[(ky,kx,ci)][co] (flattened fp32)."""
+    """Keras kernel -> Bt[co][(ky, kx, ci)] (flattened fp32, N-major GEMM operand)."""
     kernel = np.asarray(kernel, dtype=np.float32)
     if op.kind == "conv":
         assert kernel.shape == (op.k, op.k, op.cin, op.cout), kernel.shape
-        return np.ascontiguousarray(kernel).reshape(-1)
+        return np.ascontiguousarray(kernel.transpose(3, 0, 1, 2)).reshape(-1)
     assert kernel.shape == (op.k, op.k, op.cout, op.cin), kernel.shape
-    return np.ascontiguousarray(kernel[::-1, ::-1].transpose(0, 1, 3, 2)).reshape(-1)
+    return np.ascontiguousarray(kernel[::-1, ::-1].transpose(2, 0, 1, 3)).reshape(-1)
 
 
 def gemm_to_keras(op: ConvOp, flat: np.ndarray) -> np.ndarray:
-    bf = np.asarray(flat, dtype=np.float32).reshape(op.k, op.k, op.cin, op.cout)
+    bt = np.asarray(flat, dtype=np.float32).reshape(op.cout, op.k, op.k, op.cin)
     if op.kind == "conv":
-        return bf.copy()
-    return np.ascontiguousarray(bf[::-1, ::-1].transpose(0, 1, 3, 2))
+        return np.ascontiguousarray(bt.transpose(1, 2, 3, 0))
+    return np.ascontiguousarray(bt[:, ::-1, ::-1, :].transpose(1, 2, 0, 3))
 
 
 class AutoencoderEngine:

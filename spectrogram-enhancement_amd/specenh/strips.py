@@ -1,0 +1,91 @@
+"""Drop-in for the strip glue of VAE/manual_scan_3layers.py:28-54 (same copies in
+manual_scan.py, hyperparam_scan.py, graphs.ipynb):
+
+    patch(arr)    list of spectrograms (256, T >= 3840) -> (30 * len, 256, 128) float64
+    unpatch(arr)  (30 * n, 256, 128) -> (n, 256, 3840) float64
+    reshape(arr)  (N, 256, 128) -> (N, 256, 128, 1)
+
+numpy in -> numpy float64 out like the reference (patchify views, ``np.empty`` float64);
+the copies run on the GPU (csrc/strips.hip). ``patch_batch`` / ``unpatch_batch`` are the
+device fast path: fp32 spectrograms [B, F, T] -> AE input [B*30, 256, 128, 1] already in
+the AE's compute dtype (bf16 or fp32), and back.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+ROWS, WIDTH, N_STRIPS = 256, 128, 30
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+def _stream(dev):
+    return ctypes.c_void_p(_lib.current_stream_handle(dev))
+
+
+def patch_batch(S: torch.Tensor, dtype=torch.float32, rows=ROWS, width=WIDTH,
+                n_strips=N_STRIPS, out=None) -> torch.Tensor:
+    """S: device fp32 [B, F, T] (row-major, each spectrogram contiguous) ->
+    [B * n_strips, rows, width, 1] in ``dtype``."""
+    if not isinstance(S, torch.Tensor) or S.device.type != "cuda":
+        raise RuntimeError("specenh.strips runs on the GPU only (no CPU fallback)")
+    if S.dim() == 2:
+        S = S.unsqueeze(0)
+    if S.dtype != torch.float32:
+        raise TypeError("spectrograms must be float32")
+    if not (S.stride(2) == 1 and S.stride(1) == S.shape[2]):
+        S = S.contiguous()
+    B, F, T = S.shape
+    if out is None:
+        out = torch.empty((B * n_strips, rows, width, 1), dtype=dtype, device=S.device)
+    _lib.check(_lib.lib().specenh_strips_pack(
+        _DT[dtype], ctypes.c_void_p(S.data_ptr()), B, F, T, S.stride(0), rows, width, n_strips,
+        ctypes.c_void_p(out.data_ptr()), _stream(S.device)), "strips_pack")
+    return out
+
+
+def unpatch_batch(strips: torch.Tensor, rows=ROWS, width=WIDTH, n_strips=N_STRIPS,
+                  out=None) -> torch.Tensor:
+    """strips: device [B * n_strips, rows, width(, 1)] fp32/bf16 -> fp32 [B, rows, n*width]."""
+    if not isinstance(strips, torch.Tensor) or strips.device.type != "cuda":
+        raise RuntimeError("specenh.strips runs on the GPU only (no CPU fallback)")
+    strips = strips.contiguous()
+    if strips.shape[0] % n_strips or tuple(strips.shape[1:3]) != (rows, width):
+        raise ValueError(f"strips must be [k*{n_strips}, {rows}, {width}(, 1)]")
+    B = strips.shape[0] // n_strips
+    if out is None:
+        out = torch.empty((B, rows, n_strips * width), dtype=torch.float32, device=strips.device)
+    _lib.check(_lib.lib().specenh_strips_unpack(
+        _DT[strips.dtype], ctypes.c_void_p(strips.data_ptr()), B, rows, width, n_strips,
+        ctypes.c_void_p(out.data_ptr()), _stream(strips.device)), "strips_unpack")
+    return out
+
+
+def _gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError("specenh requires a ROCm GPU (HIP); there is no CPU fallback")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def patch(arr):
+    """manual_scan_3layers.py:28-36."""
+    dev = _gpu()
+    S = torch.stack([torch.as_tensor(np.asarray(a), dtype=torch.float32) for a in arr]).to(dev)
+    return patch_batch(S)[..., 0].double().cpu().numpy()
+
+
+def unpatch(arr):
+    """manual_scan_3layers.py:39-50 (len(arr) // 30 spectrograms of (256, 3840))."""
+    a = np.asarray(arr)
+    n = (len(a) // N_STRIPS) * N_STRIPS
+    t = torch.as_tensor(a[:n], dtype=torch.float32).to(_gpu())
+    return unpatch_batch(t).double().cpu().numpy()
+
+
+def reshape(arr):
+    """manual_scan_3layers.py:53-55."""
+    return np.reshape(arr, (len(arr), ROWS, WIDTH, 1))

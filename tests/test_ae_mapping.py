@@ -18,7 +18,7 @@ from specenh.keras import layers, mixed_precision
 from specenh.keras.models import Model, load_model
 
 
-def igemm(x, bf, k, OH, OW, geom):
+def igemm(x, bt, k, OH, OW, geom):
     """numpy restatement of the specenh_conv2d gather (include/specenh.h)."""
     stride, pt, pl, dil = geom
     N, IH, IW, C = x.shape
@@ -35,11 +35,14 @@ def igemm(x, bf, k, OH, OW, geom):
             ix = np.clip(vx // dil, 0, IW - 1)
             ok = (okx & oky)[None, :, :, None]
             A[:, :, :, ky, kx, :] = np.where(ok, x[:, iy, ix, :], 0.0)
-    return A.reshape(N * OH * OW, -1), (A.reshape(N * OH * OW, -1) @ bf).reshape(N, OH, OW, -1)
+    A = A.reshape(N * OH * OW, -1)
+    return A, (A @ bt.T).reshape(N, OH, OW, -1)
 
 
-def flip_transpose(bf_flat, k, ci, co):
-    return bf_flat.reshape(k, k, ci, co)[::-1, ::-1].transpose(0, 1, 3, 2).reshape(k * k * co, ci)
+def flip_transpose(bt_flat, k, ci, co):
+    """specenh_weight_flip_transpose: bd[ci][a][b][co] = bt[co][k-1-a][k-1-b][ci]."""
+    bt = bt_flat.reshape(co, k, k, ci)
+    return np.ascontiguousarray(bt[:, ::-1, ::-1, :].transpose(3, 1, 2, 0)).reshape(ci, k * k * co)
 
 
 CASES = [("conv", 1, 16, 5, 12, 10), ("conv", 16, 8, 3, 9, 7), ("conv", 8, 1, 5, 8, 8),
@@ -61,22 +64,22 @@ def test_forward_dgrad_wgrad_lowering(kind, cin, cout, k, H, W):
     OH, OW = op.out_hw(H, W)
     assert ref.shape == (2, OH, OW, cout)
 
-    bf = ae.keras_to_gemm(op, Wk.astype(np.float32)).astype(np.float64)
+    bt = ae.keras_to_gemm(op, Wk.astype(np.float32)).astype(np.float64)
     # keras_to_gemm casts to fp32: compare against the fp32-rounded kernel
     Wt32 = torch.tensor(Wk.astype(np.float32).astype(np.float64), requires_grad=True)
     ref = f(xt, Wt32, b)
-    A, out = igemm(x, bf.reshape(-1, cout), k, OH, OW, op.fwd_geom())
+    A, out = igemm(x, bt.reshape(cout, -1), k, OH, OW, op.fwd_geom())
     np.testing.assert_allclose(out, ref.detach().numpy(), rtol=1e-12, atol=1e-12)
 
     # backward: dX via the dgrad conv, dW via A^T dZ
     dz = rng.standard_normal(ref.shape)
     ref.backward(torch.tensor(dz))
-    bd = flip_transpose(bf, k, cin, cout)
+    bd = flip_transpose(bt, k, cin, cout)
     _, dx = igemm(dz, bd, k, H, W, op.dgrad_geom())
     np.testing.assert_allclose(dx, xt.grad.numpy(), rtol=1e-11, atol=1e-11)
-    dbf = A.T @ dz.reshape(-1, cout)
-    bfk = dbf.reshape(k, k, cin, cout)
-    dW = bfk if kind == "conv" else bfk[::-1, ::-1].transpose(0, 1, 3, 2)
+    dbt = dz.reshape(-1, cout).T @ A  # [co][k], the specenh_conv2d_wgrad layout
+    bt4 = dbt.reshape(cout, k, k, cin)
+    dW = bt4.transpose(1, 2, 3, 0) if kind == "conv" else bt4[:, ::-1, ::-1, :].transpose(1, 2, 0, 3)
     np.testing.assert_allclose(dW, Wt32.grad.numpy(), rtol=1e-11, atol=1e-11)
 
 

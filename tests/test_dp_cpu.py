@@ -1,0 +1,164 @@
+"""Data-parallel fit() on CPU with gloo, world_size 2.
+
+Model.fit under torch.distributed takes each global batch, gives every rank its slice,
+SUM-all-reduces the ONE flat gradient buffer, scales it by 1/world inside Adam and
+all-reduces the epoch loss. These tests run that orchestration with a test-only engine:
+the oracle's autograd on CPU behind the engine interface (the HIP engine needs a GPU).
+Two gloo ranks must then end with the weights and history a single process gets on the
+same global batches.
+"""
+import math
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import autoencoder as ora
+
+
+class OracleEngine:
+    """CPU stand-in for specenh.ae.AutoencoderEngine (same methods fit() calls)."""
+
+    def __init__(self, ops, input_shape, compute_dtype="float32", device=None):
+        self.ops = ops
+        self.input_shape = tuple(input_shape)
+        self.device = torch.device("cpu")
+        self.tdt = torch.float64
+        self.spec = [("pool",) if op.kind == "pool" else (op.kind, op.cin, op.cout, op.k, op.act)
+                     for op in ops]
+        self.t = 0
+        self.params = None
+
+    def set_keras_weights(self, ws):
+        it = iter(ws)
+        self.params = []
+        for s in self.spec:
+            if s[0] == "pool":
+                self.params.append(None)
+            else:
+                self.params.append({"W": torch.tensor(next(it), dtype=torch.float64),
+                                    "b": torch.tensor(next(it), dtype=torch.float64)})
+        flat = self._flat()
+        self.g = torch.zeros_like(flat)
+        self.m = torch.zeros_like(flat)
+        self.v = torch.zeros_like(flat)
+
+    def _tensors(self):
+        return [t for p in self.params if p is not None for t in (p["W"], p["b"])]
+
+    def _flat(self):
+        return torch.cat([t.reshape(-1) for t in self._tensors()])
+
+    def get_keras_weights(self):
+        return [t.detach().numpy().astype(np.float32) for t in self._tensors()]
+
+    def to_compute(self, x):
+        return torch.as_tensor(x).to(torch.float64)
+
+    def forward(self, x, train=False):
+        for t in self._tensors():
+            t.requires_grad_(train)
+            t.grad = None
+        out, self._z = ora.forward(self.spec, self.params, x, return_logits=True)
+        return out
+
+    def loss_and_grad(self, y, want_grad=True, accumulate=None):
+        z = self._z
+        per = torch.clamp(z, min=0) - z * y + torch.log1p(torch.exp(-torch.abs(z)))
+        if want_grad:
+            per.mean().backward()
+        accumulate += per.sum().detach()
+        return accumulate
+
+    def backward(self):
+        self.g = torch.cat([t.grad.reshape(-1) for t in self._tensors()])
+
+    def adam(self, lr, b1, b2, eps, grad_scale=1.0):
+        self.t += 1
+        lr_t = lr * math.sqrt(1 - b2 ** self.t) / (1 - b1 ** self.t)
+        g = self.g * grad_scale
+        self.m = b1 * self.m + (1 - b1) * g
+        self.v = b2 * self.v + (1 - b2) * g * g
+        flat = self._flat().detach() - lr_t * self.m / (self.v.sqrt() + eps)
+        off = 0
+        with torch.no_grad():
+            for t in self._tensors():
+                n = t.numel()
+                t.copy_(flat[off:off + n].reshape(t.shape))
+                off += n
+
+
+def _build():
+    from specenh.keras import layers, utils
+    from specenh.keras.models import Model
+    utils.set_random_seed(0)
+    inp = layers.Input(shape=(16, 16, 1))
+    x = layers.Conv2D(4, 3, activation="relu", padding="same")(inp)
+    x = layers.MaxPooling2D((2, 2), padding="same")(x)
+    x = layers.Conv2DTranspose(4, 3, strides=2, activation="relu", padding="same")(x)
+    x = layers.Conv2D(1, 3, activation="sigmoid", padding="same")(x)
+    m = Model(inp, x)
+    m.compile(optimizer="adam", loss="binary_crossentropy")
+    return m
+
+
+def _data():
+    rng = np.random.default_rng(42)
+    x = rng.uniform(0, 1, (24, 16, 16, 1)).astype(np.float32)
+    y = (x > 0.6).astype(np.float32)
+    return x, y
+
+
+def _fit(out_q=None, rank=0, world=1, port=0):
+    from specenh import ae
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    real_engine = ae.AutoencoderEngine
+    ae.AutoencoderEngine = OracleEngine  # test-only: CPU autograd behind the engine API
+    try:
+        m = _build()
+        x, y = _data()
+        hist = m.fit(x, y, epochs=2, batch_size=8, shuffle=True, validation_data=(x[:8], y[:8]),
+                     verbose=0)
+        res = ([w.copy() for w in m.get_weights()], dict(hist.history))
+    finally:
+        ae.AutoencoderEngine = real_engine
+        if world > 1:
+            dist.destroy_process_group()
+    if out_q is not None:
+        out_q.put((rank, res))
+    return res
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_dp_fit_world2_matches_single_process():
+    ref_w, ref_h = _fit()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fit, args=(q, r, 2, port)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in (0, 1):
+        w, h = results[rank]
+        for a, b in zip(w, ref_w):
+            np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-7)
+        for key in ("loss", "val_loss"):
+            np.testing.assert_allclose(h[key], ref_h[key], rtol=1e-10)
+    # every rank applied the identical update
+    for a, b in zip(results[0][0], results[1][0]):
+        np.testing.assert_array_equal(a, b)

@@ -100,10 +100,11 @@ int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long
  * Primitives under the Keras-shaped facade (specenh.keras) that replaces the model of
  * VAE/manual_scan_3layers.py:186-212 (Conv2D / MaxPooling2D / Conv2DTranspose,
  * padding "same", Adam + binary_crossentropy). Tensors are NHWC, device resident.
- * dtype codes: SPECENH_DTYPE_F32 / SPECENH_DTYPE_BF16 (MFMA operands; accumulation,
- * biases, master weights, gradients of weights and the loss stay fp32). */
+ * dtype codes: SPECENH_DTYPE_F32 / _BF16 / _F16 (MFMA operands and activations;
+ * accumulation, biases, master weights, weight gradients and the loss stay fp32). */
 #define SPECENH_DTYPE_F32 0
 #define SPECENH_DTYPE_BF16 1
+#define SPECENH_DTYPE_F16 2
 #define SPECENH_ACT_NONE 0
 #define SPECENH_ACT_RELU 1
 #define SPECENH_ACT_SIGMOID 2
@@ -151,15 +152,15 @@ int specenh_bce_logits(const float* z, const void* target, int target_dtype, lon
                        void* grad, int grad_dtype, double* loss_sum, void* stream);
 /* Keras Adam on fp32 master weights, with g = grad_scale * grad (1/world_size after a
  * summing all-reduce): m = b1 m + (1-b1) g, v = b2 v + (1-b2) g^2,
- * w -= lr_t m / (sqrt(v) + eps); w_bf16 (optional) receives bf16(w). */
+ * w -= lr_t m / (sqrt(v) + eps); w_lowp (optional) receives w in lowp_dtype (BF16/F16). */
 int specenh_adam_step(float* w, const float* g, float* m, float* v, long long n, float lr_t,
-                      float b1, float b2, float eps, float grad_scale, void* w_bf16,
-                      void* stream);
+                      float b1, float b2, float eps, float grad_scale, void* w_lowp,
+                      int lowp_dtype, void* stream);
 /* bd[i][a][b][o] = bt[o][k-1-a][k-1-b][i] (bt: [co][k][k][ci], bd: [ci][k][k][co]):
  * the GEMM weights of a convolution's input gradient from its forward GEMM weights. */
 int specenh_weight_flip_transpose(int dtype, const void* bt, int k, int ci, int co, void* bd,
                                   void* stream);
-/* Element conversion f32 <-> bf16 (round to nearest even). */
+/* Element conversion between f32, bf16 and f16 (round to nearest even). */
 int specenh_cast(int src_dtype, const void* src, int dst_dtype, void* dst, long long n,
                  void* stream);
 

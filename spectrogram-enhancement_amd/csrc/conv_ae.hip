@@ -34,6 +34,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "specenh.h"
@@ -42,16 +43,20 @@ namespace specenh {
 int set_error(int code, const std::string& msg);  // stft_psd.hip
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(__bf16 x) { return (float)x; }
+__device__ __forceinline__ float to_f(_Float16 x) { return (float)x; }
 template <typename T>
 __device__ __forceinline__ T from_f(float x);
 template <>
 __device__ __forceinline__ float from_f<float>(float x) { return x; }
 template <>
 __device__ __forceinline__ __bf16 from_f<__bf16>(float x) { return (__bf16)x; }
+template <>
+__device__ __forceinline__ _Float16 from_f<_Float16>(float x) { return (_Float16)x; }
 
 // Barrier for LDS hand-off only: does not drain outstanding global loads (the prefetch).
 __device__ __forceinline__ void lds_sync() {
@@ -85,6 +90,10 @@ struct Tile;
 template <>
 struct Tile<__bf16> {
   static constexpr int BK = 64, LD = 80;  // 160-byte LDS rows
+};
+template <>
+struct Tile<_Float16> {
+  static constexpr int BK = 64, LD = 80;
 };
 template <>
 struct Tile<float> {
@@ -124,6 +133,9 @@ __device__ __forceinline__ void zero8(V8<T>& v) {
 
 __device__ __forceinline__ uint32_t bits(float x) { return __float_as_uint(x); }
 __device__ __forceinline__ uint32_t bits(__bf16 x) {
+  return (uint32_t)__builtin_bit_cast(unsigned short, x);
+}
+__device__ __forceinline__ uint32_t bits(_Float16 x) {
   return (uint32_t)__builtin_bit_cast(unsigned short, x);
 }
 
@@ -201,12 +213,19 @@ __device__ __forceinline__ V8<T> gather_b8(const T* __restrict__ W, const Geo& g
 template <typename T>
 __device__ __forceinline__ f32x4 mfma_slab(const T* sa, const T* sb, f32x4 acc, int lane) {
   constexpr int BK = Tile<T>::BK, LD = Tile<T>::LD;
-  if constexpr (sizeof(T) == 2) {
+  if constexpr (__is_same(T, __bf16)) {
 #pragma unroll
     for (int s = 0; s < BK / 32; ++s) {
       const bf16x8 a = *reinterpret_cast<const bf16x8*>(sa + (lane & 15) * LD + 32 * s + 8 * (lane >> 4));
       const bf16x8 b = *reinterpret_cast<const bf16x8*>(sb + (lane & 15) * LD + 32 * s + 8 * (lane >> 4));
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+    }
+  } else if constexpr (__is_same(T, _Float16)) {
+#pragma unroll
+    for (int s = 0; s < BK / 32; ++s) {
+      const f16x8 a = *reinterpret_cast<const f16x8*>(sa + (lane & 15) * LD + 32 * s + 8 * (lane >> 4));
+      const f16x8 b = *reinterpret_cast<const f16x8*>(sb + (lane & 15) * LD + 32 * s + 8 * (lane >> 4));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc, 0, 0, 0);
     }
   } else {
 #pragma unroll
@@ -320,6 +339,192 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
       if (m >= M) continue;
       const int n = m / hw, rem = m - (m / hw) * hw;
       const int oy = rem / g.OW, ox = rem - (rem / g.OW) * g.OW;
+      const long long pix =
+          ((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int col = n0 + 16 * j + (lane & 15);
+        if (col >= g.CO) continue;
+        const long long idx = pix * g.CO + col;
+        float v = acc[i][j][reg] + (a.bias ? a.bias[col] : 0.f);
+        if (a.logits) a.logits[idx] = v;
+        if (a.mask && !(to_f(reinterpret_cast<const T*>(a.mask)[idx]) > 0.f)) v = 0.f;
+        if (a.act == 1) v = fmaxf(v, 0.f);
+        else if (a.act == 2) v = 1.f / (1.f + __expf(-v));
+        if (a.out_f32) reinterpret_cast<float*>(a.out)[idx] = v;
+        else reinterpret_cast<T*>(a.out)[idx] = from_f<T>(v);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ LDS-patch forward
+// Stride-1 convolutions in bf16/f16 (every Conv2D forward, every Conv2DTranspose phase,
+// Conv2D input gradients): the workgroup's 16x16 output tile needs a (16+KH-1) x (16+KW-1)
+// input patch, staged in LDS once per 32-channel chunk; A fragments are read from the
+// patch (ds_read_b128, conflict-free pixel strides), so each input element is fetched
+// from HBM/L2 about (20/16)^2 times instead of KH*KW times. B fragments (the small,
+// L2-resident weights) are loaded per k-step straight into registers, one step ahead.
+// CC = channels per chunk: 32 (C % 32 == 0), 16 (C == 16: two taps per MFMA), 1 (C == 1:
+// all <= 32 taps in one MFMA).
+template <int CC>
+struct Patch;
+template <>
+struct Patch<32> { static constexpr int PST = 48; };  // 96-byte pixels
+template <>
+struct Patch<16> { static constexpr int PST = 16; };  // 32-byte pixels
+template <>
+struct Patch<1> { static constexpr int PST = 1; };
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma32(const V8<T>& a, const V8<T>& b, f32x4 acc) {
+  if constexpr (__is_same(T, __bf16)) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+  } else {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), acc, 0, 0, 0);
+  }
+}
+
+template <typename T, int NT, int CC>
+__global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
+  constexpr int TILE = 16, KMAX = 5, PMAX = TILE + KMAX - 1;
+  constexpr int PST = Patch<CC>::PST;
+  constexpr int MT = 4;  // output rows per wave
+  __shared__ __attribute__((aligned(16))) T sP[PMAX * PMAX * PST];
+  __shared__ int sTap[32];  // patch offset of tap t (elements), -1 past the last tap
+  __shared__ int sCol[32];  // weight column of tap t at ci = 0
+
+  const Geo& g = a.g[blockIdx.z];
+  const int ntx = (g.OW + TILE - 1) / TILE, nty = (g.OH + TILE - 1) / TILE;
+  const int tiles = g.N * nty * ntx;
+  if ((int)blockIdx.x >= tiles) return;
+  const int n = blockIdx.x / (nty * ntx);
+  const int trem = blockIdx.x - n * (nty * ntx);
+  const int ty = trem / ntx, tx = trem - (trem / ntx) * ntx;
+  const int oy0 = ty * TILE, ox0 = tx * TILE;
+  const int iy0 = oy0 - g.pad_t, ix0 = ox0 - g.pad_l;
+  const int PW = TILE + g.KW - 1, PH = TILE + g.KH - 1;
+  const int ntap = g.KH * g.KW;
+  const int n0 = blockIdx.y * 16 * NT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
+  const T* __restrict__ W = reinterpret_cast<const T*>(a.w);
+
+  if (tid < 32) {
+    const int jy = tid / g.KW, jx = tid - (tid / g.KW) * g.KW;
+    sTap[tid] = tid < ntap ? (jy * PW + jx) * PST : -1;
+    sCol[tid] = tid < ntap ? ((g.ky0 + g.kstep * jy) * g.KWf + g.kx0 + g.kstep * jx) * g.C : 0;
+  }
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // lane's A row base in the patch for each of its MT output rows
+  int rbase[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) rbase[i] = ((wave * MT + i) * PW + (lane & 15)) * PST;
+  const int kgrp = lane >> 4;
+
+  const int nchunk = CC == 1 ? 1 : g.C / CC;
+  for (int c = 0; c < nchunk; ++c) {
+    // ---- stage the patch of channel chunk c ----
+    if constexpr (CC == 1) {
+      for (int e = tid; e < PH * PW; e += 256) {
+        const int py = e / PW, px = e - (e / PW) * PW;
+        const int iy = iy0 + py, ix = ix0 + px;
+        const bool ok = (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW;
+        const T v = in[ok ? (n * g.IH + iy) * g.IW + ix : 0];
+        sP[e] = ok ? v : from_f<T>(0.f);
+      }
+    } else {
+      constexpr int GP = CC / 8;  // 8-channel groups per pixel
+      for (int e = tid; e < PH * PW * GP; e += 256) {
+        const int pix = e / GP, cg = e - (e / GP) * GP;
+        const int py = pix / PW, px = pix - (pix / PW) * PW;
+        const int iy = iy0 + py, ix = ix0 + px;
+        const bool ok = (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW;
+        V8<T> v = ld8(in + (ok ? ((n * g.IH + iy) * g.IW + ix) * g.C + c * CC + 8 * cg : 0));
+        if (!ok) zero8(v);
+        st8(sP + pix * PST + 8 * cg, v);
+      }
+    }
+    lds_sync();
+
+    // ---- k-steps over the taps of this chunk ----
+    const int nsteps = CC == 32 ? ntap : (CC == 16 ? (ntap + 1) / 2 : 1);
+    auto load_b = [&](int s, V8<T> (&b)[NT]) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int co = n0 + 16 * j + (lane & 15);
+        zero8(b[j]);
+        if constexpr (CC == 32) {
+          if (co < g.CO) b[j] = ld8(W + co * g.Kf + sCol[s] + c * CC + 8 * kgrp);
+        } else if constexpr (CC == 16) {
+          const int t = 2 * s + (kgrp >> 1);
+          if (co < g.CO && t < ntap) b[j] = ld8(W + co * g.Kf + sCol[t] + 8 * (kgrp & 1));
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int t = 8 * kgrp + q;
+            if (co < g.CO && t < ntap) set_elem(b[j], q, W[co * g.Kf + sCol[t]]);
+          }
+        }
+      }
+    };
+    V8<T> bcur[NT], bnxt[NT];
+    load_b(0, bcur);
+    for (int s = 0; s < nsteps; ++s) {
+      if (s + 1 < nsteps) load_b(s + 1, bnxt);
+      // A fragments for this step
+      int aoff;
+      bool aon = true;
+      if constexpr (CC == 32) {
+        aoff = sTap[s] + 8 * kgrp;
+      } else if constexpr (CC == 16) {
+        const int t = 2 * s + (kgrp >> 1);
+        aon = t < ntap;
+        aoff = (aon ? sTap[t] : 0) + 8 * (kgrp & 1);
+      } else {
+        aoff = 0;
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        V8<T> av;
+        if constexpr (CC == 1) {
+          zero8(av);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int t = 8 * kgrp + q;
+            const int off = t < 32 ? sTap[t] : -1;
+            if (off >= 0) set_elem(av, q, sP[rbase[i] + off]);
+          }
+        } else {
+          av = *reinterpret_cast<const V8<T>*>(sP + rbase[i] + aoff);
+          if (!aon) zero8(av);
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(av, bcur[j], acc[i][j]);
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bcur[j] = bnxt[j];
+    }
+    lds_sync();  // the patch is overwritten by the next chunk
+  }
+
+  // ---- epilogue: D[row = pixel x][col = channel], row = 4*(lane>>4) + reg ----
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int oy = oy0 + wave * MT + i;
+    if (oy >= g.OH) continue;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int ox = ox0 + 4 * (lane >> 4) + reg;
+      if (ox >= g.OW) continue;
       const long long pix =
           ((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0;
 #pragma unroll
@@ -595,6 +800,12 @@ __global__ void cast_kernel(const TS* __restrict__ s, TD* __restrict__ d, long l
     d[i] = from_f<TD>(to_f(s[i]));
 }
 
+// Developer switch read once per process (A/B of kernel variants on the GPU box).
+inline bool getenv_flag(const char* name) {
+  const char* v = std::getenv(name);
+  return v && *v && *v != '0';
+}
+
 inline unsigned grid1d(long long n) {
   return (unsigned)std::max<long long>(1, std::min<long long>((n + 255) / 256, 65536));
 }
@@ -640,8 +851,48 @@ int check_sizes(long long N, long long IH, long long IW, long long C, long long 
   return SPECENH_OK;
 }
 
+template <typename T, int CC>
+int launch_patch(const ConvArgs& a, int nph, hipStream_t st) {
+  unsigned tiles = 0;
+  for (int i = 0; i < nph; ++i)
+    tiles = std::max(tiles, (unsigned)(a.g[i].N * ((a.g[i].OH + 15) / 16) * ((a.g[i].OW + 15) / 16)));
+  const int CO = a.g[0].CO;
+  const int nt = std::min(4, (CO + 15) / 16);
+  const dim3 grid(tiles, (unsigned)((CO + 16 * nt - 1) / (16 * nt)), nph);
+#define SPECENH_PATCH(NT) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC>), grid, dim3(256), 0, st, a)
+  if (nt == 1) SPECENH_PATCH(1);
+  else if (nt == 2) SPECENH_PATCH(2);
+  else if (nt == 3) SPECENH_PATCH(3);
+  else SPECENH_PATCH(4);
+#undef SPECENH_PATCH
+  return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "conv launch");
+}
+
+// which LDS-patch chunking applies (0 = none: use the generic gather kernel)
+int patch_cc(const ConvArgs& a, int nph) {
+  for (int i = 0; i < nph; ++i) {
+    const Geo& g = a.g[i];
+    if (g.stride != 1 || g.KH > 5 || g.KW > 5 || g.KH * g.KW > 32) return 0;
+  }
+  const int C = a.g[0].C;
+  if (C % 32 == 0) return 32;
+  if (C == 16) return 16;
+  if (C == 1) return 1;
+  return 0;
+}
+
 template <typename T>
 int launch_fwd(const ConvArgs& a, int nph, hipStream_t st) {
+  if constexpr (!__is_same(T, float)) {
+    if (!getenv_flag("SPECENH_CONV_NO_PATCH")) {
+      switch (patch_cc(a, nph)) {
+        case 32: return launch_patch<T, 32>(a, nph, st);
+        case 16: return launch_patch<T, 16>(a, nph, st);
+        case 1: return launch_patch<T, 1>(a, nph, st);
+        default: break;
+      }
+    }
+  }
   int maxM = 0;
   for (int i = 0; i < nph; ++i) maxM = std::max(maxM, a.g[i].N * a.g[i].OH * a.g[i].OW);
   const int CO = a.g[0].CO;
@@ -718,7 +969,7 @@ int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, cons
     return set_error(SPECENH_EINVAL, "bad convolution geometry");
   if (!in || !w_gemm || !out) return set_error(SPECENH_EINVAL, "null pointer");
   if (act < 0 || act > 2) return set_error(SPECENH_EINVAL, "bad activation");
-  if (dtype != 0 && dtype != 1) return set_error(SPECENH_EINVAL, "dtype must be 0 (f32) or 1 (bf16)");
+  if (dtype < 0 || dtype > 2) return set_error(SPECENH_EINVAL, "dtype must be f32, bf16 or f16");
   ConvArgs a{};
   int nph = 0;
   if (int e = plan_phases(N, IH, IW, C, CO, KH, KW, stride, pad_t, pad_l, in_dil, OH, OW, a.g, &nph))
@@ -726,7 +977,9 @@ int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, cons
   a.in = in; a.w = w_gemm; a.bias = bias; a.out = out; a.out_f32 = out_f32;
   a.mask = mask; a.act = act; a.logits = logits;
   hipStream_t st = (hipStream_t)stream;
-  return dtype == 0 ? launch_fwd<float>(a, nph, st) : launch_fwd<__bf16>(a, nph, st);
+  if (dtype == SPECENH_DTYPE_F32) return launch_fwd<float>(a, nph, st);
+  if (dtype == SPECENH_DTYPE_BF16) return launch_fwd<__bf16>(a, nph, st);
+  return launch_fwd<_Float16>(a, nph, st);
 }
 
 size_t specenh_conv2d_wgrad_workspace_bytes(int N, int OH, int OW, int KH, int KW, int C,
@@ -745,7 +998,7 @@ int specenh_conv2d_wgrad(int dtype, const void* in, int N, int IH, int IW, int C
   if (!in || !dout || !dw || !workspace) return set_error(SPECENH_EINVAL, "null pointer");
   if (in_dil > KH || in_dil > KW)
     return set_error(SPECENH_EUNSUPPORTED, "wgrad needs kernel_size >= in_dil");
-  if (dtype != 0 && dtype != 1) return set_error(SPECENH_EINVAL, "dtype must be 0 (f32) or 1 (bf16)");
+  if (dtype < 0 || dtype > 2) return set_error(SPECENH_EINVAL, "dtype must be f32, bf16 or f16");
   WgradArgs a{};
   int nph = 0;
   if (int e = plan_phases(N, IH, IW, C, CO, KH, KW, stride, pad_t, pad_l, in_dil, OH, OW, a.g, &nph))
@@ -756,8 +1009,9 @@ int specenh_conv2d_wgrad(int dtype, const void* in, int N, int IH, int IW, int C
   a.part = (float*)workspace;
   a.bpart = dbias ? a.part + (size_t)p.Z * CO * KH * KW * C : nullptr;
   hipStream_t st = (hipStream_t)stream;
-  return dtype == 0 ? launch_wgrad<float>(a, nph, dw, dbias, st)
-                    : launch_wgrad<__bf16>(a, nph, dw, dbias, st);
+  if (dtype == SPECENH_DTYPE_F32) return launch_wgrad<float>(a, nph, dw, dbias, st);
+  if (dtype == SPECENH_DTYPE_BF16) return launch_wgrad<__bf16>(a, nph, dw, dbias, st);
+  return launch_wgrad<_Float16>(a, nph, dw, dbias, st);
 }
 
 int specenh_maxpool2_fwd(int dtype, const void* in, int N, int H, int W, int C, void* out,
@@ -773,6 +1027,9 @@ int specenh_maxpool2_fwd(int dtype, const void* in, int N, int H, int W, int C, 
   else if (dtype == 1)
     hipLaunchKernelGGL(maxpool2_fwd_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st,
                        (const __bf16*)in, N, H, W, C, (__bf16*)out, argmax);
+  else if (dtype == 2)
+    hipLaunchKernelGGL(maxpool2_fwd_kernel<_Float16>, dim3(grid1d(n)), dim3(256), 0, st,
+                       (const _Float16*)in, N, H, W, C, (_Float16*)out, argmax);
   else
     return set_error(SPECENH_EINVAL, "dtype");
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "maxpool fwd");
@@ -793,6 +1050,10 @@ int specenh_maxpool2_bwd(int dtype, const void* dout, const unsigned char* argma
     hipLaunchKernelGGL(maxpool2_bwd_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st,
                        (const __bf16*)dout, argmax, (const __bf16*)relu_in, N, H, W, C,
                        (__bf16*)din);
+  else if (dtype == 2)
+    hipLaunchKernelGGL(maxpool2_bwd_kernel<_Float16>, dim3(grid1d(n)), dim3(256), 0, st,
+                       (const _Float16*)dout, argmax, (const _Float16*)relu_in, N, H, W, C,
+                       (_Float16*)din);
   else
     return set_error(SPECENH_EINVAL, "dtype");
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "maxpool bwd");
@@ -810,17 +1071,27 @@ int specenh_bce_logits(const float* z, const void* target, int target_dtype, lon
   else if (target_dtype == 0 && grad_dtype == 1) SPECENH_BCE(float, __bf16);
   else if (target_dtype == 1 && grad_dtype == 0) SPECENH_BCE(__bf16, float);
   else if (target_dtype == 1 && grad_dtype == 1) SPECENH_BCE(__bf16, __bf16);
+  else if (target_dtype == 0 && grad_dtype == 2) SPECENH_BCE(float, _Float16);
+  else if (target_dtype == 2 && grad_dtype == 0) SPECENH_BCE(_Float16, float);
+  else if (target_dtype == 2 && grad_dtype == 2) SPECENH_BCE(_Float16, _Float16);
   else return set_error(SPECENH_EINVAL, "dtype");
 #undef SPECENH_BCE
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "bce");
 }
 
 int specenh_adam_step(float* w, const float* g, float* m, float* v, long long n, float lr_t,
-                      float b1, float b2, float eps, float grad_scale, void* w_bf16,
-                      void* stream) {
+                      float b1, float b2, float eps, float grad_scale, void* w_lowp,
+                      int lowp_dtype, void* stream) {
   if (!w || !g || !m || !v || n <= 0) return set_error(SPECENH_EINVAL, "adam args");
-  hipLaunchKernelGGL(adam_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, (hipStream_t)stream, w,
-                     g, m, v, n, lr_t, b1, b2, eps, grad_scale, (__bf16*)w_bf16);
+  hipStream_t st = (hipStream_t)stream;
+  if (lowp_dtype == SPECENH_DTYPE_F16)
+    hipLaunchKernelGGL(adam_kernel<_Float16>, dim3(grid1d(n)), dim3(256), 0, st, w, g, m, v, n,
+                       lr_t, b1, b2, eps, grad_scale, (_Float16*)w_lowp);
+  else if (lowp_dtype == SPECENH_DTYPE_BF16 || !w_lowp)
+    hipLaunchKernelGGL(adam_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st, w, g, m, v, n,
+                       lr_t, b1, b2, eps, grad_scale, (__bf16*)w_lowp);
+  else
+    return set_error(SPECENH_EINVAL, "adam: low-precision copy must be bf16 or f16");
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "adam");
 }
 
@@ -835,6 +1106,9 @@ int specenh_weight_flip_transpose(int dtype, const void* bt, int k, int ci, int 
   else if (dtype == 1)
     hipLaunchKernelGGL(flip_transpose_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st,
                        (const __bf16*)bt, k, ci, co, (__bf16*)bd);
+  else if (dtype == 2)
+    hipLaunchKernelGGL(flip_transpose_kernel<_Float16>, dim3(grid1d(n)), dim3(256), 0, st,
+                       (const _Float16*)bt, k, ci, co, (_Float16*)bd);
   else
     return set_error(SPECENH_EINVAL, "dtype");
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "flip");
@@ -845,14 +1119,20 @@ int specenh_cast(int src_dtype, const void* src, int dst_dtype, void* dst, long 
   if (!src || !dst || n < 0) return set_error(SPECENH_EINVAL, "cast args");
   if (n == 0) return SPECENH_OK;
   hipStream_t st = (hipStream_t)stream;
-  if (src_dtype == 0 && dst_dtype == 1)
-    hipLaunchKernelGGL((cast_kernel<float, __bf16>), dim3(grid1d(n)), dim3(256), 0, st,
-                       (const float*)src, (__bf16*)dst, n);
-  else if (src_dtype == 1 && dst_dtype == 0)
-    hipLaunchKernelGGL((cast_kernel<__bf16, float>), dim3(grid1d(n)), dim3(256), 0, st,
-                       (const __bf16*)src, (float*)dst, n);
-  else
-    return set_error(SPECENH_EINVAL, "cast supports f32<->bf16");
+  const dim3 g(grid1d(n)), b(256);
+#define SPECENH_CAST(TS, TD) \
+  hipLaunchKernelGGL((cast_kernel<TS, TD>), g, b, 0, st, (const TS*)src, (TD*)dst, n)
+  const int key = src_dtype * 3 + dst_dtype;
+  switch (src_dtype < 0 || src_dtype > 2 || dst_dtype < 0 || dst_dtype > 2 ? -1 : key) {
+    case 0 * 3 + 1: SPECENH_CAST(float, __bf16); break;
+    case 0 * 3 + 2: SPECENH_CAST(float, _Float16); break;
+    case 1 * 3 + 0: SPECENH_CAST(__bf16, float); break;
+    case 2 * 3 + 0: SPECENH_CAST(_Float16, float); break;
+    case 1 * 3 + 2: SPECENH_CAST(__bf16, _Float16); break;
+    case 2 * 3 + 1: SPECENH_CAST(_Float16, __bf16); break;
+    default: return set_error(SPECENH_EINVAL, "cast: dtypes must differ, each f32/bf16/f16");
+  }
+#undef SPECENH_CAST
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "cast");
 }
 

@@ -21,8 +21,10 @@ namespace {
 
 __device__ __forceinline__ void put(float* p, float v) { *p = v; }
 __device__ __forceinline__ void put(__bf16* p, float v) { *p = (__bf16)v; }
+__device__ __forceinline__ void put(_Float16* p, float v) { *p = (_Float16)v; }
 __device__ __forceinline__ float get(const float* p) { return *p; }
 __device__ __forceinline__ float get(const __bf16* p) { return (float)*p; }
+__device__ __forceinline__ float get(const _Float16* p) { return (float)*p; }
 
 // out[(b*n + x)][r][c] = S[b][r][x*width + c]
 template <typename TD>
@@ -93,6 +95,9 @@ int specenh_strips_pack(int dst_dtype, const float* S, long long batch, int F, i
   else if (dst_dtype == SPECENH_DTYPE_BF16)
     hipLaunchKernelGGL(pack_kernel<__bf16>, dim3(blocks_for(total)), dim3(256), 0, st, S, batch,
                        T, s_stride, rows, width, n_strips, (__bf16*)out);
+  else if (dst_dtype == SPECENH_DTYPE_F16)
+    hipLaunchKernelGGL(pack_kernel<_Float16>, dim3(blocks_for(total)), dim3(256), 0, st, S,
+                       batch, T, s_stride, rows, width, n_strips, (_Float16*)out);
   else
     return set_error(SPECENH_EINVAL, "strips_pack: dtype");
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "strips_pack");
@@ -111,6 +116,9 @@ int specenh_strips_unpack(int src_dtype, const void* strips, long long batch, in
   else if (src_dtype == SPECENH_DTYPE_BF16)
     hipLaunchKernelGGL(unpack_kernel<__bf16>, dim3(blocks_for(total)), dim3(256), 0, st,
                        (const __bf16*)strips, batch, rows, width, n_strips, out);
+  else if (src_dtype == SPECENH_DTYPE_F16)
+    hipLaunchKernelGGL(unpack_kernel<_Float16>, dim3(blocks_for(total)), dim3(256), 0, st,
+                       (const _Float16*)strips, batch, rows, width, n_strips, out);
   else
     return set_error(SPECENH_EINVAL, "strips_unpack: dtype");
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "strips_unpack");

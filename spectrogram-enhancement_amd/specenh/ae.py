@@ -32,7 +32,10 @@ import torch
 
 from . import _lib
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
+_DTYPES = {"float32": F32, "bfloat16": BF16, "bf16": BF16, "mixed_bfloat16": BF16,
+           "float16": F16, "fp16": F16, "mixed_float16": F16}
+_TORCH = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16}
 ACT = {None: 0, "linear": 0, "relu": 1, "sigmoid": 2}
 _ALIGN = 64  # elements; keeps every layer's GEMM weights 16-byte aligned for bf16 x8 loads
 
@@ -120,8 +123,10 @@ class AutoencoderEngine:
         self.L = _lib.lib()
         self.ops = list(ops)
         self.input_shape = tuple(input_shape)  # (H, W, C)
-        self.dt = BF16 if compute_dtype in ("bfloat16", "bf16", "mixed_bfloat16") else F32
-        self.tdt = torch.bfloat16 if self.dt == BF16 else torch.float32
+        if compute_dtype not in _DTYPES:
+            raise ValueError(f"compute dtype {compute_dtype!r} (choose from {sorted(_DTYPES)})")
+        self.dt = _DTYPES[compute_dtype]
+        self.tdt = _TORCH[self.dt]
         self._validate()
         off = 0
         for op in self.ops:
@@ -136,7 +141,7 @@ class AutoencoderEngine:
         self.g = torch.zeros(off, dtype=torch.float32, device=dev)   # gradients
         self.m = torch.zeros(off, dtype=torch.float32, device=dev)   # Adam moments
         self.v = torch.zeros(off, dtype=torch.float32, device=dev)
-        self.w_lp = torch.zeros(off, dtype=self.tdt, device=dev) if self.dt == BF16 else None
+        self.w_lp = torch.zeros(off, dtype=self.tdt, device=dev) if self.dt != F32 else None
         # flipped/transposed copies for the input gradients (compute dtype)
         self.w_d = {i: torch.zeros(op.n_w, dtype=self.tdt, device=dev)
                     for i, op in enumerate(self.ops) if isinstance(op, ConvOp) and i > 0}
@@ -246,10 +251,10 @@ class AutoencoderEngine:
 
     def _refresh_lowp(self):
         st = self._stream()
-        if self.dt == BF16:
-            _lib.check(self.L.specenh_cast(F32, _vp(self.w), BF16, _vp(self.w_lp), self.n_flat,
+        if self.dt != F32:
+            _lib.check(self.L.specenh_cast(F32, _vp(self.w), self.dt, _vp(self.w_lp), self.n_flat,
                                            st), "cast")
-        src = self.w_lp if self.dt == BF16 else self.w
+        src = self.w_lp if self.dt != F32 else self.w
         for i, wd in self.w_d.items():
             op = self.ops[i]
             _lib.check(self.L.specenh_weight_flip_transpose(
@@ -257,7 +262,7 @@ class AutoencoderEngine:
                 op.cin, op.cout, _vp(wd), st), "flip_transpose")
 
     def _wptr(self, op):
-        src = self.w_lp if self.dt == BF16 else self.w
+        src = self.w_lp if self.dt != F32 else self.w
         return ctypes.c_void_p(src.data_ptr() + op.off_w * src.element_size())
 
     def _bptr(self, op, buf=None):
@@ -276,9 +281,11 @@ class AutoencoderEngine:
             _vp(out), int(out.dtype == torch.float32), self._stream()),
             "conv2d")
 
-    def forward(self, x, train=False):
+    def forward(self, x, train=False, timing=None):
         """x: device [N, H, W, C] in the compute dtype. Returns the output buffer
-        (fp32 for inference, compute dtype for training; reused between calls)."""
+        (fp32 for inference, compute dtype for training; reused between calls).
+        ``timing``: optional list; a (start, end) pair of torch.cuda.Event recorded on the
+        launch stream is appended around every convolution launch."""
         N = x.shape[0]
         if x.dtype != self.tdt or not x.is_contiguous() or tuple(x.shape[1:]) != self.input_shape:
             raise ValueError(f"forward expects a contiguous {self.tdt} [N, *{self.input_shape}]")
@@ -303,9 +310,15 @@ class AutoencoderEngine:
                                                        _vp(am), st), "maxpool2_fwd")
                 continue
             last = i == n_ops - 1
+            if timing is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record(torch.cuda.current_stream(self.device))
             self._conv(op, hin, hout, weights=self._wptr(op), geom=op.fwd_geom(), act=op.act,
                        logits=b["z"] if (train and last) else None,
                        out_shape=hout.shape[1:3], cout=op.cout)
+            if timing is not None:
+                ev[1].record(torch.cuda.current_stream(self.device))
+                timing.append(ev)
         return b["h"][n_ops]
 
     def loss_and_grad(self, y, want_grad=True, accumulate=None):
@@ -316,14 +329,15 @@ class AutoencoderEngine:
         mean is sum / y.numel()). Fills the last layer's gradient when want_grad."""
         if tuple(y.shape) != (self._last_train_N,) + self.output_shape:
             raise ValueError(f"targets must have shape (N, *{self.output_shape})")
-        if y.dtype not in (torch.bfloat16, torch.float32) or not y.is_contiguous():
-            raise TypeError("targets must be contiguous float32 or bfloat16")
+        inv = {v: k for k, v in _TORCH.items()}
+        if y.dtype not in inv or not y.is_contiguous():
+            raise TypeError("targets must be contiguous float32, bfloat16 or float16")
         b = self._buffers(self._last_train_N, True)
         z = b["z"]
         if accumulate is None:
             accumulate = self._loss
             accumulate.zero_()
-        ydt = BF16 if y.dtype == torch.bfloat16 else F32
+        ydt = inv[y.dtype]
         _lib.check(self.L.specenh_bce_logits(
             _vp(z), _vp(y), ydt, z.numel(), _vp(b["d"][-1]) if want_grad else ctypes.c_void_p(0),
             self.dt, _vp(accumulate), self._stream()), "bce_logits")
@@ -369,9 +383,9 @@ class AutoencoderEngine:
         lr_t = lr * math.sqrt(1.0 - beta_2 ** self.t) / (1.0 - beta_1 ** self.t)
         _lib.check(self.L.specenh_adam_step(
             _vp(self.w), _vp(self.g), _vp(self.m), _vp(self.v), self.n_flat, lr_t, beta_1, beta_2,
-            epsilon, grad_scale, _vp(self.w_lp), self._stream()), "adam_step")
+            epsilon, grad_scale, _vp(self.w_lp), self.dt, self._stream()), "adam_step")
         if self.w_d:
-            src = self.w_lp if self.dt == BF16 else self.w
+            src = self.w_lp if self.dt != F32 else self.w
             st = self._stream()
             for i, wd in self.w_d.items():
                 op = self.ops[i]

@@ -1,10 +1,11 @@
 """keras.mixed_precision subset: the compute dtype of the conv kernels.
 
-"float32" (Keras' default) runs the MFMA f32 path; "mixed_bfloat16" runs bf16 MFMA
-operands and activations with fp32 accumulation, fp32 master weights, fp32 Adam state
-and fp32 logits for the loss (the C4 training configuration, SURVEY.md §8 d).
+"float32" (Keras' default) runs the MFMA f32 path; "mixed_bfloat16" / "mixed_float16"
+run bf16 / fp16 MFMA operands and activations with fp32 accumulation, fp32 master
+weights, fp32 Adam state and fp32 logits for the loss (C4 trains in bf16, C5 infers in
+fp16, SURVEY.md §8 d). Keras' loss scaling for mixed_float16 is not applied.
 """
-_POLICIES = ("float32", "mixed_bfloat16")
+_POLICIES = ("float32", "mixed_bfloat16", "mixed_float16")
 _global = "float32"
 
 
@@ -16,7 +17,7 @@ class Policy:
 
     @property
     def compute_dtype(self):
-        return "bfloat16" if self.name == "mixed_bfloat16" else "float32"
+        return {"mixed_bfloat16": "bfloat16", "mixed_float16": "float16"}.get(self.name, "float32")
 
     @property
     def variable_dtype(self):

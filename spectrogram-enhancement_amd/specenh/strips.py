@@ -20,7 +20,7 @@ import torch
 from . import _lib
 
 ROWS, WIDTH, N_STRIPS = 256, 128, 30
-_DT = {torch.float32: 0, torch.bfloat16: 1}
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 
 
 def _stream(dev):

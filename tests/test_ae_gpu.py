@@ -254,7 +254,7 @@ def test_adam_kernel_formula(gpu_device):
     lr_t, b1, b2, eps, sc = 1e-3 * math.sqrt(1 - 0.999 ** 3) / (1 - 0.9 ** 3), 0.9, 0.999, 1e-7, 0.5
     import ctypes
     _lib.check(L.specenh_adam_step(*(ctypes.c_void_p(t.data_ptr()) for t in d), n, lr_t, b1, b2,
-                                   eps, sc, ctypes.c_void_p(wb.data_ptr()), None))
+                                   eps, sc, ctypes.c_void_p(wb.data_ptr()), 1, None))
     torch.cuda.synchronize()
     g2 = g.astype(np.float64) * sc
     m2 = b1 * m + (1 - b1) * g2
@@ -393,3 +393,13 @@ def test_backward_is_bitwise_deterministic(gpu_device):
         eng.backward()
         grads.append(eng.g.clone())
     assert torch.equal(grads[0], grads[1])
+
+
+def test_reference_model_fp16_forward_psnr(gpu_device):
+    """C5 runs the autoencoder forward in fp16 (MFMA f16, fp32 accumulation)."""
+    ops = ref_model_ops()
+    eng, params = make(ops, (128, 128, 1), dtype="float16", seed=17)
+    x = np.random.default_rng(10).uniform(0, 1, (4, 128, 128, 1)).astype(np.float32)
+    ref, _ = ref_forward(ops, params, x)
+    got = eng.forward(upload(eng, x), train=False).cpu().numpy()
+    assert psnr(got, ref) >= PSNR_MIN

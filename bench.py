@@ -135,8 +135,20 @@ def cpu_baseline(n_shots: int) -> dict:
     cores = min(16, len(os.sched_getaffinity(0)))
     x = plasma_chirps(n_shots, L5, seed0=0, dtype=np.float16).astype(np.float64)
     chunks = [x[i::cores] for i in range(cores)]
-    ctx = mp.get_context("fork")  # before any GPU initialisation in this process
-    with ctx.Pool(cores) as pool:
+    # one BLAS/OpenMP thread per worker, set before the workers import numpy/torch
+    saved = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS",
+                                             "MKL_NUM_THREADS")}
+    os.environ.update({k: "1" for k in saved})
+    ctx = mp.get_context("spawn")  # fresh interpreters: never touch the GPU
+    try:
+        pool = ctx.Pool(cores)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    with pool:
         pool.map(_cpu_worker, [c[:1] for c in chunks])  # warm imports
         t0 = time.perf_counter()
         done = sum(pool.map(_cpu_worker, chunks))

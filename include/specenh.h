@@ -123,11 +123,15 @@ int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long
  * zero holes are never gathered or multiplied.
  * logits (optional, fp32 [M][CO]) receives the pre-activation; mask (optional, dtype
  * [M][CO]) zeroes outputs where mask <= 0 (backward through a ReLU); out is fp32 when
- * out_f32 != 0, else dtype. bias may be NULL. */
+ * out_f32 != 0, else dtype. bias may be NULL.
+ * pool2 != 0 fuses the following MaxPooling2D((2,2)): out is [N][OH/2][OW/2][CO] (dtype)
+ * and argmax (optional, same shape, uint8 dy*2+dx) is what specenh_maxpool2_fwd would
+ * give; the full-resolution output is never written. Needs bf16/f16, in_dil 1, even
+ * OH/OW, no mask/logits/out_f32 (SPECENH_EUNSUPPORTED otherwise). */
 int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, const void* w_gemm,
                    int KH, int KW, int CO, const float* bias, int stride, int pad_t, int pad_l,
                    int in_dil, int OH, int OW, int act, const void* mask, float* logits,
-                   void* out, int out_f32, void* stream);
+                   void* out, int out_f32, int pool2, unsigned char* argmax, void* stream);
 /* Weight gradient of the same convolution: dw[co][k] += sum_m dout[m][co] * A[m][k]
  * (fp32, w_gemm layout, accumulated), dbias[co] += sum_m dout[m][co] (optional). Deterministic: pixel
  * chunks are reduced in a fixed order through `workspace`, which must hold
@@ -141,9 +145,11 @@ int specenh_conv2d_wgrad(int dtype, const void* in, int N, int IH, int IW, int C
 /* MaxPooling2D((2,2), padding="same") on even H, W: out [N][H/2][W/2][C] + argmax (0..3). */
 int specenh_maxpool2_fwd(int dtype, const void* in, int N, int H, int W, int C, void* out,
                          unsigned char* argmax, void* stream);
-/* din [N][H][W][C] = dout routed to the argmax, times (relu_in > 0) when relu_in != NULL. */
+/* din [N][H][W][C] = dout routed to the argmax; when pooled (the pool's output, same shape
+ * as dout) is given, positions with pooled <= 0 get 0 — the ReLU mask of the pool's input
+ * at its argmax. */
 int specenh_maxpool2_bwd(int dtype, const void* dout, const unsigned char* argmax,
-                         const void* relu_in, int N, int H, int W, int C, void* din,
+                         const void* pooled, int N, int H, int W, int C, void* din,
                          void* stream);
 /* binary_crossentropy after a sigmoid, from the fp32 logits z (Keras graph mode):
  * *loss_sum += sum_i max(z,0) - z t + log1p(exp(-|z|)) (fp64, zero it first);

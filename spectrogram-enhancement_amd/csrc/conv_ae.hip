@@ -248,6 +248,9 @@ struct ConvArgs {
   float* logits;      // same shape, fp32 pre-activation, or null
   int out_f32;
   int act;            // 0 none, 1 relu, 2 sigmoid
+  int nph;            // output phases (1, or in_dil^2)
+  int pool;           // 1: fused 2x2/2 max-pool, out is [N][OH/2][OW/2][CO]
+  unsigned char* argmax;  // pooled argmax (dy*2+dx), or null
 };
 
 // ------------------------------------------------------------------ forward / dgrad
@@ -361,14 +364,22 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
 // ------------------------------------------------------------------ LDS-patch forward
 // Stride-1 convolutions in bf16/f16 (every Conv2D forward, every Conv2DTranspose phase,
 // Conv2D input gradients): the workgroup's 16x16 output tile needs a (16+KH-1) x (16+KW-1)
-// input patch, staged in LDS once per 32-channel chunk; A fragments are read from the
-// patch (ds_read_b128, conflict-free pixel strides), so each input element is fetched
-// from HBM/L2 about (20/16)^2 times instead of KH*KW times. B fragments (the small,
-// L2-resident weights) are loaded per k-step straight into registers, one step ahead.
-// CC = channels per chunk: 32 (C % 32 == 0), 16 (C == 16: two taps per MFMA), 1 (C == 1:
-// all <= 32 taps in one MFMA).
+// input patch, staged in LDS once per channel chunk; A fragments are read from the patch
+// (ds_read_b128, bank-conflict-free pixel strides), so each input element is fetched
+// about (20/16)^2 times instead of KH*KW times. B fragments (the small, L2-resident
+// weights) go straight to registers, one k-step ahead.
+// CC = channels per chunk: 64 or 32 (C % 32 == 0), 16 (C == 16: two taps per MFMA), 1
+// (C == 1: all <= 32 taps in one MFMA).
+// Epilogue: the tile goes through LDS and leaves as 16-byte stores; with POOL the 2x2
+// max-pool (+argmax) is taken in registers first — a wave's 4 output rows and a lane's
+// 4 consecutive pixels are exactly 2x2 windows — so the full-resolution tensor is never
+// written. Phases of a dilated conv (Conv2DTranspose) run in workgroups on the same XCD
+// one after the other (blockIdx.x % 8 picks the XCD): they share the input patch and
+// interleave into the same output lines in that XCD's L2.
 template <int CC>
 struct Patch;
+template <>
+struct Patch<64> { static constexpr int PST = 80; };  // 160-byte pixels
 template <>
 struct Patch<32> { static constexpr int PST = 48; };  // 96-byte pixels
 template <>
@@ -387,27 +398,51 @@ __device__ __forceinline__ f32x4 mfma32(const V8<T>& a, const V8<T>& b, f32x4 ac
   }
 }
 
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == 1) return fmaxf(v, 0.f);
+  if (act == 2) return 1.f / (1.f + __expf(-v));
+  return v;
+}
+
 template <typename T, int NT, int CC>
+struct PatchSmem {
+  static constexpr int PMAX = 20;
+  static constexpr int PATCH = PMAX * PMAX * Patch<CC>::PST * (int)sizeof(T);
+  // plain output tile [256 px][16*NT]: fp32 only when NT <= 2 (patch_cc rejects CO > 32)
+  static constexpr int OUT = 256 * 16 * NT * (NT <= 2 ? 4 : (int)sizeof(T));
+  static constexpr int BYTES = PATCH > OUT ? PATCH : OUT;
+};
+
+template <typename T, int NT, int CC, bool POOL>
 __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
-  constexpr int TILE = 16, KMAX = 5, PMAX = TILE + KMAX - 1;
+  constexpr int TILE = 16, PMAX = 20;
   constexpr int PST = Patch<CC>::PST;
   constexpr int MT = 4;  // output rows per wave
-  __shared__ __attribute__((aligned(16))) T sP[PMAX * PMAX * PST];
+  constexpr int COT = 16 * NT;
+  __shared__ __attribute__((aligned(16))) char smem[PatchSmem<T, NT, CC>::BYTES];
   __shared__ int sTap[32];  // patch offset of tap t (elements), -1 past the last tap
   __shared__ int sCol[32];  // weight column of tap t at ci = 0
+  T* sP = reinterpret_cast<T*>(smem);
 
-  const Geo& g = a.g[blockIdx.z];
+  // ---- which tile and phase (the phases of a tile share an XCD) ----
+  int phase = 0, tile = blockIdx.x;
+  if (a.nph > 1) {
+    const int r = blockIdx.x & 31;
+    phase = r >> 3;
+    tile = (blockIdx.x >> 5) * 8 + (r & 7);
+    if (phase >= a.nph) return;
+  }
+  const Geo& g = a.g[phase];
   const int ntx = (g.OW + TILE - 1) / TILE, nty = (g.OH + TILE - 1) / TILE;
-  const int tiles = g.N * nty * ntx;
-  if ((int)blockIdx.x >= tiles) return;
-  const int n = blockIdx.x / (nty * ntx);
-  const int trem = blockIdx.x - n * (nty * ntx);
+  if (tile >= g.N * nty * ntx) return;
+  const int n = tile / (nty * ntx);
+  const int trem = tile - n * (nty * ntx);
   const int ty = trem / ntx, tx = trem - (trem / ntx) * ntx;
   const int oy0 = ty * TILE, ox0 = tx * TILE;
   const int iy0 = oy0 - g.pad_t, ix0 = ox0 - g.pad_l;
   const int PW = TILE + g.KW - 1, PH = TILE + g.KH - 1;
   const int ntap = g.KH * g.KW;
-  const int n0 = blockIdx.y * 16 * NT;
+  const int n0 = blockIdx.y * COT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
   const T* __restrict__ W = reinterpret_cast<const T*>(a.w);
@@ -424,7 +459,6 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // lane's A row base in the patch for each of its MT output rows
   int rbase[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) rbase[i] = ((wave * MT + i) * PW + (lane & 15)) * PST;
@@ -455,15 +489,17 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
     }
     lds_sync();
 
-    // ---- k-steps over the taps of this chunk ----
-    const int nsteps = CC == 32 ? ntap : (CC == 16 ? (ntap + 1) / 2 : 1);
+    // ---- k-steps: one MFMA K=32 slab each ----
+    constexpr int SUB = CC >= 32 ? CC / 32 : 1;  // 32-channel slabs per tap
+    const int nsteps = CC >= 32 ? ntap * SUB : (CC == 16 ? (ntap + 1) / 2 : 1);
     auto load_b = [&](int s, V8<T> (&b)[NT]) {
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int co = n0 + 16 * j + (lane & 15);
         zero8(b[j]);
-        if constexpr (CC == 32) {
-          if (co < g.CO) b[j] = ld8(W + co * g.Kf + sCol[s] + c * CC + 8 * kgrp);
+        if constexpr (CC >= 32) {
+          const int t = s / SUB, h = s - (s / SUB) * SUB;
+          if (co < g.CO) b[j] = ld8(W + co * g.Kf + sCol[t] + c * CC + 32 * h + 8 * kgrp);
         } else if constexpr (CC == 16) {
           const int t = 2 * s + (kgrp >> 1);
           if (co < g.CO && t < ntap) b[j] = ld8(W + co * g.Kf + sCol[t] + 8 * (kgrp & 1));
@@ -480,17 +516,15 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
     load_b(0, bcur);
     for (int s = 0; s < nsteps; ++s) {
       if (s + 1 < nsteps) load_b(s + 1, bnxt);
-      // A fragments for this step
-      int aoff;
+      int aoff = 0;
       bool aon = true;
-      if constexpr (CC == 32) {
-        aoff = sTap[s] + 8 * kgrp;
+      if constexpr (CC >= 32) {
+        const int t = s / SUB, h = s - (s / SUB) * SUB;
+        aoff = sTap[t] + 32 * h + 8 * kgrp;
       } else if constexpr (CC == 16) {
         const int t = 2 * s + (kgrp >> 1);
         aon = t < ntap;
         aoff = (aon ? sTap[t] : 0) + 8 * (kgrp & 1);
-      } else {
-        aoff = 0;
       }
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
@@ -499,8 +533,7 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
           zero8(av);
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            const int t = 8 * kgrp + q;
-            const int off = t < 32 ? sTap[t] : -1;
+            const int off = sTap[8 * kgrp + q];
             if (off >= 0) set_elem(av, q, sP[rbase[i] + off]);
           }
         } else {
@@ -513,32 +546,140 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
 #pragma unroll
       for (int j = 0; j < NT; ++j) bcur[j] = bnxt[j];
     }
-    lds_sync();  // the patch is overwritten by the next chunk
+    lds_sync();  // the patch is overwritten by the next chunk / the output tile
   }
 
-  // ---- epilogue: D[row = pixel x][col = channel], row = 4*(lane>>4) + reg ----
+  // ---- epilogue. D element (i, j, reg): output row oy0 + 4*wave + i, column
+  // ox0 + 4*(lane>>4) + reg, channel n0 + 16*j + (lane&15) ----
+  const int colv = (int)min(COT, g.CO - n0);  // valid channels of this tile
+  if (a.mask || a.logits) {
+    // training paths (dgrad with a ReLU mask / last layer's logits): direct stores
 #pragma unroll
-  for (int i = 0; i < MT; ++i) {
-    const int oy = oy0 + wave * MT + i;
-    if (oy >= g.OH) continue;
+    for (int i = 0; i < MT; ++i) {
+      const int oy = oy0 + wave * MT + i;
+      if (oy >= g.OH) continue;
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const int ox = ox0 + 4 * (lane >> 4) + reg;
-      if (ox >= g.OW) continue;
-      const long long pix =
-          ((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0;
+      for (int reg = 0; reg < 4; ++reg) {
+        const int ox = ox0 + 4 * (lane >> 4) + reg;
+        if (ox >= g.OW) continue;
+        const long long pix =
+            ((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0;
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int col = n0 + 16 * j + (lane & 15);
-        if (col >= g.CO) continue;
-        const long long idx = pix * g.CO + col;
-        float v = acc[i][j][reg] + (a.bias ? a.bias[col] : 0.f);
-        if (a.logits) a.logits[idx] = v;
-        if (a.mask && !(to_f(reinterpret_cast<const T*>(a.mask)[idx]) > 0.f)) v = 0.f;
-        if (a.act == 1) v = fmaxf(v, 0.f);
-        else if (a.act == 2) v = 1.f / (1.f + __expf(-v));
-        if (a.out_f32) reinterpret_cast<float*>(a.out)[idx] = v;
-        else reinterpret_cast<T*>(a.out)[idx] = from_f<T>(v);
+        for (int j = 0; j < NT; ++j) {
+          const int col = n0 + 16 * j + (lane & 15);
+          if (col >= g.CO) continue;
+          const long long idx = pix * g.CO + col;
+          float v = acc[i][j][reg] + (a.bias ? a.bias[col] : 0.f);
+          if (a.logits) a.logits[idx] = v;
+          if (a.mask && !(to_f(reinterpret_cast<const T*>(a.mask)[idx]) > 0.f)) v = 0.f;
+          v = apply_act(v, a.act);
+          if (a.out_f32) reinterpret_cast<float*>(a.out)[idx] = v;
+          else reinterpret_cast<T*>(a.out)[idx] = from_f<T>(v);
+        }
+      }
+    }
+    return;
+  }
+
+  if constexpr (POOL) {
+    // 2x2 windows: rows (2*ip, 2*ip+1) of this wave, columns (2*rp, 2*rp+1) of this lane
+    T* sO = sP;                                                   // [64 px][COT]
+    unsigned char* sAm = reinterpret_cast<unsigned char*>(smem) + 64 * COT * sizeof(T);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int ch = 16 * j + (lane & 15);
+      const float bv = (a.bias && n0 + ch < g.CO) ? a.bias[n0 + ch] : 0.f;
+#pragma unroll
+      for (int ip = 0; ip < 2; ++ip)
+#pragma unroll
+        for (int rp = 0; rp < 2; ++rp) {
+          // compare the values the layer would store (rounded to T), first max wins: the
+          // same argmax as MaxPooling2D on the stored activation
+          float best = to_f(from_f<T>(apply_act(acc[2 * ip][j][2 * rp] + bv, a.act)));
+          int arg = 0;
+#pragma unroll
+          for (int q = 1; q < 4; ++q) {
+            const float v =
+                to_f(from_f<T>(apply_act(acc[2 * ip + (q >> 1)][j][2 * rp + (q & 1)] + bv, a.act)));
+            if (v > best) { best = v; arg = q; }
+          }
+          const int pp = (2 * wave + ip) * 8 + 2 * (lane >> 4) + rp;  // pooled pixel in 8x8
+          sO[pp * COT + ch] = from_f<T>(best);
+          sAm[pp * COT + ch] = (unsigned char)arg;
+        }
+    }
+    lds_sync();
+    const int PHo = g.OH / 2, PWo = g.OW / 2;
+    const int py0 = oy0 / 2, px0 = ox0 / 2;
+    if (colv == COT && (g.CO & 7) == 0) {
+      constexpr int GPP = COT / 8;  // 16-byte chunks per pooled pixel
+      for (int e = tid; e < 64 * GPP; e += 256) {
+        const int pp = e / GPP, cg = e - (e / GPP) * GPP;
+        const int py = py0 + pp / 8, px = px0 + (pp & 7);
+        if (py >= PHo || px >= PWo) continue;
+        const long long o = (((long long)n * PHo + py) * PWo + px) * g.CO + n0 + 8 * cg;
+        *reinterpret_cast<uint4*>(reinterpret_cast<T*>(a.out) + o) =
+            *reinterpret_cast<const uint4*>(sO + pp * COT + 8 * cg);
+        if (a.argmax)
+          *reinterpret_cast<uint2*>(a.argmax + o) =
+              *reinterpret_cast<const uint2*>(sAm + pp * COT + 8 * cg);
+      }
+    } else {
+      for (int e = tid; e < 64 * COT; e += 256) {
+        const int pp = e / COT, ch = e - (e / COT) * COT;
+        const int py = py0 + pp / 8, px = px0 + (pp & 7);
+        if (ch >= colv || py >= PHo || px >= PWo) continue;
+        const long long o = (((long long)n * PHo + py) * PWo + px) * g.CO + n0 + ch;
+        reinterpret_cast<T*>(a.out)[o] = sO[pp * COT + ch];
+        if (a.argmax) a.argmax[o] = sAm[pp * COT + ch];
+      }
+    }
+    return;
+  } else {
+    // plain tile [256 px][COT] through LDS, in the output dtype
+    const bool f32o = a.out_f32 != 0;
+    float* sOf = reinterpret_cast<float*>(smem);
+    T* sOt = sP;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int ch = 16 * j + (lane & 15);
+      const float bv = (a.bias && n0 + ch < g.CO) ? a.bias[n0 + ch] : 0.f;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int px = (wave * MT + i) * 16 + 4 * (lane >> 4) + reg;
+          const float v = apply_act(acc[i][j][reg] + bv, a.act);
+          if (f32o) sOf[px * COT + ch] = v;
+          else sOt[px * COT + ch] = from_f<T>(v);
+        }
+    }
+    lds_sync();
+    const int esz = f32o ? 4 : (int)sizeof(T);
+    const int cpc = 16 / esz;  // channels per 16-byte chunk
+    if (colv == COT && (g.CO % cpc) == 0) {
+      const int gpp = COT / cpc;
+      for (int e = tid; e < 256 * gpp; e += 256) {
+        const int px = e / gpp, cg = e - (e / gpp) * gpp;
+        const int oy = oy0 + px / 16, ox = ox0 + (px & 15);
+        if (oy >= g.OH || ox >= g.OW) continue;
+        const long long o =
+            (((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0) * g.CO +
+            n0 + cpc * cg;
+        const char* src = smem + ((long long)px * COT + cpc * cg) * esz;
+        char* dst = reinterpret_cast<char*>(a.out) + o * esz;
+        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+      }
+    } else {
+      for (int e = tid; e < 256 * COT; e += 256) {
+        const int px = e / COT, ch = e - (e / COT) * COT;
+        const int oy = oy0 + px / 16, ox = ox0 + (px & 15);
+        if (ch >= colv || oy >= g.OH || ox >= g.OW) continue;
+        const long long o =
+            (((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0) * g.CO +
+            n0 + ch;
+        if (f32o) reinterpret_cast<float*>(a.out)[o] = sOf[px * COT + ch];
+        else reinterpret_cast<T*>(a.out)[o] = sOt[px * COT + ch];
       }
     }
   }
@@ -712,10 +853,11 @@ __global__ void maxpool2_fwd_kernel(const T* __restrict__ in, int N, int H, int 
   }
 }
 
-// dIn = dOut routed to the argmax, times (relu_in > 0); dIn fully written.
+// dIn = dOut routed to the argmax, times (pooled > 0) — the ReLU mask of the pool's input
+// at its argmax; dIn fully written.
 template <typename T>
 __global__ void maxpool2_bwd_kernel(const T* __restrict__ dout, const unsigned char* __restrict__ am,
-                                    const T* __restrict__ relu_in, int N, int H, int W, int C,
+                                    const T* __restrict__ pooled, int N, int H, int W, int C,
                                     T* __restrict__ din) {
   const long long total = (long long)N * (H / 2) * (W / 2) * C;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -726,13 +868,12 @@ __global__ void maxpool2_bwd_kernel(const T* __restrict__ dout, const unsigned c
     r /= (W / 2);
     const int y = (int)(r % (H / 2));
     const int n = (int)(r / (H / 2));
-    const float gv = to_f(dout[i]);
+    const float gv = (!pooled || to_f(pooled[i]) > 0.f) ? to_f(dout[i]) : 0.f;
     const int arg = am[i];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const long long o = (((long long)n * H + 2 * y + (q >> 1)) * W + 2 * x + (q & 1)) * C + c;
-      const bool on = q == arg && (!relu_in || to_f(relu_in[o]) > 0.f);
-      din[o] = from_f<T>(on ? gv : 0.f);
+      din[o] = from_f<T>(q == arg ? gv : 0.f);
     }
   }
 }
@@ -856,25 +997,36 @@ int launch_patch(const ConvArgs& a, int nph, hipStream_t st) {
   unsigned tiles = 0;
   for (int i = 0; i < nph; ++i)
     tiles = std::max(tiles, (unsigned)(a.g[i].N * ((a.g[i].OH + 15) / 16) * ((a.g[i].OW + 15) / 16)));
+  const unsigned gx = nph == 1 ? tiles : ((tiles + 7) / 8) * 32;  // phases: 4 x 8-tile groups
   const int CO = a.g[0].CO;
   const int nt = std::min(4, (CO + 15) / 16);
-  const dim3 grid(tiles, (unsigned)((CO + 16 * nt - 1) / (16 * nt)), nph);
-#define SPECENH_PATCH(NT) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC>), grid, dim3(256), 0, st, a)
-  if (nt == 1) SPECENH_PATCH(1);
-  else if (nt == 2) SPECENH_PATCH(2);
-  else if (nt == 3) SPECENH_PATCH(3);
-  else SPECENH_PATCH(4);
+  const dim3 grid(gx, (unsigned)((CO + 16 * nt - 1) / (16 * nt)), 1);
+#define SPECENH_PATCH(NT, P) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC, P>), grid, dim3(256), 0, st, a)
+  if (a.pool) {
+    if (nt == 1) SPECENH_PATCH(1, true);
+    else if (nt == 2) SPECENH_PATCH(2, true);
+    else if (nt == 3) SPECENH_PATCH(3, true);
+    else SPECENH_PATCH(4, true);
+  } else {
+    if (nt == 1) SPECENH_PATCH(1, false);
+    else if (nt == 2) SPECENH_PATCH(2, false);
+    else if (nt == 3) SPECENH_PATCH(3, false);
+    else SPECENH_PATCH(4, false);
+  }
 #undef SPECENH_PATCH
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "conv launch");
 }
 
 // which LDS-patch chunking applies (0 = none: use the generic gather kernel)
 int patch_cc(const ConvArgs& a, int nph) {
+  if (nph != 1 && nph != 4) return 0;
   for (int i = 0; i < nph; ++i) {
     const Geo& g = a.g[i];
     if (g.stride != 1 || g.KH > 5 || g.KW > 5 || g.KH * g.KW > 32) return 0;
+    if (a.out_f32 && a.g[0].CO > 32) return 0;  // fp32 output tile must fit the LDS union
   }
   const int C = a.g[0].C;
+  if (C % 64 == 0) return 64;
   if (C % 32 == 0) return 32;
   if (C == 16) return 16;
   if (C == 1) return 1;
@@ -886,6 +1038,7 @@ int launch_fwd(const ConvArgs& a, int nph, hipStream_t st) {
   if constexpr (!__is_same(T, float)) {
     if (!getenv_flag("SPECENH_CONV_NO_PATCH")) {
       switch (patch_cc(a, nph)) {
+        case 64: return launch_patch<T, 64>(a, nph, st);
         case 32: return launch_patch<T, 32>(a, nph, st);
         case 16: return launch_patch<T, 16>(a, nph, st);
         case 1: return launch_patch<T, 1>(a, nph, st);
@@ -893,6 +1046,7 @@ int launch_fwd(const ConvArgs& a, int nph, hipStream_t st) {
       }
     }
   }
+  if (a.pool) return set_error(SPECENH_EUNSUPPORTED, "fused max-pool needs the LDS-patch path");
   int maxM = 0;
   for (int i = 0; i < nph; ++i) maxM = std::max(maxM, a.g[i].N * a.g[i].OH * a.g[i].OW);
   const int CO = a.g[0].CO;
@@ -963,7 +1117,7 @@ extern "C" {
 int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, const void* w_gemm,
                    int KH, int KW, int CO, const float* bias, int stride, int pad_t, int pad_l,
                    int in_dil, int OH, int OW, int act, const void* mask, float* logits,
-                   void* out, int out_f32, void* stream) {
+                   void* out, int out_f32, int pool2, unsigned char* argmax, void* stream) {
   if (int e = check_sizes(N, IH, IW, C, OH, OW, CO)) return e;
   if (KH <= 0 || KW <= 0 || stride <= 0 || in_dil <= 0)
     return set_error(SPECENH_EINVAL, "bad convolution geometry");
@@ -975,7 +1129,11 @@ int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, cons
   if (int e = plan_phases(N, IH, IW, C, CO, KH, KW, stride, pad_t, pad_l, in_dil, OH, OW, a.g, &nph))
     return e;
   a.in = in; a.w = w_gemm; a.bias = bias; a.out = out; a.out_f32 = out_f32;
-  a.mask = mask; a.act = act; a.logits = logits;
+  a.mask = mask; a.act = act; a.logits = logits; a.nph = nph;
+  a.pool = pool2 ? 1 : 0;
+  a.argmax = argmax;
+  if (a.pool && (nph != 1 || (OH & 1) || (OW & 1) || mask || logits || out_f32))
+    return set_error(SPECENH_EUNSUPPORTED, "fused max-pool: plain conv with even output only");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == SPECENH_DTYPE_F32) return launch_fwd<float>(a, nph, st);
   if (dtype == SPECENH_DTYPE_BF16) return launch_fwd<__bf16>(a, nph, st);
@@ -1036,7 +1194,7 @@ int specenh_maxpool2_fwd(int dtype, const void* in, int N, int H, int W, int C, 
 }
 
 int specenh_maxpool2_bwd(int dtype, const void* dout, const unsigned char* argmax,
-                         const void* relu_in, int N, int H, int W, int C, void* din,
+                         const void* pooled, int N, int H, int W, int C, void* din,
                          void* stream) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || (H & 1) || (W & 1))
     return set_error(SPECENH_EINVAL, "maxpool2 needs even H, W");
@@ -1045,14 +1203,14 @@ int specenh_maxpool2_bwd(int dtype, const void* dout, const unsigned char* argma
   hipStream_t st = (hipStream_t)stream;
   if (dtype == 0)
     hipLaunchKernelGGL(maxpool2_bwd_kernel<float>, dim3(grid1d(n)), dim3(256), 0, st,
-                       (const float*)dout, argmax, (const float*)relu_in, N, H, W, C, (float*)din);
+                       (const float*)dout, argmax, (const float*)pooled, N, H, W, C, (float*)din);
   else if (dtype == 1)
     hipLaunchKernelGGL(maxpool2_bwd_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st,
-                       (const __bf16*)dout, argmax, (const __bf16*)relu_in, N, H, W, C,
+                       (const __bf16*)dout, argmax, (const __bf16*)pooled, N, H, W, C,
                        (__bf16*)din);
   else if (dtype == 2)
     hipLaunchKernelGGL(maxpool2_bwd_kernel<_Float16>, dim3(grid1d(n)), dim3(256), 0, st,
-                       (const _Float16*)dout, argmax, (const _Float16*)relu_in, N, H, W, C,
+                       (const _Float16*)dout, argmax, (const _Float16*)pooled, N, H, W, C,
                        (_Float16*)din);
   else
     return set_error(SPECENH_EINVAL, "dtype");

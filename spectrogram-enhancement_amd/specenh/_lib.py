@@ -60,7 +60,7 @@ SIGNATURES = {
                                   _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_void_p,
                                   _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
                                   _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int,
-                                  _c.c_void_p]),
+                                  _c.c_int, _c.c_void_p, _c.c_void_p]),
     "specenh_conv2d_wgrad": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
                                         _c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
                                         _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int,

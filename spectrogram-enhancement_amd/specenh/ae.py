@@ -145,6 +145,11 @@ class AutoencoderEngine:
         # flipped/transposed copies for the input gradients (compute dtype)
         self.w_d = {i: torch.zeros(op.n_w, dtype=self.tdt, device=dev)
                     for i, op in enumerate(self.ops) if isinstance(op, ConvOp) and i > 0}
+        # conv i followed by MaxPooling2D: one launch (bf16/f16 LDS-patch kernel)
+        self.fused = {i for i, op in enumerate(self.ops[:-1])
+                      if self.dt != F32 and isinstance(op, ConvOp) and op.kind == "conv"
+                      and isinstance(self.ops[i + 1], PoolOp) and op.k <= 5
+                      and (op.cin in (1, 16) or op.cin % 32 == 0)}
         self.t = 0  # Adam iterations
         self._bufs = {}
         self._loss = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -199,7 +204,8 @@ class AutoencoderEngine:
             H, W, C = shp[i]
             last = i == len(self.ops)
             dtype = torch.float32 if (last and not train) else self.tdt
-            b["h"][i] = torch.empty((N, H, W, C), dtype=dtype, device=dev)
+            if (i - 1) not in self.fused:  # a fused conv's full-resolution output is never stored
+                b["h"][i] = torch.empty((N, H, W, C), dtype=dtype, device=dev)
             if train:
                 b["d"][i] = torch.empty((N, H, W, C), dtype=self.tdt, device=dev)
         for i, op in enumerate(self.ops):
@@ -271,14 +277,14 @@ class AutoencoderEngine:
 
     # ------------------------------------------------------------------ passes
     def _conv(self, op, x, out, *, weights, geom, act, mask=None, logits=None, bias=True,
-              out_shape=None, cin=None, cout=None):
+              out_shape=None, cin=None, cout=None, pool=False, argmax=None):
         N, IH, IW, C = x.shape
         OH, OW = out_shape
         s, pt, pl, dil = geom
         _lib.check(self.L.specenh_conv2d(
             self.dt, _vp(x), N, IH, IW, C, weights, op.k, op.k, cout, self._bptr(op) if bias
             else ctypes.c_void_p(0), s, pt, pl, dil, OH, OW, ACT[act], _vp(mask), _vp(logits),
-            _vp(out), int(out.dtype == torch.float32), self._stream()),
+            _vp(out), int(out.dtype == torch.float32), int(pool), _vp(argmax), self._stream()),
             "conv2d")
 
     def forward(self, x, train=False, timing=None):
@@ -295,8 +301,26 @@ class AutoencoderEngine:
             self._last_train_N = N
         st = self._stream()
         n_ops = len(self.ops)
+        skip = False
         for i, op in enumerate(self.ops):
+            if skip:  # the pool that was fused into the previous conv
+                skip = False
+                continue
             hin, hout = b["h"][i], b["h"][i + 1]
+            if i in self.fused:
+                if timing is not None:
+                    ev = (torch.cuda.Event(enable_timing=True),
+                          torch.cuda.Event(enable_timing=True))
+                    ev[0].record(torch.cuda.current_stream(self.device))
+                _, H, W, _ = hin.shape
+                self._conv(op, hin, b["h"][i + 2], weights=self._wptr(op), geom=op.fwd_geom(),
+                           act=op.act, out_shape=(H, W), cout=op.cout, pool=True,
+                           argmax=b["am"][i + 1] if train else None)
+                if timing is not None:
+                    ev[1].record(torch.cuda.current_stream(self.device))
+                    timing.append(ev)
+                skip = True
+                continue
             if isinstance(op, PoolOp):
                 _, H, W, C = hin.shape
                 am = b["am"][i]
@@ -355,14 +379,16 @@ class AutoencoderEngine:
             d_out = b["d"][i + 1]
             hin = b["h"][i]
             prev = self.ops[i - 1] if i > 0 else None
-            relu_mask = hin if (isinstance(prev, ConvOp) and prev.act == "relu") else None
+            prev_relu = isinstance(prev, ConvOp) and prev.act == "relu"
+            relu_mask = hin if prev_relu else None
             if isinstance(op, PoolOp):
                 if i == 0:
                     continue  # nothing upstream needs the gradient
-                _, H, W, C = hin.shape
-                _lib.check(self.L.specenh_maxpool2_bwd(self.dt, _vp(d_out), _vp(b["am"][i]),
-                                                       _vp(relu_mask), N, H, W, C,
-                                                       _vp(b["d"][i]), st), "maxpool2_bwd")
+                _, H, W, C = d_out.shape
+                # ReLU mask of the pool's input at its argmax == (pooled output > 0)
+                _lib.check(self.L.specenh_maxpool2_bwd(
+                    self.dt, _vp(d_out), _vp(b["am"][i]), _vp(b["h"][i + 1] if prev_relu else None),
+                    N, 2 * H, 2 * W, C, _vp(b["d"][i]), st), "maxpool2_bwd")
                 continue
             if op.act == "sigmoid" and i != n_ops - 1:
                 raise NotImplementedError("sigmoid activation before the last layer")

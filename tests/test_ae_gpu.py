@@ -377,7 +377,7 @@ def test_errors(gpu_device):
         _lib.check(L.specenh_maxpool2_fwd(0, None, 1, 3, 4, 1, None, None, None))
     with pytest.raises(ValueError):
         _lib.check(L.specenh_conv2d(0, None, 1, 4, 4, 1, None, 3, 3, 1, None, 1, 1, 1, 1, 4, 4,
-                                    0, None, None, None, 1, None))
+                                    0, None, None, None, 1, 0, None, None))
 
 
 def test_backward_is_bitwise_deterministic(gpu_device):
@@ -403,3 +403,26 @@ def test_reference_model_fp16_forward_psnr(gpu_device):
     ref, _ = ref_forward(ops, params, x)
     got = eng.forward(upload(eng, x), train=False).cpu().numpy()
     assert psnr(got, ref) >= PSNR_MIN
+
+
+@pytest.mark.parametrize("dtype", ["mixed_bfloat16", "float16"])
+def test_fused_conv_pool_is_bitwise_identical_to_unfused(gpu_device, dtype):
+    """Conv2D + MaxPooling2D in one launch (pool taken in the conv's registers) gives the
+    same forward output and the same gradients as the two launches."""
+    ops = ref_model_ops()
+    fused, _ = make(ops, (64, 64, 1), dtype=dtype, seed=41)
+    plain, _ = make(ops, (64, 64, 1), dtype=dtype, seed=41)
+    assert fused.fused == {0, 2, 4}
+    plain.fused = set()
+    rng = np.random.default_rng(11)
+    x = rng.uniform(0, 1, (6, 64, 64, 1)).astype(np.float32)
+    y = rng.uniform(0, 1, (6, 64, 64, 1)).astype(np.float32)
+    outs, grads = [], []
+    for eng in (fused, plain):
+        outs.append(eng.forward(upload(eng, x)).clone())
+        eng.forward(upload(eng, x), train=True)
+        eng.loss_and_grad(upload(eng, y))
+        eng.backward()
+        grads.append(eng.g.clone())
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(grads[0], grads[1])

@@ -146,7 +146,8 @@ class AutoencoderEngine:
         self.w_d = {i: torch.zeros(op.n_w, dtype=self.tdt, device=dev)
                     for i, op in enumerate(self.ops) if isinstance(op, ConvOp) and i > 0}
         # conv i followed by MaxPooling2D: one launch (bf16/f16 LDS-patch kernel)
-        self.fused = {i for i, op in enumerate(self.ops[:-1])
+        # (not when the pool is the model's output: that buffer is fp32 for inference)
+        self.fused = {i for i, op in enumerate(self.ops[:-2])
                       if self.dt != F32 and isinstance(op, ConvOp) and op.kind == "conv"
                       and isinstance(self.ops[i + 1], PoolOp) and op.k <= 5
                       and (op.cin in (1, 16) or op.cin % 32 == 0)}

@@ -251,6 +251,8 @@ struct ConvArgs {
   int nph;            // output phases (1, or in_dil^2)
   int pool;           // 1: fused 2x2/2 max-pool, out is [N][OH/2][OW/2][CO]
   unsigned char* argmax;  // pooled argmax (dy*2+dx), or null
+  // LDS-patch kernel, all phases in one workgroup: union patch origin/extent
+  int ph_shared, upt, upl, PH, PW;
 };
 
 // ------------------------------------------------------------------ forward / dgrad
@@ -404,282 +406,246 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   return v;
 }
 
-template <typename T, int NT, int CC>
-struct PatchSmem {
-  static constexpr int PMAX = 20;
-  static constexpr int PATCH = PMAX * PMAX * Patch<CC>::PST * (int)sizeof(T);
-  // plain output tile [256 px][16*NT]: fp32 only when NT <= 2 (patch_cc rejects CO > 32)
-  static constexpr int OUT = 256 * 16 * NT * (NT <= 2 ? 4 : (int)sizeof(T));
-  static constexpr int BYTES = PATCH > OUT ? PATCH : OUT;
-};
-
 template <typename T, int NT, int CC, bool POOL>
 __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
   constexpr int TILE = 16, PMAX = 20;
   constexpr int PST = Patch<CC>::PST;
   constexpr int MT = 4;  // output rows per wave
-  constexpr int COT = 16 * NT;
-  __shared__ __attribute__((aligned(16))) char smem[PatchSmem<T, NT, CC>::BYTES];
-  __shared__ int sTap[32];  // patch offset of tap t (elements), -1 past the last tap
-  __shared__ int sCol[32];  // weight column of tap t at ci = 0
-  T* sP = reinterpret_cast<T*>(smem);
+  __shared__ __attribute__((aligned(16))) T sP[PMAX * PMAX * PST];
+  __shared__ int sTap[MAXPH][32];  // patch offset of tap t (elements), -1 past the last tap
+  __shared__ int sCol[MAXPH][32];  // weight column of tap t at ci = 0
 
-  // ---- which tile and phase (the phases of a tile share an XCD) ----
-  int phase = 0, tile = blockIdx.x;
-  if (a.nph > 1) {
-    const int r = blockIdx.x & 31;
-    phase = r >> 3;
-    tile = (blockIdx.x >> 5) * 8 + (r & 7);
-    if (phase >= a.nph) return;
-  }
-  const Geo& g = a.g[phase];
-  const int ntx = (g.OW + TILE - 1) / TILE, nty = (g.OH + TILE - 1) / TILE;
-  if (tile >= g.N * nty * ntx) return;
-  const int n = tile / (nty * ntx);
-  const int trem = tile - n * (nty * ntx);
+  // ---- phases of this workgroup: all of them over one shared patch, or blockIdx.z ----
+  const bool shared = a.ph_shared != 0;
+  const int ph_lo = shared ? 0 : (int)blockIdx.z, ph_hi = shared ? a.nph : ph_lo + 1;
+  const Geo& g0 = a.g[ph_lo];
+  const int ntx = (g0.OW + TILE - 1) / TILE, nty = (g0.OH + TILE - 1) / TILE;
+  if ((int)blockIdx.x >= g0.N * nty * ntx) return;
+  const int n = blockIdx.x / (nty * ntx);
+  const int trem = blockIdx.x - n * (nty * ntx);
   const int ty = trem / ntx, tx = trem - (trem / ntx) * ntx;
   const int oy0 = ty * TILE, ox0 = tx * TILE;
-  const int iy0 = oy0 - g.pad_t, ix0 = ox0 - g.pad_l;
-  const int PW = TILE + g.KW - 1, PH = TILE + g.KH - 1;
-  const int ntap = g.KH * g.KW;
-  const int n0 = blockIdx.y * COT;
+  const int upt = shared ? a.upt : g0.pad_t, upl = shared ? a.upl : g0.pad_l;
+  const int PH = shared ? a.PH : TILE + g0.KH - 1, PW = shared ? a.PW : TILE + g0.KW - 1;
+  const int iy0 = oy0 - upt, ix0 = ox0 - upl;
+  const int n0 = blockIdx.y * 16 * NT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kgrp = lane >> 4, px = lane & 15;
   const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
   const T* __restrict__ W = reinterpret_cast<const T*>(a.w);
 
-  if (tid < 32) {
-    const int jy = tid / g.KW, jx = tid - (tid / g.KW) * g.KW;
-    sTap[tid] = tid < ntap ? (jy * PW + jx) * PST : -1;
-    sCol[tid] = tid < ntap ? ((g.ky0 + g.kstep * jy) * g.KWf + g.kx0 + g.kstep * jx) * g.C : 0;
+  if (tid < 32 * (ph_hi - ph_lo)) {
+    const int p = ph_lo + (tid >> 5), t = tid & 31;
+    const Geo& g = a.g[p];
+    const int jy = t / g.KW, jx = t - (t / g.KW) * g.KW;
+    const int dy = upt - g.pad_t, dx = upl - g.pad_l;  // this phase's shift in the patch
+    sTap[p][t] = t < g.KH * g.KW ? ((jy + dy) * PW + jx + dx) * PST : -1;
+    sCol[p][t] = t < g.KH * g.KW ? ((g.ky0 + g.kstep * jy) * g.KWf + g.kx0 + g.kstep * jx) * g.C : 0;
   }
 
-  f32x4 acc[MT][NT];
+  int rbase[MT];  // this lane's pixel (row i of the wave, column px) in the patch
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < MT; ++i) rbase[i] = ((wave * MT + i) * PW + px) * PST;
 
-  int rbase[MT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i) rbase[i] = ((wave * MT + i) * PW + (lane & 15)) * PST;
-  const int kgrp = lane >> 4;
-
-  const int nchunk = CC == 1 ? 1 : g.C / CC;
-  for (int c = 0; c < nchunk; ++c) {
-    // ---- stage the patch of channel chunk c ----
+  auto stage = [&](int c) {
     if constexpr (CC == 1) {
       for (int e = tid; e < PH * PW; e += 256) {
-        const int py = e / PW, px = e - (e / PW) * PW;
-        const int iy = iy0 + py, ix = ix0 + px;
-        const bool ok = (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW;
-        const T v = in[ok ? (n * g.IH + iy) * g.IW + ix : 0];
+        const int py = e / PW, pxx = e - (e / PW) * PW;
+        const int iy = iy0 + py, ix = ix0 + pxx;
+        const bool ok = (unsigned)iy < (unsigned)g0.IH && (unsigned)ix < (unsigned)g0.IW;
+        const T v = in[ok ? (n * g0.IH + iy) * g0.IW + ix : 0];
         sP[e] = ok ? v : from_f<T>(0.f);
       }
     } else {
       constexpr int GP = CC / 8;  // 8-channel groups per pixel
       for (int e = tid; e < PH * PW * GP; e += 256) {
         const int pix = e / GP, cg = e - (e / GP) * GP;
-        const int py = pix / PW, px = pix - (pix / PW) * PW;
-        const int iy = iy0 + py, ix = ix0 + px;
-        const bool ok = (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW;
-        V8<T> v = ld8(in + (ok ? ((n * g.IH + iy) * g.IW + ix) * g.C + c * CC + 8 * cg : 0));
-        if (!ok) zero8(v);
-        st8(sP + pix * PST + 8 * cg, v);
+        const int py = pix / PW, pxx = pix - (pix / PW) * PW;
+        const int iy = iy0 + py, ix = ix0 + pxx;
+        const bool ok = (unsigned)iy < (unsigned)g0.IH && (unsigned)ix < (unsigned)g0.IW;
+        const uint4 v = ok ? *reinterpret_cast<const uint4*>(
+                                 in + ((n * g0.IH + iy) * g0.IW + ix) * g0.C + c * CC + 8 * cg)
+                           : uint4{0u, 0u, 0u, 0u};
+        *reinterpret_cast<uint4*>(sP + pix * PST + 8 * cg) = v;
       }
     }
-    lds_sync();
+  };
 
-    // ---- k-steps: one MFMA K=32 slab each ----
-    constexpr int SUB = CC >= 32 ? CC / 32 : 1;  // 32-channel slabs per tap
-    const int nsteps = CC >= 32 ? ntap * SUB : (CC == 16 ? (ntap + 1) / 2 : 1);
-    auto load_b = [&](int s, V8<T> (&b)[NT]) {
+  const int nchunk = CC == 1 ? 1 : g0.C / CC;
+  for (int p = ph_lo; p < ph_hi; ++p) {
+    const Geo& g = a.g[p];
+    const int ntap = g.KH * g.KW;
+    f32x4 acc[MT][NT];
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int co = n0 + 16 * j + (lane & 15);
-        zero8(b[j]);
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int c = 0; c < nchunk; ++c) {
+      if (p == ph_lo || nchunk > 1) {
+        if (c > 0 || p > ph_lo) lds_sync();  // previous chunk's fragment reads are done
+        stage(c);
+        lds_sync();
+      }
+      // ---- k-steps: one MFMA K=32 slab each; weights are the A operand (rows = output
+      // channels), the patch the B operand (columns = pixels): D[channel][pixel] ----
+      constexpr int SUB = CC >= 32 ? CC / 32 : 1;  // 32-channel slabs per tap
+      const int nsteps = CC >= 32 ? ntap * SUB : (CC == 16 ? (ntap + 1) / 2 : 1);
+      auto load_w = [&](int st, V8<T> (&b)[NT]) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int co = n0 + 16 * j + px;
+          zero8(b[j]);
+          if constexpr (CC >= 32) {
+            const int t = st / SUB, h = st - (st / SUB) * SUB;
+            if (co < g.CO) b[j] = ld8(W + co * g.Kf + sCol[p][t] + c * CC + 32 * h + 8 * kgrp);
+          } else if constexpr (CC == 16) {
+            const int t = 2 * st + (kgrp >> 1);
+            if (co < g.CO && t < ntap) b[j] = ld8(W + co * g.Kf + sCol[p][t] + 8 * (kgrp & 1));
+          } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const int t = 8 * kgrp + q;
+              if (co < g.CO && t < ntap) set_elem(b[j], q, W[co * g.Kf + sCol[p][t]]);
+            }
+          }
+        }
+      };
+      V8<T> wcur[NT], wnxt[NT];
+      load_w(0, wcur);
+      for (int st = 0; st < nsteps; ++st) {
+        if (st + 1 < nsteps) load_w(st + 1, wnxt);
+        int aoff = 0;
+        bool aon = true;
         if constexpr (CC >= 32) {
-          const int t = s / SUB, h = s - (s / SUB) * SUB;
-          if (co < g.CO) b[j] = ld8(W + co * g.Kf + sCol[t] + c * CC + 32 * h + 8 * kgrp);
+          const int t = st / SUB, h = st - (st / SUB) * SUB;
+          aoff = sTap[p][t] + 32 * h + 8 * kgrp;
         } else if constexpr (CC == 16) {
-          const int t = 2 * s + (kgrp >> 1);
-          if (co < g.CO && t < ntap) b[j] = ld8(W + co * g.Kf + sCol[t] + 8 * (kgrp & 1));
-        } else {
+          const int t = 2 * st + (kgrp >> 1);
+          aon = t < ntap;
+          aoff = (aon ? sTap[p][t] : 0) + 8 * (kgrp & 1);
+        }
 #pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const int t = 8 * kgrp + q;
-            if (co < g.CO && t < ntap) set_elem(b[j], q, W[co * g.Kf + sCol[t]]);
+        for (int i = 0; i < MT; ++i) {
+          V8<T> pv;
+          if constexpr (CC == 1) {
+            zero8(pv);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const int off = sTap[p][8 * kgrp + q];
+              if (off >= 0) set_elem(pv, q, sP[rbase[i] + off]);
+            }
+          } else {
+            const uint4 u = *reinterpret_cast<const uint4*>(sP + rbase[i] + aoff);  // ds_read_b128
+            pv.w[0] = u.x; pv.w[1] = u.y; pv.w[2] = u.z; pv.w[3] = u.w;
+            if (!aon) zero8(pv);
+          }
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wcur[j], pv, acc[i][j]);
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) wcur[j] = wnxt[j];
+      }
+    }
+
+    // ---- epilogue: lane holds channels n0 + 16j + 4*kgrp + r (r = 0..3) of output
+    // pixel (row oy0 + 4*wave + i, column ox0 + px) — 4 consecutive NHWC channels ----
+    float bv[NT][4];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ch = n0 + 16 * j + 4 * kgrp + r;
+        bv[j][r] = (a.bias && ch < g.CO) ? a.bias[ch] : 0.f;
+      }
+    const int ox = ox0 + px;
+    if constexpr (POOL) {
+      // 2x2 windows: rows (2ip, 2ip+1) of this wave in registers, columns (px, px^1) across
+      // the lane pair; values compared as stored (rounded to T), first max wins
+      const int PHo = g.OH / 2, PWo = g.OW / 2;
+#pragma unroll
+      for (int ip = 0; ip < 2; ++ip) {
+        const int oy = oy0 + wave * MT + 2 * ip;
+        const int py = oy / 2, pxo = ox / 2;
+        const bool store = (px & 1) == 0 && py < PHo && pxo < PWo;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          float best[4];
+          unsigned arg4 = 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v00 = to_f(from_f<T>(apply_act(acc[2 * ip][j][r] + bv[j][r], a.act)));
+            const float v10 = to_f(from_f<T>(apply_act(acc[2 * ip + 1][j][r] + bv[j][r], a.act)));
+            const float v01 = __shfl_xor(v00, 1);
+            const float v11 = __shfl_xor(v10, 1);
+            float b = v00;
+            unsigned q = 0;
+            if (v01 > b) { b = v01; q = 1; }
+            if (v10 > b) { b = v10; q = 2; }
+            if (v11 > b) { b = v11; q = 3; }
+            best[r] = b;
+            arg4 |= q << (8 * r);
+          }
+          const int ch0 = n0 + 16 * j + 4 * kgrp;
+          if (store && ch0 < g.CO) {
+            const long long o = (((long long)n * PHo + py) * PWo + pxo) * g.CO + ch0;
+            T* dst = reinterpret_cast<T*>(a.out) + o;
+            if ((g.CO & 3) == 0) {
+              V8<T> pk;
+              zero8(pk);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) set_elem(pk, r, from_f<T>(best[r]));
+              *reinterpret_cast<uint2*>(dst) = uint2{pk.w[0], pk.w[1]};
+              if (a.argmax) *reinterpret_cast<unsigned*>(a.argmax + o) = arg4;
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (ch0 + r < g.CO) {
+                  dst[r] = from_f<T>(best[r]);
+                  if (a.argmax) a.argmax[o + r] = (unsigned char)(arg4 >> (8 * r));
+                }
+            }
           }
         }
       }
-    };
-    V8<T> bcur[NT], bnxt[NT];
-    load_b(0, bcur);
-    for (int s = 0; s < nsteps; ++s) {
-      if (s + 1 < nsteps) load_b(s + 1, bnxt);
-      int aoff = 0;
-      bool aon = true;
-      if constexpr (CC >= 32) {
-        const int t = s / SUB, h = s - (s / SUB) * SUB;
-        aoff = sTap[t] + 32 * h + 8 * kgrp;
-      } else if constexpr (CC == 16) {
-        const int t = 2 * s + (kgrp >> 1);
-        aon = t < ntap;
-        aoff = (aon ? sTap[t] : 0) + 8 * (kgrp & 1);
-      }
+    } else {
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
-        V8<T> av;
-        if constexpr (CC == 1) {
-          zero8(av);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const int off = sTap[8 * kgrp + q];
-            if (off >= 0) set_elem(av, q, sP[rbase[i] + off]);
-          }
-        } else {
-          av = *reinterpret_cast<const V8<T>*>(sP + rbase[i] + aoff);
-          if (!aon) zero8(av);
-        }
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(av, bcur[j], acc[i][j]);
-      }
-#pragma unroll
-      for (int j = 0; j < NT; ++j) bcur[j] = bnxt[j];
-    }
-    lds_sync();  // the patch is overwritten by the next chunk / the output tile
-  }
-
-  // ---- epilogue. D element (i, j, reg): output row oy0 + 4*wave + i, column
-  // ox0 + 4*(lane>>4) + reg, channel n0 + 16*j + (lane&15) ----
-  const int colv = (int)min(COT, g.CO - n0);  // valid channels of this tile
-  if (a.mask || a.logits) {
-    // training paths (dgrad with a ReLU mask / last layer's logits): direct stores
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      const int oy = oy0 + wave * MT + i;
-      if (oy >= g.OH) continue;
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int ox = ox0 + 4 * (lane >> 4) + reg;
-        if (ox >= g.OW) continue;
+        const int oy = oy0 + wave * MT + i;
+        if (oy >= g.OH || ox >= g.OW) continue;
         const long long pix =
             ((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0;
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
-          const int col = n0 + 16 * j + (lane & 15);
-          if (col >= g.CO) continue;
-          const long long idx = pix * g.CO + col;
-          float v = acc[i][j][reg] + (a.bias ? a.bias[col] : 0.f);
-          if (a.logits) a.logits[idx] = v;
-          if (a.mask && !(to_f(reinterpret_cast<const T*>(a.mask)[idx]) > 0.f)) v = 0.f;
-          v = apply_act(v, a.act);
-          if (a.out_f32) reinterpret_cast<float*>(a.out)[idx] = v;
-          else reinterpret_cast<T*>(a.out)[idx] = from_f<T>(v);
-        }
-      }
-    }
-    return;
-  }
-
-  if constexpr (POOL) {
-    // 2x2 windows: rows (2*ip, 2*ip+1) of this wave, columns (2*rp, 2*rp+1) of this lane
-    T* sO = sP;                                                   // [64 px][COT]
-    unsigned char* sAm = reinterpret_cast<unsigned char*>(smem) + 64 * COT * sizeof(T);
+          const int ch0 = n0 + 16 * j + 4 * kgrp;
+          if (ch0 >= g.CO) continue;
+          const long long o = pix * g.CO + ch0;
+          float v[4];
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int ch = 16 * j + (lane & 15);
-      const float bv = (a.bias && n0 + ch < g.CO) ? a.bias[n0 + ch] : 0.f;
+          for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv[j][r];
+          if (a.mask || a.logits || (g.CO & 3) != 0) {
 #pragma unroll
-      for (int ip = 0; ip < 2; ++ip)
+            for (int r = 0; r < 4; ++r) {
+              if (ch0 + r >= g.CO) continue;
+              float x = v[r];
+              if (a.logits) a.logits[o + r] = x;
+              if (a.mask && !(to_f(reinterpret_cast<const T*>(a.mask)[o + r]) > 0.f)) x = 0.f;
+              x = apply_act(x, a.act);
+              if (a.out_f32) reinterpret_cast<float*>(a.out)[o + r] = x;
+              else reinterpret_cast<T*>(a.out)[o + r] = from_f<T>(x);
+            }
+          } else if (a.out_f32) {
+            *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.out) + o) =
+                float4{apply_act(v[0], a.act), apply_act(v[1], a.act), apply_act(v[2], a.act),
+                       apply_act(v[3], a.act)};
+          } else {
+            V8<T> pk;
+            zero8(pk);
 #pragma unroll
-        for (int rp = 0; rp < 2; ++rp) {
-          // compare the values the layer would store (rounded to T), first max wins: the
-          // same argmax as MaxPooling2D on the stored activation
-          float best = to_f(from_f<T>(apply_act(acc[2 * ip][j][2 * rp] + bv, a.act)));
-          int arg = 0;
-#pragma unroll
-          for (int q = 1; q < 4; ++q) {
-            const float v =
-                to_f(from_f<T>(apply_act(acc[2 * ip + (q >> 1)][j][2 * rp + (q & 1)] + bv, a.act)));
-            if (v > best) { best = v; arg = q; }
+            for (int r = 0; r < 4; ++r) set_elem(pk, r, from_f<T>(apply_act(v[r], a.act)));
+            *reinterpret_cast<uint2*>(reinterpret_cast<T*>(a.out) + o) = uint2{pk.w[0], pk.w[1]};
           }
-          const int pp = (2 * wave + ip) * 8 + 2 * (lane >> 4) + rp;  // pooled pixel in 8x8
-          sO[pp * COT + ch] = from_f<T>(best);
-          sAm[pp * COT + ch] = (unsigned char)arg;
         }
-    }
-    lds_sync();
-    const int PHo = g.OH / 2, PWo = g.OW / 2;
-    const int py0 = oy0 / 2, px0 = ox0 / 2;
-    if (colv == COT && (g.CO & 7) == 0) {
-      constexpr int GPP = COT / 8;  // 16-byte chunks per pooled pixel
-      for (int e = tid; e < 64 * GPP; e += 256) {
-        const int pp = e / GPP, cg = e - (e / GPP) * GPP;
-        const int py = py0 + pp / 8, px = px0 + (pp & 7);
-        if (py >= PHo || px >= PWo) continue;
-        const long long o = (((long long)n * PHo + py) * PWo + px) * g.CO + n0 + 8 * cg;
-        *reinterpret_cast<uint4*>(reinterpret_cast<T*>(a.out) + o) =
-            *reinterpret_cast<const uint4*>(sO + pp * COT + 8 * cg);
-        if (a.argmax)
-          *reinterpret_cast<uint2*>(a.argmax + o) =
-              *reinterpret_cast<const uint2*>(sAm + pp * COT + 8 * cg);
-      }
-    } else {
-      for (int e = tid; e < 64 * COT; e += 256) {
-        const int pp = e / COT, ch = e - (e / COT) * COT;
-        const int py = py0 + pp / 8, px = px0 + (pp & 7);
-        if (ch >= colv || py >= PHo || px >= PWo) continue;
-        const long long o = (((long long)n * PHo + py) * PWo + px) * g.CO + n0 + ch;
-        reinterpret_cast<T*>(a.out)[o] = sO[pp * COT + ch];
-        if (a.argmax) a.argmax[o] = sAm[pp * COT + ch];
-      }
-    }
-    return;
-  } else {
-    // plain tile [256 px][COT] through LDS, in the output dtype
-    const bool f32o = a.out_f32 != 0;
-    float* sOf = reinterpret_cast<float*>(smem);
-    T* sOt = sP;
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int ch = 16 * j + (lane & 15);
-      const float bv = (a.bias && n0 + ch < g.CO) ? a.bias[n0 + ch] : 0.f;
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-          const int px = (wave * MT + i) * 16 + 4 * (lane >> 4) + reg;
-          const float v = apply_act(acc[i][j][reg] + bv, a.act);
-          if (f32o) sOf[px * COT + ch] = v;
-          else sOt[px * COT + ch] = from_f<T>(v);
-        }
-    }
-    lds_sync();
-    const int esz = f32o ? 4 : (int)sizeof(T);
-    const int cpc = 16 / esz;  // channels per 16-byte chunk
-    if (colv == COT && (g.CO % cpc) == 0) {
-      const int gpp = COT / cpc;
-      for (int e = tid; e < 256 * gpp; e += 256) {
-        const int px = e / gpp, cg = e - (e / gpp) * gpp;
-        const int oy = oy0 + px / 16, ox = ox0 + (px & 15);
-        if (oy >= g.OH || ox >= g.OW) continue;
-        const long long o =
-            (((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0) * g.CO +
-            n0 + cpc * cg;
-        const char* src = smem + ((long long)px * COT + cpc * cg) * esz;
-        char* dst = reinterpret_cast<char*>(a.out) + o * esz;
-        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
-      }
-    } else {
-      for (int e = tid; e < 256 * COT; e += 256) {
-        const int px = e / COT, ch = e - (e / COT) * COT;
-        const int oy = oy0 + px / 16, ox = ox0 + (px & 15);
-        if (ch >= colv || oy >= g.OH || ox >= g.OW) continue;
-        const long long o =
-            (((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0) * g.CO +
-            n0 + ch;
-        if (f32o) reinterpret_cast<float*>(a.out)[o] = sOf[px * COT + ch];
-        else reinterpret_cast<T*>(a.out)[o] = sOt[px * COT + ch];
       }
     }
   }
@@ -993,14 +959,40 @@ int check_sizes(long long N, long long IH, long long IW, long long C, long long 
 }
 
 template <typename T, int CC>
-int launch_patch(const ConvArgs& a, int nph, hipStream_t st) {
+int launch_patch(ConvArgs a, int nph, hipStream_t st) {
+  // all phases of a dilated conv in one workgroup when they share a tile grid and the
+  // input fits one channel chunk: one staged patch serves every phase, and the phases'
+  // interleaved output lines are completed by the same workgroup
+  a.ph_shared = 0;
+  const int nchunk = CC == 1 ? 1 : a.g[0].C / CC;
+  if (nph > 1 && nchunk == 1) {
+    bool same = true;
+    int upt = -1 << 20, upl = -1 << 20, lo_y = 1 << 20, hi_y = -(1 << 20), lo_x = 1 << 20,
+        hi_x = -(1 << 20);
+    for (int i = 0; i < nph; ++i) {
+      const Geo& g = a.g[i];
+      same = same && g.OH == a.g[0].OH && g.OW == a.g[0].OW;
+      upt = std::max(upt, g.pad_t);
+      upl = std::max(upl, g.pad_l);
+      lo_y = std::min(lo_y, -g.pad_t);
+      hi_y = std::max(hi_y, 15 - g.pad_t + g.KH - 1);
+      lo_x = std::min(lo_x, -g.pad_l);
+      hi_x = std::max(hi_x, 15 - g.pad_l + g.KW - 1);
+    }
+    if (same && hi_y - lo_y + 1 <= 20 && hi_x - lo_x + 1 <= 20) {
+      a.ph_shared = 1;
+      a.upt = upt;
+      a.upl = upl;
+      a.PH = hi_y - lo_y + 1;
+      a.PW = hi_x - lo_x + 1;
+    }
+  }
   unsigned tiles = 0;
   for (int i = 0; i < nph; ++i)
     tiles = std::max(tiles, (unsigned)(a.g[i].N * ((a.g[i].OH + 15) / 16) * ((a.g[i].OW + 15) / 16)));
-  const unsigned gx = nph == 1 ? tiles : ((tiles + 7) / 8) * 32;  // phases: 4 x 8-tile groups
   const int CO = a.g[0].CO;
   const int nt = std::min(4, (CO + 15) / 16);
-  const dim3 grid(gx, (unsigned)((CO + 16 * nt - 1) / (16 * nt)), 1);
+  const dim3 grid(tiles, (unsigned)((CO + 16 * nt - 1) / (16 * nt)), a.ph_shared ? 1 : nph);
 #define SPECENH_PATCH(NT, P) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC, P>), grid, dim3(256), 0, st, a)
   if (a.pool) {
     if (nt == 1) SPECENH_PATCH(1, true);
@@ -1023,7 +1015,6 @@ int patch_cc(const ConvArgs& a, int nph) {
   for (int i = 0; i < nph; ++i) {
     const Geo& g = a.g[i];
     if (g.stride != 1 || g.KH > 5 || g.KW > 5 || g.KH * g.KW > 32) return 0;
-    if (a.out_f32 && a.g[0].CO > 32) return 0;  // fp32 output tile must fit the LDS union
   }
   const int C = a.g[0].C;
   if (C % 64 == 0) return 64;

@@ -38,9 +38,14 @@ def main():
             ops += [ae.PoolOp(), ae.ConvOp("conv", cout, 16, 1, "relu")]
         eng = ae.AutoencoderEngine(ops, (H, H, cin), compute_dtype=a.dtype, device="cuda:0")
         rng = np.random.default_rng(0)
-        shape = (5, 5, cin, cout) if kind == "conv" else (5, 5, cout, cin)
-        eng.set_keras_weights([rng.uniform(-0.1, 0.1, shape).astype(np.float32),
-                               np.zeros(cout, np.float32)])
+        ws = []
+        for op in ops:
+            if isinstance(op, ae.ConvOp):
+                shape = ((op.k, op.k, op.cin, op.cout) if op.kind == "conv"
+                         else (op.k, op.k, op.cout, op.cin))
+                ws += [rng.uniform(-0.1, 0.1, shape).astype(np.float32),
+                       np.zeros(op.cout, np.float32)]
+        eng.set_keras_weights(ws)
         x = eng.to_compute(torch.rand(a.batch, H, H, cin, device="cuda:0"))
         for _ in range(3):
             eng.forward(x)

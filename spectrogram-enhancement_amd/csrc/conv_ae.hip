@@ -41,6 +41,10 @@
 
 namespace specenh {
 int set_error(int code, const std::string& msg);  // stft_psd.hip
+int launch_conv_narrow(int dtype, const void* in, int N, int IH, int IW, int C, const void* w,
+                       int KH, int KW, int CO, const float* bias, int pad_t, int pad_l, int OH,
+                       int OW, int act, void* out, int out_f32, float* logits, int pool,
+                       unsigned char* argmax, hipStream_t st);  // conv_narrow.hip
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -511,10 +515,22 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
           }
         }
       };
-      V8<T> wcur[NT], wnxt[NT];
-      load_w(0, wcur);
-      for (int st = 0; st < nsteps; ++st) {
-        if (st + 1 < nsteps) load_w(st + 1, wnxt);
+      // weight fragments PD k-steps ahead in a register ring: they come from L2, and one
+      // k-step of MFMA work (4*NT MFMAs, 64-256 cycles) does not cover that latency
+      constexpr int PD = NT >= 3 ? (CC == 64 ? 1 : 2) : (NT == 2 ? 4 : 8);
+      V8<T> wring[PD][NT];
+#pragma unroll
+      for (int u = 0; u < PD; ++u)
+        if (u < nsteps) load_w(u, wring[u]);
+      for (int s0 = 0; s0 < nsteps; s0 += PD)
+#pragma unroll
+      for (int u = 0; u < PD; ++u) {
+        const int st = s0 + u;
+        if (st >= nsteps) break;
+        V8<T> wcur[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) wcur[j] = wring[u][j];
+        if (st + PD < nsteps) load_w(st + PD, wring[u]);
         int aoff = 0;
         bool aon = true;
         if constexpr (CC >= 32) {
@@ -543,8 +559,6 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
 #pragma unroll
           for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wcur[j], pv, acc[i][j]);
         }
-#pragma unroll
-        for (int j = 0; j < NT; ++j) wcur[j] = wnxt[j];
       }
     }
 
@@ -1126,6 +1140,12 @@ int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, cons
   if (a.pool && (nph != 1 || (OH & 1) || (OW & 1) || mask || logits || out_f32))
     return set_error(SPECENH_EUNSUPPORTED, "fused max-pool: plain conv with even output only");
   hipStream_t st = (hipStream_t)stream;
+  // 1 input or 1 output channel: direct VALU convolution (conv_narrow.hip)
+  if (stride == 1 && in_dil == 1 && !mask && !getenv_flag("SPECENH_CONV_NO_NARROW")) {
+    const int r = launch_conv_narrow(dtype, in, N, IH, IW, C, w_gemm, KH, KW, CO, bias, pad_t,
+                                     pad_l, OH, OW, act, out, out_f32, logits, pool2, argmax, st);
+    if (r != 0) return r < 0 ? r : SPECENH_OK;
+  }
   if (dtype == SPECENH_DTYPE_F32) return launch_fwd<float>(a, nph, st);
   if (dtype == SPECENH_DTYPE_BF16) return launch_fwd<__bf16>(a, nph, st);
   return launch_fwd<_Float16>(a, nph, st);

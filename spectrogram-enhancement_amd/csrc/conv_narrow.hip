@@ -1,0 +1,446 @@
+// conv_narrow.hip — the autoencoder's narrow-channel convolutions on the VALU (gfx950).
+//
+// The first Conv2D of the reference model (1 -> 16 channels, VAE/manual_scan_3layers.py:187)
+// and the last one (16 -> 1, sigmoid, :199) have a GEMM dimension of 1: on the MFMA path
+// (conv_ae.hip) they fill 1/16 of a 16x16 tile and their fragments are gathered element by
+// element. Here they are direct convolutions with packed dot products (v_dot2_f32_f16: two
+// products + fp32 accumulate per lane and instruction; bf16 unpacks by a shift), the input
+// patch staged once per workgroup in LDS and the weights read as LDS broadcasts:
+//
+//   conv_c1_kernel<T, K, POOL>   C == 1, any CO (16-channel blocks): each lane computes a
+//       2x2 output block x 16 channels; the K taps of a kernel row are paired along x
+//       ((kx, kx+1) -> one dot2), the odd column shift is one v_alignbit. POOL fuses the
+//       following MaxPooling2D((2,2)) (+ argmax) exactly like the MFMA path does (values
+//       compared as stored in T, first max wins), so fused and unfused results are equal.
+//   conv_co1_kernel<T, C, K>     CO == 1, C in {16, 32}: each lane computes P consecutive
+//       output pixels of a row (P = 64 / C) and reuses every loaded input column for the K
+//       taps it meets; channels pair naturally in NHWC (one 32-bit word = 2 channels). The
+//       patch is stored in groups of P pixels padded by 16 bytes (group stride 144 B), which
+//       makes the lanes' ds_read_b128 conflict-free.
+// Accumulation is fp32 in both (products of two 16-bit values are exact in fp32).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "specenh.h"
+
+namespace specenh {
+int set_error(int code, const std::string& msg);  // stft_psd.hip
+
+namespace {
+
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+struct NarrowArgs {
+  const void* in;
+  const void* w;  // w_gemm [CO][K][K][C]
+  const float* bias;
+  void* out;
+  float* logits;
+  unsigned char* argmax;
+  int N, IH, IW, C, OH, OW, CO;
+  int pad_t, pad_l;
+  int act, out_f32;
+};
+
+__device__ __forceinline__ float act_f(float v, int act) {
+  if (act == SPECENH_ACT_RELU) return fmaxf(v, 0.f);
+  if (act == SPECENH_ACT_SIGMOID) return 1.f / (1.f + __expf(-v));
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ uint32_t tbits(T x) {
+  return (uint32_t)__builtin_bit_cast(unsigned short, x);
+}
+template <typename T>
+__device__ __forceinline__ T from_bits(uint32_t b) {
+  return __builtin_bit_cast(T, (unsigned short)b);
+}
+
+// c + a.lo*b.lo + a.hi*b.hi for two packed 16-bit values of T
+template <typename T>
+__device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
+  if constexpr (__is_same(T, _Float16)) {
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, a), __builtin_bit_cast(f16x2, b), c,
+                                  false);
+  } else {  // bf16 -> fp32 is a shift: exact products, fp32 accumulate
+    c = fmaf(__uint_as_float(a << 16), __uint_as_float(b << 16), c);
+    return fmaf(__uint_as_float(a & 0xffff0000u), __uint_as_float(b & 0xffff0000u), c);
+  }
+}
+
+// ------------------------------------------------------------------ C == 1
+constexpr int C1_TILE = 32;  // output rows and columns per workgroup (16 x 16 lanes x 2 x 2)
+
+template <typename T, int K, bool POOL>
+__global__ __launch_bounds__(256) void conv_c1_kernel(NarrowArgs a) {
+  constexpr int NPX = (K + 1) / 2;                    // tap pairs per kernel row
+  constexpr int NQ = K * NPX;                         // tap pairs per output channel
+  constexpr int NQ4 = (NQ + 3) / 4 * 4;
+  constexpr int WR = K + 1;                           // window rows/columns of a 2x2 block
+  constexpr int PST = C1_TILE + K + (K & 1 ? 1 : 0);  // patch row stride (even)
+  constexpr int PH = C1_TILE + K - 1;
+  __shared__ __attribute__((aligned(16))) T sP[PH * PST];
+  __shared__ __attribute__((aligned(16))) uint32_t sW[16][NQ4];
+  __shared__ float sB[16];
+
+  const int tid = threadIdx.x;
+  const int ntx = (a.OW + C1_TILE - 1) / C1_TILE, nty = (a.OH + C1_TILE - 1) / C1_TILE;
+  const int n = blockIdx.x / (ntx * nty);
+  const int trem = blockIdx.x - n * (ntx * nty);
+  const int oy0 = (trem / ntx) * C1_TILE, ox0 = (trem % ntx) * C1_TILE;
+  const int cb = blockIdx.y * 16;
+  const int iy0 = oy0 - a.pad_t, ix0 = ox0 - a.pad_l;
+  const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
+  const T* __restrict__ W = reinterpret_cast<const T*>(a.w);
+
+  for (int e = tid; e < PH * PST; e += 256) {
+    const int py = e / PST, px = e - (e / PST) * PST;
+    const int iy = iy0 + py, ix = ix0 + px;
+    const bool ok = px < C1_TILE + K - 1 && (unsigned)iy < (unsigned)a.IH &&
+                    (unsigned)ix < (unsigned)a.IW;
+    sP[e] = ok ? in[((long long)n * a.IH + iy) * a.IW + ix] : (T)0.f;
+  }
+  for (int e = tid; e < 16 * NQ4; e += 256) {
+    const int cl = e / NQ4, q = e - (e / NQ4) * NQ4;
+    const int ky = q / NPX, j = q - (q / NPX) * NPX;
+    const int co = cb + cl;
+    uint32_t v = 0;
+    if (co < a.CO && q < NQ) {
+      const T* wr = W + (long long)co * K * K + ky * K;
+      v = tbits(wr[2 * j]);
+      if (2 * j + 1 < K) v |= tbits(wr[2 * j + 1]) << 16;
+    }
+    sW[cl][q] = v;
+  }
+  if (tid < 16) sB[tid] = (a.bias && cb + tid < a.CO) ? a.bias[cb + tid] : 0.f;
+  __syncthreads();
+
+  const int tx = tid & 15, ty = tid >> 4;
+  // pairs of window row r: pa = columns (2m, 2m+1), pb = columns (2m+1, 2m+2); a pair's
+  // second tap past the kernel edge meets a zero weight (inputs are finite)
+  uint32_t pa[WR][NPX], pb[WR][NPX];
+#pragma unroll
+  for (int r = 0; r < WR; ++r) {
+    uint32_t raw[NPX + 1];
+    const T* row = sP + (2 * ty + r) * PST + 2 * tx;
+#pragma unroll
+    for (int m = 0; m <= NPX; ++m)
+      raw[m] = (2 * m < WR) ? *reinterpret_cast<const uint32_t*>(row + 2 * m) : 0u;
+#pragma unroll
+    for (int m = 0; m < NPX; ++m) {
+      pa[r][m] = raw[m];
+      pb[r][m] = __builtin_amdgcn_alignbit(raw[m + 1], raw[m], 16);
+    }
+  }
+
+  // per output channel: accumulate the 2x2 block, then pool / pack it at once (no
+  // 64-float accumulator array stays live)
+  const int oy = oy0 + 2 * ty, ox = ox0 + 2 * tx;
+  const int nco = min(16, a.CO - cb);
+  uint32_t pk[2][2][8], am[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pk[0][0][i] = pk[0][1][i] = pk[1][0][i] = pk[1][1][i] = 0u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) am[i] = 0u;
+  long long opix[2][2];
+  bool okpix[2][2];
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      okpix[dy][dx] = oy + dy < a.OH && ox + dx < a.OW;
+      opix[dy][dx] = (((long long)n * a.OH + oy + dy) * a.OW + ox + dx) * a.CO + cb;
+    }
+#pragma unroll
+  for (int cl = 0; cl < 16; ++cl) {
+    uint32_t wq[NQ4];
+#pragma unroll
+    for (int q4 = 0; q4 < NQ4 / 4; ++q4) {
+      const uint4 u = *reinterpret_cast<const uint4*>(&sW[cl][4 * q4]);  // broadcast
+      wq[4 * q4] = u.x;
+      wq[4 * q4 + 1] = u.y;
+      wq[4 * q4 + 2] = u.z;
+      wq[4 * q4 + 3] = u.w;
+    }
+    float s[2][2];
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+        for (int j = 0; j < NPX; ++j) {
+          s0 = dot2<T>(pa[dy + ky][j], wq[ky * NPX + j], s0);
+          s1 = dot2<T>(pb[dy + ky][j], wq[ky * NPX + j], s1);
+        }
+      s[dy][0] = s0;
+      s[dy][1] = s1;
+    }
+    const float bb = sB[cl];
+    if constexpr (POOL) {
+      const float v00 = (float)(T)act_f(s[0][0] + bb, a.act);
+      const float v01 = (float)(T)act_f(s[0][1] + bb, a.act);
+      const float v10 = (float)(T)act_f(s[1][0] + bb, a.act);
+      const float v11 = (float)(T)act_f(s[1][1] + bb, a.act);
+      float b = v00;
+      uint32_t q = 0;
+      if (v01 > b) { b = v01; q = 1; }
+      if (v10 > b) { b = v10; q = 2; }
+      if (v11 > b) { b = v11; q = 3; }
+      pk[0][0][cl >> 1] |= tbits((T)b) << (16 * (cl & 1));
+      am[cl >> 2] |= q << (8 * (cl & 3));
+    } else {
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx) {
+          const float v = act_f(s[dy][dx] + bb, a.act);
+          if (a.out_f32) {
+            if (okpix[dy][dx] && cl < nco) reinterpret_cast<float*>(a.out)[opix[dy][dx] + cl] = v;
+          } else {
+            pk[dy][dx][cl >> 1] |= tbits((T)v) << (16 * (cl & 1));
+          }
+        }
+    }
+    // keep the scheduler from hoisting every channel's weight reads (register pressure)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  if constexpr (POOL) {
+    const int PHo = a.OH / 2, PWo = a.OW / 2, py = oy / 2, px = ox / 2;
+    if (py >= PHo || px >= PWo) return;
+    const long long o = (((long long)n * PHo + py) * PWo + px) * a.CO + cb;
+    T* dst = reinterpret_cast<T*>(a.out) + o;
+    if (nco == 16 && (a.CO & 7) == 0) {
+      reinterpret_cast<uint4*>(dst)[0] = uint4{pk[0][0][0], pk[0][0][1], pk[0][0][2], pk[0][0][3]};
+      reinterpret_cast<uint4*>(dst)[1] = uint4{pk[0][0][4], pk[0][0][5], pk[0][0][6], pk[0][0][7]};
+    } else {
+      for (int cl = 0; cl < nco; ++cl)
+        dst[cl] = from_bits<T>(pk[0][0][cl >> 1] >> (16 * (cl & 1)));
+    }
+    if (a.argmax) {
+      if (nco == 16 && (a.CO & 15) == 0)
+        *reinterpret_cast<uint4*>(a.argmax + o) = uint4{am[0], am[1], am[2], am[3]};
+      else
+        for (int cl = 0; cl < nco; ++cl)
+          a.argmax[o + cl] = (unsigned char)(am[cl >> 2] >> (8 * (cl & 3)));
+    }
+  } else if (!a.out_f32) {
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        if (!okpix[dy][dx]) continue;
+        T* dst = reinterpret_cast<T*>(a.out) + opix[dy][dx];
+        const uint32_t* w8 = pk[dy][dx];
+        if (nco == 16 && (a.CO & 7) == 0) {
+          reinterpret_cast<uint4*>(dst)[0] = uint4{w8[0], w8[1], w8[2], w8[3]};
+          reinterpret_cast<uint4*>(dst)[1] = uint4{w8[4], w8[5], w8[6], w8[7]};
+        } else {
+          for (int cl = 0; cl < nco; ++cl) dst[cl] = from_bits<T>(w8[cl >> 1] >> (16 * (cl & 1)));
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------------ CO == 1
+template <int C>
+struct Co1 {
+  static constexpr int P = 64 / C;            // output pixels per lane
+  static constexpr int TW = 128;              // output columns per workgroup
+  static constexpr int TR = 256 / (TW / P);   // output rows per workgroup (8 or 4)
+  static constexpr int GS = P * C * 2 + 16;   // bytes per group of P patch pixels (144)
+};
+
+template <typename T, int C, int K>
+__global__ __launch_bounds__(256) void conv_co1_kernel(NarrowArgs a) {
+  using G = Co1<C>;
+  constexpr int P = G::P, TR = G::TR, TW = G::TW, GS = G::GS;
+  constexpr int NG = (TW + K - 1 + P - 1) / P;  // groups per patch row
+  constexpr int RB = NG * GS;                   // bytes per patch row
+  constexpr int PR = TR + K - 1;                // patch rows
+  constexpr int CW = C / 2;                     // 32-bit words per pixel
+  constexpr int C8 = C / 8;                     // 16-byte pieces per pixel
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* sP = smem;                                    // PR x RB
+  uint32_t* sW = reinterpret_cast<uint32_t*>(smem + PR * RB);  // [K][K][CW]
+
+  const int tid = threadIdx.x;
+  const int ntx = (a.OW + TW - 1) / TW, nty = (a.OH + TR - 1) / TR;
+  const int n = blockIdx.x / (ntx * nty);
+  const int trem = blockIdx.x - n * (ntx * nty);
+  const int oy0 = (trem / ntx) * TR, ox0 = (trem % ntx) * TW;
+  const int iy0 = oy0 - a.pad_t, ix0 = ox0 - a.pad_l;
+  const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
+
+  // patch pixel (py, px), 16-byte piece h -> row py, group px / P, slot px % P
+  for (int e = tid; e < PR * NG * P * C8; e += 256) {
+    const int h = e % C8;
+    const int pix = e / C8;
+    const int py = pix / (NG * P), px = pix - (pix / (NG * P)) * (NG * P);
+    const int iy = iy0 + py, ix = ix0 + px;
+    const bool ok = (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
+    const uint4 v = ok ? *reinterpret_cast<const uint4*>(
+                             in + (((long long)n * a.IH + iy) * a.IW + ix) * C + 8 * h)
+                       : uint4{0u, 0u, 0u, 0u};
+    *reinterpret_cast<uint4*>(sP + py * RB + (px / P) * GS + (px % P) * (2 * C) + 16 * h) = v;
+  }
+  for (int e = tid; e < K * K * CW; e += 256)
+    sW[e] = reinterpret_cast<const uint32_t*>(a.w)[e];  // [ky][kx][ci pairs] (CO == 1)
+  __syncthreads();
+
+  const int g = tid % (TW / P), r = tid / (TW / P);
+  float acc[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) acc[p] = 0.f;
+#pragma unroll 1
+  for (int ky = 0; ky < K; ++ky) {
+    const unsigned char* row = sP + (r + ky) * RB + g * GS;
+#pragma unroll
+    for (int c = 0; c < P + K - 1; ++c) {
+      uint32_t col[CW];
+      const unsigned char* src = row + (c / P) * GS + (c % P) * (2 * C);
+#pragma unroll
+      for (int h = 0; h < C8; ++h) {
+        const uint4 u = *reinterpret_cast<const uint4*>(src + 16 * h);
+        col[4 * h] = u.x;
+        col[4 * h + 1] = u.y;
+        col[4 * h + 2] = u.z;
+        col[4 * h + 3] = u.w;
+      }
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) {
+        const int p = c - kx;
+        if (p < 0 || p >= P) continue;  // compile-time
+        const uint32_t* wr = sW + (ky * K + kx) * CW;
+#pragma unroll
+        for (int h = 0; h < C8; ++h) {
+          const uint4 w4 = *reinterpret_cast<const uint4*>(wr + 4 * h);  // broadcast
+          acc[p] = dot2<T>(col[4 * h], w4.x, acc[p]);
+          acc[p] = dot2<T>(col[4 * h + 1], w4.y, acc[p]);
+          acc[p] = dot2<T>(col[4 * h + 2], w4.z, acc[p]);
+          acc[p] = dot2<T>(col[4 * h + 3], w4.w, acc[p]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one input column live at a time
+    }
+  }
+
+  const int oy = oy0 + r, ox = ox0 + g * P;
+  if (oy >= a.OH || ox >= a.OW) return;
+  const float bb = a.bias ? a.bias[0] : 0.f;
+  const long long o = ((long long)n * a.OH + oy) * a.OW + ox;
+  float v[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) v[p] = acc[p] + bb;
+  const bool full = ox + P <= a.OW && (a.OW % P) == 0;
+  if (a.logits) {
+    if (full && P == 4) {
+      *reinterpret_cast<float4*>(a.logits + o) = float4{v[0], v[1], v[P > 2 ? 2 : 0], v[P - 1]};
+    } else {
+      for (int p = 0; p < P; ++p)
+        if (ox + p < a.OW) a.logits[o + p] = v[p];
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < P; ++p) v[p] = act_f(v[p], a.act);
+  if (a.out_f32) {
+    float* dst = reinterpret_cast<float*>(a.out) + o;
+    if (full && P == 4) {
+      *reinterpret_cast<float4*>(dst) = float4{v[0], v[1], v[P > 2 ? 2 : 0], v[P - 1]};
+    } else if (full && P == 2) {
+      *reinterpret_cast<float2*>(dst) = float2{v[0], v[1]};
+    } else {
+      for (int p = 0; p < P; ++p)
+        if (ox + p < a.OW) dst[p] = v[p];
+    }
+  } else {
+    T* dst = reinterpret_cast<T*>(a.out) + o;
+    for (int p = 0; p < P; ++p)
+      if (ox + p < a.OW) dst[p] = (T)v[p];
+  }
+}
+
+template <typename T, int C, int K>
+int launch_co1(const NarrowArgs& a, hipStream_t st) {
+  using G = Co1<C>;
+  constexpr int NG = (G::TW + K - 1 + G::P - 1) / G::P;
+  constexpr int LDS = (G::TR + K - 1) * NG * G::GS + K * K * (C / 2) * 4;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)conv_co1_kernel<T, C, K>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
+      return set_error(SPECENH_EHIP, "conv_co1 attribute");
+    attr = true;
+  }
+  const long long tiles =
+      (long long)a.N * ((a.OH + G::TR - 1) / G::TR) * ((a.OW + G::TW - 1) / G::TW);
+  hipLaunchKernelGGL((conv_co1_kernel<T, C, K>), dim3((unsigned)tiles), dim3(256), LDS, st, a);
+  return hipGetLastError() == hipSuccess ? 1 : set_error(SPECENH_EHIP, "conv_co1 launch");
+}
+
+template <typename T, int K>
+int launch_c1(const NarrowArgs& a, bool pool, hipStream_t st) {
+  const long long tiles = (long long)a.N * ((a.OH + C1_TILE - 1) / C1_TILE) *
+                          ((a.OW + C1_TILE - 1) / C1_TILE);
+  const dim3 grid((unsigned)tiles, (unsigned)((a.CO + 15) / 16));
+  if (pool) hipLaunchKernelGGL((conv_c1_kernel<T, K, true>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((conv_c1_kernel<T, K, false>), grid, dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? 1 : set_error(SPECENH_EHIP, "conv_c1 launch");
+}
+
+template <typename T>
+int dispatch(const NarrowArgs& a, int K, bool pool, hipStream_t st) {
+  if (a.C == 1) {
+    if (a.logits) return 0;
+    switch (K) {
+      case 3: return launch_c1<T, 3>(a, pool, st);
+      case 5: return launch_c1<T, 5>(a, pool, st);
+      case 7: return launch_c1<T, 7>(a, pool, st);
+      default: return 0;
+    }
+  }
+  if (a.CO == 1 && !pool) {
+    if (a.C == 16) {
+      switch (K) {
+        case 3: return launch_co1<T, 16, 3>(a, st);
+        case 5: return launch_co1<T, 16, 5>(a, st);
+        case 7: return launch_co1<T, 16, 7>(a, st);
+        default: return 0;
+      }
+    }
+    if (a.C == 32) {
+      switch (K) {
+        case 3: return launch_co1<T, 32, 3>(a, st);
+        case 5: return launch_co1<T, 32, 5>(a, st);
+        case 7: return launch_co1<T, 32, 7>(a, st);
+        default: return 0;
+      }
+    }
+  }
+  return 0;
+}
+
+}  // namespace
+
+// Narrow-channel direct convolution (C == 1, or CO == 1 with C in {16, 32}), bf16/f16,
+// stride 1, undilated, square odd kernel <= 7, no ReLU mask. Returns 1 when launched, 0
+// when the shape is not covered (the caller takes the MFMA path), < 0 on error.
+int launch_conv_narrow(int dtype, const void* in, int N, int IH, int IW, int C, const void* w,
+                       int KH, int KW, int CO, const float* bias, int pad_t, int pad_l, int OH,
+                       int OW, int act, void* out, int out_f32, float* logits, int pool,
+                       unsigned char* argmax, hipStream_t st) {
+  if (dtype == SPECENH_DTYPE_F32 || KH != KW || (KH & 1) == 0 || KH > 7) return 0;
+  if (C != 1 && CO != 1) return 0;
+  if (pool && ((OH & 1) || (OW & 1))) return 0;
+  NarrowArgs a{in, w, bias, out, logits, argmax, N, IH, IW, C, OH, OW, CO,
+               pad_t, pad_l, act, out_f32};
+  if (dtype == SPECENH_DTYPE_BF16) return dispatch<__bf16>(a, KH, pool != 0, st);
+  return dispatch<_Float16>(a, KH, pool != 0, st);
+}
+
+}  // namespace specenh

@@ -113,6 +113,7 @@ __device__ void gemm_GZ(const float* G, int r, const float* sZ, float* sY) {
     float acc[P];
 #pragma unroll
     for (int c = 0; c < P; ++c) acc[c] = 0.f;
+#pragma unroll 8
     for (int j = 0; j < r; ++j) {
       const float g = G[(long long)j * r + i];
       const float4* zj = reinterpret_cast<const float4*>(sZ + j * P);
@@ -218,7 +219,9 @@ __device__ void jacobi(float* sH, float* sQ, float* sCS, int* sPair) {
       off += __shfl_xor(off, m);
       diag += __shfl_xor(diag, m);
     }
-    if (off <= 1e-28 * diag) break;  // uniform
+    // uniform; H is stored in fp32, so an off-diagonal mass ~1e-13 of the diagonal (entries
+    // ~3e-7 relative) is its rounding floor: converged
+    if (off <= 1e-13 * diag) break;
     for (int round = 0; round < P - 1; ++round) {
       if (lane < P / 2) {  // tournament pairing: player 0 fixed, others rotate
         auto player = [&](int k) { return k == 0 ? 0 : 1 + (k - 1 + round) % (P - 1); };
@@ -423,8 +426,10 @@ hipError_t launch_subspace_t(const float* G, int r, int K, float* V, float* thet
   hipError_t e = hipFuncSetAttribute((const void*)subspace_kernel<P>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
+  // 3 rounds when the subspace oversamples the wanted K by >= 8 columns, else 5
+  const int iters = P >= K + 8 ? 3 : 5;
   hipLaunchKernelGGL(subspace_kernel<P>, dim3((unsigned)batch), dim3(SS_THREADS), lds, st, G, r,
-                     K, 3, V, theta);
+                     K, iters, V, theta);
   return hipGetLastError();
 }
 
@@ -505,8 +510,9 @@ int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long
     return set_error(SPECENH_EUNSUPPORTED,
                      "GPU SVD denoiser needs a top-K subspace with K <= 40 (K = stop, or start "
                      "when stop == r)");
-  // subspace width: K + 8 oversampling, multiple of 8, <= r (rounded down to 8)
-  int p = std::max(8, ((K + 8 + 7) / 8) * 8);
+  // subspace width: K + 7 oversampling rounded up to a multiple of 8 (8 for the default
+  // K = 1), <= r (rounded down to 8)
+  int p = std::max(8, ((K + 7 + 7) / 8) * 8);
   if (p > r) p = (r / 8) * 8;
   if (p < K || p < 8)
     return set_error(SPECENH_EUNSUPPORTED, "matrix too small for the GPU subspace solver");

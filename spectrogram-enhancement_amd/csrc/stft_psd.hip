@@ -361,6 +361,106 @@ __device__ __forceinline__ void fft_pair(const StftArgs& a, PairSamples<N>& in, 
   if constexpr (C::R3 > 1) stockham_pass<N, G, C::R3, R1 * C::R2>(buf, s_tw + TwOff<N>::P3, gl);
 }
 
+// Separate the two frames of this lane group's FFT pair (Z in `buf`), PSD (+log2 / ln) of
+// bins gl + i*G in registers, running min/max. DC bins come from the fp64 path.
+template <int N>
+__device__ __forceinline__ void pair_psd(const StftArgs& a, const float2* buf, int gl, double dca,
+                                         double dcb, bool want_log, bool log2_out,
+                                         float (&pv)[Layout<N>::IB][2], float& lmin, float& lmax) {
+  using Lo = Layout<N>;
+  constexpr int G = Cfg<N>::G;
+  constexpr int IB = Lo::IB;
+  const float scale_mid = 0.5f * a.scale, scale_end = 0.25f * a.scale;
+#pragma unroll
+  for (int i = 0; i < IB; ++i) {
+    // bins k = gl + i*G: only i == 0 holds k = 0 (gl == 0), only i == IB-1 can hold
+    // k = N/2 and k > N/2 (clamped to a duplicate of bin gl), all compile-time known.
+    const int k = gl + i * G;
+    const int kk = (i == IB - 1 && k >= Lo::NBINS) ? gl : k;
+    const float2 zk = buf[pad(kk)];
+    const float2 zm = buf[pad((N - kk) & (N - 1))];
+    const float ar = zk.x + zm.x, ai = zk.y - zm.y;
+    const float br = zk.x - zm.x, bi = zk.y + zm.y;
+    float qa = fmaf(ar, ar, ai * ai);
+    float qb = fmaf(br, br, bi * bi);
+    float sc = scale_mid;
+    if (i == IB - 1 && (N / 2) % G == 0) sc = (kk == N / 2) ? scale_end : scale_mid;
+    float pa, pb;
+    if (want_log) {
+      pa = __log2f(fmaf(qa, sc, a.eps));
+      pb = __log2f(fmaf(qb, sc, a.eps));
+    } else {
+      pa = qa * sc;
+      pb = qb * sc;
+    }
+    if (i == 0) {  // DC of both frames from the fp64 path (lane gl == 0 only)
+      const float da = (float)(dca * dca * (double)a.scale);
+      const float db = (float)(dcb * dcb * (double)a.scale);
+      if (gl == 0) {
+        pa = want_log ? __log2f(da + a.eps) : da;
+        pb = want_log ? __log2f(db + a.eps) : db;
+      }
+    }
+    if (want_log && !log2_out) {
+      pa *= 0.69314718055994530942f;
+      pb *= 0.69314718055994530942f;
+    }
+    lmin = fmin3(lmin, pa, pb);
+    lmax = fmax3(lmax, pa, pb);
+    pv[i][0] = pa;
+    pv[i][1] = pb;
+  }
+}
+
+// The workgroup's (bins x TF frames) tile through LDS (it aliases the FFT buffers) and out
+// as frequency-row segments out[k][t0 : t0 + tfv]; with `norm` each value is rescaled
+// (v - mn) * inv on the way. Starts and ends with a workgroup LDS barrier.
+template <int N>
+__device__ __forceinline__ void tile_store(const StftArgs& a, float* s_tile,
+                                           const float (&pv)[Layout<N>::IB][2], int gl, int fi,
+                                           int tid, __amdgpu_buffer_rsrc_t orr, int t0, float mn,
+                                           float inv, bool norm) {
+  using Lo = Layout<N>;
+  constexpr int G = Cfg<N>::G;
+  constexpr int IB = Lo::IB;
+  lds_barrier();  // every group is done with its FFT buffer: reuse as the tile
+  const int fl = 2 * fi;
+#pragma unroll
+  for (int i = 0; i < IB; ++i) {
+    const int k = gl + i * G;
+    if (k < Lo::NBINS) {
+      s_tile[k * Lo::TS + fl] = norm ? (pv[i][0] - mn) * inv : pv[i][0];
+      s_tile[k * Lo::TS + fl + 1] = norm ? (pv[i][1] - mn) * inv : pv[i][1];
+    }
+  }
+  lds_barrier();
+  // ---- store frequency-row segments: out[shot][k][t0 : t0+tfv] ----
+  // Compile-time trip count: the compiler can then count these stores in its partial
+  // vmcnt waits for the prefetched samples instead of draining everything.
+  const int tfv = min(Lo::TF, a.T - t0);
+  if (!(a.flags & SPECENH_STFT_DEV_NOSTORE)) {
+    constexpr int ST = (Lo::NBINS * Lo::TF + Lo::THREADS - 1) / Lo::THREADS;
+    constexpr int ROWS_PER_IT = Lo::THREADS >> Lo::LOG_TF;
+    const int k0 = tid >> Lo::LOG_TF;
+    const int f = tid & (Lo::TF - 1);
+    // one VGPR offset for all stores of this tile; the row step is a scalar soffset
+    const int voff = (k0 * a.T + t0 + f) * 4;
+    const int sstep = ROWS_PER_IT * a.T * 4;
+    int soff = 0;
+    asm volatile("" : "+s"(soff));  // opaque: keeps the 33 offsets from being hoisted
+                                    // out of the tile loop into (spilled) SGPRs
+#pragma unroll
+    for (int it = 0; it < ST; ++it) {
+      const int k = k0 + it * ROWS_PER_IT;
+      if (k < a.F_out && f < tfv)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s_tile[k * Lo::TS + f]), orr,
+                                              voff, soff, 0);
+      soff += sstep;
+    }
+  }
+  lds_barrier();  // tile (= FFT buffers) free for the next tile's FFTs
+}
+
 // One workgroup per spectrogram (shot): loops over tiles of TF frames. Tables are
 // staged in LDS once per shot; each lane group's next-tile samples are prefetched
 // into registers while the current tile computes. Per tile every lane group runs one
@@ -399,7 +499,6 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + shot * a.x_stride, a.x_stride * 4);
   const bool want_log = (a.flags & (SPECENH_STFT_LOG | SPECENH_STFT_NORMALIZE)) != 0;
   const bool log2_out = (a.flags & SPECENH_STFT_NORMALIZE) != 0;
-  const float scale_mid = 0.5f * a.scale, scale_end = 0.25f * a.scale;
   const int ntiles = (a.T + Lo::TF - 1) / Lo::TF;
   float* o_shot = a.out + shot * (long long)a.F_out * a.T;
   float lmin = INFINITY, lmax = -INFINITY;
@@ -420,81 +519,8 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
 
     // ---- separate the two frames, PSD (+log2/ln), running min/max; values in registers ----
     float pv[IB][2];
-#pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      // bins k = gl + i*G: only i == 0 holds k = 0 (gl == 0), only i == IB-1 can hold
-      // k = N/2 and k > N/2 (clamped to a duplicate of bin gl), all compile-time known.
-      const int k = gl + i * G;
-      const int kk = (i == IB - 1 && k >= Lo::NBINS) ? gl : k;
-      const float2 zk = buf[pad(kk)];
-      const float2 zm = buf[pad((N - kk) & (N - 1))];
-      const float ar = zk.x + zm.x, ai = zk.y - zm.y;
-      const float br = zk.x - zm.x, bi = zk.y + zm.y;
-      float qa = fmaf(ar, ar, ai * ai);
-      float qb = fmaf(br, br, bi * bi);
-      float sc = scale_mid;
-      if (i == IB - 1 && (N / 2) % G == 0) sc = (kk == N / 2) ? scale_end : scale_mid;
-      float pa, pb;
-      if (want_log) {
-        pa = __log2f(fmaf(qa, sc, a.eps));
-        pb = __log2f(fmaf(qb, sc, a.eps));
-      } else {
-        pa = qa * sc;
-        pb = qb * sc;
-      }
-      if (i == 0) {  // DC of both frames from the fp64 path (lane gl == 0 only)
-        const float da = (float)(dca * dca * (double)a.scale);
-        const float db = (float)(dcb * dcb * (double)a.scale);
-        if (gl == 0) {
-          pa = want_log ? __log2f(da + a.eps) : da;
-          pb = want_log ? __log2f(db + a.eps) : db;
-        }
-      }
-      if (want_log && !log2_out) {
-        pa *= 0.69314718055994530942f;
-        pb *= 0.69314718055994530942f;
-      }
-      lmin = fmin3(lmin, pa, pb);
-      lmax = fmax3(lmax, pa, pb);
-      pv[i][0] = pa;
-      pv[i][1] = pb;
-    }
-    lds_barrier();  // every group is done with its FFT buffer: reuse as the tile
-    const int fl = 2 * fi;
-#pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      const int k = gl + i * G;
-      if (k < Lo::NBINS) {
-        s_tile[k * Lo::TS + fl] = pv[i][0];
-        s_tile[k * Lo::TS + fl + 1] = pv[i][1];
-      }
-    }
-    lds_barrier();
-    // ---- store frequency-row segments: out[shot][k][t0 : t0+tfv] ----
-    // Compile-time trip count: the compiler can then count these stores in its partial
-    // vmcnt waits for the prefetched samples instead of draining everything.
-    const int tfv = min(Lo::TF, a.T - t0);
-    if (!(a.flags & SPECENH_STFT_DEV_NOSTORE)) {
-      constexpr int ST = (Lo::NBINS * Lo::TF + Lo::THREADS - 1) / Lo::THREADS;
-      constexpr int ROWS_PER_IT = Lo::THREADS >> Lo::LOG_TF;
-      const int k0 = tid >> Lo::LOG_TF;
-      const int f = tid & (Lo::TF - 1);
-      // one VGPR offset for all stores of this tile; the row step is a scalar soffset
-      const int voff = (k0 * a.T + t0 + f) * 4;
-      const int sstep = ROWS_PER_IT * a.T * 4;
-      int soff = 0;
-      asm volatile("" : "+s"(soff));  // opaque: keeps the 33 offsets from being hoisted
-                                      // out of the tile loop into (spilled) SGPRs
-#pragma unroll
-      for (int it = 0; it < ST; ++it) {
-        const int k = k0 + it * ROWS_PER_IT;
-        if (k < a.F_out && f < tfv)
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s_tile[k * Lo::TS + f]), orr,
-                                                voff, soff, 0);
-        soff += sstep;
-      }
-    }
-    lds_barrier();  // tile (= FFT buffers) free for the next tile's FFTs
+    pair_psd<N>(a, buf, gl, dca, dcb, want_log, log2_out, pv, lmin, lmax);
+    tile_store<N>(a, s_tile, pv, gl, fi, tid, orr, t0, 0.f, 1.f, false);
   }
 
   if (a.flags & SPECENH_STFT_NORMALIZE) {
@@ -548,6 +574,213 @@ hipError_t launch_stft(const StftArgs& a, long long batch, hipStream_t stream) {
   hipLaunchKernelGGL(stft_psd_kernel<N>, dim3((unsigned)batch), dim3(Lo::THREADS), Lo::BYTES,
                      stream, a);
   return hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------- team schedule (NORMALIZE)
+// The min-max normalisation (pipeline_data.py:34) needs a spectrogram's extremes before
+// any of its values can be stored. stft_psd_kernel (one workgroup per shot) therefore
+// re-reads and rewrites its whole output once (518 KB per C2 shot, mostly from beyond
+// L2). Here a shot's frame tiles are computed by a TEAM of M workgroups, one tile each:
+// a member keeps its tile in registers, publishes its local extremes as ONE 8-byte
+// granule {maxkey, ~minkey} (an agent-scope store; both halves are nonzero for any
+// non-NaN value, so the granule is its own ready flag), and stores its normalised tile
+// once the team's M granules are in — every output byte is written exactly once.
+// The grid is persistent and no larger than the device's resident capacity, so all
+// members of a team are co-resident; tasks are pipelined: a workgroup publishes task i,
+// computes task i+1, and only then waits for task i's team (deadlock-free by induction
+// over i: every publish precedes the same workgroup's next wait). Spins are bounded: a
+// missing member sets the timeout word and the tile is normalised by what arrived.
+constexpr int TEAM_MAX = 64;           // one wave polls a team's granules
+constexpr int STFT_DEV_NOTEAM = 1 << 17;     // development flag: force stft_psd_kernel
+constexpr int STFT_DEV_FORCETEAM = 1 << 18;  // development flag: team even for small shots
+
+__device__ __forceinline__ void team_minmax(const unsigned long long* g, int M, int lane,
+                                            unsigned* tmo, float& mn, float& mx) {
+  unsigned long long v = 0;
+  for (unsigned spins = 0;; ++spins) {
+    if (lane < M) v = __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool ok = lane >= M || ((unsigned)v != 0u && (unsigned)(v >> 32) != 0u);
+    if (__all(ok)) break;
+    if (spins >= (1u << 20) ||
+        __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+      if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  unsigned kmax = lane < M ? (unsigned)v : 0u;
+  unsigned kinv = lane < M ? (unsigned)(v >> 32) : 0u;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    kmax = max(kmax, (unsigned)__shfl_xor((int)kmax, m));
+    kinv = max(kinv, (unsigned)__shfl_xor((int)kinv, m));
+  }
+  mx = key2f(kmax);
+  mn = key2f(~kinv);
+}
+
+template <int N>
+__global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_kernel(
+    StftArgs a, unsigned long long* gran, long long batch, int M, int Q, unsigned* tmo) {
+  using C = Cfg<N>;
+  using Lo = Layout<N>;
+  constexpr int G = C::G;
+  constexpr int IB = Lo::IB;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* s_dc = reinterpret_cast<double*>(smem + Lo::OFF_DC);
+  float2* s_tw = reinterpret_cast<float2*>(smem + Lo::OFF_TW);
+  float* s_win = reinterpret_cast<float*>(smem + Lo::OFF_WIN);
+  float* s_tile = reinterpret_cast<float*>(smem + Lo::OFF_BUF);
+  float* s_red = reinterpret_cast<float*>(smem + Lo::OFF_RED);  // [2*WAVES] + team {mn, mx}
+
+  if ((int)blockIdx.x >= Q * M) return;  // whole workgroup: spare slots of the grid
+  const int tid = threadIdx.x;
+  const int q = blockIdx.x / M, mem = blockIdx.x - (blockIdx.x / M) * M;
+  for (int i = tid; i < Lo::TWN; i += Lo::THREADS) s_tw[i] = a.twiddle[i];
+  for (int i = tid; i < N; i += Lo::THREADS) {
+    s_win[i] = a.window[i];
+    s_dc[i] = a.dc_coef[i];
+  }
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int gl = lane % G;
+  const int fi = wave * (64 / G) + lane / G;
+  float2* buf = reinterpret_cast<float2*>(smem + Lo::OFF_BUF) + fi * Lo::BUF;
+  const int t0 = mem * Lo::TF;  // this member's tile: frames [t0, t0 + TF)
+  const int fa = t0 + 2 * fi;
+  const long long ntask = (batch - q + Q - 1) / Q;  // shots q, q + Q, ... < batch
+  const long long plane = (long long)a.F_out * a.T;
+  const long long xbytes = a.x_stride * 4;
+
+  PairSamples<N> nxt;
+  load_pair<N>(nxt, make_rsrc(a.x + q * a.x_stride, xbytes), a.hop, fa, a.T, gl);
+  float pvp[IB][2];
+#pragma unroll
+  for (int i = 0; i < IB; ++i) pvp[i][0] = pvp[i][1] = 0.f;
+  __syncthreads();
+
+  for (long long it = 0; it <= ntask; ++it) {
+    const long long shot = q + it * Q;
+    const bool cur = it < ntask;
+    float pvc[IB][2];
+    float lmin = INFINITY, lmax = -INFINITY;
+    if (cur) {
+      const bool pf = it + 1 < ntask;
+      const __amdgpu_buffer_rsrc_t xn = make_rsrc(a.x + (pf ? shot + Q : shot) * a.x_stride, xbytes);
+      double dca, dcb;
+      fft_pair<N>(a, nxt, true, true, s_tw, s_win, s_dc, buf, gl, dca, dcb, xn, fa, pf);
+      float dmin = INFINITY, dmax = -INFINITY;  // (pair_psd's running extremes: unused)
+      pair_psd<N>(a, buf, gl, dca, dcb, true, true, pvc, dmin, dmax);
+      // the tile's extremes from the held values themselves (the v_min3/v_max3 running
+      // pair in pair_psd came out wrong in this kernel's schedule: measured on gfx950)
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        lmin = fminf(lmin, fminf(pvc[i][0], pvc[i][1]));
+        lmax = fmaxf(lmax, fmaxf(pvc[i][0], pvc[i][1]));
+      }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      lmin = fminf(lmin, __shfl_xor(lmin, m));
+      lmax = fmaxf(lmax, __shfl_xor(lmax, m));
+    }
+    if (lane == 0) {
+      s_red[wave] = lmin;
+      s_red[C::WAVES + wave] = lmax;
+    }
+    lds_barrier();  // s_red complete; every lane is done reading its FFT buffer
+    if (cur && tid == 0) {
+      float mn = s_red[0], mx = s_red[C::WAVES];
+#pragma unroll
+      for (int w = 1; w < C::WAVES; ++w) {
+        mn = fminf(mn, s_red[w]);
+        mx = fmaxf(mx, s_red[C::WAVES + w]);
+      }
+      const unsigned long long gv =
+          ((unsigned long long)(~f2key(mn)) << 32) | (unsigned long long)f2key(mx);
+      __hip_atomic_store(gran + shot * M + mem, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (it > 0) {  // the previous task's tile: team extremes, normalise, store
+      const long long sp = shot - Q;
+      if (wave == 0) {
+        float mn, mx;
+        team_minmax(gran + sp * M, M, lane, tmo, mn, mx);
+        if (lane == 0) {
+          s_red[2 * C::WAVES] = mn;
+          s_red[2 * C::WAVES + 1] = mx;
+        }
+      }
+      lds_barrier();
+      const float mn = s_red[2 * C::WAVES];
+      const float inv = 1.0f / (s_red[2 * C::WAVES + 1] - mn);  // max == min -> NaN (0/0)
+      const __amdgpu_buffer_rsrc_t orr = make_rsrc(a.out + sp * plane, plane * 4);
+      tile_store<N>(a, s_tile, pvp, gl, fi, tid, orr, t0, mn, inv, true);
+    } else {
+      lds_barrier();  // s_red is rewritten by the next task only after thread 0 read it
+    }
+    if (cur) {
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        pvp[i][0] = pvc[i][0];
+        pvp[i][1] = pvc[i][1];
+      }
+    }
+  }
+}
+
+// Launch the team schedule when it applies (NORMALIZE, workspace given, team size <=
+// TEAM_MAX and <= the resident capacity). *launched = false: the caller falls back.
+template <int N>
+hipError_t launch_team(const StftArgs& a, long long batch, void* workspace, hipStream_t stream,
+                       bool* launched) {
+  using Lo = Layout<N>;
+  *launched = false;
+  const int M = (a.T + Lo::TF - 1) / Lo::TF;
+  if (M > TEAM_MAX) return hipSuccess;
+  static int cap[64] = {};  // resident workgroups per device (0 = not queried)
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) return hipSuccess;
+  if (cap[dev] == 0) {
+    e = hipFuncSetAttribute((const void*)stft_team_kernel<N>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Lo::BYTES);
+    if (e != hipSuccess) return e;
+    int per_cu = 0, cus = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)stft_team_kernel<N>,
+                                                     Lo::THREADS, Lo::BYTES);
+    if (e != hipSuccess) return e;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    // never trust the occupancy answer alone (co-residency is a correctness condition
+    // here): bound it by the register file (512 VGPR+AGPR per lane and SIMD, 8-register
+    // granules, 4 SIMDs per CU) and by LDS as well
+    hipFuncAttributes fa{};
+    e = hipFuncGetAttributes(&fa, (const void*)stft_team_kernel<N>);
+    if (e != hipSuccess) return e;
+    const int regs = ((fa.numRegs + 7) / 8) * 8;
+    const int waves_per_simd = regs > 0 ? std::min(8, 512 / regs) : 8;
+    const int by_regs = waves_per_simd * 4 / Cfg<N>::WAVES;
+    const int by_lds = (160 * 1024) / Lo::BYTES;
+    per_cu = std::min(per_cu, std::min(by_regs, by_lds));
+    cap[dev] = per_cu * cus > 0 ? per_cu * cus : -1;
+  }
+  if (cap[dev] < M) return hipSuccess;
+  long long Q = cap[dev] / M;
+  if (Q > batch) Q = batch;
+  // workspace: [timeout word, 16 B][granules: batch x M x 8 B], zeroed every call
+  unsigned* tmo = reinterpret_cast<unsigned*>(workspace);
+  unsigned long long* gran =
+      reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + 16);
+  const size_t zero = 16 + (((size_t)batch * M * 8 + 15) / 16) * 16;
+  e = hipMemsetAsync(workspace, 0, zero, stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(stft_team_kernel<N>, dim3((unsigned)(Q * M)), dim3(Lo::THREADS), Lo::BYTES,
+                     stream, a, gran, batch, M, (int)Q, tmo);
+  e = hipGetLastError();
+  *launched = e == hipSuccess;
+  return e;
 }
 
 }  // namespace specenh
@@ -672,8 +905,8 @@ int specenh_stft_plan_destroy(specenh_stft_plan* plan) {
 
 size_t specenh_stft_workspace_bytes(const specenh_stft_plan* plan, long long batch) {
   (void)plan;
-  (void)batch;
-  return 0;
+  if (batch <= 0) return 16;
+  return 16 + (size_t)batch * TEAM_MAX * 8;  // team schedule: timeout word + granules
 }
 
 int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long batch,
@@ -688,7 +921,6 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
   if (T < 0) return (int)T;
   if (x_stride < length) return set_error(SPECENH_EINVAL, "x_stride < length");
   if (T > (1ll << 30)) return set_error(SPECENH_EINVAL, "too many frames");
-  (void)workspace;  // no workspace needed (min/max is workgroup-local); kept for ABI stability
   hipStream_t st = (hipStream_t)stream;
   StftArgs a{};
   a.x = x;
@@ -706,6 +938,25 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
   a.twiddle = plan->d_twiddle;
   a.dc_coef = plan->d_dc;
   const long long F_out = a.F_out;
+  // team schedule for large spectrograms (C2: 518 KB each); small ones (C5: 64 KB) are
+  // re-read from L2 by the sweep for less than the team's hand-off costs (measured)
+  const bool team = (F_out * T * 4 >= (256ll << 10)) || (flags & STFT_DEV_FORCETEAM);
+  if ((flags & SPECENH_STFT_NORMALIZE) && workspace && !(flags & STFT_DEV_NOTEAM) && team &&
+      batch <= (1ll << 30)) {
+    bool launched = false;
+    hipError_t e = hipSuccess;
+    switch (N) {
+      case 64: e = launch_team<64>(a, batch, workspace, st, &launched); break;
+      case 128: e = launch_team<128>(a, batch, workspace, st, &launched); break;
+      case 256: e = launch_team<256>(a, batch, workspace, st, &launched); break;
+      case 512: e = launch_team<512>(a, batch, workspace, st, &launched); break;
+      case 1024: e = launch_team<1024>(a, batch, workspace, st, &launched); break;
+      default: break;  // 2048 / 4096: the held tile would spill; one workgroup per shot
+    }
+    if (e != hipSuccess)
+      return set_error(SPECENH_EHIP, std::string("stft team launch: ") + hipGetErrorString(e));
+    if (launched) return SPECENH_OK;
+  }
   for (long long b0 = 0; b0 < batch; b0 += 1 << 30) {
     const long long nb = std::min<long long>(1 << 30, batch - b0);
     StftArgs c = a;

@@ -27,6 +27,7 @@ extern "C" {
 #define SPECENH_EUNSUPPORTED -2 /* valid for scipy, not implemented here (NotImplementedError) */
 #define SPECENH_EHIP -3       /* HIP runtime error (RuntimeError) */
 #define SPECENH_ENOMEM -4
+#define SPECENH_ERANGE -5     /* index out of range, as the reference raises (IndexError) */
 
 /* Output-mode flags for specenh_stft_psd. */
 #define SPECENH_STFT_LOG 1          /* natural log(P + eps)                  pipeline_data.py:33 */
@@ -95,6 +96,27 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
 size_t specenh_svd_workspace_bytes(long long batch, int m, int n, int kmax);
 int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long a_stride,
                         int start, int stop, float* out, void* workspace, void* stream);
+
+/* Gavish-Donoho optimal hard-threshold modes of the same denoiser:
+ *   num_sing = #{ s_i > omega(beta) * median(s) },  beta = min(m, n) / max(m, n),
+ *   omega(beta) = 0.56 beta^3 - 0.95 beta^2 + 1.82 beta + 1.43   (denoising_by_svd.ipynb:155-159)
+ *   SPECENH_SVD_OPTIMAL  keep components [0, num_sing - 1): denoiseSignal(A, use_optimal=True)
+ *                        (:210-217, then the :224-227 clamping; num_sing <= 1 gives zeros)
+ *   SPECENH_SVD_COMPUTE  keep components [1, 2 num_sing): computeSignal(A) (:161-186); the
+ *                        reference raises IndexError when 2 num_sing > min(m, n):
+ *                        SPECENH_ERANGE, nothing written.
+ * The singular values come from the fp64 Gram matrix (Householder tridiagonalisation +
+ * Sturm bisection for the two middle order statistics and the count); the kept range is
+ * then reconstructed as in specenh_svd_denoise. Needs min(m, n) <= 256 and a kept range
+ * ending at K <= 40 (SPECENH_EUNSUPPORTED otherwise). num_sing (device int[batch]) and
+ * median_sv (device double[batch]) are optional outputs. Synchronises `stream` once (the
+ * subspace width depends on the counts). */
+#define SPECENH_SVD_OPTIMAL 0
+#define SPECENH_SVD_COMPUTE 1
+size_t specenh_svd_optimal_workspace_bytes(long long batch, int m, int n);
+int specenh_svd_denoise_optimal(const float* A, long long batch, int m, int n, long long a_stride,
+                                int mode, float* out, int* num_sing, double* median_sv,
+                                void* workspace, void* stream);
 
 /* ---------------------------------------------------------------- conv autoencoder
  * Primitives under the Keras-shaped facade (specenh.keras) that replaces the model of

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cmath>
 #include <string>
+#include <vector>
 
 #include "fft_common.hpp"
 #include "specenh.h"
@@ -359,16 +360,24 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
 //   out = Y[:, lo:hi] V[:, lo:hi]^T     (RB x r)      phase 2 (complement: X_blk - ...)
 constexpr int RB = 32;
 
+// ranges (optional, device int[2 * batch]): a per-matrix [lo, hi) replacing the uniform
+// one (always the direct, non-complement form); hi <= lo gives zeros.
 template <int KP>
 __global__ __launch_bounds__(256) void recon_kernel(XView x, int Kr, int r, const float* V,
                                                     int K, int lo, int hi, int complement,
-                                                    float* out, long long out_bstride,
-                                                    long long osk, long long osi) {
+                                                    const int* ranges, float* out,
+                                                    long long out_bstride, long long osk,
+                                                    long long osi) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* sV = reinterpret_cast<float*>(smem);  // r x KP (zero-padded columns)
   float* sX = sV + r * KP;                      // RB x (r + 1)
   float* sY = sX + RB * (r + 1);                // RB x KP
   const long long b = blockIdx.y;
+  if (ranges) {
+    lo = ranges[2 * b];
+    hi = ranges[2 * b + 1];
+    complement = 0;
+  }
   const int k0 = blockIdx.x * RB;
   const int tid = threadIdx.x;
   const float* X = x.base + b * x.batch_stride;
@@ -413,6 +422,218 @@ __global__ __launch_bounds__(256) void recon_kernel(XView x, int Kr, int r, cons
   }
 }
 
+
+// ---------------------------------------------------------------- optimal hard threshold
+// use_optimal / computeSignal (denoising_by_svd.ipynb:174-181, 210-217) need the median of
+// ALL singular values and how many exceed omega(beta) * median. They come from the
+// eigenvalues of the Gram matrix in fp64 (the noise singular values sit ~1e-3 below the
+// largest; an fp32 Gram would bury their squares in its rounding): Householder reduction
+// to tridiagonal form, then Sturm-count bisection for exactly the three numbers needed
+// (the two middle order statistics and the count above the threshold).
+
+// fp64 Gram G = X^T X: 64x64 tile per workgroup (upper-triangle tiles, mirrored), 16 rows
+// of X per LDS stage, 4x4 outputs per thread. Products of fp32 inputs are exact in fp64.
+__global__ __launch_bounds__(256) void gram64_kernel(XView x, int K, int r, double* G, int nts) {
+  __shared__ double sa[16][65], sb[16][65];
+  int t = blockIdx.x, ti = 0;
+  while (t >= nts - ti) {
+    t -= nts - ti;
+    ++ti;
+  }
+  const int tj = ti + t;
+  const long long b = blockIdx.y;
+  const float* X = x.base + b * x.batch_stride;
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  double acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    for (int idx = tid; idx < 16 * 64; idx += 256) {
+      int kk, c;
+      if (x.si == 1) {  // rows of X contiguous: coalesce along the column index
+        kk = idx >> 6;
+        c = idx & 63;
+      } else {
+        c = idx >> 4;
+        kk = idx & 15;
+      }
+      const int k = k0 + kk, ci = ti * 64 + c, cj = tj * 64 + c;
+      sa[kk][c] = (k < K && ci < r) ? (double)X[(long long)k * x.sk + (long long)ci * x.si] : 0.0;
+      sb[kk][c] = (k < K && cj < r) ? (double)X[(long long)k * x.sk + (long long)cj * x.si] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int kk = 0; kk < 16; ++kk) {
+      double av[4], bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        av[i] = sa[kk][ty * 4 + i];
+        bv[i] = sb[kk][tx * 4 + i];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fma(av[i], bv[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+  double* Gb = G + b * (long long)r * r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = ti * 64 + ty * 4 + i, col = tj * 64 + tx * 4 + j;
+      if (row < r && col < r) {
+        Gb[(long long)row * r + col] = acc[i][j];
+        Gb[(long long)col * r + row] = acc[i][j];
+      }
+    }
+}
+
+__device__ __forceinline__ double block_sum256(double v, double* red) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  __syncthreads();  // red is reused call after call
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// Householder tridiagonalisation of the symmetric n x n fp64 matrix A (in place, global,
+// n <= 256, one workgroup per matrix; thread i owns column i of the trailing block):
+// d = diagonal, e = off-diagonal. Step k: v from A[k+1:, k], p = tau A22 v,
+// w = p - (tau/2)(p.v) v, A22 -= v w^T + w v^T (LAPACK dsytd2 / dlarfg arithmetic).
+__global__ __launch_bounds__(256) void tridiag_kernel(double* G, int n, double* dg, double* eg) {
+  __shared__ double sv[256], sw[256], red[4];
+  const long long b = blockIdx.x;
+  double* A = G + b * (long long)n * n;
+  double* d = dg + b * n;
+  double* e = eg + b * n;
+  const int tid = threadIdx.x;
+  for (int k = 0; k + 2 < n; ++k) {
+    const int len = n - k - 1;
+    const double* rowk = A + (long long)k * n + k + 1;  // = column k below the diagonal
+    const double xv = tid < len ? rowk[tid] : 0.0;
+    const double s2 = block_sum256(tid >= 1 && tid < len ? xv * xv : 0.0, red);
+    const double alpha = rowk[0];
+    if (tid == 0) d[k] = A[(long long)k * n + k];
+    if (s2 == 0.0) {  // uniform: already tridiagonal in this column
+      if (tid == 0) e[k] = alpha;
+      continue;
+    }
+    const double beta = -copysign(sqrt(alpha * alpha + s2), alpha);
+    const double tau = (beta - alpha) / beta;
+    const double scal = 1.0 / (alpha - beta);
+    if (tid == 0) e[k] = beta;
+    const double vi = tid == 0 ? 1.0 : (tid < len ? xv * scal : 0.0);
+    if (tid < len) sv[tid] = vi;
+    __syncthreads();
+    double p = 0.0;
+    if (tid < len) {
+      const double* col = A + (long long)(k + 1) * n + (k + 1) + tid;
+#pragma unroll 8
+      for (int j = 0; j < len; ++j) p = fma(col[(long long)j * n], sv[j], p);
+      p *= tau;
+    }
+    const double pv = block_sum256(tid < len ? p * vi : 0.0, red);
+    const double w = p - 0.5 * tau * pv * vi;
+    if (tid < len) sw[tid] = w;
+    __syncthreads();
+    if (tid < len) {
+      double* col = A + (long long)(k + 1) * n + (k + 1) + tid;
+#pragma unroll 8
+      for (int j = 0; j < len; ++j) col[(long long)j * n] -= sv[j] * w + sw[j] * vi;
+    }
+    __syncthreads();  // the next step reads what other threads just wrote (same CU)
+  }
+  if (tid == 0) {
+    if (n >= 2) {
+      d[n - 2] = A[(long long)(n - 2) * n + n - 2];
+      e[n - 2] = A[(long long)(n - 2) * n + n - 1];
+    }
+    d[n - 1] = A[(long long)(n - 1) * n + n - 1];
+  }
+}
+
+// Number of eigenvalues < x of the symmetric tridiagonal (d, e2 = e^2) (Sturm sequence,
+// LAPACK dstebz pivmin guard).
+__device__ int sturm_count(const double* d, const double* e2, int n, double x, double pivmin) {
+  double q = d[0] - x;
+  if (fabs(q) < pivmin) q = -pivmin;
+  int c = q < 0.0;
+  for (int i = 1; i < n; ++i) {
+    q = d[i] - x - e2[i - 1] / q;
+    if (fabs(q) < pivmin) q = -pivmin;
+    c += q < 0.0;
+  }
+  return c;
+}
+
+// k-th smallest eigenvalue (0-based) by 65-way multisection: each lane counts at one point.
+__device__ double kth_eig(const double* d, const double* e2, int n, int k, double lo, double hi,
+                          double pivmin, int lane) {
+  for (int it = 0; it < 16 && hi > lo; ++it) {
+    const double x = lo + (hi - lo) * (double)(lane + 1) / 65.0;
+    const int c = sturm_count(d, e2, n, x, pivmin);
+    const unsigned long long m = __ballot(c > k);
+    const int first = m ? __ffsll((long long)m) - 1 : 64;
+    const double nlo = first == 0 ? lo : lo + (hi - lo) * (double)first / 65.0;
+    const double nhi = first == 64 ? hi : lo + (hi - lo) * (double)(first + 1) / 65.0;
+    if (!(nhi < hi) && !(nlo > lo)) break;  // no progress at double resolution
+    lo = nlo;
+    hi = nhi;
+  }
+  return 0.5 * (lo + hi);
+}
+
+// One wave per matrix: median singular value and num_sing = #(s > omega * median)
+// (s = sqrt(max(lambda, 0)), lambda the Gram eigenvalues; numpy's median of r values).
+__global__ __launch_bounds__(64) void optimal_rank_kernel(const double* dg, const double* eg,
+                                                          int n, double omega, int* num_sing,
+                                                          double* median) {
+  __shared__ double sd[256], se2[256];
+  const long long b = blockIdx.x;
+  const int lane = threadIdx.x;
+  double lo = INFINITY, hi = -INFINITY, emax = 0.0;
+  for (int i = lane; i < n; i += 64) {
+    const double di = dg[b * n + i];
+    const double el = i > 0 ? fabs(eg[b * n + i - 1]) : 0.0;
+    const double er = i + 1 < n ? fabs(eg[b * n + i]) : 0.0;
+    sd[i] = di;
+    if (i + 1 < n) se2[i] = er * er;
+    lo = fmin(lo, di - el - er);
+    hi = fmax(hi, di + el + er);
+    emax = fmax(emax, er * er);
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, m));
+    hi = fmax(hi, __shfl_xor(hi, m));
+    emax = fmax(emax, __shfl_xor(emax, m));
+  }
+  __syncthreads();
+  const double span = fmax(hi - lo, fmax(fabs(hi), fabs(lo))) * 4e-16 + 1e-300;
+  lo -= span;
+  hi += span;
+  const double pivmin = 2.2250738585072014e-308 * fmax(1.0, emax);
+  double med;
+  if (n & 1) {
+    med = sqrt(fmax(kth_eig(sd, se2, n, n / 2, lo, hi, pivmin, lane), 0.0));
+  } else {
+    const double a1 = kth_eig(sd, se2, n, n / 2 - 1, lo, hi, pivmin, lane);
+    const double a2 = kth_eig(sd, se2, n, n / 2, lo, hi, pivmin, lane);
+    med = 0.5 * (sqrt(fmax(a1, 0.0)) + sqrt(fmax(a2, 0.0)));
+  }
+  const double t = omega * med;
+  const int below = sturm_count(sd, se2, n, t * t, pivmin);  // s < t (s == t: measure zero)
+  if (lane == 0) {
+    num_sing[b] = n - below;
+    if (median) median[b] = med;
+  }
+}
+
 }  // namespace specenh
 
 using namespace specenh;
@@ -448,24 +669,25 @@ hipError_t launch_subspace(int p, const float* G, int r, int K, float* V, float*
 
 template <int KP>
 hipError_t launch_recon_t(XView xb, int Kr, int r, const float* V, int K, int lo, int hi,
-                          int comp, float* out, long long ob, long long osk, long long osi,
-                          long long nb, hipStream_t st) {
+                          int comp, const int* ranges, float* out, long long ob, long long osk,
+                          long long osi, long long nb, hipStream_t st) {
   const size_t lds = (size_t)r * KP * 4 + (size_t)RB * (r + 1) * 4 + (size_t)RB * KP * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipError_t e = hipFuncSetAttribute((const void*)recon_kernel<KP>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(recon_kernel<KP>, dim3((Kr + RB - 1) / RB, (unsigned)nb), dim3(256), lds,
-                     st, xb, Kr, r, V, K, lo, hi, comp, out, ob, osk, osi);
+                     st, xb, Kr, r, V, K, lo, hi, comp, ranges, out, ob, osk, osi);
   return hipGetLastError();
 }
 
 hipError_t launch_recon(int KP, XView xb, int Kr, int r, const float* V, int K, int lo, int hi,
-                        int comp, float* out, long long ob, long long osk, long long osi,
-                        long long nb, hipStream_t st) {
+                        int comp, const int* ranges, float* out, long long ob, long long osk,
+                        long long osi, long long nb, hipStream_t st) {
   switch (KP) {
-#define SPECENH_RC(n) \
-  case n: return launch_recon_t<n>(xb, Kr, r, V, K, lo, hi, comp, out, ob, osk, osi, nb, st);
+#define SPECENH_RC(n)                                                                        \
+  case n:                                                                                    \
+    return launch_recon_t<n>(xb, Kr, r, V, K, lo, hi, comp, ranges, out, ob, osk, osi, nb, st);
     SPECENH_RC(8) SPECENH_RC(16) SPECENH_RC(24) SPECENH_RC(32) SPECENH_RC(40) SPECENH_RC(48)
 #undef SPECENH_RC
     default: return hipErrorInvalidValue;
@@ -549,10 +771,152 @@ int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long
     XView xb = xv;
     xb.base = A + b0 * a_stride;
     e = launch_recon(KP, xb, Kr, r, V + b0 * (long long)r * K, K, lo, hi, complement ? 1 : 0,
-                     out + b0 * ob, ob, osk, osi, nb, st);
+                     nullptr, out + b0 * ob, ob, osk, osi, nb, st);
     if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("recon: ") + hipGetErrorString(e));
   }
   if (hipGetLastError() != hipSuccess) return set_error(SPECENH_EHIP, "recon launch");
+  return SPECENH_OK;
+}
+
+
+size_t specenh_svd_optimal_workspace_bytes(long long batch, int m, int n) {
+  if (batch <= 0 || m <= 0 || n <= 0) return 16;
+  const size_t r = (size_t)std::min(m, n);
+  size_t off = (size_t)batch * r * r * 8 + 2 * (size_t)batch * r * 8;  // G64, d, e
+  off += (size_t)batch * (4 + 4 + 8);                                  // num, ranges, median
+  off = (off + 255) / 256 * 256;
+  return off + specenh_svd_workspace_bytes(batch, m, n, PMAX - 8);
+}
+
+int specenh_svd_denoise_optimal(const float* A, long long batch, int m, int n,
+                                long long a_stride, int mode, float* out, int* num_sing,
+                                double* median_sv, void* workspace, void* stream) {
+  if (batch < 0 || m <= 0 || n <= 0) return set_error(SPECENH_EINVAL, "bad matrix shape");
+  if (mode != SPECENH_SVD_OPTIMAL && mode != SPECENH_SVD_COMPUTE)
+    return set_error(SPECENH_EINVAL, "mode must be SPECENH_SVD_OPTIMAL or SPECENH_SVD_COMPUTE");
+  if (batch == 0) return SPECENH_OK;
+  if (!A || !out || !workspace) return set_error(SPECENH_EINVAL, "null pointer");
+  if (a_stride < (long long)m * n) return set_error(SPECENH_EINVAL, "a_stride < m*n");
+  const int r = std::min(m, n);
+  if (r > 256)
+    return set_error(SPECENH_EUNSUPPORTED, "optimal threshold path needs min(m, n) <= 256");
+  hipStream_t st = (hipStream_t)stream;
+  // workspace carve (specenh_svd_optimal_workspace_bytes)
+  char* w = (char*)workspace;
+  double* G64 = (double*)w;
+  double* dd = G64 + batch * (long long)r * r;
+  double* ee = dd + batch * (long long)r;
+  int* num = (int*)(ee + batch * (long long)r);
+  int* ranges = num + batch;
+  double* med = (double*)(ranges + 2 * batch);
+  size_t off = (size_t)batch * r * r * 8 + 2 * (size_t)batch * r * 8 + (size_t)batch * 16;
+  off = (off + 255) / 256 * 256;
+  float* G = (float*)(w + off);
+  XView xv;
+  xv.base = A;
+  xv.batch_stride = a_stride;
+  int Kr;
+  long long osk, osi;
+  if (m >= n) {
+    xv.sk = n; xv.si = 1; Kr = m; osk = n; osi = 1;
+  } else {
+    xv.sk = 1; xv.si = n; Kr = n; osk = 1; osi = n;
+  }
+  // 1-3: fp64 Gram, tridiagonal form, median and count above the threshold
+  const int nts64 = (r + 63) / 64;
+  const int ntri64 = nts64 * (nts64 + 1) / 2;
+  for (long long b0 = 0; b0 < batch; b0 += 65535) {
+    const long long nb = std::min<long long>(65535, batch - b0);
+    XView xb = xv;
+    xb.base = A + b0 * a_stride;
+    hipLaunchKernelGGL(gram64_kernel, dim3(ntri64, (unsigned)nb), dim3(256), 0, st, xb, Kr, r,
+                       G64 + b0 * (long long)r * r, nts64);
+  }
+  hipLaunchKernelGGL(tridiag_kernel, dim3((unsigned)batch), dim3(256), 0, st, G64, r, dd, ee);
+  const double beta = (double)r / (double)std::max(m, n);
+  // omega(beta), denoising_by_svd.ipynb:155-159: sum of coef * beta**(3 - i), Python's order
+  const double omega = ((0.0 + 0.56 * std::pow(beta, 3.0)) + -0.95 * std::pow(beta, 2.0)) +
+                       1.82 * std::pow(beta, 1.0) + 1.43 * std::pow(beta, 0.0);
+  hipLaunchKernelGGL(optimal_rank_kernel, dim3((unsigned)batch), dim3(64), 0, st, dd, ee, r,
+                     omega, num, med);
+  if (hipGetLastError() != hipSuccess) return set_error(SPECENH_EHIP, "optimal rank launch");
+  // 4: the kept range per matrix decides the subspace width: one host round trip
+  std::vector<int> hn((size_t)batch);
+  if (hipMemcpyAsync(hn.data(), num, (size_t)batch * sizeof(int), hipMemcpyDeviceToHost, st) !=
+          hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return set_error(SPECENH_EHIP, "num_sing readback");
+  if (num_sing &&
+      hipMemcpyAsync(num_sing, num, (size_t)batch * sizeof(int), hipMemcpyDeviceToDevice, st) !=
+          hipSuccess)
+    return set_error(SPECENH_EHIP, "num_sing copy");
+  if (median_sv &&
+      hipMemcpyAsync(median_sv, med, (size_t)batch * sizeof(double), hipMemcpyDeviceToDevice,
+                     st) != hipSuccess)
+    return set_error(SPECENH_EHIP, "median copy");
+  std::vector<int> hr(2 * (size_t)batch);
+  int K = 0;
+  for (long long b = 0; b < batch; ++b) {
+    const int ns = hn[b];
+    int lo, hi;
+    if (mode == SPECENH_SVD_OPTIMAL) {  // :216-217 start = 0, stop = num_sing - 1
+      lo = 0;
+      hi = ns - 1;
+    } else {  // computeSignal :181-185: s[idx] for idx in range(1, 2 num_sing)
+      if (2 * ns - 1 > r - 1 && ns > 0)
+        return set_error(SPECENH_ERANGE, "index " + std::to_string(2 * ns - 1) +
+                                             " is out of bounds for axis 0 with size " +
+                                             std::to_string(r));
+      lo = 1;
+      hi = 2 * ns;
+    }
+    if (lo < 0) lo = 0;  // :224-227 clamping
+    if (hi > r) hi = r;
+    hr[2 * b] = lo;
+    hr[2 * b + 1] = hi;
+    if (hi > lo) K = std::max(K, hi);
+  }
+  if (K == 0) {
+    if (hipMemsetAsync(out, 0, (size_t)batch * m * n * sizeof(float), st) != hipSuccess)
+      return set_error(SPECENH_EHIP, "memset");
+    return SPECENH_OK;
+  }
+  if (K > PMAX - 8 || K > r)
+    return set_error(SPECENH_EUNSUPPORTED,
+                     "the kept range needs a top-" + std::to_string(K) +
+                         " singular subspace; the GPU subspace solver handles K <= 40");
+  if (hipMemcpy(ranges, hr.data(), hr.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+    return set_error(SPECENH_EHIP, "ranges upload");
+  int p = std::max(8, ((K + 7 + 7) / 8) * 8);
+  if (p > r) p = (r / 8) * 8;
+  if (p < K || p < 8)
+    return set_error(SPECENH_EUNSUPPORTED, "matrix too small for the GPU subspace solver");
+  // 5: fp32 Gram, top-K subspace, per-matrix reconstruction
+  float* V = G + batch * (long long)r * r;
+  float* theta = V + batch * (long long)r * K;
+  const int nts = (r + 31) / 32;
+  const int ntri = nts * (nts + 1) / 2;
+  for (long long b0 = 0; b0 < batch; b0 += 65535) {
+    const long long nb = std::min<long long>(65535, batch - b0);
+    XView xb = xv;
+    xb.base = A + b0 * a_stride;
+    hipLaunchKernelGGL(gram_kernel, dim3((ntri + 3) / 4, (unsigned)nb), dim3(256), 0, st, xb,
+                       Kr, r, G + b0 * (long long)r * r, nts);
+  }
+  hipError_t e = launch_subspace(p, G, r, K, V, theta, batch, st);
+  if (e != hipSuccess)
+    return set_error(SPECENH_EHIP, std::string("subspace: ") + hipGetErrorString(e));
+  const int KP = (K + 7) / 8 * 8;
+  const long long ob = (long long)m * n;
+  for (long long b0 = 0; b0 < batch; b0 += 65535) {
+    const long long nb = std::min<long long>(65535, batch - b0);
+    XView xb = xv;
+    xb.base = A + b0 * a_stride;
+    e = launch_recon(KP, xb, Kr, r, V + b0 * (long long)r * K, K, 0, 0, 0, ranges + 2 * b0,
+                     out + b0 * ob, ob, osk, osi, nb, st);
+    if (e != hipSuccess)
+      return set_error(SPECENH_EHIP, std::string("recon: ") + hipGetErrorString(e));
+  }
   return SPECENH_OK;
 }
 

@@ -22,6 +22,9 @@ SPECENH_EINVAL = -1
 SPECENH_EUNSUPPORTED = -2
 SPECENH_EHIP = -3
 SPECENH_ENOMEM = -4
+SPECENH_ERANGE = -5
+SVD_OPTIMAL = 0
+SVD_COMPUTE = 1
 
 STFT_LOG = 1
 STFT_NORMALIZE = 2
@@ -56,6 +59,11 @@ SIGNATURES = {
     "specenh_svd_denoise": (_c.c_int, [_c.c_void_p, _c.c_longlong, _c.c_int, _c.c_int,
                                        _c.c_longlong, _c.c_int, _c.c_int, _c.c_void_p,
                                        _c.c_void_p, _c.c_void_p]),
+    "specenh_svd_optimal_workspace_bytes": (_c.c_size_t, [_c.c_longlong, _c.c_int, _c.c_int]),
+    "specenh_svd_denoise_optimal": (_c.c_int, [_c.c_void_p, _c.c_longlong, _c.c_int, _c.c_int,
+                                               _c.c_longlong, _c.c_int, _c.c_void_p,
+                                               _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                               _c.c_void_p]),
     "specenh_conv2d": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
                                   _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_void_p,
                                   _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
@@ -129,6 +137,8 @@ def check(rc: int, what: str = "") -> int:
         raise NotImplementedError(msg)
     if rc == SPECENH_ENOMEM:
         raise MemoryError(msg)
+    if rc == SPECENH_ERANGE:
+        raise IndexError(msg)
     raise RuntimeError(msg)
 
 

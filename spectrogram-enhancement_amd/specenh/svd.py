@@ -10,12 +10,16 @@ Same names, arguments and semantics as the notebook (:155-229):
         start<0 -> 0 and stop>r -> r; start>=stop gives zeros.
   * ``denoise_batch(A[B, m, n], start, stop)`` — device tensors in/out (fast path).
 
+  * ``computeSignal(matrix)``  components [1, 2*num_sing) (:161-186), IndexError when
+        2*num_sing > min(m, n) like the notebook
+  * ``optimal_batch(A[B, m, n], mode)`` — use_optimal / computeSignal on device tensors.
+
 The arithmetic runs on the GPU (csrc/svd_denoise.hip through the C-ABI
-``specenh_svd_denoise``): fp32-MFMA Gram matrix, top-K subspace iteration with fp64
-CholeskyQR2 + Rayleigh-Ritz, reconstruction ``A V V^T``. numpy inputs come back as
-float64 numpy arrays like the reference. ``use_optimal`` / ``computeSignal`` need
-every singular value (the median); they are not on the GPU path yet and raise
-NotImplementedError.
+``specenh_svd_denoise`` / ``specenh_svd_denoise_optimal``): fp32-MFMA Gram matrix, top-K
+subspace iteration with fp64 CholeskyQR2 + Rayleigh-Ritz, reconstruction ``A V V^T``; the
+optimal threshold's median and count come from the fp64 Gram's eigenvalues (Householder
+tridiagonalisation + Sturm bisection). numpy inputs come back as float64 numpy arrays like
+the reference.
 """
 from __future__ import annotations
 
@@ -80,22 +84,57 @@ def denoise_batch(A: torch.Tensor, start=None, stop=None,
     return out[0] if squeeze else out
 
 
-def denoiseSignal(matrix, start=None, stop=None, use_optimal=False):
-    """denoising_by_svd.ipynb:188-229."""
-    if use_optimal:
-        raise NotImplementedError("use_optimal needs every singular value (median); not on the "
-                                  "GPU path yet")
+def optimal_batch(A: torch.Tensor, mode: int = _lib.SVD_OPTIMAL, out: torch.Tensor | None = None,
+                  return_rank: bool = False):
+    """Optimal hard-threshold modes on device tensors ``A[B, m, n]`` (or ``[m, n]``) fp32:
+    ``mode`` SVD_OPTIMAL = denoiseSignal(use_optimal=True), SVD_COMPUTE = computeSignal.
+    With ``return_rank`` also returns (num_sing int32[B], median singular value f64[B])."""
+    if not isinstance(A, torch.Tensor) or A.device.type != "cuda":
+        raise RuntimeError("specenh.svd.optimal_batch runs on the GPU only (no CPU fallback)")
+    squeeze = A.dim() == 2
+    if squeeze:
+        A = A.unsqueeze(0)
+    if A.dim() != 3:
+        raise ValueError("A must be [batch, m, n]")
+    if A.dtype != torch.float32:
+        A = A.float()
+    if not (A.stride(2) == 1 and A.stride(1) == A.shape[2]):
+        A = A.contiguous()
+    B, m, n = A.shape
+    if out is None:
+        out = torch.empty((B, m, n), dtype=torch.float32, device=A.device)
+    L = _lib.lib()
+    ws = torch.empty(max(16, int(L.specenh_svd_optimal_workspace_bytes(B, m, n))),
+                     dtype=torch.uint8, device=A.device)
+    ns = torch.empty(B, dtype=torch.int32, device=A.device)
+    med = torch.empty(B, dtype=torch.float64, device=A.device)
+    _lib.check(L.specenh_svd_denoise_optimal(
+        ctypes.c_void_p(A.data_ptr()), B, m, n, A.stride(0), int(mode),
+        ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ns.data_ptr()),
+        ctypes.c_void_p(med.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+        ctypes.c_void_p(_lib.current_stream_handle(A.device))), "svd_denoise_optimal")
+    res = out[0] if squeeze else out
+    return (res, ns, med) if return_rank else res
+
+
+def _host(matrix, fn):
     if isinstance(matrix, torch.Tensor):
-        return denoise_batch(matrix, start, stop)
+        return fn(matrix)
     a = np.asarray(matrix)
     if not torch.cuda.is_available():
         raise RuntimeError("specenh requires a ROCm GPU (HIP); there is no CPU fallback")
     t = torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device="cuda")
-    return denoise_batch(t, start, stop).double().cpu().numpy()
+    return fn(t).double().cpu().numpy()
+
+
+def denoiseSignal(matrix, start=None, stop=None, use_optimal=False):
+    """denoising_by_svd.ipynb:188-229."""
+    if use_optimal:  # :210-217 (start/stop are overridden, as in the notebook)
+        return _host(matrix, lambda t: optimal_batch(t, _lib.SVD_OPTIMAL))
+    return _host(matrix, lambda t: denoise_batch(t, start, stop))
 
 
 def computeSignal(matrix):
-    """denoising_by_svd.ipynb:161-186 (components [1, 2*num_sing) with the optimal
-    threshold): needs the median singular value — not on the GPU path yet."""
-    raise NotImplementedError("computeSignal needs every singular value (median); not on the "
-                              "GPU path yet")
+    """denoising_by_svd.ipynb:161-186: components [1, 2*num_sing) of the optimal threshold
+    (IndexError when 2*num_sing > min(m, n), as the notebook's s[idx])."""
+    return _host(matrix, lambda t: optimal_batch(t, _lib.SVD_COMPUTE))

@@ -66,14 +66,72 @@ def test_wide_matrix_reference_usage(gpu_device):
     assert _rel(out, ref.denoiseSignal(Sw.astype(np.float32).astype(np.float64))) <= 1e-4
 
 
+@pytest.mark.parametrize("case", svd_cases())
+def test_optimal_threshold_matches_notebook(case, gpu_device):
+    """use_optimal (:210-217): components [0, num_sing - 1) of the Gavish-Donoho threshold;
+    num_sing and the median come from the fp64 Gram's eigenvalues on the GPU."""
+    import torch
+
+    from specenh import svd
+
+    g = load_golden(f"svd_{case}")
+    A = g["A"]
+    out = svd.denoiseSignal(A, use_optimal=True)
+    assert out.dtype == np.float64 and out.shape == A.shape
+    assert _rel(out, g["optimal"]) <= TOL, _rel(out, g["optimal"])
+    _, ns, med = svd.optimal_batch(torch.as_tensor(A.astype(np.float32), device=gpu_device),
+                                   return_rank=True)
+    assert int(ns[0]) == ref.optimal_rank(g["s"], A.shape)
+    assert float(med[0]) == pytest.approx(float(np.median(g["s"])), rel=1e-5)
+
+
+@pytest.mark.parametrize("case", svd_cases())
+def test_compute_signal_matches_notebook(case, gpu_device):
+    """computeSignal (:161-186): components [1, 2*num_sing). The band ends inside the noise
+    bulk (indices 16..31 of ~uniform noise singular values), where the individual noise
+    components are not determined to fp32 (no spectral gap): the signal part is pinned to
+    1e-5 of the output norm and the rest is bounded by the noise band's own norm."""
+    from specenh import svd
+
+    g = load_golden(f"svd_{case}")
+    A = g["A"]
+    out = svd.computeSignal(A)
+    ref_out = g["compute"]
+    s = g["s"]
+    noise = np.sqrt(np.sum(s[16:] ** 2))
+    assert np.linalg.norm(out - ref_out) <= 2 * noise
+    # the signal components 1..15 exactly: project out everything past the gap
+    u, _, vh = np.linalg.svd(A.astype(np.float64), full_matrices=False)
+    P = lambda X: u[:, :16].T @ X @ vh[:16].T  # noqa: E731
+    assert _rel(P(out), P(ref_out)) <= TOL
+
+
+def test_optimal_batched_c3_shape(gpu_device):
+    """513 x 256 gapped matrices (BASELINE config 3 geometry), use_optimal in one batch."""
+    import os
+    import sys
+
+    import torch
+
+    from specenh import svd
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import gapped_matrix
+
+    A = np.stack([gapped_matrix(950 + i, 513, 256, dtype=np.float32) for i in range(6)])
+    out, ns, _ = svd.optimal_batch(torch.as_tensor(A, device=gpu_device), return_rank=True)
+    out = out.double().cpu().numpy()
+    for b in range(6):
+        r64 = A[b].astype(np.float64)
+        assert int(ns[b]) == ref.optimal_rank(np.linalg.svd(r64, compute_uv=False), r64.shape)
+        assert _rel(out[b], ref.denoiseSignal(r64, use_optimal=True)) <= TOL
+
+
 def test_unsupported_modes_raise(gpu_device):
     from specenh import svd
 
-    A = np.random.default_rng(0).standard_normal((64, 48))
-    with pytest.raises(NotImplementedError):
-        svd.denoiseSignal(A, use_optimal=True)
-    with pytest.raises(NotImplementedError):
-        svd.computeSignal(A)
     big = np.random.default_rng(1).standard_normal((128, 96))
     with pytest.raises(NotImplementedError):
         svd.denoiseSignal(big, 0, 80)   # needs a top-80 subspace (> 40)
+    with pytest.raises(NotImplementedError):
+        svd.denoiseSignal(np.random.default_rng(2).standard_normal((300, 280)),
+                          use_optimal=True)  # min(m, n) > 256 on the optimal path

@@ -247,139 +247,186 @@ __global__ __launch_bounds__(256) void conv_c1_kernel(NarrowArgs a) {
 }
 
 // ------------------------------------------------------------------ CO == 1
+// One workgroup streams a 128-column strip of one image top to bottom, TR output rows per
+// step. The input rows live in an LDS ring of TR + K - 1 rows: each step reads only its TR
+// new rows from HBM (no halo re-reads), and they are loaded into registers one step ahead,
+// while the current rows compute.
 template <int C>
 struct Co1 {
   static constexpr int P = 64 / C;            // output pixels per lane
   static constexpr int TW = 128;              // output columns per workgroup
-  static constexpr int TR = 256 / (TW / P);   // output rows per workgroup (8 or 4)
+  static constexpr int TR = 256 / (TW / P);   // output rows per step (8 or 4)
   static constexpr int GS = P * C * 2 + 16;   // bytes per group of P patch pixels (144)
+};
+
+template <int C, int K>
+struct Co1Ring {
+  using G = Co1<C>;
+  static constexpr int NG = (G::TW + K - 1 + G::P - 1) / G::P;  // groups per ring row
+  static constexpr int RB = NG * G::GS;                          // bytes per ring row
+  static constexpr int RN = G::TR + K - 1;                       // ring rows
+  static constexpr int C8 = C / 8;                               // 16-byte pieces per pixel
+  static constexpr int PIECES = G::TR * NG * G::P * C8;          // per step (new rows)
+  static constexpr int PPT = (PIECES + 255) / 256;               // pieces per thread
+  static constexpr int LDS = RN * RB + K * K * (C / 2) * 4;
 };
 
 template <typename T, int C, int K>
 __global__ __launch_bounds__(256) void conv_co1_kernel(NarrowArgs a) {
   using G = Co1<C>;
+  using Rg = Co1Ring<C, K>;
   constexpr int P = G::P, TR = G::TR, TW = G::TW, GS = G::GS;
-  constexpr int NG = (TW + K - 1 + P - 1) / P;  // groups per patch row
-  constexpr int RB = NG * GS;                   // bytes per patch row
-  constexpr int PR = TR + K - 1;                // patch rows
-  constexpr int CW = C / 2;                     // 32-bit words per pixel
-  constexpr int C8 = C / 8;                     // 16-byte pieces per pixel
+  constexpr int NG = Rg::NG, RB = Rg::RB, RN = Rg::RN, C8 = Rg::C8;
+  constexpr int CW = C / 2;  // 32-bit words per pixel
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* sP = smem;                                    // PR x RB
-  uint32_t* sW = reinterpret_cast<uint32_t*>(smem + PR * RB);  // [K][K][CW]
+  unsigned char* sP = smem;                                    // RN x RB ring
+  uint32_t* sW = reinterpret_cast<uint32_t*>(smem + RN * RB);  // [K][K][CW]
 
   const int tid = threadIdx.x;
-  const int ntx = (a.OW + TW - 1) / TW, nty = (a.OH + TR - 1) / TR;
-  const int n = blockIdx.x / (ntx * nty);
-  const int trem = blockIdx.x - n * (ntx * nty);
-  const int oy0 = (trem / ntx) * TR, ox0 = (trem % ntx) * TW;
-  const int iy0 = oy0 - a.pad_t, ix0 = ox0 - a.pad_l;
+  const int ntx = (a.OW + TW - 1) / TW;
+  const int n = blockIdx.x / ntx;
+  const int ox0 = (blockIdx.x - n * ntx) * TW;
+  const int ix0 = ox0 - a.pad_l;
+  const int nsteps = (a.OH + TR - 1) / TR;
   const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
+  const T* __restrict__ img = in + (long long)n * a.IH * a.IW * C;
 
-  // patch pixel (py, px), 16-byte piece h -> row py, group px / P, slot px % P
-  for (int e = tid; e < PR * NG * P * C8; e += 256) {
-    const int h = e % C8;
-    const int pix = e / C8;
-    const int py = pix / (NG * P), px = pix - (pix / (NG * P)) * (NG * P);
-    const int iy = iy0 + py, ix = ix0 + px;
-    const bool ok = (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
-    const uint4 v = ok ? *reinterpret_cast<const uint4*>(
-                             in + (((long long)n * a.IH + iy) * a.IW + ix) * C + 8 * h)
-                       : uint4{0u, 0u, 0u, 0u};
-    *reinterpret_cast<uint4*>(sP + py * RB + (px / P) * GS + (px % P) * (2 * C) + 16 * h) = v;
+  // piece e of input row iy: pixel px = e / C8 of the strip, 16-byte piece h = e % C8
+  auto fetch = [&](int iy, int e) -> uint4 {
+    const int px = e / C8, h = e - (e / C8) * C8;
+    const int ix = ix0 + px;
+    const bool ok = px < NG * P && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
+    return ok ? *reinterpret_cast<const uint4*>(img + ((long long)iy * a.IW + ix) * C + 8 * h)
+              : uint4{0u, 0u, 0u, 0u};
+  };
+  auto put = [&](int iy, int e, uint4 v) {
+    const int px = e / C8, h = e - (e / C8) * C8;
+    const int slot = (iy + a.pad_t) % RN;
+    if (px < NG * P)
+      *reinterpret_cast<uint4*>(sP + slot * RB + (px / P) * GS + (px % P) * (2 * C) + 16 * h) = v;
+  };
+  constexpr int ROWP = NG * P * C8;  // pieces per input row
+
+  // prologue: the first step's RN rows
+  for (int e = tid; e < RN * ROWP; e += 256) {
+    const int rr = e / ROWP, pe = e - rr * ROWP;
+    const int iy = -a.pad_t + rr;
+    put(iy, pe, fetch(iy, pe));
   }
   for (int e = tid; e < K * K * CW; e += 256)
     sW[e] = reinterpret_cast<const uint32_t*>(a.w)[e];  // [ky][kx][ci pairs] (CO == 1)
   __syncthreads();
 
   const int g = tid % (TW / P), r = tid / (TW / P);
-  float acc[P];
+  const float bb = a.bias ? a.bias[0] : 0.f;
+  for (int step = 0; step < nsteps; ++step) {
+    // next step's TR new rows into registers (their latency hides under this step)
+    const int ny0 = (step + 1) * TR - a.pad_t + K - 1;  // first new input row of step + 1
+    uint4 nx[Rg::PPT];
+    const bool more = step + 1 < nsteps;
 #pragma unroll
-  for (int p = 0; p < P; ++p) acc[p] = 0.f;
+    for (int j = 0; j < Rg::PPT; ++j) {
+      const int e = tid + j * 256;
+      nx[j] = uint4{0u, 0u, 0u, 0u};
+      if (more && e < Rg::PIECES) nx[j] = fetch(ny0 + e / ROWP, e % ROWP);
+    }
+
+    float acc[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) acc[p] = 0.f;
+    const int iyb = step * TR - a.pad_t + r;  // input row of (r, ky = 0)
 #pragma unroll 1
-  for (int ky = 0; ky < K; ++ky) {
-    const unsigned char* row = sP + (r + ky) * RB + g * GS;
+    for (int ky = 0; ky < K; ++ky) {
+      const unsigned char* row = sP + ((iyb + ky + a.pad_t) % RN) * RB + g * GS;
 #pragma unroll
-    for (int c = 0; c < P + K - 1; ++c) {
-      uint32_t col[CW];
-      const unsigned char* src = row + (c / P) * GS + (c % P) * (2 * C);
-#pragma unroll
-      for (int h = 0; h < C8; ++h) {
-        const uint4 u = *reinterpret_cast<const uint4*>(src + 16 * h);
-        col[4 * h] = u.x;
-        col[4 * h + 1] = u.y;
-        col[4 * h + 2] = u.z;
-        col[4 * h + 3] = u.w;
-      }
-#pragma unroll
-      for (int kx = 0; kx < K; ++kx) {
-        const int p = c - kx;
-        if (p < 0 || p >= P) continue;  // compile-time
-        const uint32_t* wr = sW + (ky * K + kx) * CW;
+      for (int c = 0; c < P + K - 1; ++c) {
+        uint32_t col[CW];
+        const unsigned char* src = row + (c / P) * GS + (c % P) * (2 * C);
 #pragma unroll
         for (int h = 0; h < C8; ++h) {
-          const uint4 w4 = *reinterpret_cast<const uint4*>(wr + 4 * h);  // broadcast
-          acc[p] = dot2<T>(col[4 * h], w4.x, acc[p]);
-          acc[p] = dot2<T>(col[4 * h + 1], w4.y, acc[p]);
-          acc[p] = dot2<T>(col[4 * h + 2], w4.z, acc[p]);
-          acc[p] = dot2<T>(col[4 * h + 3], w4.w, acc[p]);
+          const uint4 u = *reinterpret_cast<const uint4*>(src + 16 * h);
+          col[4 * h] = u.x;
+          col[4 * h + 1] = u.y;
+          col[4 * h + 2] = u.z;
+          col[4 * h + 3] = u.w;
+        }
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+          const int p = c - kx;
+          if (p < 0 || p >= P) continue;  // compile-time
+          const uint32_t* wr = sW + (ky * K + kx) * CW;
+#pragma unroll
+          for (int h = 0; h < C8; ++h) {
+            const uint4 w4 = *reinterpret_cast<const uint4*>(wr + 4 * h);  // broadcast
+            acc[p] = dot2<T>(col[4 * h], w4.x, acc[p]);
+            acc[p] = dot2<T>(col[4 * h + 1], w4.y, acc[p]);
+            acc[p] = dot2<T>(col[4 * h + 2], w4.z, acc[p]);
+            acc[p] = dot2<T>(col[4 * h + 3], w4.w, acc[p]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one input column live at a time
+      }
+    }
+
+    // epilogue: bias, logits, activation, P consecutive pixels of one row
+    const int oy = step * TR + r, ox = ox0 + g * P;
+    if (oy < a.OH && ox < a.OW) {
+      const long long o = ((long long)n * a.OH + oy) * a.OW + ox;
+      float v[P];
+#pragma unroll
+      for (int p = 0; p < P; ++p) v[p] = acc[p] + bb;
+      const bool full = ox + P <= a.OW && (a.OW % P) == 0;
+      if (a.logits) {
+        if (full && P == 4) {
+          *reinterpret_cast<float4*>(a.logits + o) = float4{v[0], v[1], v[P > 2 ? 2 : 0], v[P - 1]};
+        } else {
+          for (int p = 0; p < P; ++p)
+            if (ox + p < a.OW) a.logits[o + p] = v[p];
         }
       }
-      __builtin_amdgcn_sched_barrier(0);  // one input column live at a time
-    }
-  }
-
-  const int oy = oy0 + r, ox = ox0 + g * P;
-  if (oy >= a.OH || ox >= a.OW) return;
-  const float bb = a.bias ? a.bias[0] : 0.f;
-  const long long o = ((long long)n * a.OH + oy) * a.OW + ox;
-  float v[P];
 #pragma unroll
-  for (int p = 0; p < P; ++p) v[p] = acc[p] + bb;
-  const bool full = ox + P <= a.OW && (a.OW % P) == 0;
-  if (a.logits) {
-    if (full && P == 4) {
-      *reinterpret_cast<float4*>(a.logits + o) = float4{v[0], v[1], v[P > 2 ? 2 : 0], v[P - 1]};
-    } else {
-      for (int p = 0; p < P; ++p)
-        if (ox + p < a.OW) a.logits[o + p] = v[p];
+      for (int p = 0; p < P; ++p) v[p] = act_f(v[p], a.act);
+      if (a.out_f32) {
+        float* dst = reinterpret_cast<float*>(a.out) + o;
+        if (full && P == 4) {
+          *reinterpret_cast<float4*>(dst) = float4{v[0], v[1], v[P > 2 ? 2 : 0], v[P - 1]};
+        } else if (full && P == 2) {
+          *reinterpret_cast<float2*>(dst) = float2{v[0], v[1]};
+        } else {
+          for (int p = 0; p < P; ++p)
+            if (ox + p < a.OW) dst[p] = v[p];
+        }
+      } else {
+        T* dst = reinterpret_cast<T*>(a.out) + o;
+        for (int p = 0; p < P; ++p)
+          if (ox + p < a.OW) dst[p] = (T)v[p];
+      }
     }
-  }
+    if (!more) break;
+    __syncthreads();  // every lane is done with the ring rows the new ones replace
 #pragma unroll
-  for (int p = 0; p < P; ++p) v[p] = act_f(v[p], a.act);
-  if (a.out_f32) {
-    float* dst = reinterpret_cast<float*>(a.out) + o;
-    if (full && P == 4) {
-      *reinterpret_cast<float4*>(dst) = float4{v[0], v[1], v[P > 2 ? 2 : 0], v[P - 1]};
-    } else if (full && P == 2) {
-      *reinterpret_cast<float2*>(dst) = float2{v[0], v[1]};
-    } else {
-      for (int p = 0; p < P; ++p)
-        if (ox + p < a.OW) dst[p] = v[p];
+    for (int j = 0; j < Rg::PPT; ++j) {
+      const int e = tid + j * 256;
+      if (e < Rg::PIECES) put(ny0 + e / ROWP, e % ROWP, nx[j]);
     }
-  } else {
-    T* dst = reinterpret_cast<T*>(a.out) + o;
-    for (int p = 0; p < P; ++p)
-      if (ox + p < a.OW) dst[p] = (T)v[p];
+    __syncthreads();
   }
 }
 
 template <typename T, int C, int K>
 int launch_co1(const NarrowArgs& a, hipStream_t st) {
-  using G = Co1<C>;
-  constexpr int NG = (G::TW + K - 1 + G::P - 1) / G::P;
-  constexpr int LDS = (G::TR + K - 1) * NG * G::GS + K * K * (C / 2) * 4;
-  static_assert(LDS <= 160 * 1024, "LDS budget");
+  using Rg = Co1Ring<C, K>;
+  static_assert(Rg::LDS <= 160 * 1024, "LDS budget");
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)conv_co1_kernel<T, C, K>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Rg::LDS) != hipSuccess)
       return set_error(SPECENH_EHIP, "conv_co1 attribute");
     attr = true;
   }
-  const long long tiles =
-      (long long)a.N * ((a.OH + G::TR - 1) / G::TR) * ((a.OW + G::TW - 1) / G::TW);
-  hipLaunchKernelGGL((conv_co1_kernel<T, C, K>), dim3((unsigned)tiles), dim3(256), LDS, st, a);
+  const long long strips = (long long)a.N * ((a.OW + Co1<C>::TW - 1) / Co1<C>::TW);
+  hipLaunchKernelGGL((conv_co1_kernel<T, C, K>), dim3((unsigned)strips), dim3(256), Rg::LDS, st,
+                     a);
   return hipGetLastError() == hipSuccess ? 1 : set_error(SPECENH_EHIP, "conv_co1 launch");
 }
 

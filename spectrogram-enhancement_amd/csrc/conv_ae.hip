@@ -517,7 +517,7 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
       };
       // weight fragments PD k-steps ahead in a register ring: they come from L2, and one
       // k-step of MFMA work (4*NT MFMAs, 64-256 cycles) does not cover that latency
-      constexpr int PD = NT >= 3 ? (CC == 64 ? 1 : 2) : (NT == 2 ? 4 : 8);
+      constexpr int PD = NT >= 3 ? (CC == 64 ? 1 : 2) : (NT == 2 ? 2 : 8);
       V8<T> wring[PD][NT];
 #pragma unroll
       for (int u = 0; u < PD; ++u)

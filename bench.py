@@ -21,11 +21,14 @@ Shots shard across ranks (each rank owns its B shots; no collective in the data 
 weak scaling); value = all ranks' spectrograms / max-over-ranks wall time.
 
 Rank 0 prints ONE JSON line with, besides the contract fields:
-  roofline      the dominant kernel of a step, conv_fwd_kernel (the 7 convolution launches
-                of the AE forward), MFMA-bound: achieved = algorithmic FLOPs (2 x the
-                useful MACs of the 7 layers, 0.498 GFLOP per 128x128 sample)
-                / the launches' summed duration, both per launch on average, timed live
-                with HIP events on the launch stream; peak = 2500 TFLOP/s dense fp16.
+  roofline      the dominant kernel of a step: the autoencoder layer launch with the largest
+                measured time (HIP events around every launch, on its stream). Its bound is
+                whichever floor is higher: algorithmic HBM bytes (activations read once and
+                written once + weights, ae_layer_costs) / 8 TB/s, or useful FLOPs (SURVEY §8
+                A7 MACs x 2) / the unit's peak (MFMA 2.5 PFLOP/s dense fp16; the 1-in / 1-out
+                channel layers run on the VALU, v_dot2 314.6 TFLOP/s). traffic = measured HBM
+                bytes of that launch from profiles/pmc_traffic.json (rocprofv3 --pmc passes of
+                tools/pmc_traffic.sh at the same shapes); stages.ae_layers has every layer.
   stages        per-stage ms of one step, and the C2 STFT-only configuration (4096 x
                 65,536 fp32, nperseg 1024 / hop 256) with its HBM roofline.
   cpu_baseline  the same chain on the host CPU (scipy.signal.spectrogram + log/min-max,
@@ -102,6 +105,42 @@ def ae_flops_per_sample(h=HW5, w=HW5):
         else:
             macs += hh * ww * cin * cout * k * k
     return 2 * macs
+
+
+VALU_DOT2_PEAK_TFLOPS = 314.6         # v_dot2_f32_f16: 4 FLOP/lane/instr, 128 lanes/clk/CU
+LAYER_NAMES = ["conv1+pool", "conv2+pool", "conv3+pool", "convT1", "convT2", "convT3",
+               "conv_out"]
+
+
+def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4):
+    """Per launch of the fused forward (conv+pool fused): useful FLOPs and algorithmic HBM
+    bytes per sample (activations read once + written once, weights), and the unit that
+    bounds the arithmetic (the narrow 1-in / 1-out channel layers run on the VALU)."""
+    lays = ae_layers()
+    res, hh, ww, i = [], h, w, 0
+    while i < len(lays):
+        kind, cin, cout, k, _ = lays[i]
+        pool = i + 1 < len(lays) and lays[i + 1][0] == "pool"
+        oh, ow = (2 * hh, 2 * ww) if kind == "convT" else (hh, ww)
+        macs = hh * ww * cin * cout * k * k
+        sh, sw = (oh // 2, ow // 2) if pool else (oh, ow)
+        last = i + (2 if pool else 1) >= len(lays)
+        nbytes = (hh * ww * cin * act_bytes + sh * sw * cout * (out_bytes if last else act_bytes)
+                  + k * k * cin * cout * act_bytes)
+        unit = "valu" if (cin == 1 or cout == 1) else "mfma"
+        res.append({"flops": 2 * macs, "bytes": nbytes, "unit": unit})
+        hh, ww = sh, sw
+        i += 2 if pool else 1
+    return res
+
+
+def load_pmc_traffic():
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return {}
 
 
 # ------------------------------------------------------------------ CPU baseline
@@ -267,10 +306,28 @@ def main():
         torch.cuda.synchronize()
         conv_ms.append([a.elapsed_time(b) for a, b in timing])
     conv_ms = np.array(conv_ms)                       # [reps, 7]
-    n_conv = conv_ms.shape[1]
-    per_step_conv_ms = float(np.median(conv_ms.sum(axis=1)))
-    flops_step = ae_flops_per_sample() * B
-    achieved = flops_step / (per_step_conv_ms * 1e-3) / 1e12
+    layer_ms = np.median(conv_ms, axis=0)
+    pmc = load_pmc_traffic()
+    layers = []
+    for name, c, ms in zip(LAYER_NAMES, ae_layer_costs(), layer_ms):
+        peak_c = MFMA_PEAK_TFLOPS if c["unit"] == "mfma" else VALU_DOT2_PEAK_TFLOPS
+        t_c = c["flops"] * B / (peak_c * 1e12)
+        t_m = c["bytes"] * B / (HBM_PEAK_GBPS * 1e9)
+        if t_m >= t_c:
+            ach = c["bytes"] * B / (ms * 1e-3) / 1e9
+            rl = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                  "frac": ach / HBM_PEAK_GBPS}
+        else:
+            ach = c["flops"] * B / (ms * 1e-3) / 1e12
+            rl = {"bound": c["unit"], "achieved": ach, "peak": peak_c, "unit": "TFLOP/s",
+                  "frac": ach / peak_c}
+        tr = pmc.get(name)
+        rl.update({"layer": name, "kernel_ms": float(ms), "alg_bytes_per_launch": c["bytes"] * B,
+                   "flops_per_launch": c["flops"] * B,
+                   "traffic": tr["hbm_bytes"] if tr else None,
+                   "traffic_kernel": tr["kernel"] if tr else None})
+        layers.append(rl)
+    dom = layers[int(np.argmax(layer_ms))]
 
     # ---- per-stage breakdown of one step (events between stages) ----
     stages = None
@@ -290,7 +347,8 @@ def main():
         acc /= reps
         stages = {"ms": dict(zip(["cast_in", "stft_specgr", "svd_denoise", "cast_ae",
                                   "ae_forward"], acc.round(4).tolist())),
-                  "conv_ms_per_layer": np.median(conv_ms, axis=0).round(4).tolist()}
+                  "conv_ms_per_layer": layer_ms.round(4).tolist(),
+                  "ae_layers": layers}
         # C2: the STFT-only configuration (BASELINE config 2) and its HBM roofline
         B2 = 4096
         x2 = plasma_chirps_torch(B2, L2, seed=7, device=dev)
@@ -305,6 +363,7 @@ def main():
         e1.synchronize()
         k_ms = e0.elapsed_time(e1) / 5
         ach2 = ALG_BYTES_C2 * B2 / (k_ms * 1e-3) / 1e9
+        tr2 = pmc.get("stft_c2")
         stages["stft_c2"] = {
             "workload": "4096 x 65536 fp32, nperseg 1024 hop 256 hamm, linear, density, "
                         "log + min-max + drop Nyquist -> 4096 x 512 x 253",
@@ -312,7 +371,8 @@ def main():
             "kernel_ms": k_ms, "roofline": {"bound": "hbm", "achieved": ach2,
                                             "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                             "frac": ach2 / HBM_PEAK_GBPS,
-                                            "alg_bytes_per_launch": ALG_BYTES_C2 * B2}}
+                                            "alg_bytes_per_launch": ALG_BYTES_C2 * B2,
+                                            "traffic": tr2["hbm_bytes"] if tr2 else None}}
         del x2, o2
 
     # ---- PSNR vs the fp64 CPU chain on sample shots ----
@@ -368,11 +428,14 @@ def main():
                    "shots_per_step": B, "samples": L5, "stft_dtype": "fp32",
                    "svd_dtype": "fp32 (fp64 small algebra)", "ae_dtype": "fp16",
                    "parallelism": f"shot-sharded x{world}"},
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": MFMA_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / MFMA_PEAK_TFLOPS, "traffic": None,
-                     "kernel": f"conv_fwd_kernel ({n_conv} launches per step, all layers)",
-                     "kernel_ms": per_step_conv_ms / n_conv,
-                     "flops_per_launch": flops_step / n_conv},
+        "roofline": {k: dom[k] for k in ("bound", "achieved", "peak", "unit", "frac",
+                                           "traffic")} |
+                    {"kernel": f"{dom['layer']} launch of the autoencoder forward "
+                               f"({dom['traffic_kernel'] or 'see profiles/'})",
+                     "kernel_ms": dom["kernel_ms"], "alg_bytes_per_launch":
+                     dom["alg_bytes_per_launch"], "flops_per_launch": dom["flops_per_launch"],
+                     "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 "
+                                       "+ WRITE_SIZE, separate passes, same shapes)"},
         "cpu_baseline": cpu,
         "psnr_db": psnr,
         "stages": stages,

@@ -114,8 +114,9 @@ LAYER_NAMES = ["conv1+pool", "conv2+pool", "conv3+pool", "convT1", "convT2", "co
 
 def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4):
     """Per launch of the fused forward (conv+pool fused): useful FLOPs and algorithmic HBM
-    bytes per sample (activations read once + written once, weights), and the unit that
-    bounds the arithmetic (the narrow 1-in / 1-out channel layers run on the VALU)."""
+    bytes per sample (activations read once + written once), the weights read once per
+    launch, and the unit that bounds the arithmetic (the narrow 1-in / 1-out channel
+    layers run on the VALU)."""
     lays = ae_layers()
     res, hh, ww, i = [], h, w, 0
     while i < len(lays):
@@ -125,10 +126,10 @@ def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4):
         macs = hh * ww * cin * cout * k * k
         sh, sw = (oh // 2, ow // 2) if pool else (oh, ow)
         last = i + (2 if pool else 1) >= len(lays)
-        nbytes = (hh * ww * cin * act_bytes + sh * sw * cout * (out_bytes if last else act_bytes)
-                  + k * k * cin * cout * act_bytes)
+        nbytes = hh * ww * cin * act_bytes + sh * sw * cout * (out_bytes if last else act_bytes)
         unit = "valu" if (cin == 1 or cout == 1) else "mfma"
-        res.append({"flops": 2 * macs, "bytes": nbytes, "unit": unit})
+        res.append({"flops": 2 * macs, "bytes": nbytes, "weight_bytes": k * k * cin * cout *
+                    act_bytes + 4 * cout, "unit": unit})
         hh, ww = sh, sw
         i += 2 if pool else 1
     return res
@@ -312,9 +313,10 @@ def main():
     for name, c, ms in zip(LAYER_NAMES, ae_layer_costs(), layer_ms):
         peak_c = MFMA_PEAK_TFLOPS if c["unit"] == "mfma" else VALU_DOT2_PEAK_TFLOPS
         t_c = c["flops"] * B / (peak_c * 1e12)
-        t_m = c["bytes"] * B / (HBM_PEAK_GBPS * 1e9)
+        nb = c["bytes"] * B + c["weight_bytes"]
+        t_m = nb / (HBM_PEAK_GBPS * 1e9)
         if t_m >= t_c:
-            ach = c["bytes"] * B / (ms * 1e-3) / 1e9
+            ach = nb / (ms * 1e-3) / 1e9
             rl = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                   "frac": ach / HBM_PEAK_GBPS}
         else:
@@ -322,7 +324,7 @@ def main():
             rl = {"bound": c["unit"], "achieved": ach, "peak": peak_c, "unit": "TFLOP/s",
                   "frac": ach / peak_c}
         tr = pmc.get(name)
-        rl.update({"layer": name, "kernel_ms": float(ms), "alg_bytes_per_launch": c["bytes"] * B,
+        rl.update({"layer": name, "kernel_ms": float(ms), "alg_bytes_per_launch": nb,
                    "flops_per_launch": c["flops"] * B,
                    "traffic": tr["hbm_bytes"] if tr else None,
                    "traffic_kernel": tr["kernel"] if tr else None})

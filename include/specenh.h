@@ -127,6 +127,7 @@ int specenh_svd_denoise_optimal(const float* A, long long batch, int m, int n, l
 #define SPECENH_DTYPE_F32 0
 #define SPECENH_DTYPE_BF16 1
 #define SPECENH_DTYPE_F16 2
+#define SPECENH_DTYPE_F64 3 /* label filters only */
 #define SPECENH_ACT_NONE 0
 #define SPECENH_ACT_RELU 1
 #define SPECENH_ACT_SIGMOID 2
@@ -191,6 +192,26 @@ int specenh_weight_flip_transpose(int dtype, const void* bt, int k, int ci, int 
 /* Element conversion between f32, bf16 and f16 (round to nearest even). */
 int specenh_cast(int src_dtype, const void* src, int dst_dtype, void* dst, long long n,
                  void* stream);
+
+/* ---------------------------------------------------------------- label filters
+ * The image-filter helpers of spec_denoising/pipeline_data.py:38-61 (the training-label
+ * chain) on a batch of spectrograms, each a rows x cols row-major block at
+ * S + b*stride (dtype SPECENH_DTYPE_F32 or _F64; out may alias S). Statistics are per
+ * spectrogram, accumulated in fp64:
+ *   SPECENH_FILTER_NORM     (x - mean) / std                 norm,     :38-41 (np.std, ddof 0)
+ *   SPECENH_FILTER_RESCALE  (x - min) / (max - min)          rescale,  :43-44
+ *   SPECENH_FILTER_MEANSUB  rescale(|x - mean of its row|)   meansub,  :58-61
+ * workspace >= specenh_filter_workspace_bytes(batch, rows).
+ * specenh_quantfilt: x < q(column) ? 0 : x with q the numpy 'linear' thr-quantile of each
+ * column (np.quantile(src, thr, axis=0), quantfilt :46-49); rows <= 1264. */
+#define SPECENH_FILTER_NORM 0
+#define SPECENH_FILTER_RESCALE 1
+#define SPECENH_FILTER_MEANSUB 2
+size_t specenh_filter_workspace_bytes(long long batch, int rows);
+int specenh_filter(int op, int dtype, const void* S, long long batch, int rows, int cols,
+                   long long stride, void* out, void* workspace, void* stream);
+int specenh_quantfilt(int dtype, const void* S, long long batch, int rows, int cols,
+                      long long stride, double thr, void* out, void* stream);
 
 /* ---------------------------------------------------------------- strip glue
  * patch / unpatch / reshape of VAE/manual_scan_3layers.py:28-54:

@@ -1,0 +1,283 @@
+// filters.hip — the label-generator helpers of spec_denoising/pipeline_data.py:38-61 on the
+// GPU: norm, rescale, meansub and quantfilt over a batch of spectrograms.
+//
+// Each spectrogram is one rows x cols block (row-major, like the reference's F x T arrays);
+// statistics are per spectrogram and accumulated in fp64. T = float or double: the numpy
+// API uploads the reference's float64 arrays unchanged, so the double path reproduces
+// numpy up to the order of its fp64 sums; elementwise results follow numpy's formulas in T.
+// quantfilt's per-column quantile is numpy's 'linear' method exactly: the virtual index
+// n*q + (1 - q) - 1 (numpy's alpha = beta = 1 expression, evaluated on the host), the two
+// neighbouring order statistics found by stable rank counting in LDS, numpy's two-sided
+// _lerp in fp64 (explicitly rounded operations, no contraction), then x < q ? 0 : x.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <string>
+
+#include "specenh.h"
+
+namespace specenh {
+int set_error(int code, const std::string& msg);  // stft_psd.hip
+
+namespace {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+__device__ double block_sum(double v, double* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__device__ void block_minmax(double& mn, double& mx, double* red) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    mn = fmin(mn, __shfl_xor(mn, m));
+    mx = fmax(mx, __shfl_xor(mx, m));
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = mn;
+    red[4 + (threadIdx.x >> 6)] = mx;
+  }
+  __syncthreads();
+  mn = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
+  mx = fmax(fmax(red[4], red[5]), fmax(red[6], red[7]));
+}
+
+// mean of every row (meansub, :59): one wave per row
+template <typename T>
+__global__ __launch_bounds__(256) void rowmean_kernel(const T* S, long long batch, int rows,
+                                                      int cols, long long stride, double* rm) {
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= batch * rows) return;
+  const long long b = row / rows;
+  const int r = (int)(row - b * rows);
+  const T* p = S + b * stride + (long long)r * cols;
+  double acc = 0.0;
+  for (int c = threadIdx.x & 63; c < cols; c += 64) acc += (double)p[c];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) rm[row] = acc / (double)cols;
+}
+
+// per-spectrogram statistics: NORM {mean, std}; RESCALE {min, max}; MEANSUB {min, max} of
+// |x - rowmean| (as T, like numpy's array of that dtype)
+template <typename T>
+__global__ __launch_bounds__(256) void stats_kernel(const T* S, int rows, int cols,
+                                                    long long stride, int op, const double* rm,
+                                                    double* stats) {
+  __shared__ double red[8];
+  const long long b = blockIdx.x;
+  const T* s = S + b * stride;
+  const long long n = (long long)rows * cols;
+  if (op == SPECENH_FILTER_NORM) {
+    double acc = 0.0;
+    for (long long e = threadIdx.x; e < n; e += 256) acc += (double)s[e];
+    const double mean = block_sum(acc, red) / (double)n;
+    double a2 = 0.0;
+    for (long long e = threadIdx.x; e < n; e += 256) {
+      const double d = (double)s[e] - mean;
+      a2 += d * d;
+    }
+    const double var = block_sum(a2, red) / (double)n;
+    if (threadIdx.x == 0) {
+      stats[2 * b] = mean;
+      stats[2 * b + 1] = sqrt(var);
+    }
+    return;
+  }
+  double mn = INFINITY, mx = -INFINITY;
+  for (long long e = threadIdx.x; e < n; e += 256) {
+    double v = (double)s[e];
+    if (op == SPECENH_FILTER_MEANSUB)
+      v = (double)(T)fabs((double)s[e] - rm[b * rows + e / cols]);
+    mn = fmin(mn, v);
+    mx = fmax(mx, v);
+  }
+  block_minmax(mn, mx, red);
+  if (threadIdx.x == 0) {
+    stats[2 * b] = mn;
+    stats[2 * b + 1] = mx;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void apply_kernel(const T* S, T* out, long long batch, int rows,
+                                                    int cols, long long stride, int op,
+                                                    const double* rm, const double* stats) {
+  const long long n = (long long)rows * cols;
+  const long long total = batch * n;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total;
+       i += (long long)gridDim.x * 256) {
+    const long long b = i / n, e = i - b * n;
+    const T x = S[b * stride + e];
+    const double s0 = stats[2 * b], s1 = stats[2 * b + 1];
+    T y;
+    if (op == SPECENH_FILTER_NORM) {  // (data - mn) / std
+      y = (T)(x - (T)s0) / (T)s1;
+    } else if (op == SPECENH_FILTER_RESCALE) {  // (data - min) / (max - min)
+      y = (T)(x - (T)s0) / (T)((T)s1 - (T)s0);
+    } else {  // rescale(|src - mn|)
+      const T d = (T)fabs((double)x - rm[b * rows + e / cols]);
+      y = (T)(d - (T)s0) / (T)((T)s1 - (T)s0);
+    }
+    out[b * stride + e] = y;
+  }
+}
+
+constexpr int QF_COLS = 16;  // columns per workgroup
+
+// quantfilt: order statistics lo/hi of each column by stable rank counting, numpy's lerp,
+// threshold. Columns of the tile live column-major in LDS.
+template <typename T>
+__global__ __launch_bounds__(256) void quantfilt_kernel(const T* S, T* out, int rows, int cols,
+                                                        long long stride, int lo, int hi,
+                                                        double gamma) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* col = reinterpret_cast<T*>(smem);  // [QF_COLS][rows]
+  __shared__ double sel[QF_COLS][2];
+  const long long b = blockIdx.y;
+  const int c0 = blockIdx.x * QF_COLS;
+  const int nc = min(QF_COLS, cols - c0);
+  const T* s = S + b * stride;
+  for (int idx = threadIdx.x; idx < rows * QF_COLS; idx += 256) {
+    const int r = idx / QF_COLS, c = idx - (idx / QF_COLS) * QF_COLS;
+    col[c * rows + r] = c < nc ? s[(long long)r * cols + c0 + c] : (T)0;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < rows * nc; idx += 256) {
+    const int c = idx / rows, i = idx - (idx / rows) * rows;
+    const T* v = col + c * rows;
+    const T vi = v[i];
+    int rank = 0;
+    for (int j = 0; j < rows; ++j) {
+      const T vj = v[j];
+      rank += (vj < vi) || (vj == vi && j < i);
+    }
+    if (rank == lo) sel[c][0] = (double)vi;
+    if (rank == hi) sel[c][1] = (double)vi;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < rows * nc; idx += 256) {
+    const int r = idx / nc, c = idx - (idx / nc) * nc;
+    const double a = sel[c][0], bb = sel[c][1];
+    const double diff = __dsub_rn(bb, a);  // numpy _lerp, :4653-4657
+    const double q = gamma >= 0.5 ? __dsub_rn(bb, __dmul_rn(diff, __dsub_rn(1.0, gamma)))
+                                  : __dadd_rn(a, __dmul_rn(diff, gamma));
+    const T x = col[c * rows + r];
+    out[b * stride + (long long)r * cols + c0 + c] = ((double)x < q) ? (T)0 : x;
+  }
+}
+
+inline unsigned grid_for(long long n) {
+  const long long g = (n + 255) / 256;
+  return (unsigned)(g < 1 ? 1 : (g > 65536 ? 65536 : g));
+}
+
+template <typename T>
+int run_filter(int op, const T* S, long long batch, int rows, int cols, long long stride, T* out,
+               double* ws, hipStream_t st) {
+  double* stats = ws;
+  double* rm = ws + 2 * batch;
+  if (op == SPECENH_FILTER_MEANSUB)
+    hipLaunchKernelGGL(rowmean_kernel<T>, dim3(grid_for(batch * rows * 64)), dim3(256), 0, st, S,
+                       batch, rows, cols, stride, rm);
+  hipLaunchKernelGGL(stats_kernel<T>, dim3((unsigned)batch), dim3(256), 0, st, S, rows, cols,
+                     stride, op, rm, stats);
+  hipLaunchKernelGGL(apply_kernel<T>, dim3(grid_for(batch * rows * cols)), dim3(256), 0, st, S,
+                     out, batch, rows, cols, stride, op, rm, stats);
+  return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "filter launch");
+}
+
+template <typename T>
+int run_quantfilt(const T* S, long long batch, int rows, int cols, long long stride, int lo,
+                  int hi, double gamma, T* out, hipStream_t st) {
+  const size_t lds = (size_t)rows * QF_COLS * sizeof(T);
+  if (hipFuncSetAttribute((const void*)quantfilt_kernel<T>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return set_error(SPECENH_EHIP, "quantfilt attribute");
+  for (long long b0 = 0; b0 < batch; b0 += 65535) {
+    const long long nb = std::min<long long>(65535, batch - b0);
+    hipLaunchKernelGGL(quantfilt_kernel<T>, dim3((cols + QF_COLS - 1) / QF_COLS, (unsigned)nb),
+                       dim3(256), lds, st, S + b0 * stride, out + b0 * stride, rows, cols, stride,
+                       lo, hi, gamma);
+  }
+  return hipGetLastError() == hipSuccess ? SPECENH_OK
+                                         : set_error(SPECENH_EHIP, "quantfilt launch");
+}
+
+int check_common(int dtype, const void* S, long long batch, int rows, int cols, long long stride,
+                 const void* out) {
+  if (dtype != SPECENH_DTYPE_F32 && dtype != SPECENH_DTYPE_F64)
+    return set_error(SPECENH_EINVAL, "filters take float32 or float64 spectrograms");
+  if (batch < 0 || rows <= 0 || cols <= 0) return set_error(SPECENH_EINVAL, "bad shape");
+  if (stride < (long long)rows * cols) return set_error(SPECENH_EINVAL, "stride < rows*cols");
+  if (batch > 0 && (!S || !out)) return set_error(SPECENH_EINVAL, "null pointer");
+  return SPECENH_OK;
+}
+
+}  // namespace
+}  // namespace specenh
+
+using namespace specenh;
+
+extern "C" {
+
+size_t specenh_filter_workspace_bytes(long long batch, int rows) {
+  if (batch <= 0 || rows <= 0) return 16;
+  return (size_t)batch * (2 + (size_t)rows) * sizeof(double);
+}
+
+int specenh_filter(int op, int dtype, const void* S, long long batch, int rows, int cols,
+                   long long stride, void* out, void* workspace, void* stream) {
+  if (int e = check_common(dtype, S, batch, rows, cols, stride, out)) return e;
+  if (op != SPECENH_FILTER_NORM && op != SPECENH_FILTER_RESCALE && op != SPECENH_FILTER_MEANSUB)
+    return set_error(SPECENH_EINVAL, "unknown filter op");
+  if (batch == 0) return SPECENH_OK;
+  if (!workspace) return set_error(SPECENH_EINVAL, "null workspace");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == SPECENH_DTYPE_F64)
+    return run_filter<double>(op, (const double*)S, batch, rows, cols, stride, (double*)out,
+                              (double*)workspace, st);
+  return run_filter<float>(op, (const float*)S, batch, rows, cols, stride, (float*)out,
+                           (double*)workspace, st);
+}
+
+int specenh_quantfilt(int dtype, const void* S, long long batch, int rows, int cols,
+                      long long stride, double thr, void* out, void* stream) {
+  if (int e = check_common(dtype, S, batch, rows, cols, stride, out)) return e;
+  if (!(thr >= 0.0 && thr <= 1.0)) return set_error(SPECENH_EINVAL, "Quantiles must be in the range [0, 1]");
+  if ((size_t)rows * QF_COLS * (dtype == SPECENH_DTYPE_F64 ? 8 : 4) > 160 * 1024 - 512)
+    return set_error(SPECENH_EUNSUPPORTED, "quantfilt on the GPU needs rows <= 1264");
+  if (batch == 0) return SPECENH_OK;
+  // numpy 'linear' (alpha = beta = 1): virtual index, neighbours, gamma (_quantile)
+  const double vi = (double)rows * thr + (1.0 + thr * (1.0 - 1.0 - 1.0)) - 1.0;
+  int lo, hi;
+  double gamma;
+  if (vi >= rows - 1) {
+    lo = hi = rows - 1;
+    gamma = 0.0;  // a == b: the lerp returns the maximum
+  } else if (vi < 0) {
+    lo = hi = 0;
+    gamma = 0.0;
+  } else {
+    const double fl = std::floor(vi);
+    lo = (int)fl;
+    hi = lo + 1;
+    gamma = vi - fl;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == SPECENH_DTYPE_F64)
+    return run_quantfilt<double>((const double*)S, batch, rows, cols, stride, lo, hi, gamma,
+                                 (double*)out, st);
+  return run_quantfilt<float>((const float*)S, batch, rows, cols, stride, lo, hi, gamma,
+                              (float*)out, st);
+}
+
+}  // extern "C"

@@ -24,6 +24,9 @@ SPECENH_EHIP = -3
 SPECENH_ENOMEM = -4
 SPECENH_ERANGE = -5
 SVD_OPTIMAL = 0
+FILTER_NORM = 0
+FILTER_RESCALE = 1
+FILTER_MEANSUB = 2
 SVD_COMPUTE = 1
 
 STFT_LOG = 1
@@ -90,6 +93,12 @@ SIGNATURES = {
                                                  _c.c_int, _c.c_void_p, _c.c_void_p]),
     "specenh_cast": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_void_p, _c.c_longlong,
                                 _c.c_void_p]),
+    "specenh_filter_workspace_bytes": (_c.c_size_t, [_c.c_longlong, _c.c_int]),
+    "specenh_filter": (_c.c_int, [_c.c_int, _c.c_int, _c.c_void_p, _c.c_longlong, _c.c_int,
+                                  _c.c_int, _c.c_longlong, _c.c_void_p, _c.c_void_p,
+                                  _c.c_void_p]),
+    "specenh_quantfilt": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_longlong, _c.c_int, _c.c_int,
+                                     _c.c_longlong, _c.c_double, _c.c_void_p, _c.c_void_p]),
     "specenh_strips_pack": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_longlong, _c.c_int, _c.c_int,
                                        _c.c_longlong, _c.c_int, _c.c_int, _c.c_int, _c.c_void_p,
                                        _c.c_void_p]),

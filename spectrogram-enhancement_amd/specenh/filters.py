@@ -1,0 +1,93 @@
+"""GPU label filters: norm / rescale / meansub / quantfilt of spec_denoising/pipeline_data.py
+(:38-61) through the C-ABI (csrc/filters.hip). The reference-named functions live in
+``specenh.pipeline_data``; this module holds the device paths.
+
+  * numpy input (the reference's float64 spectrograms): uploaded unchanged, computed in
+    fp64 on the GPU, returned as float64 numpy (numpy's formulas; fp64 sums reordered).
+  * torch input on the GPU (float32 / float64): device-resident; 2-D = one spectrogram,
+    3-D ``[B, rows, cols]`` = a batch, every spectrogram filtered independently.
+N-D numpy inputs keep the reference's whole-array semantics: norm / rescale over all
+elements, quantfilt per column of axis 0, meansub over axis 1 with one global rescale.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_DT = {torch.float32: 0, torch.float64: 3}
+
+
+def _device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("specenh requires a ROCm GPU (HIP); there is no CPU fallback")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _run(kind, t: torch.Tensor, arg):
+    """t: contiguous device tensor [B, rows, cols] float32/float64."""
+    if t.device.type != "cuda":
+        raise RuntimeError("specenh.filters runs on the GPU only (no CPU fallback)")
+    if t.dtype not in _DT:
+        t = t.double()
+    t = t.contiguous()
+    B, rows, cols = t.shape
+    out = torch.empty_like(t)
+    L = _lib.lib()
+    st = ctypes.c_void_p(_lib.current_stream_handle(t.device))
+    if kind == "quantfilt":
+        _lib.check(L.specenh_quantfilt(_DT[t.dtype], ctypes.c_void_p(t.data_ptr()), B, rows, cols,
+                                       rows * cols, float(arg), ctypes.c_void_p(out.data_ptr()),
+                                       st), "quantfilt")
+    else:
+        ws = torch.empty(max(16, int(L.specenh_filter_workspace_bytes(B, rows))),
+                         dtype=torch.uint8, device=t.device)
+        _lib.check(L.specenh_filter(arg, _DT[t.dtype], ctypes.c_void_p(t.data_ptr()), B, rows,
+                                    cols, rows * cols, ctypes.c_void_p(out.data_ptr()),
+                                    ctypes.c_void_p(ws.data_ptr()), st), kind)
+    return out
+
+
+def _apply(kind, src, arg, to2d, back):
+    if isinstance(src, torch.Tensor):
+        if src.dim() == 2:
+            return _run(kind, src.unsqueeze(0), arg)[0]
+        if src.dim() == 3:
+            return _run(kind, src, arg)
+        raise ValueError("device tensors must be [rows, cols] or [batch, rows, cols]")
+    a = np.asarray(src)
+    if a.dtype != np.float32:
+        a = a.astype(np.float64)
+    a2 = to2d(a)
+    t = torch.as_tensor(np.ascontiguousarray(a2), device=_device()).unsqueeze(0)
+    return back(_run(kind, t, arg)[0].cpu().numpy(), a)
+
+
+def norm(data):
+    return _apply("norm", data, _lib.FILTER_NORM, lambda a: a.reshape(1, -1),
+                  lambda r, a: r.reshape(a.shape))
+
+
+def rescale(data):
+    return _apply("rescale", data, _lib.FILTER_RESCALE, lambda a: a.reshape(1, -1),
+                  lambda r, a: r.reshape(a.shape))
+
+
+def quantfilt(src, thr=0.9):
+    return _apply("quantfilt", src, thr, lambda a: a.reshape(a.shape[0], -1),
+                  lambda r, a: r.reshape(a.shape))
+
+
+def meansub(src):
+    def to2d(a):  # rows = every index but axis 1, cols = axis 1
+        m = np.moveaxis(a, 1, -1)
+        return m.reshape(-1, a.shape[1])
+
+    def back(r, a):
+        m = np.moveaxis(a, 1, -1)
+        return np.moveaxis(r.reshape(m.shape), -1, 1)
+
+    return _apply("meansub", src, _lib.FILTER_MEANSUB, to2d, back)

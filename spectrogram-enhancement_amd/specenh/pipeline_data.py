@@ -12,10 +12,10 @@ arrays like the reference (computed in fp32 on the device; tolerance in
 DESIGN.md). ``specgr_batch`` is the tensor-in/tensor-out fast path that keeps
 data on the device.
 
-The image-filter helpers ``norm/rescale/quantfilt/meansub`` (:38-61) are the
-label-generator chain; they are SURVEY §8(f1) ("next") and currently accept
-numpy (exact reference arithmetic) or device tensors (torch ops on the device).
-``gaussblr``/``morph`` need OpenCV semantics (cv2 is absent here): not yet built.
+The image-filter helpers ``norm/rescale/quantfilt/meansub`` (:38-61), the
+label-generator chain, run as HIP kernels too (csrc/filters.hip):
+numpy inputs come back as float64 numpy, device tensors stay on the device.
+``gaussblr``/``morph`` need OpenCV semantics (cv2 is absent here): not built.
 """
 from __future__ import annotations
 
@@ -24,6 +24,7 @@ import pickle
 import numpy as np
 import torch
 
+from . import filters as _filters
 from . import stft as _stft
 
 
@@ -78,39 +79,26 @@ def specgr(fname, ecen, spec_params, cut_shot=2, key_format="\\tecef%.2i", field
 
 
 # ------------------------------------------------------------- filter helpers
-def _is_tensor(a):
-    return isinstance(a, torch.Tensor)
-
-
+# The label-generator chain (:38-61) on the GPU (csrc/filters.hip via specenh.filters):
+# numpy in -> numpy out (float64, like the reference), device tensors stay on the device.
 def norm(data):
-    """pipeline_data.py:38-41."""
-    if _is_tensor(data):
-        return (data - data.mean()) / data.std(unbiased=False)
-    mn = data.mean()
-    std = data.std()
-    return (data - mn) / std
+    """pipeline_data.py:38-41: (data - mean) / std over the whole array."""
+    return _filters.norm(data)
 
 
 def rescale(data):
-    """pipeline_data.py:43-44."""
-    return (data - data.min()) / (data.max() - data.min())
+    """pipeline_data.py:43-44: min-max to [0, 1] over the whole array."""
+    return _filters.rescale(data)
 
 
 def quantfilt(src, thr=0.9):
-    """pipeline_data.py:46-49: zero entries below their column's thr-quantile."""
-    if _is_tensor(src):
-        filt = torch.quantile(src, thr, dim=0, interpolation="linear")
-        return torch.where(src < filt, torch.zeros_like(src), src)
-    filt = np.quantile(src, thr, axis=0)
-    return np.where(src < filt, 0, src)
+    """pipeline_data.py:46-49: zero entries below their column's thr-quantile (axis 0)."""
+    return _filters.quantfilt(src, thr)
 
 
 def meansub(src):
-    """pipeline_data.py:58-61."""
-    if _is_tensor(src):
-        return rescale((src - src.mean(dim=1, keepdim=True)).abs())
-    mn = np.mean(src, axis=1)[:, np.newaxis]
-    return rescale(np.absolute(src - mn))
+    """pipeline_data.py:58-61: |src - mean over axis 1|, then rescale."""
+    return _filters.meansub(src)
 
 
 def gaussblr(src, filt=(31, 3)):

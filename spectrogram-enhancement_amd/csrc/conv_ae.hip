@@ -410,23 +410,47 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   return v;
 }
 
-template <typename T, int NT, int CC, bool POOL>
-__global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
-  constexpr int TILE = 16, PMAX = 20;
+// PAIR (Conv2DTranspose, stride 2): the workgroup owns one output-row phase py of a tile
+// and computes its two column phases (py, 0) and (py, 1) over one staged patch. Phase
+// (py, 0) waits in registers, packed to T; after (py, 1) the patch is dead, so both are
+// interleaved into an LDS image of the 16 output rows x 32 pixels x CO channels that
+// aliases the patch, and leave as 16-byte stores of whole rows. Without it every 128-B
+// output line is completed by two phase stores microseconds apart, and the half-written
+// line is evicted in between (2-2.6x the algorithmic write traffic). The
+// two row phases of a tile run on one XCD back to back and share its input lines in L2.
+template <int CC, int NT, bool PAIR>
+struct PatchLds {
+  static constexpr int patch = 20 * 20 * Patch<CC>::PST;
+  static constexpr int stage = 16 * 16 * (32 * NT + 8);  // 16 rows x 16 pixel pairs, padded
+  static constexpr int elems = PAIR && stage > patch ? stage : patch;
+};
+
+template <typename T, int NT, int CC, bool POOL, bool PAIR = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PAIR && NT == 1 ? 4 : 1)))
+void conv_patch_kernel(ConvArgs a) {
+  constexpr int TILE = 16;
   constexpr int PST = Patch<CC>::PST;
   constexpr int MT = 4;  // output rows per wave
-  __shared__ __attribute__((aligned(16))) T sP[PMAX * PMAX * PST];
+  __shared__ __attribute__((aligned(16))) T sP[PatchLds<CC, NT, PAIR>::elems];
   __shared__ int sTap[MAXPH][32];  // patch offset of tap t (elements), -1 past the last tap
   __shared__ int sCol[MAXPH][32];  // weight column of tap t at ci = 0
 
-  // ---- phases of this workgroup: all of them over one shared patch, or blockIdx.z ----
-  const bool shared = a.ph_shared != 0;
-  const int ph_lo = shared ? 0 : (int)blockIdx.z, ph_hi = shared ? a.nph : ph_lo + 1;
+  // ---- phases of this workgroup: all of them over one shared patch, a row-phase pair
+  // (PAIR), or blockIdx.z ----
+  int bx = (int)blockIdx.x, pyp = 0;
+  if constexpr (PAIR) {  // blocks 16q + 8py + x: tile 8q + x, row phase py, XCD x
+    const int j = bx >> 3;
+    pyp = j & 1;
+    bx = (j >> 1) * 8 + (bx & 7);
+  }
+  const bool shared = PAIR || a.ph_shared != 0;
+  const int ph_lo = PAIR ? 2 * pyp : (shared ? 0 : (int)blockIdx.z);
+  const int ph_hi = PAIR ? ph_lo + 2 : (shared ? a.nph : ph_lo + 1);
   const Geo& g0 = a.g[ph_lo];
   const int ntx = (g0.OW + TILE - 1) / TILE, nty = (g0.OH + TILE - 1) / TILE;
-  if ((int)blockIdx.x >= g0.N * nty * ntx) return;
-  const int n = blockIdx.x / (nty * ntx);
-  const int trem = blockIdx.x - n * (nty * ntx);
+  if (bx >= g0.N * nty * ntx) return;
+  const int n = bx / (nty * ntx);
+  const int trem = bx - n * (nty * ntx);
   const int ty = trem / ntx, tx = trem - (trem / ntx) * ntx;
   const int oy0 = ty * TILE, ox0 = tx * TILE;
   const int upt = shared ? a.upt : g0.pad_t, upl = shared ? a.upl : g0.pad_l;
@@ -462,13 +486,17 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
       }
     } else {
       constexpr int GP = CC / 8;  // 8-channel groups per pixel
+      // pix / PW as a multiply-shift (exact: pix * (PW - 1) < 2^16), 32-bit offsets
+      // (check_sizes bounds every tensor below 2^31 elements)
+      const int pwinv = (65536 + PW - 1) / PW;
+      const int IHl = g0.IH, IWl = g0.IW, Cl = g0.C;
+      const T* __restrict__ inb = in + n * IHl * IWl * Cl + c * CC;
       for (int e = tid; e < PH * PW * GP; e += 256) {
         const int pix = e / GP, cg = e - (e / GP) * GP;
-        const int py = pix / PW, pxx = pix - (pix / PW) * PW;
+        const int py = (pix * pwinv) >> 16, pxx = pix - py * PW;
         const int iy = iy0 + py, ix = ix0 + pxx;
-        const bool ok = (unsigned)iy < (unsigned)g0.IH && (unsigned)ix < (unsigned)g0.IW;
-        const uint4 v = ok ? *reinterpret_cast<const uint4*>(
-                                 in + ((n * g0.IH + iy) * g0.IW + ix) * g0.C + c * CC + 8 * cg)
+        const bool ok = (unsigned)iy < (unsigned)IHl && (unsigned)ix < (unsigned)IWl;
+        const uint4 v = ok ? *reinterpret_cast<const uint4*>(inb + (iy * IWl + ix) * Cl + 8 * cg)
                            : uint4{0u, 0u, 0u, 0u};
         *reinterpret_cast<uint4*>(sP + pix * PST + 8 * cg) = v;
       }
@@ -476,6 +504,7 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
   };
 
   const int nchunk = CC == 1 ? 1 : g0.C / CC;
+  uint32_t hold[MT][NT][2];  // PAIR: phase (py, 0), packed to T
   for (int p = ph_lo; p < ph_hi; ++p) {
     const Geo& g = a.g[p];
     const int ntap = g.KH * g.KW;
@@ -491,73 +520,133 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
         stage(c);
         lds_sync();
       }
-      // ---- k-steps: one MFMA K=32 slab each; weights are the A operand (rows = output
-      // channels), the patch the B operand (columns = pixels): D[channel][pixel] ----
-      constexpr int SUB = CC >= 32 ? CC / 32 : 1;  // 32-channel slabs per tap
-      const int nsteps = CC >= 32 ? ntap * SUB : (CC == 16 ? (ntap + 1) / 2 : 1);
-      auto load_w = [&](int st, V8<T> (&b)[NT]) {
+      if constexpr (CC >= 32) {
+        // ---- k-steps: one MFMA K=32 slab each; weights are the A operand (rows = output
+        // channels), the patch the B operand (columns = pixels): D[channel][pixel]. Tap
+        // geometry is wave-uniform scalar arithmetic; weight loads are unconditional from
+        // clamped rows (a clamped row only feeds output channels >= CO, never stored), so
+        // the prefetch ring has no branches and no WAW waits on in-flight loads ----
+        constexpr int SUB = CC / 32;  // 32-channel slabs per tap
+        const int KWl = g.KW, Kfl = g.Kf, Cl = g.C, KWf = g.KWf, ks = g.kstep;
+        const int ky0 = g.ky0, kx0 = g.kx0;
+        const int dy = upt - g.pad_t, dx = upl - g.pad_l;  // this phase's shift in the patch
+        const int kwinv = (65536 + KWl - 1) / KWl;         // t / KW == (t * kwinv) >> 16, t < 32
+        const int nsteps = ntap * SUB;
+        const T* wl[NT];
 #pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          const int co = n0 + 16 * j + px;
-          zero8(b[j]);
+        for (int j = 0; j < NT; ++j)
+          wl[j] = W + (long long)min(n0 + 16 * j + px, g.CO - 1) * Kfl + c * CC + 8 * kgrp;
+        auto wcol_of = [&](int st) {
+          const int t = st / SUB, h = st - (st / SUB) * SUB;
+          const int jy = (t * kwinv) >> 16, jx = t - jy * KWl;
+          return ((ky0 + ks * jy) * KWf + kx0 + ks * jx) * Cl + 32 * h;
+        };
+        auto aoff_of = [&](int st) {
+          const int t = st / SUB, h = st - (st / SUB) * SUB;
+          const int jy = (t * kwinv) >> 16, jx = t - jy * KWl;
+          return ((jy + dy) * PW + jx + dx) * PST + 32 * h;
+        };
+        constexpr int PD = NT >= 3 ? (CC == 64 ? 1 : 2) : (NT == 2 ? 2 : 8);
+        V8<T> wring[PD][NT];
+#pragma unroll
+        for (int u = 0; u < PD; ++u)
+          if (u < nsteps) {
+            const int col = wcol_of(u);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) wring[u][j] = ld8(wl[j] + col);
+          }
+        for (int s0 = 0; s0 < nsteps; s0 += PD)
+#pragma unroll
+        for (int u = 0; u < PD; ++u) {
+          const int st = s0 + u;
+          if (st >= nsteps) break;
+          V8<T> wcur[NT];
+#pragma unroll
+          for (int j = 0; j < NT; ++j) wcur[j] = wring[u][j];
+          if (st + PD < nsteps) {
+            const int col = wcol_of(st + PD);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) wring[u][j] = ld8(wl[j] + col);
+          }
+          const int aoff = aoff_of(st) + 8 * kgrp;
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            const uint4 q = *reinterpret_cast<const uint4*>(sP + rbase[i] + aoff);  // ds_read_b128
+            V8<T> pv;
+            pv.w[0] = q.x; pv.w[1] = q.y; pv.w[2] = q.z; pv.w[3] = q.w;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wcur[j], pv, acc[i][j]);
+          }
+        }
+      } else {
+        // ---- k-steps: one MFMA K=32 slab each; weights are the A operand (rows = output
+        // channels), the patch the B operand (columns = pixels): D[channel][pixel] ----
+        constexpr int SUB = CC >= 32 ? CC / 32 : 1;  // 32-channel slabs per tap
+        const int nsteps = CC >= 32 ? ntap * SUB : (CC == 16 ? (ntap + 1) / 2 : 1);
+        auto load_w = [&](int st, V8<T> (&b)[NT]) {
+  #pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            const int co = n0 + 16 * j + px;
+            zero8(b[j]);
+            if constexpr (CC >= 32) {
+              const int t = st / SUB, h = st - (st / SUB) * SUB;
+              if (co < g.CO) b[j] = ld8(W + co * g.Kf + sCol[p][t] + c * CC + 32 * h + 8 * kgrp);
+            } else if constexpr (CC == 16) {
+              const int t = 2 * st + (kgrp >> 1);
+              if (co < g.CO && t < ntap) b[j] = ld8(W + co * g.Kf + sCol[p][t] + 8 * (kgrp & 1));
+            } else {
+  #pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                const int t = 8 * kgrp + q;
+                if (co < g.CO && t < ntap) set_elem(b[j], q, W[co * g.Kf + sCol[p][t]]);
+              }
+            }
+          }
+        };
+        // weight fragments PD k-steps ahead in a register ring: they come from L2, and one
+        // k-step of MFMA work (4*NT MFMAs, 64-256 cycles) does not cover that latency
+        constexpr int PD = NT >= 3 ? (CC == 64 ? 1 : 2) : (NT == 2 ? 2 : 8);
+        V8<T> wring[PD][NT];
+  #pragma unroll
+        for (int u = 0; u < PD; ++u)
+          if (u < nsteps) load_w(u, wring[u]);
+        for (int s0 = 0; s0 < nsteps; s0 += PD)
+  #pragma unroll
+        for (int u = 0; u < PD; ++u) {
+          const int st = s0 + u;
+          if (st >= nsteps) break;
+          V8<T> wcur[NT];
+  #pragma unroll
+          for (int j = 0; j < NT; ++j) wcur[j] = wring[u][j];
+          if (st + PD < nsteps) load_w(st + PD, wring[u]);
+          int aoff = 0;
+          bool aon = true;
           if constexpr (CC >= 32) {
             const int t = st / SUB, h = st - (st / SUB) * SUB;
-            if (co < g.CO) b[j] = ld8(W + co * g.Kf + sCol[p][t] + c * CC + 32 * h + 8 * kgrp);
+            aoff = sTap[p][t] + 32 * h + 8 * kgrp;
           } else if constexpr (CC == 16) {
             const int t = 2 * st + (kgrp >> 1);
-            if (co < g.CO && t < ntap) b[j] = ld8(W + co * g.Kf + sCol[p][t] + 8 * (kgrp & 1));
-          } else {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              const int t = 8 * kgrp + q;
-              if (co < g.CO && t < ntap) set_elem(b[j], q, W[co * g.Kf + sCol[p][t]]);
-            }
+            aon = t < ntap;
+            aoff = (aon ? sTap[p][t] : 0) + 8 * (kgrp & 1);
           }
-        }
-      };
-      // weight fragments PD k-steps ahead in a register ring: they come from L2, and one
-      // k-step of MFMA work (4*NT MFMAs, 64-256 cycles) does not cover that latency
-      constexpr int PD = NT >= 3 ? (CC == 64 ? 1 : 2) : (NT == 2 ? 2 : 8);
-      V8<T> wring[PD][NT];
-#pragma unroll
-      for (int u = 0; u < PD; ++u)
-        if (u < nsteps) load_w(u, wring[u]);
-      for (int s0 = 0; s0 < nsteps; s0 += PD)
-#pragma unroll
-      for (int u = 0; u < PD; ++u) {
-        const int st = s0 + u;
-        if (st >= nsteps) break;
-        V8<T> wcur[NT];
-#pragma unroll
-        for (int j = 0; j < NT; ++j) wcur[j] = wring[u][j];
-        if (st + PD < nsteps) load_w(st + PD, wring[u]);
-        int aoff = 0;
-        bool aon = true;
-        if constexpr (CC >= 32) {
-          const int t = st / SUB, h = st - (st / SUB) * SUB;
-          aoff = sTap[p][t] + 32 * h + 8 * kgrp;
-        } else if constexpr (CC == 16) {
-          const int t = 2 * st + (kgrp >> 1);
-          aon = t < ntap;
-          aoff = (aon ? sTap[p][t] : 0) + 8 * (kgrp & 1);
-        }
-#pragma unroll
-        for (int i = 0; i < MT; ++i) {
-          V8<T> pv;
-          if constexpr (CC == 1) {
-            zero8(pv);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              const int off = sTap[p][8 * kgrp + q];
-              if (off >= 0) set_elem(pv, q, sP[rbase[i] + off]);
+  #pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            V8<T> pv;
+            if constexpr (CC == 1) {
+              zero8(pv);
+  #pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                const int off = sTap[p][8 * kgrp + q];
+                if (off >= 0) set_elem(pv, q, sP[rbase[i] + off]);
+              }
+            } else {
+              const uint4 u = *reinterpret_cast<const uint4*>(sP + rbase[i] + aoff);  // ds_read_b128
+              pv.w[0] = u.x; pv.w[1] = u.y; pv.w[2] = u.z; pv.w[3] = u.w;
+              if (!aon) zero8(pv);
             }
-          } else {
-            const uint4 u = *reinterpret_cast<const uint4*>(sP + rbase[i] + aoff);  // ds_read_b128
-            pv.w[0] = u.x; pv.w[1] = u.y; pv.w[2] = u.z; pv.w[3] = u.w;
-            if (!aon) zero8(pv);
+  #pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wcur[j], pv, acc[i][j]);
           }
-#pragma unroll
-          for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wcur[j], pv, acc[i][j]);
         }
       }
     }
@@ -620,6 +709,77 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a) {
                 }
             }
           }
+        }
+      }
+    } else if constexpr (PAIR) {
+      uint32_t pk[MT][NT][2];
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          V8<T> q;
+          zero8(q);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) set_elem(q, r, from_f<T>(apply_act(acc[i][j][r] + bv[j][r], a.act)));
+          pk[i][j][0] = q.w[0];
+          pk[i][j][1] = q.w[1];
+        }
+      if (p == ph_lo) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            hold[i][j][0] = pk[i][j][0];
+            hold[i][j][1] = pk[i][j][1];
+          }
+      } else {
+        constexpr int CO = 16 * NT;  // the workgroup holds every channel (host-checked)
+        constexpr int PS = 2 * CO + 8;  // a pixel pair + 16 B: spreads the lanes' 8-B writes
+        constexpr int QV = 2 * CO / 8;  // 16-byte vectors per pixel pair
+        lds_sync();  // every wave's fragment reads of the patch are done
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            const int o = ((wave * MT + i) * 16 + px) * PS + 16 * j + 4 * kgrp;
+            *reinterpret_cast<uint2*>(sP + o) = uint2{hold[i][j][0], hold[i][j][1]};
+            *reinterpret_cast<uint2*>(sP + o + CO) = uint2{pk[i][j][0], pk[i][j][1]};
+          }
+        lds_sync();
+        T* __restrict__ out = reinterpret_cast<T*>(a.out);
+        const int obase = ((n * g.OHs + pyp) * g.OWs + 2 * ox0) * CO;
+        for (int e = tid; e < 16 * 16 * QV; e += 256) {
+          const int r = e / (16 * QV), c = e - r * (16 * QV);  // row, vector in the row
+          const int q = c / QV;                                 // pixel pair = input column
+          if (oy0 + r >= g.OH || ox0 + q >= g.OW) continue;
+          const int o = obase + 2 * (oy0 + r) * g.OWs * CO + 8 * c;
+          *reinterpret_cast<uint4*>(out + o) =
+              *reinterpret_cast<const uint4*>(sP + (r * 16 + q) * PS + 8 * (c - q * QV));
+        }
+      }
+    } else if (!a.mask && !a.logits && !a.out_f32 && (g.CO & 3) == 0 && a.act <= 1) {
+      // the inference/activation-store path: 32-bit offsets, branch-free ReLU, 8-byte stores
+      const bool relu = a.act == 1;
+      const int CO = g.CO, OWs = g.OWs;
+      const int pbase = (n * g.OHs + g.oy0) * OWs + g.ox0 + ox * g.oxs;
+      T* __restrict__ out = reinterpret_cast<T*>(a.out);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int oy = oy0 + wave * MT + i;
+        if (oy >= g.OH || ox >= g.OW) continue;
+        const int o = (pbase + oy * g.oys * OWs) * CO;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int ch0 = n0 + 16 * j + 4 * kgrp;
+          if (ch0 >= CO) continue;
+          V8<T> pk;
+          zero8(pk);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = acc[i][j][r] + bv[j][r];
+            set_elem(pk, r, from_f<T>(relu ? fmaxf(v, 0.f) : v));
+          }
+          *reinterpret_cast<uint2*>(out + o + ch0) = uint2{pk.w[0], pk.w[1]};
         }
       }
     } else {
@@ -1006,6 +1166,24 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
     tiles = std::max(tiles, (unsigned)(a.g[i].N * ((a.g[i].OH + 15) / 16) * ((a.g[i].OW + 15) / 16)));
   const int CO = a.g[0].CO;
   const int nt = std::min(4, (CO + 15) / 16);
+  // Conv2DTranspose stride 2: (tile, row phase) workgroups with whole-row stores
+  bool pair = a.ph_shared && nph == 4 && !a.pool && !a.mask && !a.logits && !a.out_f32 &&
+              CO == 16 * nt && getenv_flag("SPECENH_CONVT_PAIR");
+  for (int i = 0; pair && i < nph; ++i) {
+    const Geo& g = a.g[i];
+    pair = g.oys == 2 && g.oxs == 2 && g.oy0 == i / 2 && g.ox0 == i % 2 && g.OHs == 2 * g.OH &&
+           g.OWs == 2 * g.OW;
+  }
+  if (pair) {
+    const dim3 grid2((tiles + 7) / 8 * 16, 1, 1);
+#define SPECENH_PAIR(NT) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC, false, true>), grid2, dim3(256), 0, st, a)
+    if (nt == 1) SPECENH_PAIR(1);
+    else if (nt == 2) SPECENH_PAIR(2);
+    else if (nt == 3) SPECENH_PAIR(3);
+    else SPECENH_PAIR(4);
+#undef SPECENH_PAIR
+    return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "conv launch");
+  }
   const dim3 grid(tiles, (unsigned)((CO + 16 * nt - 1) / (16 * nt)), a.ph_shared ? 1 : nph);
 #define SPECENH_PATCH(NT, P) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC, P>), grid, dim3(256), 0, st, a)
   if (a.pool) {

@@ -426,3 +426,30 @@ def test_fused_conv_pool_is_bitwise_identical_to_unfused(gpu_device, dtype):
         grads.append(eng.g.clone())
     assert torch.equal(outs[0], outs[1])
     assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.parametrize("dtype", ["mixed_bfloat16", "float16"])
+@pytest.mark.parametrize("hw", [(128, 128), (40, 56), (24, 8)])
+def test_convt_row_phase_pairs_bitwise_identical(gpu_device, dtype, hw, monkeypatch):
+    """Conv2DTranspose forward in (tile, row-phase) workgroups with LDS-staged whole-row
+    stores (opt-in: SPECENH_CONVT_PAIR=1, measured slower) gives the same
+    bits as the four-phase workgroups with per-phase stores, at
+    tile-aligned and ragged sizes, in inference and in training (which keeps the
+    per-phase path only where it needs the pre-activation)."""
+    ops = ref_model_ops()
+    H, W = hw
+    eng, _ = make(ops, (H, W, 1), dtype=dtype, seed=43)
+    rng = np.random.default_rng(12)
+    x = rng.uniform(0, 1, (5, H, W, 1)).astype(np.float32)
+    y = rng.uniform(0, 1, (5, H, W, 1)).astype(np.float32)
+    outs, grads = [], []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SPECENH_CONVT_PAIR", flag)
+        outs.append(eng.forward(upload(eng, x), train=False).clone())
+        eng.forward(upload(eng, x), train=True)
+        eng.loss_and_grad(upload(eng, y))
+        eng.backward()
+        grads.append(eng.g.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(grads[0], grads[1])

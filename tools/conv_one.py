@@ -34,8 +34,10 @@ def main():
         kind, cin, cout, H, pool = LAYERS[name]
         ops = [ae.ConvOp(kind, cin, cout, 5, "sigmoid" if name == "last" else "relu",
                          stride=2 if kind == "convT" else 1)]
-        if pool:  # pool + a 1x1-free tail so the pool is fused as in the model
+        if pool:  # pool + a 1x1 tail so the pool is fused as in the model
             ops += [ae.PoolOp(), ae.ConvOp("conv", cout, 16, 1, "relu")]
+        elif kind == "convT":  # a 1x1 tail: the layer writes T activations as in the model
+            ops += [ae.ConvOp("conv", cout, 16, 1, "relu")]
         eng = ae.AutoencoderEngine(ops, (H, H, cin), compute_dtype=a.dtype, device="cuda:0")
         rng = np.random.default_rng(0)
         ws = []

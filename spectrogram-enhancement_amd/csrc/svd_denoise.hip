@@ -134,6 +134,82 @@ __device__ void gemm_GZ(const float* G, int r, const float* sZ, float* sY) {
   }
 }
 
+// P = 8 (the default K = 1 subspace) ------------------------------------------------
+// The generic helpers above give each output to one thread, which then walks all r rows:
+// latency chains of r dependent LDS reads (cholqr's Gram, Rayleigh-Ritz) or of r/8
+// batches of L2 loads (G Z). With P = 8 every thread of the workgroup takes part instead.
+
+// out[a][b] = sum_i A[i][a] B[i][b] in fp64 for all 8 x 8 (a, b). Lane (row i, quarter q)
+// forms the 16 products of rows a in {2q, 2q + 1}; the 16 lanes of a quarter sum by
+// butterflies, the 4 waves through sPart[4][64]. Ends with the result visible to all.
+__device__ void prod8(const float* sA, const float* sB, int r, double* sPart, double* out) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4;
+  double acc[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) acc[k] = 0.0;
+  for (int i = 16 * wave + (lane & 15); i < r; i += 16 * (SS_THREADS / 64)) {
+    const float2 a = *reinterpret_cast<const float2*>(sA + i * 8 + 2 * q);
+    const float4 b0 = *reinterpret_cast<const float4*>(sB + i * 8);
+    const float4 b1 = *reinterpret_cast<const float4*>(sB + i * 8 + 4);
+    const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[k] = fma((double)(k < 8 ? a.x : a.y), (double)bv[k & 7], acc[k]);
+  }
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[k] += __shfl_xor(acc[k], m);
+  if ((lane & 15) == 0)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sPart[wave * 64 + 16 * q + k] = acc[k];
+  __syncthreads();
+  if (tid < 64) {
+    double v = 0.0;
+#pragma unroll
+    for (int w = 0; w < SS_THREADS / 64; ++w) v += sPart[w * 64 + tid];
+    out[tid] = v;
+  }
+  __syncthreads();
+}
+
+// Y = G Z for P = 8: thread (row i, j-half) sums over half of the rows of G with 16 loads
+// in flight; the two halves meet in sT (r x 8).
+__device__ void gemm_GZ8(const float* G, int r, const float* sZ, float* sY, float* sT) {
+  const int tid = threadIdx.x, jh = tid >> 7;
+  const int half = (r + 1) / 2, j0 = jh * half, j1 = jh ? r : half;
+  for (int i = tid & 127; i < r; i += 128) {
+    float acc[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+    int j = j0;
+    for (; j + 16 <= j1; j += 16) {
+      float g[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) g[u] = G[(long long)(j + u) * r + i];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const float4 z0 = *reinterpret_cast<const float4*>(sZ + (j + u) * 8);
+        const float4 z1 = *reinterpret_cast<const float4*>(sZ + (j + u) * 8 + 4);
+        acc[0] = fmaf(g[u], z0.x, acc[0]); acc[1] = fmaf(g[u], z0.y, acc[1]);
+        acc[2] = fmaf(g[u], z0.z, acc[2]); acc[3] = fmaf(g[u], z0.w, acc[3]);
+        acc[4] = fmaf(g[u], z1.x, acc[4]); acc[5] = fmaf(g[u], z1.y, acc[5]);
+        acc[6] = fmaf(g[u], z1.z, acc[6]); acc[7] = fmaf(g[u], z1.w, acc[7]);
+      }
+    }
+    for (; j < j1; ++j) {
+      const float gj = G[(long long)j * r + i];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[c] = fmaf(gj, sZ[j * 8 + c], acc[c]);
+    }
+    float* dst = jh ? sT : sY;
+    *reinterpret_cast<float4*>(dst + i * 8) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *reinterpret_cast<float4*>(dst + i * 8 + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  }
+  __syncthreads();
+  for (int idx = tid; idx < r * 8; idx += SS_THREADS) sY[idx] += sT[idx];
+  __syncthreads();
+}
+
 // Orthonormalise the columns of Y (r x P, LDS) into Z with CholeskyQR in fp64:
 // S = Y^T Y, S = R^T R, Z = Y R^-1. fp64 keeps the Gram of Y (condition up to ~1e12
 // here) factorisable; callers run it twice (CholeskyQR2) for fp32-level orthogonality.
@@ -141,6 +217,9 @@ template <int P>
 __device__ void cholqr(const float* sY, float* sZ, int r, double* sS, double* sRi) {
   const int tid = threadIdx.x;
   constexpr int NPAIRS = P * (P + 1) / 2;
+  if constexpr (P == 8) {
+    prod8(sY, sY, r, sS + 2 * P * P, sS);  // scratch [4][64] past sS, sRi (SsLayout)
+  } else
   for (int q = tid; q < NPAIRS; q += SS_THREADS) {
     int a = 0, rem = q;
     while (rem >= P - a) {
@@ -268,11 +347,13 @@ __device__ void jacobi(float* sH, float* sQ, float* sCS, int* sPair) {
   }
 }
 
+// P = 8 adds the prod8 scratch ([4][64] doubles after sRi) and gemm_GZ8's sT (r x 8).
 template <int P>
 struct SsLayout {
+  static constexpr int part = P == 8 ? 4 * 64 : 0;  // doubles
   static size_t bytes(int r) {
-    return (size_t)2 * r * P * 4 + (size_t)2 * P * P * 8 + (size_t)2 * P * P * 4 + P * 4 + P * 8 +
-           64;
+    return (size_t)2 * r * P * 4 + (size_t)(2 * P * P + part) * 8 + (size_t)2 * P * P * 4 +
+           P * 4 + P * 8 + 64 + (P == 8 ? (size_t)r * 8 * 4 : 0);
   }
 };
 
@@ -284,25 +365,31 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* sS = reinterpret_cast<double*>(smem);            // P x P
   double* sRi = sS + P * P;                                  // P x P
-  float* sZ = reinterpret_cast<float*>(sRi + P * P);        // r x P
+  double* sPart = sRi + P * P;                               // SsLayout<P>::part
+  float* sZ = reinterpret_cast<float*>(sPart + SsLayout<P>::part);  // r x P
   float* sY = sZ + r * P;                                    // r x P
   float* sH = sY + r * P;                                    // P x P
   float* sQ = sH + P * P;                                    // P x P
   float* sCS = sQ + P * P;                                   // P (c, s per pair)
   int* sPair = reinterpret_cast<int*>(sCS + P);              // P
   int* sOrd = sPair + P;                                     // P
+  float* sT = reinterpret_cast<float*>(sOrd + P + 16);      // r x 8 (P = 8)
   const long long b = blockIdx.x;
   const float* Gb = G + b * (long long)r * r;
   const int tid = threadIdx.x;
 
+  auto GZ = [&](const float* z, float* y) {
+    if constexpr (P == 8) gemm_GZ8(Gb, r, z, y, sT);
+    else gemm_GZ<P>(Gb, r, z, y);
+  };
   for (int idx = tid; idx < r * P; idx += SS_THREADS) sZ[idx] = hash_unit(idx / P, idx % P);
   __syncthreads();
-  gemm_GZ<P>(Gb, r, sZ, sY);
+  GZ(sZ, sY);
   __syncthreads();
   for (int it = 0; it < iters; ++it) {
     cholqr<P>(sY, sZ, r, sS, sRi);  // Z = orth(Y)
     cholqr<P>(sZ, sY, r, sS, sRi);  // second pass into Y ...
-    gemm_GZ<P>(Gb, r, sY, sZ); // ... Z = G * orth(Y)
+    GZ(sY, sZ);                     // ... Z = G * orth(Y)
     __syncthreads();
     // swap names: basis in sY, product in sZ -> keep (Y := product, Z := basis)
     float* t = sY;
@@ -310,11 +397,16 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
     sZ = t;
   }
   // Rayleigh-Ritz: H = Z^T (G Z) = Z^T Y
-  for (int q = tid; q < P * P; q += SS_THREADS) {
-    const int a = q / P, c = q % P;
-    double s = 0.0;
-    for (int i = 0; i < r; ++i) s += (double)sZ[i * P + a] * (double)sY[i * P + c];
-    sH[q] = (float)s;
+  if constexpr (P == 8) {
+    prod8(sZ, sY, r, sPart, sS);
+    if (tid < 64) sH[tid] = (float)sS[tid];
+  } else {
+    for (int q = tid; q < P * P; q += SS_THREADS) {
+      const int a = q / P, c = q % P;
+      double s = 0.0;
+      for (int i = 0; i < r; ++i) s += (double)sZ[i * P + a] * (double)sY[i * P + c];
+      sH[q] = (float)s;
+    }
   }
   __syncthreads();
   for (int q = tid; q < P * P; q += SS_THREADS) {  // symmetrise

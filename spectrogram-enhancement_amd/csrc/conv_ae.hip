@@ -426,7 +426,7 @@ struct PatchLds {
 };
 
 template <typename T, int NT, int CC, bool POOL, bool PAIR = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PAIR && NT == 1 ? 4 : 1)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((PAIR && NT == 1) || (CC == 16 && NT == 2) ? 4 : 1)))
 void conv_patch_kernel(ConvArgs a) {
   constexpr int TILE = 16;
   constexpr int PST = Patch<CC>::PST;
@@ -569,6 +569,68 @@ void conv_patch_kernel(ConvArgs a) {
             for (int j = 0; j < NT; ++j) wring[u][j] = ld8(wl[j] + col);
           }
           const int aoff = aoff_of(st) + 8 * kgrp;
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            const uint4 q = *reinterpret_cast<const uint4*>(sP + rbase[i] + aoff);  // ds_read_b128
+            V8<T> pv;
+            pv.w[0] = q.x; pv.w[1] = q.y; pv.w[2] = q.z; pv.w[3] = q.w;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wcur[j], pv, acc[i][j]);
+          }
+        }
+      } else if constexpr (CC == 16) {
+        // ---- 16 channels: one MFMA K=32 slab = two taps (lane groups kgrp 0-1: tap 2st,
+        // 2-3: tap 2st+1). Same branch-free scheme as above; the missing second tap of an
+        // odd tap count is a zeroed weight fragment on the last step ----
+        const int KWl = g.KW, Kfl = g.Kf, Cl = g.C, KWf = g.KWf, ks = g.kstep;
+        const int ky0 = g.ky0, kx0 = g.kx0;
+        const int dy = upt - g.pad_t, dx = upl - g.pad_l;
+        const int kwinv = (65536 + KWl - 1) / KWl;
+        const int nsteps = (ntap + 1) / 2;
+        const bool second = (kgrp >> 1) != 0;
+        const T* wl[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          wl[j] = W + (long long)min(n0 + 16 * j + px, g.CO - 1) * Kfl + 8 * (kgrp & 1);
+        auto wcol_t = [&](int t) {
+          const int jy = (t * kwinv) >> 16, jx = t - jy * KWl;
+          return ((ky0 + ks * jy) * KWf + kx0 + ks * jx) * Cl;
+        };
+        auto aoff_t = [&](int t) {
+          const int jy = (t * kwinv) >> 16, jx = t - jy * KWl;
+          return ((jy + dy) * PW + jx + dx) * PST;
+        };
+        auto wcol_of = [&](int st) {
+          const int c0 = wcol_t(2 * st), c1 = wcol_t(min(2 * st + 1, ntap - 1));
+          return second ? c1 : c0;
+        };
+        constexpr int PD = NT >= 3 ? 2 : (NT == 2 ? 2 : 8);
+        V8<T> wring[PD][NT];
+#pragma unroll
+        for (int u = 0; u < PD; ++u)
+          if (u < nsteps) {
+            const int col = wcol_of(u);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) wring[u][j] = ld8(wl[j] + col);
+          }
+        for (int s0 = 0; s0 < nsteps; s0 += PD)
+#pragma unroll
+        for (int u = 0; u < PD; ++u) {
+          const int st = s0 + u;
+          if (st >= nsteps) break;
+          V8<T> wcur[NT];
+#pragma unroll
+          for (int j = 0; j < NT; ++j) wcur[j] = wring[u][j];
+          if (2 * st + 1 >= ntap && second)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) zero8(wcur[j]);
+          if (st + PD < nsteps) {
+            const int col = wcol_of(st + PD);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) wring[u][j] = ld8(wl[j] + col);
+          }
+          const int a0 = aoff_t(2 * st), a1 = aoff_t(min(2 * st + 1, ntap - 1));
+          const int aoff = (second ? a1 : a0) + 8 * (kgrp & 1);
 #pragma unroll
           for (int i = 0; i < MT; ++i) {
             const uint4 q = *reinterpret_cast<const uint4*>(sP + rbase[i] + aoff);  // ds_read_b128

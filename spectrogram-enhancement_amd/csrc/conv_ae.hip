@@ -426,7 +426,7 @@ struct PatchLds {
 };
 
 template <typename T, int NT, int CC, bool POOL, bool PAIR = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((PAIR && NT == 1) || (CC == 16 && NT == 2) ? 4 : 1)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((PAIR && NT == 1) || (CC == 16 && NT == 2) ? 4 : (CC == 32 && NT == 4 ? 3 : 1))))
 void conv_patch_kernel(ConvArgs a) {
   constexpr int TILE = 16;
   constexpr int PST = Patch<CC>::PST;
@@ -546,6 +546,7 @@ void conv_patch_kernel(ConvArgs a) {
           const int jy = (t * kwinv) >> 16, jx = t - jy * KWl;
           return ((jy + dy) * PW + jx + dx) * PST + 32 * h;
         };
+        // ring of PD weight fragments consumed in place (no copies) and refilled PD steps ahead
         constexpr int PD = NT >= 3 ? (CC == 64 ? 1 : 2) : (NT == 2 ? 2 : 8);
         V8<T> wring[PD][NT];
 #pragma unroll
@@ -560,22 +561,21 @@ void conv_patch_kernel(ConvArgs a) {
         for (int u = 0; u < PD; ++u) {
           const int st = s0 + u;
           if (st >= nsteps) break;
-          V8<T> wcur[NT];
+          const int aoff = aoff_of(st) + 8 * kgrp;
+          V8<T> pv[MT];
 #pragma unroll
-          for (int j = 0; j < NT; ++j) wcur[j] = wring[u][j];
+          for (int i = 0; i < MT; ++i) {
+            const uint4 q = *reinterpret_cast<const uint4*>(sP + rbase[i] + aoff);  // ds_read_b128
+            pv[i].w[0] = q.x; pv[i].w[1] = q.y; pv[i].w[2] = q.z; pv[i].w[3] = q.w;
+          }
+#pragma unroll
+          for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wring[u][j], pv[i], acc[i][j]);
           if (st + PD < nsteps) {
             const int col = wcol_of(st + PD);
 #pragma unroll
             for (int j = 0; j < NT; ++j) wring[u][j] = ld8(wl[j] + col);
-          }
-          const int aoff = aoff_of(st) + 8 * kgrp;
-#pragma unroll
-          for (int i = 0; i < MT; ++i) {
-            const uint4 q = *reinterpret_cast<const uint4*>(sP + rbase[i] + aoff);  // ds_read_b128
-            V8<T> pv;
-            pv.w[0] = q.x; pv.w[1] = q.y; pv.w[2] = q.z; pv.w[3] = q.w;
-#pragma unroll
-            for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wcur[j], pv, acc[i][j]);
           }
         }
       } else if constexpr (CC == 16) {
@@ -618,26 +618,27 @@ void conv_patch_kernel(ConvArgs a) {
         for (int u = 0; u < PD; ++u) {
           const int st = s0 + u;
           if (st >= nsteps) break;
-          V8<T> wcur[NT];
+          const int a0 = aoff_t(2 * st), a1 = aoff_t(min(2 * st + 1, ntap - 1));
+          const int aoff = (second ? a1 : a0) + 8 * (kgrp & 1);
+          V8<T> pv[MT];
 #pragma unroll
-          for (int j = 0; j < NT; ++j) wcur[j] = wring[u][j];
-          if (2 * st + 1 >= ntap && second)
+          for (int i = 0; i < MT; ++i) {
+            const uint4 q = *reinterpret_cast<const uint4*>(sP + rbase[i] + aoff);  // ds_read_b128
+            pv[i].w[0] = q.x; pv[i].w[1] = q.y; pv[i].w[2] = q.z; pv[i].w[3] = q.w;
+          }
+          if (2 * st + 1 >= ntap) {  // last step of an odd tap count: no second tap
 #pragma unroll
-            for (int j = 0; j < NT; ++j) zero8(wcur[j]);
+            for (int i = 0; i < MT; ++i)
+              if (second) zero8(pv[i]);
+          }
+#pragma unroll
+          for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wring[u][j], pv[i], acc[i][j]);
           if (st + PD < nsteps) {
             const int col = wcol_of(st + PD);
 #pragma unroll
             for (int j = 0; j < NT; ++j) wring[u][j] = ld8(wl[j] + col);
-          }
-          const int a0 = aoff_t(2 * st), a1 = aoff_t(min(2 * st + 1, ntap - 1));
-          const int aoff = (second ? a1 : a0) + 8 * (kgrp & 1);
-#pragma unroll
-          for (int i = 0; i < MT; ++i) {
-            const uint4 q = *reinterpret_cast<const uint4*>(sP + rbase[i] + aoff);  // ds_read_b128
-            V8<T> pv;
-            pv.w[0] = q.x; pv.w[1] = q.y; pv.w[2] = q.z; pv.w[3] = q.w;
-#pragma unroll
-            for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wcur[j], pv, acc[i][j]);
           }
         }
       } else {

@@ -96,6 +96,12 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
 size_t specenh_svd_workspace_bytes(long long batch, int m, int n, int kmax);
 int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long a_stride,
                         int start, int stop, float* out, void* workspace, void* stream);
+/* The same with the output written as out_dtype (SPECENH_DTYPE_F32 / _BF16 / _F16, codes
+ * below): the C5 stream hands the denoised spectrograms to the fp16 autoencoder without a
+ * separate cast pass. Arithmetic is unchanged (fp32, rounded once at the store). */
+int specenh_svd_denoise_ex(const float* A, long long batch, int m, int n, long long a_stride,
+                           int start, int stop, void* out, int out_dtype, void* workspace,
+                           void* stream);
 
 /* Gavish-Donoho optimal hard-threshold modes of the same denoiser:
  *   num_sing = #{ s_i > omega(beta) * median(s) },  beta = min(m, n) / max(m, n),

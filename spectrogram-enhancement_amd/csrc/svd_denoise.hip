@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -86,6 +87,117 @@ __global__ __launch_bounds__(256) void gram_kernel(XView x, int K, int r, float*
     if (row < r && col < r) {
       Gb[(long long)row * r + col] = acc[reg];
       Gb[(long long)col * r + row] = acc[reg];
+    }
+  }
+}
+
+// r <= 128: one workgroup per matrix. X is staged through LDS in chunks of 32 rows
+// (coalesced 16-byte loads, the next chunk in registers while the current one is used);
+// the upper triangle of 16x16 tiles (36 at r = 128) is dealt round-robin to the 4 waves,
+// v_mfma_f32_16x16x4_f32 reads both operands from the chunk (ds_read_b32, row pitch
+// r + 16 words: conflict-free). Same fp32 products as gram_kernel, in another order.
+constexpr int GL_KC = 32;
+__global__ __launch_bounds__(256) void gram_lds_kernel(XView x, int K, int r, float* G) {
+  __shared__ float sX[GL_KC * (128 + 16)];
+  const int ld = r + 16;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const float* X = x.base + (long long)blockIdx.x * x.batch_stride;
+  const int nt = (r + 15) / 16, ntri = nt * (nt + 1) / 2;
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  f32x4v acc[9];
+  int tI[9], tJ[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    acc[q] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    int t = wave + 4 * q, ti = 0;
+    if (t >= ntri) t = -1;
+    if (t >= 0) {
+      while (t >= nt - ti) { t -= nt - ti; ++ti; }
+      tI[q] = ti; tJ[q] = ti + t;
+    } else {
+      tI[q] = -1; tJ[q] = -1;
+    }
+  }
+  // staging: GL_KC x r elements; row-major X (si == 1): float4 along i, else along k
+  const bool rowmaj = x.si == 1;
+  const int nvec = GL_KC * r / 4;  // r % 4 == 0 (host-checked)
+  float4 reg[4];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u;
+      reg[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < nvec) {
+        if (rowmaj) {
+          const int kk = e / (r / 4), i4 = e - (e / (r / 4)) * (r / 4);
+          if (k0 + kk < K)
+            reg[u] = *reinterpret_cast<const float4*>(X + (long long)(k0 + kk) * x.sk + 4 * i4);
+        } else {  // X[k][i] = base[k + i * si]: 4 consecutive k of one column i
+          const int i = e / (GL_KC / 4), k4 = e - (e / (GL_KC / 4)) * (GL_KC / 4);
+          const float* src = X + (long long)i * x.si + k0 + 4 * k4;
+          if (k0 + 4 * k4 + 3 < K) {
+            reg[u] = make_float4(src[0], src[1], src[2], src[3]);
+          } else {
+            float v[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int c = 0; c < 4; ++c)
+              if (k0 + 4 * k4 + c < K) v[c] = src[c];
+            reg[u] = make_float4(v[0], v[1], v[2], v[3]);
+          }
+        }
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u;
+      if (e >= nvec) continue;
+      if (rowmaj) {
+        const int kk = e / (r / 4), i4 = e - (e / (r / 4)) * (r / 4);
+        *reinterpret_cast<float4*>(sX + kk * ld + 4 * i4) = reg[u];
+      } else {
+        const int i = e / (GL_KC / 4), k4 = e - (e / (GL_KC / 4)) * (GL_KC / 4);
+        sX[(4 * k4 + 0) * ld + i] = reg[u].x;
+        sX[(4 * k4 + 1) * ld + i] = reg[u].y;
+        sX[(4 * k4 + 2) * ld + i] = reg[u].z;
+        sX[(4 * k4 + 3) * ld + i] = reg[u].w;
+      }
+    }
+  };
+  // columns r .. 16*nt - 1 of the chunk stay zero
+  for (int e = tid; e < GL_KC * (16 * nt - r); e += 256) {
+    const int kk = e / (16 * nt - r), i = r + e - kk * (16 * nt - r);
+    sX[kk * ld + i] = 0.f;
+  }
+  fetch(0);
+  const int kr = lane >> 4, cl = lane & 15;
+  for (int k0 = 0; k0 < K; k0 += GL_KC) {
+    __syncthreads();  // previous chunk fully consumed
+    store();
+    __syncthreads();
+    if (k0 + GL_KC < K) fetch(k0 + GL_KC);
+#pragma unroll
+    for (int s4 = 0; s4 < GL_KC / 4; ++s4) {
+      const float* row = sX + (4 * s4 + kr) * ld + cl;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        if (tI[q] < 0) continue;  // wave-uniform
+        const float a = row[16 * tI[q]], b = row[16 * tJ[q]];
+        acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[q], 0, 0, 0);
+      }
+    }
+  }
+  float* Gb = G + (long long)blockIdx.x * r * r;
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    if (tI[q] < 0) continue;
+#pragma unroll
+    for (int reg4 = 0; reg4 < 4; ++reg4) {
+      const int row = 16 * tI[q] + 4 * kr + reg4, col = 16 * tJ[q] + cl;
+      if (row < r && col < r) {
+        Gb[(long long)row * r + col] = acc[q][reg4];
+        Gb[(long long)col * r + row] = acc[q][reg4];
+      }
     }
   }
 }
@@ -454,10 +566,15 @@ constexpr int RB = 32;
 
 // ranges (optional, device int[2 * batch]): a per-matrix [lo, hi) replacing the uniform
 // one (always the direct, non-complement form); hi <= lo gives zeros.
-template <int KP>
+template <typename TO>
+__device__ __forceinline__ TO to_out(float v) { return (TO)v; }
+
+// TO: output element type (float, or _Float16 / __bf16 when the consumer computes in half
+// precision: the cast rides on the reconstruction's store, no separate pass)
+template <int KP, typename TO>
 __global__ __launch_bounds__(256) void recon_kernel(XView x, int Kr, int r, const float* V,
                                                     int K, int lo, int hi, int complement,
-                                                    const int* ranges, float* out,
+                                                    const int* ranges, TO* out,
                                                     long long out_bstride, long long osk,
                                                     long long osi) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -501,7 +618,7 @@ __global__ __launch_bounds__(256) void recon_kernel(XView x, int Kr, int r, cons
   }
   __syncthreads();
   // phase 2: out rows, thread per column i (coalesced along i for m >= n)
-  float* Ob = out + b * out_bstride;
+  TO* Ob = out + b * out_bstride;
   for (int e = tid; e < RB * r; e += 256) {
     int kk, i;
     if (osi == 1) { kk = e / r; i = e % r; } else { i = e / RB; kk = e % RB; }
@@ -510,7 +627,7 @@ __global__ __launch_bounds__(256) void recon_kernel(XView x, int Kr, int r, cons
 #pragma unroll
     for (int c = 0; c < KP; ++c) s = fmaf(sY[kk * KP + c], sV[i * KP + c], s);
     const float v = complement ? sX[kk * (r + 1) + i] - s : s;
-    Ob[(long long)(k0 + kk) * osk + (long long)i * osi] = v;
+    Ob[(long long)(k0 + kk) * osk + (long long)i * osi] = to_out<TO>(v);
   }
 }
 
@@ -731,6 +848,30 @@ __global__ __launch_bounds__(64) void optimal_rank_kernel(const double* dg, cons
 using namespace specenh;
 
 namespace {
+bool getenv_set(const char* name) {
+  const char* v = std::getenv(name);
+  return v && *v && *v != '0';
+}
+
+// G = X^T X for every matrix: the LDS-chunked kernel for r <= 128 (r % 4 == 0), else
+// one wave per 32x32 tile.
+void launch_gram(const XView& xv, int Kr, int r, float* G, long long batch, hipStream_t st) {
+  const bool lds = r <= 128 && r % 4 == 0 && !getenv_set("SPECENH_SVD_GRAM_TILES");
+  const int nts = (r + 31) / 32;
+  const int ntri = nts * (nts + 1) / 2;
+  for (long long b0 = 0; b0 < batch; b0 += 65535) {
+    const long long nb = std::min<long long>(65535, batch - b0);
+    XView xb = xv;
+    xb.base = xv.base + b0 * xv.batch_stride;
+    if (lds)
+      hipLaunchKernelGGL(gram_lds_kernel, dim3((unsigned)nb), dim3(256), 0, st, xb, Kr, r,
+                         G + b0 * (long long)r * r);
+    else
+      hipLaunchKernelGGL(gram_kernel, dim3((ntri + 3) / 4, (unsigned)nb), dim3(256), 0, st, xb,
+                         Kr, r, G + b0 * (long long)r * r, nts);
+  }
+}
+
 template <int P>
 hipError_t launch_subspace_t(const float* G, int r, int K, float* V, float* theta,
                              long long batch, hipStream_t st) {
@@ -759,32 +900,47 @@ hipError_t launch_subspace(int p, const float* G, int r, int K, float* V, float*
   }
 }
 
-template <int KP>
+template <int KP, typename TO>
 hipError_t launch_recon_t(XView xb, int Kr, int r, const float* V, int K, int lo, int hi,
-                          int comp, const int* ranges, float* out, long long ob, long long osk,
+                          int comp, const int* ranges, void* out, long long ob, long long osk,
                           long long osi, long long nb, hipStream_t st) {
   const size_t lds = (size_t)r * KP * 4 + (size_t)RB * (r + 1) * 4 + (size_t)RB * KP * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  hipError_t e = hipFuncSetAttribute((const void*)recon_kernel<KP>,
+  hipError_t e = hipFuncSetAttribute((const void*)recon_kernel<KP, TO>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(recon_kernel<KP>, dim3((Kr + RB - 1) / RB, (unsigned)nb), dim3(256), lds,
-                     st, xb, Kr, r, V, K, lo, hi, comp, ranges, out, ob, osk, osi);
+  hipLaunchKernelGGL((recon_kernel<KP, TO>), dim3((Kr + RB - 1) / RB, (unsigned)nb), dim3(256),
+                     lds, st, xb, Kr, r, V, K, lo, hi, comp, ranges, reinterpret_cast<TO*>(out),
+                     ob, osk, osi);
   return hipGetLastError();
 }
 
-hipError_t launch_recon(int KP, XView xb, int Kr, int r, const float* V, int K, int lo, int hi,
-                        int comp, const int* ranges, float* out, long long ob, long long osk,
-                        long long osi, long long nb, hipStream_t st) {
+template <typename TO>
+hipError_t launch_recon_k(int KP, XView xb, int Kr, int r, const float* V, int K, int lo,
+                          int hi, int comp, const int* ranges, void* out, long long ob,
+                          long long osk, long long osi, long long nb, hipStream_t st) {
   switch (KP) {
-#define SPECENH_RC(n)                                                                        \
-  case n:                                                                                    \
-    return launch_recon_t<n>(xb, Kr, r, V, K, lo, hi, comp, ranges, out, ob, osk, osi, nb, st);
+#define SPECENH_RC(n)                                                                          \
+  case n:                                                                                      \
+    return launch_recon_t<n, TO>(xb, Kr, r, V, K, lo, hi, comp, ranges, out, ob, osk, osi, nb, \
+                                 st);
     SPECENH_RC(8) SPECENH_RC(16) SPECENH_RC(24) SPECENH_RC(32) SPECENH_RC(40) SPECENH_RC(48)
 #undef SPECENH_RC
     default: return hipErrorInvalidValue;
   }
 }
+
+hipError_t launch_recon(int KP, XView xb, int Kr, int r, const float* V, int K, int lo, int hi,
+                        int comp, const int* ranges, void* out, long long ob, long long osk,
+                        long long osi, long long nb, hipStream_t st, int odt = SPECENH_DTYPE_F32) {
+  if (odt == SPECENH_DTYPE_F16)
+    return launch_recon_k<_Float16>(KP, xb, Kr, r, V, K, lo, hi, comp, ranges, out, ob, osk, osi, nb, st);
+  if (odt == SPECENH_DTYPE_BF16)
+    return launch_recon_k<__bf16>(KP, xb, Kr, r, V, K, lo, hi, comp, ranges, out, ob, osk, osi, nb, st);
+  return launch_recon_k<float>(KP, xb, Kr, r, V, K, lo, hi, comp, ranges, out, ob, osk, osi, nb, st);
+}
+
+size_t dtype_size(int dt) { return dt == SPECENH_DTYPE_F32 ? 4 : 2; }
 }  // namespace
 
 extern "C" {
@@ -796,6 +952,16 @@ size_t specenh_svd_workspace_bytes(long long batch, int m, int n, int kmax) {
 
 int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long a_stride,
                         int start, int stop, float* out, void* workspace, void* stream) {
+  return specenh_svd_denoise_ex(A, batch, m, n, a_stride, start, stop, out, SPECENH_DTYPE_F32,
+                                workspace, stream);
+}
+
+int specenh_svd_denoise_ex(const float* A, long long batch, int m, int n, long long a_stride,
+                           int start, int stop, void* out, int out_dtype, void* workspace,
+                           void* stream) {
+  if (out_dtype != SPECENH_DTYPE_F32 && out_dtype != SPECENH_DTYPE_F16 &&
+      out_dtype != SPECENH_DTYPE_BF16)
+    return set_error(SPECENH_EINVAL, "svd output dtype must be f32, bf16 or f16");
   if (batch < 0 || m <= 0 || n <= 0) return set_error(SPECENH_EINVAL, "bad matrix shape");
   if (batch == 0) return SPECENH_OK;
   if (!A || !out || !workspace) return set_error(SPECENH_EINVAL, "null pointer");
@@ -806,8 +972,9 @@ int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long
   if (stop > r) stop = r;
   hipStream_t st = (hipStream_t)stream;
   const long long ob = (long long)m * n;
+  const size_t osz = dtype_size(out_dtype);
   if (stop <= start) {  // empty range: zeros (u[:, s:s] @ ... = 0)
-    if (hipMemsetAsync(out, 0, (size_t)batch * ob * sizeof(float), st) != hipSuccess)
+    if (hipMemsetAsync(out, 0, (size_t)batch * ob * osz, st) != hipSuccess)
       return set_error(SPECENH_EHIP, "memset");
     return SPECENH_OK;
   }
@@ -815,9 +982,19 @@ int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long
   const bool complement = (stop == r);
   const int K = complement ? start : stop;
   if (complement && start == 0) {  // whole range: out = A (u s vh reproduces A)
-    if (hipMemcpy2DAsync(out, ob * sizeof(float), A, a_stride * sizeof(float),
-                         ob * sizeof(float), batch, hipMemcpyDeviceToDevice, st) != hipSuccess)
-      return set_error(SPECENH_EHIP, "copy");
+    if (out_dtype == SPECENH_DTYPE_F32) {
+      if (hipMemcpy2DAsync(out, ob * sizeof(float), A, a_stride * sizeof(float),
+                           ob * sizeof(float), batch, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return set_error(SPECENH_EHIP, "copy");
+      return SPECENH_OK;
+    }
+    for (long long b = 0; b < batch; ++b) {  // cast (one call when A is dense)
+      const long long nb = a_stride == ob ? batch : 1;
+      const int rc = specenh_cast(SPECENH_DTYPE_F32, A + b * a_stride, out_dtype,
+                                  static_cast<char*>(out) + (size_t)(b * ob) * osz, nb * ob, stream);
+      if (rc != SPECENH_OK) return rc;
+      b += nb - 1;
+    }
     return SPECENH_OK;
   }
   if (K > PMAX - 8 || K > r)
@@ -845,15 +1022,7 @@ int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long
   float* G = (float*)workspace;
   float* V = G + batch * (long long)r * r;
   float* theta = V + batch * (long long)r * K;
-  const int nts = (r + 31) / 32;
-  const int ntri = nts * (nts + 1) / 2;
-  for (long long b0 = 0; b0 < batch; b0 += 65535) {
-    const long long nb = std::min<long long>(65535, batch - b0);
-    XView xb = xv;
-    xb.base = A + b0 * a_stride;
-    hipLaunchKernelGGL(gram_kernel, dim3((ntri + 3) / 4, (unsigned)nb), dim3(256), 0, st, xb,
-                       Kr, r, G + b0 * (long long)r * r, nts);
-  }
+  launch_gram(xv, Kr, r, G, batch, st);
   if (hipGetLastError() != hipSuccess) return set_error(SPECENH_EHIP, "gram launch");
   const int KP = ((hi - lo > 0 ? K : 1) + 7) / 8 * 8;
   hipError_t e = launch_subspace(p, G, r, K, V, theta, batch, st);
@@ -863,7 +1032,8 @@ int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long
     XView xb = xv;
     xb.base = A + b0 * a_stride;
     e = launch_recon(KP, xb, Kr, r, V + b0 * (long long)r * K, K, lo, hi, complement ? 1 : 0,
-                     nullptr, out + b0 * ob, ob, osk, osi, nb, st);
+                     nullptr, static_cast<char*>(out) + (size_t)(b0 * ob) * osz, ob, osk, osi, nb,
+                     st, out_dtype);
     if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("recon: ") + hipGetErrorString(e));
   }
   if (hipGetLastError() != hipSuccess) return set_error(SPECENH_EHIP, "recon launch");
@@ -986,15 +1156,7 @@ int specenh_svd_denoise_optimal(const float* A, long long batch, int m, int n,
   // 5: fp32 Gram, top-K subspace, per-matrix reconstruction
   float* V = G + batch * (long long)r * r;
   float* theta = V + batch * (long long)r * K;
-  const int nts = (r + 31) / 32;
-  const int ntri = nts * (nts + 1) / 2;
-  for (long long b0 = 0; b0 < batch; b0 += 65535) {
-    const long long nb = std::min<long long>(65535, batch - b0);
-    XView xb = xv;
-    xb.base = A + b0 * a_stride;
-    hipLaunchKernelGGL(gram_kernel, dim3((ntri + 3) / 4, (unsigned)nb), dim3(256), 0, st, xb,
-                       Kr, r, G + b0 * (long long)r * r, nts);
-  }
+  launch_gram(xv, Kr, r, G, batch, st);
   hipError_t e = launch_subspace(p, G, r, K, V, theta, batch, st);
   if (e != hipSuccess)
     return set_error(SPECENH_EHIP, std::string("subspace: ") + hipGetErrorString(e));

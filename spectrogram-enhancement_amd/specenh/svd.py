@@ -53,6 +53,9 @@ def _resolve(r: int, start, stop):
     return start, stop
 
 
+_OUT_DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}  # SPECENH_DTYPE_*
+
+
 def denoise_batch(A: torch.Tensor, start=None, stop=None,
                   out: torch.Tensor | None = None) -> torch.Tensor:
     """Batched denoiseSignal on device tensors: ``A[B, m, n]`` (or ``[m, n]``) fp32."""
@@ -72,14 +75,20 @@ def denoise_batch(A: torch.Tensor, start=None, stop=None,
     start, stop = _resolve(r, start, stop)
     if out is None:
         out = torch.empty((B, m, n), dtype=torch.float32, device=A.device)
+    # out may be fp16/bf16 (e.g. the autoencoder's input): the reconstruction stores in that
+    # type directly (specenh_svd_denoise_ex), no separate cast pass
+    odt = _OUT_DTYPES.get(out.dtype)
+    if odt is None or out.numel() != B * m * n or not out.is_contiguous() or out.device != A.device:
+        raise ValueError("out must be a contiguous [B, m, n] float32/bfloat16/float16 tensor "
+                         "on A's device")
     K = max(start, stop) if stop < r else start
     L = _lib.lib()
     ws = torch.empty(max(16, int(L.specenh_svd_workspace_bytes(B, m, n, max(K, 1)))),
                      dtype=torch.uint8, device=A.device)
-    _lib.check(L.specenh_svd_denoise(ctypes.c_void_p(A.data_ptr()), B, m, n, A.stride(0),
-                                     start, stop, ctypes.c_void_p(out.data_ptr()),
-                                     ctypes.c_void_p(ws.data_ptr()),
-                                     ctypes.c_void_p(_lib.current_stream_handle(A.device))),
+    _lib.check(L.specenh_svd_denoise_ex(ctypes.c_void_p(A.data_ptr()), B, m, n, A.stride(0),
+                                        start, stop, ctypes.c_void_p(out.data_ptr()), odt,
+                                        ctypes.c_void_p(ws.data_ptr()),
+                                        ctypes.c_void_p(_lib.current_stream_handle(A.device))),
                "svd_denoise")
     return out[0] if squeeze else out
 

@@ -135,3 +135,53 @@ def test_unsupported_modes_raise(gpu_device):
     with pytest.raises(NotImplementedError):
         svd.denoiseSignal(np.random.default_rng(2).standard_normal((300, 280)),
                           use_optimal=True)  # min(m, n) > 256 on the optimal path
+
+
+@pytest.mark.parametrize("shape", [(128, 128), (96, 128), (128, 40), (52, 100)])
+def test_gram_paths_agree(gpu_device, shape, monkeypatch):
+    """The LDS-chunked Gram (r <= 128: row-major and transposed X, ragged chunks and tiles)
+    and the one-wave-per-tile Gram give the same reconstruction to fp32 rounding, and both
+    match the oracle on a gapped matrix."""
+    import os
+    import sys
+
+    import torch
+
+    from specenh import svd
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import gapped_matrix
+
+    m, n = shape
+    A = np.stack([gapped_matrix(700 + i, m, n, dtype=np.float32) for i in range(3)])
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("SPECENH_SVD_GRAM_TILES", flag)
+        outs.append(svd.denoise_batch(torch.as_tensor(A, device=gpu_device), 0, 16).double().cpu().numpy())
+    for b in range(3):
+        truth = ref.denoiseSignal(A[b].astype(np.float64), 0, 16)
+        assert _rel(outs[0][b], truth) <= TOL
+        assert _rel(outs[1][b], truth) <= TOL
+        assert _rel(outs[0][b], outs[1][b]) <= 1e-6
+
+
+@pytest.mark.parametrize("args", [(), (0, 16), (0, 10_000), (5, 2)])
+def test_half_precision_output_is_rounded_fp32(gpu_device, args):
+    """specenh_svd_denoise_ex writes fp16/bf16 straight from the fp32 reconstruction: the
+    same bits as the fp32 output rounded once (the C5 stream's autoencoder input)."""
+    import os
+    import sys
+
+    import torch
+
+    from specenh import svd
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import gapped_matrix
+
+    A = torch.as_tensor(np.stack([gapped_matrix(40 + i, 128, 128, dtype=np.float32)
+                                  for i in range(4)]), device=gpu_device)
+    ref32 = svd.denoise_batch(A, *args)
+    for dt in (torch.float16, torch.bfloat16):
+        out = torch.empty(A.shape, dtype=dt, device=gpu_device)
+        svd.denoise_batch(A, *args, out=out)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref32.to(dt)), dt

@@ -367,7 +367,31 @@ def main():
                                             "frac": ach2 / HBM_PEAK_GBPS,
                                             "alg_bytes_per_launch": ALG_BYTES_C2 * B2,
                                             "traffic": tr2["hbm_bytes"] if tr2 else None}}
-        del x2, o2
+        del o2
+        # §8 A4 / f3: cross-power amplitude spectrogram of shot pairs at the C2 geometry
+        from specenh import cross
+        Bc = B2 // 2
+        xa, xb_ = x2[:Bc], x2[Bc:]
+        for _ in range(2):
+            _, _, oc = cross.cross_spectrogram_batch(xa, xb_, 5e5, "hamm", 1024, 768, "linear",
+                                                     "density", amplitude=True)
+        e0.record(st)
+        for _ in range(5):
+            _, _, oc = cross.cross_spectrogram_batch(xa, xb_, 5e5, "hamm", 1024, 768, "linear",
+                                                     "density", amplitude=True)
+        e1.record(st)
+        e1.synchronize()
+        c_ms = e0.elapsed_time(e1) / 5
+        algc = (2 * 4 * L2 + 4 * (F2 + 1) * T2) * Bc
+        achc = algc / (c_ms * 1e-3) / 1e9
+        stages["csd_c2"] = {
+            "workload": f"{Bc} signal pairs x 65536 fp32, nperseg 1024 hop 256 hamm, linear, "
+                        "density -> |Pxy| amplitude [pairs, 513, 253] (crosspowerspec.py:39)",
+            "pairs_per_s": Bc / (c_ms * 1e-3), "kernel": "csd_kernel", "kernel_ms": c_ms,
+            "roofline": {"bound": "hbm", "achieved": achc, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achc / HBM_PEAK_GBPS, "alg_bytes_per_launch": algc,
+                         "traffic": None}}
+        del x2, oc
 
     # ---- PSNR vs the fp64 CPU chain on sample shots ----
     psnr = None

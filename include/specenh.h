@@ -83,6 +83,26 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
                      long long length, long long x_stride, float* out, int flags,
                      void* workspace, void* stream);
 
+/* ---------------------------------------------------------------- cross spectrum
+ * Per-segment cross-spectral density of signal pairs: the
+ * arithmetic behind interferometer/crosspowerspec.py:39 (ae_co2(signal1, signal2, t),
+ * whose source co2_deps is absent) restated as scipy's two-signal _spectral_helper
+ * (scipy/signal/_spectral_py.py, mode='psd'): per frame detrend, window, rfft of both,
+ *   Pxy = conj(X) * Y * scale, one-sided bins 1..N/2-1 doubled,
+ * out [batch][F][T] frequency-major, F = nperseg/2 + 1, T = specenh_stft_frames(...).
+ * scipy.signal.csd(x, y) is the mean of Pxy over T. x, y: device fp32, pair b at
+ * x + b*x_stride, y + b*y_stride. mode COMPLEX writes float2 (re, im); AMPLITUDE writes
+ * |Pxy| as float. nperseg: a power of two in [64, 4096]; batch <= 65535 per call. */
+#define SPECENH_CSD_COMPLEX 0
+#define SPECENH_CSD_AMPLITUDE 1
+typedef struct specenh_csd_plan specenh_csd_plan;
+int specenh_csd_plan_create(specenh_csd_plan** plan, int nperseg, int noverlap,
+                            const double* window_host, double fs, int scaling, int detrend);
+int specenh_csd_plan_destroy(specenh_csd_plan* plan);
+int specenh_csd(const specenh_csd_plan* plan, const float* x, const float* y, long long batch,
+                long long length, long long x_stride, long long y_stride, void* out, int mode,
+                void* stream);
+
 /* ---------------------------------------------------------------- SVD denoiser
  * Batched replacement for denoiseSignal(matrix, start, stop, use_optimal=False)
  * (spec_denoising/denoising_by_svd.ipynb:188-229):

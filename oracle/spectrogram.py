@@ -142,3 +142,35 @@ def specgr_scipy(x, spec_params: dict):
     S = np.log(S + spec_params["eps"])
     S = (S - np.min(S)) / (np.max(S) - np.min(S))
     return S[:-1, :], f[:-1], t
+
+
+def cross_spectrogram(x, y, fs: float = 1.0, window="hann", nperseg: int = 256,
+                      noverlap: int | None = None, detrend="constant", scaling="density",
+                      compute_dtype=np.float64):
+    """(f, t, Pxy[..., F, T]): scipy's two-signal ``_spectral_helper(x, y, mode='psd')``
+    (``_spectral_py.py`` ``if not same_data: result = np.conjugate(result) * result_y``,
+    then ``result *= scale`` and the one-sided doubling), the un-averaged
+    ``scipy.signal.csd`` — what ``ae_co2`` (interferometer/crosspowerspec.py:39, source
+    absent) stands for. Same framing / detrend / window / scale as :func:`spectrogram_psd`;
+    ``noverlap`` defaults to ``nperseg // 2`` as in csd."""
+    x = np.asarray(x)
+    y = np.asarray(y)
+    if noverlap is None:
+        noverlap = nperseg // 2
+    if noverlap >= nperseg:
+        raise ValueError("noverlap must be less than nperseg.")
+    step = nperseg - noverlap
+    win = get_window(window, nperseg)
+    scale = 1.0 / (fs * (win * win).sum()) if scaling == "density" else 1.0 / win.sum() ** 2
+
+    def spec(sig):
+        fr = np.lib.stride_tricks.sliding_window_view(sig, nperseg, axis=-1)[..., ::step, :]
+        return np.fft.rfft(_detrend(fr.astype(compute_dtype), detrend) * win, axis=-1)
+
+    P = np.conjugate(spec(x)) * spec(y) * scale
+    if nperseg % 2:
+        P[..., 1:] *= 2
+    else:
+        P[..., 1:-1] *= 2
+    P = np.moveaxis(P, -1, -2)
+    return frequencies(nperseg, fs), times(x.shape[-1], nperseg, noverlap, fs), P

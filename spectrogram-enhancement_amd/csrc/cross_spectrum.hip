@@ -1,0 +1,246 @@
+// cross_spectrum.hip — batched per-segment cross-spectral density for gfx950.
+//
+// interferometer/crosspowerspec.py:39 calls
+// ae_co2(signal1, signal2, t) (co2_deps, absent from the reference) and plots
+// log(ampsp).T (:46-48). The arithmetic it stands for is scipy's two-signal branch of
+// _spectral_helper (scipy/signal/_spectral_py.py, mode='psd', x != y):
+//   frames x[k*step : k*step+N], y likewise; per-frame detrend; window;
+//   X = rfft(x_w), Y = rfft(y_w); Pxy = conj(X) * Y * scale; one-sided bins 1..N/2-1 x2;
+//   output (F, T) frequency-major, F = N/2 + 1.
+// scipy.signal.csd is the mean of Pxy over T. Parity is pinned against scipy (not ae_co2).
+//
+// One workgroup per (frame, signal pair). Both real frames ride in one complex FFT,
+// z = x_w + i*y_w, and separate afterwards: X_k = (Z_k + conj Z_{N-k}) / 2,
+// Y_k = (Z_k - conj Z_{N-k}) / 2i. Detrend sums in fp64 (wave butterflies + LDS);
+// FFT = mixed-radix Stockham (one radix-2 pass when log2 N is odd, then radix-4) in LDS
+// ping-pong buffers, twiddles W_N^t from a plan table.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "specenh.h"
+
+namespace specenh {
+int set_error(int code, const std::string& msg);  // stft_psd.hip
+}
+
+struct specenh_csd_plan {
+  int N, noverlap, step, detrend, log2n;
+  float scale;
+  float* d_window;
+  float2* d_tw;
+  int device;
+};
+
+namespace specenh {
+namespace {
+
+constexpr int CT = 256;
+
+struct CsdArgs {
+  const float* x;
+  const float* y;
+  long long xs, ys;  // row strides (elements)
+  int T, N, step, detrend, log2n, mode;
+  const float* win;
+  const float2* tw;
+  float scale;
+  void* out;  // mode 0: float2 [B][F][T]; mode 1: float |Pxy| [B][F][T]
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+__device__ __forceinline__ float2 c_mul(float2 a, float2 w) {
+  return make_float2(fmaf(a.x, w.x, -a.y * w.y), fmaf(a.x, w.y, a.y * w.x));
+}
+
+__global__ __launch_bounds__(CT) void csd_kernel(CsdArgs a) {
+  extern __shared__ float2 sm[];  // 2 x N complex
+  __shared__ double red[CT / 64][4];
+  const int N = a.N, t = blockIdx.x, tid = threadIdx.x;
+  const long long b = blockIdx.y;
+  float2* src = sm;
+  float2* dst = sm + N;
+  const float* xb = a.x + b * a.xs + (long long)t * a.step;
+  const float* yb = a.y + b * a.ys + (long long)t * a.step;
+  const double kc = 0.5 * (N - 1);
+  double sx = 0.0, skx = 0.0, sy = 0.0, sky = 0.0;
+  for (int n = tid; n < N; n += CT) {
+    const float xv = xb[n], yv = yb[n];
+    src[n] = make_float2(xv, yv);
+    const double k = n - kc;
+    sx += xv; skx += k * xv; sy += yv; sky += k * yv;
+  }
+  float mx = 0.f, my = 0.f, bx = 0.f, by = 0.f;
+  if (a.detrend != SPECENH_DETREND_NONE) {  // uniform
+    sx = wave_sum(sx); skx = wave_sum(skx); sy = wave_sum(sy); sky = wave_sum(sky);
+    if ((tid & 63) == 0) {
+      red[tid >> 6][0] = sx; red[tid >> 6][1] = skx; red[tid >> 6][2] = sy; red[tid >> 6][3] = sky;
+    }
+    __syncthreads();
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int w = 0; w < CT / 64; ++w)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s[q] += red[w][q];
+    mx = (float)(s[0] / N);
+    my = (float)(s[2] / N);
+    if (a.detrend == SPECENH_DETREND_LINEAR) {  // least squares on [n, 1], centred abscissa
+      const double skk = (double)N * ((double)N * N - 1.0) / 12.0;
+      bx = (float)(s[1] / skk);
+      by = (float)(s[3] / skk);
+    }
+  }
+  __syncthreads();
+  for (int n = tid; n < N; n += CT) {
+    const float k = (float)(n - kc), w = a.win[n];
+    const float2 v = src[n];
+    src[n] = make_float2((v.x - mx - bx * k) * w, (v.y - my - by * k) * w);
+  }
+  __syncthreads();
+  // ---- Stockham autosort FFT: natural order in, natural order out ----
+  int Ns = 1;
+  if (a.log2n & 1) {
+    for (int j = tid; j < N / 2; j += CT) {
+      const float2 v0 = src[j], v1 = src[j + N / 2];
+      dst[2 * j] = make_float2(v0.x + v1.x, v0.y + v1.y);
+      dst[2 * j + 1] = make_float2(v0.x - v1.x, v0.y - v1.y);
+    }
+    float2* tmp = src; src = dst; dst = tmp;
+    Ns = 2;
+    __syncthreads();
+  }
+  for (; Ns < N; Ns *= 4) {
+    const int q = N / 4, tstep = N / (4 * Ns);
+    for (int j = tid; j < q; j += CT) {
+      const int jm = j & (Ns - 1);
+      float2 v0 = src[j], v1 = src[j + q], v2 = src[j + 2 * q], v3 = src[j + 3 * q];
+      if (jm) {
+        const int e = jm * tstep;
+        v1 = c_mul(v1, a.tw[e]);
+        v2 = c_mul(v2, a.tw[2 * e]);
+        v3 = c_mul(v3, a.tw[(3 * e) & (N - 1)]);
+      }
+      const float2 s02 = make_float2(v0.x + v2.x, v0.y + v2.y);
+      const float2 d02 = make_float2(v0.x - v2.x, v0.y - v2.y);
+      const float2 s13 = make_float2(v1.x + v3.x, v1.y + v3.y);
+      const float2 d13 = make_float2(v1.x - v3.x, v1.y - v3.y);  // -i * d13 = (d13.y, -d13.x)
+      const int o = (j - jm) * 4 + jm;
+      dst[o] = make_float2(s02.x + s13.x, s02.y + s13.y);
+      dst[o + Ns] = make_float2(d02.x + d13.y, d02.y - d13.x);
+      dst[o + 2 * Ns] = make_float2(s02.x - s13.x, s02.y - s13.y);
+      dst[o + 3 * Ns] = make_float2(d02.x - d13.y, d02.y + d13.x);
+    }
+    float2* tmp = src; src = dst; dst = tmp;
+    __syncthreads();
+  }
+  // ---- separate X, Y; Pxy = conj(X) Y * scale, one-sided doubling ----
+  const int F = N / 2 + 1;
+  for (int k = tid; k < F; k += CT) {
+    const float2 z = src[k], zc = src[(N - k) & (N - 1)];
+    const float2 X = make_float2(0.5f * (z.x + zc.x), 0.5f * (z.y - zc.y));
+    const float2 Y = make_float2(0.5f * (z.y + zc.y), -0.5f * (z.x - zc.x));
+    const float s = (k > 0 && k < N / 2) ? 2.f * a.scale : a.scale;
+    const float2 p = make_float2((X.x * Y.x + X.y * Y.y) * s, (X.x * Y.y - X.y * Y.x) * s);
+    const long long o = (b * F + k) * a.T + t;
+    if (a.mode == 0) reinterpret_cast<float2*>(a.out)[o] = p;
+    else reinterpret_cast<float*>(a.out)[o] = sqrtf(p.x * p.x + p.y * p.y);
+  }
+}
+
+}  // namespace
+}  // namespace specenh
+
+extern "C" {
+
+int specenh_csd_plan_create(specenh_csd_plan** plan, int nperseg, int noverlap,
+                            const double* window_host, double fs, int scaling, int detrend) {
+  using specenh::set_error;
+  if (!plan || !window_host) return set_error(SPECENH_EINVAL, "null plan or window");
+  *plan = nullptr;
+  if (nperseg < 64 || nperseg > 4096 || (nperseg & (nperseg - 1)))
+    return set_error(SPECENH_EUNSUPPORTED, "cross spectrum: nperseg must be a power of two in [64, 4096]");
+  if (noverlap < 0 || noverlap >= nperseg)
+    return set_error(SPECENH_EINVAL, "noverlap must be less than nperseg.");
+  if (!(fs > 0)) return set_error(SPECENH_EINVAL, "fs must be positive");
+  if (scaling != SPECENH_SCALING_DENSITY && scaling != SPECENH_SCALING_SPECTRUM)
+    return set_error(SPECENH_EINVAL, "Unknown scaling");
+  if (detrend < SPECENH_DETREND_NONE || detrend > SPECENH_DETREND_LINEAR)
+    return set_error(SPECENH_EINVAL, "Trend type must be 'linear' or 'constant'.");
+  const int N = nperseg;
+  double s1 = 0.0, s2 = 0.0;
+  std::vector<float> win(N);
+  for (int n = 0; n < N; ++n) {
+    s1 += window_host[n];
+    s2 += window_host[n] * window_host[n];
+    win[n] = (float)window_host[n];
+  }
+  std::vector<float2> tw(N);
+  for (int n = 0; n < N; ++n) {
+    const double ang = -2.0 * M_PI * (double)n / N;
+    tw[n] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+  }
+  specenh_csd_plan* p = new specenh_csd_plan{};
+  p->N = N;
+  p->noverlap = noverlap;
+  p->step = N - noverlap;
+  p->detrend = detrend;
+  p->log2n = 0;
+  while ((1 << p->log2n) < N) ++p->log2n;
+  p->scale = (float)(scaling == SPECENH_SCALING_DENSITY ? 1.0 / (fs * s2) : 1.0 / (s1 * s1));
+  hipError_t e = hipGetDevice(&p->device);
+  if (e == hipSuccess) e = hipMalloc(&p->d_window, N * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&p->d_tw, N * sizeof(float2));
+  if (e == hipSuccess) e = hipMemcpy(p->d_window, win.data(), N * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(p->d_tw, tw.data(), N * sizeof(float2), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    if (p->d_window) (void)hipFree(p->d_window);
+    if (p->d_tw) (void)hipFree(p->d_tw);
+    delete p;
+    return set_error(SPECENH_EHIP, std::string("csd plan: ") + hipGetErrorString(e));
+  }
+  *plan = p;
+  return SPECENH_OK;
+}
+
+int specenh_csd_plan_destroy(specenh_csd_plan* plan) {
+  if (!plan) return SPECENH_OK;
+  (void)hipFree(plan->d_window);
+  (void)hipFree(plan->d_tw);
+  delete plan;
+  return SPECENH_OK;
+}
+
+int specenh_csd(const specenh_csd_plan* plan, const float* x, const float* y, long long batch,
+                long long length, long long x_stride, long long y_stride, void* out, int mode,
+                void* stream) {
+  using specenh::set_error;
+  if (!plan) return set_error(SPECENH_EINVAL, "null plan");
+  if (batch < 0 || length < 0) return set_error(SPECENH_EINVAL, "negative batch or length");
+  if (mode != SPECENH_CSD_COMPLEX && mode != SPECENH_CSD_AMPLITUDE)
+    return set_error(SPECENH_EINVAL, "cross spectrum mode must be COMPLEX or AMPLITUDE");
+  const long long T = specenh_stft_frames(length, plan->N, plan->noverlap);
+  if (T < 0) return (int)T;
+  if (batch == 0 || T == 0) return SPECENH_OK;
+  if (!x || !y || !out) return set_error(SPECENH_EINVAL, "null pointer");
+  if (batch > 65535 || T > 2147483647LL)
+    return set_error(SPECENH_EUNSUPPORTED, "cross spectrum: batch <= 65535 signal pairs per call");
+  if (x_stride < length || y_stride < length) return set_error(SPECENH_EINVAL, "stride < length");
+  specenh::CsdArgs a;
+  a.x = x; a.y = y; a.xs = x_stride; a.ys = y_stride;
+  a.T = (int)T; a.N = plan->N; a.step = plan->step; a.detrend = plan->detrend;
+  a.log2n = plan->log2n; a.mode = mode; a.win = plan->d_window; a.tw = plan->d_tw;
+  a.scale = plan->scale; a.out = out;
+  hipLaunchKernelGGL(specenh::csd_kernel, dim3((unsigned)T, (unsigned)batch), dim3(specenh::CT),
+                     2 * plan->N * sizeof(float2), (hipStream_t)stream, a);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, std::string("csd launch: ") + hipGetErrorString(e));
+}
+
+}  // extern "C"

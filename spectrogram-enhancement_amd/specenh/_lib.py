@@ -58,6 +58,13 @@ SIGNATURES = {
     "specenh_stft_psd": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_longlong, _c.c_longlong,
                                     _c.c_longlong, _c.c_void_p, _c.c_int, _c.c_void_p,
                                     _c.c_void_p]),
+    "specenh_csd_plan_create": (_c.c_int, [_c.POINTER(_c.c_void_p), _c.c_int, _c.c_int,
+                                           _c.POINTER(_c.c_double), _c.c_double, _c.c_int,
+                                           _c.c_int]),
+    "specenh_csd_plan_destroy": (_c.c_int, [_c.c_void_p]),
+    "specenh_csd": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_longlong,
+                               _c.c_longlong, _c.c_longlong, _c.c_longlong, _c.c_void_p, _c.c_int,
+                               _c.c_void_p]),
     "specenh_svd_workspace_bytes": (_c.c_size_t, [_c.c_longlong, _c.c_int, _c.c_int, _c.c_int]),
     "specenh_svd_denoise": (_c.c_int, [_c.c_void_p, _c.c_longlong, _c.c_int, _c.c_int,
                                        _c.c_longlong, _c.c_int, _c.c_int, _c.c_void_p,

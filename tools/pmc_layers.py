@@ -14,15 +14,18 @@ import statistics
 import sys
 
 LAYERS = {"ct1": "convT1", "ct2": "convT2", "ct3": "convT3", "last": "conv_out", "stft_c2": "stft_c2"}
+# the layer's own kernel (tools/conv_one.py adds a 1x1 tail conv after the convT layers)
+KERNEL = {"ct1": "Li4ELi64ELb0", "ct2": "Li2ELi64ELb0", "ct3": "Li1ELi32ELb0",
+          "last": "conv_co1", "stft_c2": "stft"}
 
 
-def one(path, skip=("cast", "flip", "Fill", "fill", "copy", "at::native", "rocclr")):
+def one(path, must="", skip=("cast", "flip", "Fill", "fill", "copy", "at::native", "rocclr")):
     per = collections.defaultdict(dict)
     names = {}
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             k = row["Kernel_Name"]
-            if "specenh" not in k or any(s in k for s in skip):
+            if "specenh" not in k or must not in k or any(s in k for s in skip):
                 continue
             d = row["Dispatch_Id"]
             per[k][d] = per[k].get(d, 0.0) + float(row["Counter_Value"])
@@ -36,8 +39,8 @@ def main():
     src, dst = sys.argv[1], sys.argv[2]
     res = {}
     for tag, name in LAYERS.items():
-        fk, fv = one(os.path.join(src, f"{tag}_FETCH_SIZE"))
-        wk, wv = one(os.path.join(src, f"{tag}_WRITE_SIZE"))
+        fk, fv = one(os.path.join(src, f"{tag}_FETCH_SIZE"), KERNEL[tag])
+        wk, wv = one(os.path.join(src, f"{tag}_WRITE_SIZE"), KERNEL[tag])
         res[name] = {"kernel": fk, "fetch_bytes": 2 * fv * 1024, "write_bytes": wv * 1024,
                      "hbm_bytes": 2 * fv * 1024 + wv * 1024,
                      "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "

@@ -239,6 +239,22 @@ int specenh_filter(int op, int dtype, const void* S, long long batch, int rows, 
 int specenh_quantfilt(int dtype, const void* S, long long batch, int rows, int cols,
                       long long stride, double thr, void* out, void* stream);
 
+/* gaussblr / morph (pipeline_data.py:52-55, :64-72): each spectrogram is
+ * quantised to uint8 as (rescale(x)*255).astype('uint8'), filtered with OpenCV's 8-bit
+ * algorithms restated (cv2 is absent: parity with cv2 unpinned, restatement in
+ * oracle/filters.py), and rescaled to [0, 1] as numpy does on a uint8 array:
+ *   specenh_gaussblr: cv2.GaussianBlur(u8, (kw, kh), sigma) — kw taps along cols, kh along
+ *                     rows, odd sizes <= 127, sigma <= 0 derives it from the size;
+ *                     integer Q8 taps, BORDER_REFLECT_101 (reference call: (31, 3), 0).
+ *   specenh_morph:    MORPH_CLOSE with a 4x4 rect, then MORPH_OPEN with a 3x1 (w x h) rect.
+ * workspace >= specenh_u8filter_workspace_bytes(batch, rows, cols). */
+size_t specenh_u8filter_workspace_bytes(long long batch, int rows, int cols);
+int specenh_gaussblr(int dtype, const void* S, long long batch, int rows, int cols,
+                     long long stride, int kw, int kh, double sigma, void* out, void* workspace,
+                     void* stream);
+int specenh_morph(int dtype, const void* S, long long batch, int rows, int cols, long long stride,
+                  void* out, void* workspace, void* stream);
+
 /* ---------------------------------------------------------------- strip glue
  * patch / unpatch / reshape of VAE/manual_scan_3layers.py:28-54:
  *   pack:   out[(b*n_strips + x)][r][c] = S[b][r][x*width + c], r < rows, c < width

@@ -13,6 +13,8 @@
 
 #include <cmath>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "specenh.h"
 
@@ -175,6 +177,130 @@ __global__ __launch_bounds__(256) void quantfilt_kernel(const T* S, T* out, int 
   }
 }
 
+
+// ---------------------------------------------------------------- cv2 steps on uint8
+// gaussblr (:52-55) and morph (:64-72): the image is quantised to uint8 exactly as
+// (rescale(src)*255).astype('uint8') (T arithmetic, truncation), filtered with OpenCV's
+// 8-bit algorithms restated (integer arithmetic: Gaussian taps in Q8 summing to 256, rows
+// then columns, (v + 2^15) >> 16, BORDER_REFLECT_101; rect dilate/erode with the anchor at
+// k/2 and outside pixels ignored), and rescaled as numpy evaluates rescale() on a uint8
+// array: (u - min) / (max - min) as a true (fp64) division. OpenCV is absent, so the
+// restatement is oracle/filters.py and parity with cv2 itself is unpinned.
+constexpr int MAX_TAPS = 127;
+struct GaussTaps {
+  int kw, kh;
+  unsigned short kx[MAX_TAPS], ky[MAX_TAPS];
+};
+
+__device__ __forceinline__ int reflect101(int p, int n) {
+  if (n == 1) return 0;
+  while (p < 0 || p >= n) {
+    if (p < 0) p = -p;
+    if (p >= n) p = 2 * n - 2 - p;
+  }
+  return p;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void quant_u8_kernel(const T* S, long long batch, int rows,
+                                                       int cols, long long stride,
+                                                       const double* stats, unsigned char* q) {
+  const long long n = (long long)rows * cols, total = batch * n;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total;
+       i += (long long)gridDim.x * 256) {
+    const long long b = i / n, e = i - b * n;
+    const T mn = (T)stats[2 * b], mx = (T)stats[2 * b + 1];
+    const T r = (T)((T)(S[b * stride + e] - mn) / (T)(mx - mn)) * (T)255;
+    q[i] = (r >= (T)0 && r < (T)256) ? (unsigned char)(int)r : (unsigned char)0;
+  }
+}
+
+__global__ __launch_bounds__(256) void gauss_rows_kernel(const unsigned char* q, long long batch,
+                                                         int rows, int cols, GaussTaps tp,
+                                                         unsigned short* h) {
+  const long long n = (long long)rows * cols, total = batch * n;
+  const int half = tp.kw / 2;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total;
+       i += (long long)gridDim.x * 256) {
+    const long long rowbase = i - i % cols;
+    const int c = (int)(i - rowbase);
+    unsigned acc = 0;
+    for (int j = 0; j < tp.kw; ++j)
+      acc += (unsigned)tp.kx[j] * q[rowbase + reflect101(c + j - half, cols)];
+    h[i] = (unsigned short)acc;  // <= 255 * 256
+  }
+}
+
+__global__ __launch_bounds__(256) void gauss_cols_kernel(const unsigned short* h, long long batch,
+                                                         int rows, int cols, GaussTaps tp,
+                                                         unsigned char* o) {
+  const long long n = (long long)rows * cols, total = batch * n;
+  const int half = tp.kh / 2;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total;
+       i += (long long)gridDim.x * 256) {
+    const long long b = i / n, e = i - b * n;
+    const int r = (int)(e / cols), c = (int)(e - (long long)r * cols);
+    const unsigned short* hb = h + b * n + c;
+    unsigned acc = 0;
+    for (int k = 0; k < tp.kh; ++k)
+      acc += (unsigned)tp.ky[k] * hb[(long long)reflect101(r + k - half, rows) * cols];
+    const unsigned v = (acc + (1u << 15)) >> 16;
+    o[i] = (unsigned char)(v > 255u ? 255u : v);
+  }
+}
+
+// rect dilate (IS_MAX) / erode over src(r + i - kh/2, c + j - kw/2); outside pixels ignored
+template <bool IS_MAX>
+__global__ __launch_bounds__(256) void morph_u8_kernel(const unsigned char* a, long long batch,
+                                                       int rows, int cols, int kh, int kw,
+                                                       unsigned char* o) {
+  const long long n = (long long)rows * cols, total = batch * n;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total;
+       i += (long long)gridDim.x * 256) {
+    const long long b = i / n, e = i - b * n;
+    const int r = (int)(e / cols), c = (int)(e - (long long)r * cols);
+    const unsigned char* ab = a + b * n;
+    unsigned v = IS_MAX ? 0u : 255u;
+    for (int y = max(r - kh / 2, 0); y < min(r - kh / 2 + kh, rows); ++y)
+      for (int x = max(c - kw / 2, 0); x < min(c - kw / 2 + kw, cols); ++x) {
+        const unsigned s = ab[(long long)y * cols + x];
+        v = IS_MAX ? max(v, s) : min(v, s);
+      }
+    o[i] = (unsigned char)v;
+  }
+}
+
+__global__ __launch_bounds__(256) void u8_stats_kernel(const unsigned char* u, int rows, int cols,
+                                                       double* stats) {
+  __shared__ double red[8];
+  const long long b = blockIdx.x, n = (long long)rows * cols;
+  const unsigned char* s = u + b * n;
+  double mn = INFINITY, mx = -INFINITY;
+  for (long long e = threadIdx.x; e < n; e += 256) {
+    const double v = (double)s[e];
+    mn = fmin(mn, v);
+    mx = fmax(mx, v);
+  }
+  block_minmax(mn, mx, red);
+  if (threadIdx.x == 0) {
+    stats[2 * b] = mn;
+    stats[2 * b + 1] = mx;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void u8_rescale_kernel(const unsigned char* u, long long batch,
+                                                         int rows, int cols, long long stride,
+                                                         const double* stats, T* out) {
+  const long long n = (long long)rows * cols, total = batch * n;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total;
+       i += (long long)gridDim.x * 256) {
+    const long long b = i / n, e = i - b * n;
+    const double mn = stats[2 * b], mx = stats[2 * b + 1];
+    out[b * stride + e] = (T)(((double)u[i] - mn) / (mx - mn));
+  }
+}
+
 inline unsigned grid_for(long long n) {
   const long long g = (n + 255) / 256;
   return (unsigned)(g < 1 ? 1 : (g > 65536 ? 65536 : g));
@@ -210,6 +336,101 @@ int run_quantfilt(const T* S, long long batch, int rows, int cols, long long str
   }
   return hipGetLastError() == hipSuccess ? SPECENH_OK
                                          : set_error(SPECENH_EHIP, "quantfilt launch");
+}
+
+
+// OpenCV's 8-bit Gaussian taps (oracle/filters.py gaussian_taps_q8): sigma from ksize when
+// sigma <= 0, fixed small tables for n <= 7, normalise, Q8 by error diffusion with the
+// centre tap taking the remainder (sum exactly 256).
+int gauss_taps_q8(int n, double sigma, unsigned short* out) {
+  if (n < 1 || n % 2 != 1 || n > MAX_TAPS)
+    return set_error(SPECENH_EINVAL, "Gaussian kernel size must be odd, positive and <= 127");
+  static const double small[4][7] = {{1.0},
+                                     {0.25, 0.5, 0.25},
+                                     {0.0625, 0.25, 0.375, 0.25, 0.0625},
+                                     {0.03125, 0.109375, 0.21875, 0.28125, 0.21875, 0.109375,
+                                      0.03125}};
+  std::vector<double> k(n);
+  const int half = n / 2;
+  if (n <= 7 && sigma <= 0) {
+    for (int i = 0; i < n; ++i) k[i] = small[half][i];
+  } else {
+    const double s = sigma > 0 ? sigma : ((n - 1) * 0.5 - 1) * 0.3 + 0.8;
+    const double scale2 = -0.5 / (s * s);
+    double tot = 0.0;
+    for (int i = 0; i < half; ++i) {
+      const double x = i - (n - 1) * 0.5;
+      k[i] = std::exp(scale2 * x * x);
+      tot += k[i];
+    }
+    tot = 2.0 * tot + 1.0;
+    for (int i = 0; i < half; ++i) k[i] /= tot;
+    k[half] = 1.0 / tot;
+  }
+  double err = 0.0;
+  int sum = 0;
+  for (int i = 0; i < half; ++i) {
+    const double adj = k[i] * 256.0 + err;
+    const int q = (int)std::nearbyint(adj);
+    err = adj - q;
+    out[i] = out[n - 1 - i] = (unsigned short)q;
+    sum += q;
+  }
+  out[half] = (unsigned short)(256 - 2 * sum);
+  return SPECENH_OK;
+}
+
+struct U8Work {
+  double* stats;
+  unsigned char* a;
+  unsigned char* b;
+  unsigned short* h;
+};
+
+inline U8Work u8_work(void* ws, long long batch, long long n) {
+  char* p = (char*)ws;
+  U8Work w;
+  w.stats = (double*)p;
+  p += ((size_t)batch * 16 + 255) / 256 * 256;
+  w.h = (unsigned short*)p;
+  p += ((size_t)n * 2 + 255) / 256 * 256;
+  w.a = (unsigned char*)p;
+  p += ((size_t)n + 255) / 256 * 256;
+  w.b = (unsigned char*)p;
+  return w;
+}
+
+template <typename T>
+int run_u8_filter(bool gauss, const T* S, long long batch, int rows, int cols, long long stride,
+                  const GaussTaps* tp, T* out, void* ws, hipStream_t st) {
+  const long long n = batch * rows * cols;
+  U8Work w = u8_work(ws, batch, n);
+  const unsigned g = grid_for(n);
+  hipLaunchKernelGGL(stats_kernel<T>, dim3((unsigned)batch), dim3(256), 0, st, S, rows, cols,
+                     stride, (int)SPECENH_FILTER_RESCALE, (const double*)nullptr, w.stats);
+  hipLaunchKernelGGL(quant_u8_kernel<T>, dim3(g), dim3(256), 0, st, S, batch, rows, cols, stride,
+                     w.stats, w.a);
+  if (gauss) {
+    hipLaunchKernelGGL(gauss_rows_kernel, dim3(g), dim3(256), 0, st, w.a, batch, rows, cols, *tp,
+                       w.h);
+    hipLaunchKernelGGL(gauss_cols_kernel, dim3(g), dim3(256), 0, st, w.h, batch, rows, cols, *tp,
+                       w.b);
+  } else {  // MORPH_CLOSE 4x4 (dilate, erode) then MORPH_OPEN 3x1 (erode, dilate)
+    hipLaunchKernelGGL(morph_u8_kernel<true>, dim3(g), dim3(256), 0, st, w.a, batch, rows, cols,
+                       4, 4, w.b);
+    hipLaunchKernelGGL(morph_u8_kernel<false>, dim3(g), dim3(256), 0, st, w.b, batch, rows, cols,
+                       4, 4, w.a);
+    hipLaunchKernelGGL(morph_u8_kernel<false>, dim3(g), dim3(256), 0, st, w.a, batch, rows, cols,
+                       1, 3, w.b);
+    hipLaunchKernelGGL(morph_u8_kernel<true>, dim3(g), dim3(256), 0, st, w.b, batch, rows, cols,
+                       1, 3, w.a);
+    std::swap(w.a, w.b);
+  }
+  hipLaunchKernelGGL(u8_stats_kernel, dim3((unsigned)batch), dim3(256), 0, st, w.b, rows, cols,
+                     w.stats);
+  hipLaunchKernelGGL(u8_rescale_kernel<T>, dim3(g), dim3(256), 0, st, w.b, batch, rows, cols,
+                     stride, w.stats, out);
+  return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "u8 filter launch");
 }
 
 int check_common(int dtype, const void* S, long long batch, int rows, int cols, long long stride,
@@ -278,6 +499,45 @@ int specenh_quantfilt(int dtype, const void* S, long long batch, int rows, int c
                                  (double*)out, st);
   return run_quantfilt<float>((const float*)S, batch, rows, cols, stride, lo, hi, gamma,
                               (float*)out, st);
+}
+
+size_t specenh_u8filter_workspace_bytes(long long batch, int rows, int cols) {
+  if (batch <= 0 || rows <= 0 || cols <= 0) return 16;
+  const size_t n = (size_t)batch * rows * cols;
+  return ((size_t)batch * 16 + 255) / 256 * 256 + (n * 2 + 255) / 256 * 256 +
+         2 * ((n + 255) / 256 * 256);
+}
+
+int specenh_gaussblr(int dtype, const void* S, long long batch, int rows, int cols,
+                     long long stride, int kw, int kh, double sigma, void* out, void* workspace,
+                     void* stream) {
+  if (int e = check_common(dtype, S, batch, rows, cols, stride, out)) return e;
+  GaussTaps tp{};
+  tp.kw = kw;
+  tp.kh = kh;
+  if (int e = gauss_taps_q8(kw, sigma, tp.kx)) return e;
+  if (int e = gauss_taps_q8(kh, sigma, tp.ky)) return e;
+  if (batch == 0) return SPECENH_OK;
+  if (!workspace) return set_error(SPECENH_EINVAL, "null workspace");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == SPECENH_DTYPE_F64)
+    return run_u8_filter<double>(true, (const double*)S, batch, rows, cols, stride, &tp,
+                                 (double*)out, workspace, st);
+  return run_u8_filter<float>(true, (const float*)S, batch, rows, cols, stride, &tp, (float*)out,
+                              workspace, st);
+}
+
+int specenh_morph(int dtype, const void* S, long long batch, int rows, int cols, long long stride,
+                  void* out, void* workspace, void* stream) {
+  if (int e = check_common(dtype, S, batch, rows, cols, stride, out)) return e;
+  if (batch == 0) return SPECENH_OK;
+  if (!workspace) return set_error(SPECENH_EINVAL, "null workspace");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == SPECENH_DTYPE_F64)
+    return run_u8_filter<double>(false, (const double*)S, batch, rows, cols, stride, nullptr,
+                                 (double*)out, workspace, st);
+  return run_u8_filter<float>(false, (const float*)S, batch, rows, cols, stride, nullptr,
+                              (float*)out, workspace, st);
 }
 
 }  // extern "C"

@@ -109,6 +109,12 @@ SIGNATURES = {
                                   _c.c_void_p]),
     "specenh_quantfilt": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_longlong, _c.c_int, _c.c_int,
                                      _c.c_longlong, _c.c_double, _c.c_void_p, _c.c_void_p]),
+    "specenh_u8filter_workspace_bytes": (_c.c_size_t, [_c.c_longlong, _c.c_int, _c.c_int]),
+    "specenh_gaussblr": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_longlong, _c.c_int, _c.c_int,
+                                    _c.c_longlong, _c.c_int, _c.c_int, _c.c_double, _c.c_void_p,
+                                    _c.c_void_p, _c.c_void_p]),
+    "specenh_morph": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_longlong, _c.c_int, _c.c_int,
+                                 _c.c_longlong, _c.c_void_p, _c.c_void_p, _c.c_void_p]),
     "specenh_strips_pack": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_longlong, _c.c_int, _c.c_int,
                                        _c.c_longlong, _c.c_int, _c.c_int, _c.c_int, _c.c_void_p,
                                        _c.c_void_p]),

@@ -1,5 +1,6 @@
-"""GPU label filters: norm / rescale / meansub / quantfilt of spec_denoising/pipeline_data.py
-(:38-61) through the C-ABI (csrc/filters.hip). The reference-named functions live in
+"""GPU label filters: norm / rescale / meansub / quantfilt / gaussblr / morph of
+spec_denoising/pipeline_data.py (:38-72) through the C-ABI (csrc/filters.hip), and the
+whole label chain of its main loop (:101-110) as ``label_pipeline``. The reference-named functions live in
 ``specenh.pipeline_data``; this module holds the device paths.
 
   * numpy input (the reference's float64 spectrograms): uploaded unchanged, computed in
@@ -38,7 +39,21 @@ def _run(kind, t: torch.Tensor, arg):
     out = torch.empty_like(t)
     L = _lib.lib()
     st = ctypes.c_void_p(_lib.current_stream_handle(t.device))
-    if kind == "quantfilt":
+    if kind in ("gaussblr", "morph"):
+        ws = torch.empty(max(16, int(L.specenh_u8filter_workspace_bytes(B, rows, cols))),
+                         dtype=torch.uint8, device=t.device)
+        if kind == "gaussblr":
+            kw, kh = arg
+            rc = L.specenh_gaussblr(_DT[t.dtype], ctypes.c_void_p(t.data_ptr()), B, rows, cols,
+                                    rows * cols, int(kw), int(kh), 0.0,
+                                    ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                    st)
+        else:
+            rc = L.specenh_morph(_DT[t.dtype], ctypes.c_void_p(t.data_ptr()), B, rows, cols,
+                                 rows * cols, ctypes.c_void_p(out.data_ptr()),
+                                 ctypes.c_void_p(ws.data_ptr()), st)
+        _lib.check(rc, kind)
+    elif kind == "quantfilt":
         _lib.check(L.specenh_quantfilt(_DT[t.dtype], ctypes.c_void_p(t.data_ptr()), B, rows, cols,
                                        rows * cols, float(arg), ctypes.c_void_p(out.data_ptr()),
                                        st), "quantfilt")
@@ -91,3 +106,36 @@ def meansub(src):
         return np.moveaxis(r.reshape(m.shape), -1, 1)
 
     return _apply("meansub", src, _lib.FILTER_MEANSUB, to2d, back)
+
+
+def _image2d(a):
+    if a.ndim != 2:
+        raise ValueError("cv2 filters take one 2-D image (or a [batch, rows, cols] device tensor)")
+    return a
+
+
+def gaussblr(src, filt=(31, 3)):
+    """pipeline_data.py:52-55: uint8 quantisation, cv2.GaussianBlur(u8, filt, 0), rescale.
+    ``filt`` is OpenCV's (width, height): width taps along columns (time), height along rows."""
+    kw, kh = (int(filt[0]), int(filt[1]))
+    return _apply("gaussblr", src, (kw, kh), _image2d, lambda r, a: r)
+
+
+def morph(src):
+    """pipeline_data.py:64-72: uint8 quantisation, MORPH_CLOSE 4x4 then MORPH_OPEN 3x1, rescale."""
+    return _apply("morph", src, None, _image2d, lambda r, a: r)
+
+
+def label_pipeline(s, thr=0.9):
+    """The label chain of pipeline_data.py:101-110 on the GPU:
+    quantfilt(thr) -> gaussblr((31, 3)) -> meansub -> morph -> meansub.
+    numpy in -> float64 numpy out; a device tensor (2-D or [B, rows, cols]) stays on device."""
+    if isinstance(s, torch.Tensor):
+        t = s
+    else:
+        a = np.asarray(s)
+        if a.ndim != 2:
+            raise ValueError("label_pipeline takes one 2-D spectrogram (or a device batch)")
+        t = torch.as_tensor(np.ascontiguousarray(a.astype(np.float64)), device=_device())
+    out = meansub(morph(meansub(gaussblr(quantfilt(t, thr), (31, 3)))))
+    return out if isinstance(s, torch.Tensor) else out.cpu().numpy()

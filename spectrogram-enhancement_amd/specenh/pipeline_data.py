@@ -102,10 +102,18 @@ def meansub(src):
 
 
 def gaussblr(src, filt=(31, 3)):
-    """pipeline_data.py:52-55 (cv2.GaussianBlur on uint8). Not built yet: SURVEY §8(f1)."""
-    raise NotImplementedError("gaussblr needs OpenCV semantics; GPU port is a §8(f1) item")
+    """pipeline_data.py:52-55: (rescale(src)*255).astype('uint8') -> cv2.GaussianBlur(., filt, 0)
+    -> rescale, on the GPU (OpenCV's 8-bit algorithm restated; cv2 absent: parity unpinned)."""
+    return _filters.gaussblr(src, filt)
 
 
 def morph(src):
-    """pipeline_data.py:64-72 (cv2 close/open on uint8). Not built yet: SURVEY §8(f1)."""
-    raise NotImplementedError("morph needs OpenCV semantics; GPU port is a §8(f1) item")
+    """pipeline_data.py:64-72: uint8 quantisation -> MORPH_CLOSE 4x4 -> MORPH_OPEN 3x1 ->
+    rescale, on the GPU (OpenCV's 8-bit algorithm restated; cv2 absent: parity unpinned)."""
+    return _filters.morph(src)
+
+
+def label_pipeline(s, thr=0.9):
+    """The label chain of pipeline_data.py:101-110 (quantfilt -> gaussblr -> meansub -> morph
+    -> meansub) on the GPU."""
+    return _filters.label_pipeline(s, thr)

@@ -95,3 +95,19 @@ def test_strip_glue_index_map():
     assert u.shape == (2, 256, 3840)
     assert np.array_equal(u[0], S[:, :3840])
     assert strips.reshape(p).shape == (60, 256, 128, 1)
+
+
+def test_cv2_restatement_properties():
+    """gaussblr / morph restatement (cv2 absent: unpinned) — properties OpenCV documents:
+    taps sum to 256 and are symmetric, sigma from ksize, the 3-tap small table, a constant
+    image is a fixed point of the blur, OPEN with the centred 3x1 rect is anti-extensive."""
+    t = filters.gaussian_taps_q8(31)
+    assert t.sum() == 256 and (t == t[::-1]).all() and t[15] == t.max()
+    assert filters.gaussian_taps_q8(3).tolist() == [64, 128, 64]
+    c = np.full((9, 40), 77, np.uint8)
+    np.testing.assert_array_equal(filters.gaussian_blur_u8(c), c)
+    u = (np.random.default_rng(3).random((32, 48)) * 255).astype(np.uint8)
+    opened = filters._morph_u8(filters._morph_u8(u, 1, 3, False), 1, 3, True)
+    assert (opened <= u).all()
+    out = filters.label_pipeline(np.random.default_rng(4).random((64, 96)))
+    assert out.min() == 0.0 and out.max() == 1.0

@@ -204,6 +204,9 @@ __global__ __launch_bounds__(256) void gram_lds_kernel(XView x, int K, int r, fl
 
 // ---------------------------------------------------------------- 2. subspace
 constexpr int SS_THREADS = 256;
+#ifndef SPECENH_SS_SINGLE_QR
+#define SPECENH_SS_SINGLE_QR 1  // single CholeskyQR in the intermediate subspace rounds
+#endif
 constexpr int PMAX = 48;  // max subspace width (LDS: r=256 -> 2 x 48 KB + tables)
 
 // deterministic pseudo-random start vectors
@@ -499,6 +502,15 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
   GZ(sZ, sY);
   __syncthreads();
   for (int it = 0; it < iters; ++it) {
+    if (it + 1 < iters && (SPECENH_SS_SINGLE_QR)) {
+      // Intermediate rounds only have to keep the block well conditioned (G Z re-amplifies
+      // the dominant directions anyway): one CholeskyQR pass. The basis that feeds the
+      // Rayleigh-Ritz step below gets the full CholeskyQR2.
+      cholqr<P>(sY, sZ, r, sS, sRi);  // Z = orth(Y) to ~cond(Y) * eps
+      GZ(sZ, sY);                     // Y = G Z
+      __syncthreads();
+      continue;
+    }
     cholqr<P>(sY, sZ, r, sS, sRi);  // Z = orth(Y)
     cholqr<P>(sZ, sY, r, sS, sRi);  // second pass into Y ...
     GZ(sY, sZ);                     // ... Z = G * orth(Y)

@@ -82,6 +82,13 @@ size_t specenh_stft_workspace_bytes(const specenh_stft_plan* plan, long long bat
 int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long batch,
                      long long length, long long x_stride, float* out, int flags,
                      void* workspace, void* stream);
+/* As specenh_stft_psd with fp16 samples (x: _Float16, x_stride in elements), widened to
+ * fp32 on load — the same arithmetic as specenh_stft_psd on x converted to fp32, without
+ * the conversion pass (the C5 stream's fp16 shots). nperseg <= 1024; one workgroup per
+ * spectrogram (no team schedule, no workspace). */
+int specenh_stft_psd_f16(const specenh_stft_plan* plan, const void* x, long long batch,
+                         long long length, long long x_stride, float* out, int flags,
+                         void* stream);
 
 /* ---------------------------------------------------------------- cross spectrum
  * Per-segment cross-spectral density of signal pairs: the

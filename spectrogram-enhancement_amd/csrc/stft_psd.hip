@@ -242,29 +242,38 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
                                            0x00020000);
 }
 
-template <int N>
+// XH: the samples are fp16 (the C5 stream's shots), widened to fp32 on load (exact).
+template <int N, bool XH = false>
 __device__ __forceinline__ void load_pair(PairSamples<N>& s, __amdgpu_buffer_rsrc_t xr, int hop,
                                           int fa, int T, int gl) {
   constexpr int G = Cfg<N>::G;
   constexpr int NB1 = N / Cfg<N>::R1;
+  constexpr int ES = XH ? 2 : 4;  // bytes per sample
   // Frames past the end duplicate the last frame: their spectra equal a valid one, so
   // they cannot move the min/max and need no masking; they are never stored.
-  const int oa = ((fa < T ? fa : T - 1) * hop + gl) * 4;
-  const int ob = ((fa + 1 < T ? fa + 1 : T - 1) * hop + gl) * 4;
+  const int oa = ((fa < T ? fa : T - 1) * hop + gl) * ES;
+  const int ob = ((fa + 1 < T ? fa + 1 : T - 1) * hop + gl) * ES;
 #pragma unroll
   for (int i = 0; i < PairSamples<N>::BPL1; ++i)
 #pragma unroll
     for (int r = 0; r < PairSamples<N>::R1; ++r) {
-      const int o = (i * G + r * NB1) * 4;
-      s.x[i][r] = make_float2(
-          __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, oa + o, 0, 0)),
-          __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ob + o, 0, 0)));
+      const int o = (i * G + r * NB1) * ES;
+      if constexpr (XH) {
+        const unsigned short ha = __builtin_amdgcn_raw_buffer_load_b16(xr, oa + o, 0, 0);
+        const unsigned short hb = __builtin_amdgcn_raw_buffer_load_b16(xr, ob + o, 0, 0);
+        s.x[i][r] = make_float2((float)__builtin_bit_cast(_Float16, ha),
+                                (float)__builtin_bit_cast(_Float16, hb));
+      } else {
+        s.x[i][r] = make_float2(
+            __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, oa + o, 0, 0)),
+            __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ob + o, 0, 0)));
+      }
     }
 }
 
 // Detrend + window + all FFT passes for one pair; leaves Z (natural order) in `buf`
 // and returns the fp64 DC bins of both frames.
-template <int N>
+template <int N, bool XH = false>
 __device__ __forceinline__ void fft_pair(const StftArgs& a, PairSamples<N>& in, bool va,
                                          bool vb, const float2* s_tw, const float* s_win,
                                          const double* s_dc, float2* buf, int gl, double& dca,
@@ -311,7 +320,7 @@ __device__ __forceinline__ void fft_pair(const StftArgs& a, PairSamples<N>& in, 
   // `in` is consumed: refill it with the next tile's samples now, so their HBM latency
   // hides under this pair's FFT (the fences keep the loads after the reads above).
   __builtin_amdgcn_sched_barrier(0);
-  if (prefetch) load_pair<N>(in, xr, a.hop, fa_next, a.T, gl);
+  if (prefetch) load_pair<N, XH>(in, xr, a.hop, fa_next, a.T, gl);
   __builtin_amdgcn_sched_barrier(0);
   dca = group_sum<G>(dca);
   dcb = group_sum<G>(dcb);
@@ -469,7 +478,7 @@ __device__ __forceinline__ void tile_store(const StftArgs& a, float* s_tile,
 // frequency-row segments of TF frames. With NORMALIZE the workgroup knows the whole
 // spectrogram's min/max at the end and rescales its own output in a final sweep
 // (the rows were written moments ago and are re-read from the on-die caches).
-template <int N>
+template <int N, bool XH = false>
 __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_kernel(
     StftArgs a) {
   using C = Cfg<N>;
@@ -496,7 +505,9 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
   const int gl = lane % G;                          // lane within the FFT group
   const int fi = wave * (64 / G) + lane / G;        // FFT index within the tile
   float2* buf = reinterpret_cast<float2*>(smem + Lo::OFF_BUF) + fi * Lo::BUF;
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + shot * a.x_stride, a.x_stride * 4);
+  constexpr int ES = XH ? 2 : 4;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(
+      reinterpret_cast<const char*>(a.x) + shot * a.x_stride * ES, a.x_stride * ES);
   const bool want_log = (a.flags & (SPECENH_STFT_LOG | SPECENH_STFT_NORMALIZE)) != 0;
   const bool log2_out = (a.flags & SPECENH_STFT_NORMALIZE) != 0;
   const int ntiles = (a.T + Lo::TF - 1) / Lo::TF;
@@ -505,16 +516,16 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
 
   const __amdgpu_buffer_rsrc_t orr = make_rsrc(o_shot, (long long)a.F_out * a.T * 4);
   PairSamples<N> nxt;
-  if constexpr (C::PF) load_pair<N>(nxt, xr, a.hop, 2 * fi, a.T, gl);
+  if constexpr (C::PF) load_pair<N, XH>(nxt, xr, a.hop, 2 * fi, a.T, gl);
   __syncthreads();
 
   for (int tile = 0; tile < ntiles; ++tile) {
     const int t0 = tile * Lo::TF;
     const int fa = t0 + 2 * fi;
     const bool va = true, vb = true;  // tail frames are clamped duplicates (load_pair)
-    if constexpr (!C::PF) load_pair<N>(nxt, xr, a.hop, fa, a.T, gl);
+    if constexpr (!C::PF) load_pair<N, XH>(nxt, xr, a.hop, fa, a.T, gl);
     double dca, dcb;
-    fft_pair<N>(a, nxt, va, vb, s_tw, s_win, s_dc, buf, gl, dca, dcb, xr, fa + Lo::TF,
+    fft_pair<N, XH>(a, nxt, va, vb, s_tw, s_win, s_dc, buf, gl, dca, dcb, xr, fa + Lo::TF,
                 C::PF && tile + 1 < ntiles);
 
     // ---- separate the two frames, PSD (+log2/ln), running min/max; values in registers ----
@@ -561,18 +572,18 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
   }
 }
 
-template <int N>
+template <int N, bool XH = false>
 hipError_t launch_stft(const StftArgs& a, long long batch, hipStream_t stream) {
   using Lo = Layout<N>;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)stft_psd_kernel<N>,
+    hipError_t e = hipFuncSetAttribute((const void*)stft_psd_kernel<N, XH>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, Lo::BYTES);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(stft_psd_kernel<N>, dim3((unsigned)batch), dim3(Lo::THREADS), Lo::BYTES,
-                     stream, a);
+  hipLaunchKernelGGL((stft_psd_kernel<N, XH>), dim3((unsigned)batch), dim3(Lo::THREADS),
+                     Lo::BYTES, stream, a);
   return hipGetLastError();
 }
 
@@ -971,6 +982,55 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
       case 1024: e = launch_stft<1024>(c, nb, st); break;
       case 2048: e = launch_stft<2048>(c, nb, st); break;
       case 4096: e = launch_stft<4096>(c, nb, st); break;
+      default: return set_error(SPECENH_EUNSUPPORTED, "unsupported nperseg");
+    }
+    if (e != hipSuccess)
+      return set_error(SPECENH_EHIP, std::string("stft launch: ") + hipGetErrorString(e));
+  }
+  return SPECENH_OK;
+}
+
+int specenh_stft_psd_f16(const specenh_stft_plan* plan, const void* x, long long batch,
+                         long long length, long long x_stride, float* out, int flags,
+                         void* stream) {
+  if (!plan) return set_error(SPECENH_EINVAL, "null plan");
+  if (batch < 0) return set_error(SPECENH_EINVAL, "batch must be >= 0");
+  if (batch == 0) return SPECENH_OK;
+  if (!x || !out) return set_error(SPECENH_EINVAL, "null x/out");
+  const int N = plan->nperseg;
+  long long T = specenh_stft_frames(length, N, plan->noverlap);
+  if (T < 0) return (int)T;
+  if (x_stride < length) return set_error(SPECENH_EINVAL, "x_stride < length");
+  if (T > (1ll << 30)) return set_error(SPECENH_EINVAL, "too many frames");
+  if (N > 1024) return set_error(SPECENH_EUNSUPPORTED, "fp16 samples need nperseg <= 1024");
+  StftArgs a{};
+  a.x = reinterpret_cast<const float*>(x);  // reinterpreted as fp16 by stft_psd_kernel<N, true>
+  a.x_stride = x_stride;
+  a.T = (int)T;
+  a.hop = plan->hop;
+  a.scale = (float)plan->scale;
+  a.eps = (float)plan->eps;
+  a.inv_kk = (float)(12.0 / ((double)N * ((double)N * N - 1.0)));
+  a.detrend = plan->detrend;
+  a.flags = flags;
+  a.F_out = (flags & SPECENH_STFT_DROP_NYQUIST) ? N / 2 : N / 2 + 1;
+  a.window = plan->d_window;
+  a.twiddle = plan->d_twiddle;
+  a.dc_coef = plan->d_dc;
+  hipStream_t st = (hipStream_t)stream;
+  const long long F_out = a.F_out;
+  for (long long b0 = 0; b0 < batch; b0 += 1 << 30) {
+    const long long nb = std::min<long long>(1 << 30, batch - b0);
+    StftArgs c = a;
+    c.x = reinterpret_cast<const float*>(reinterpret_cast<const _Float16*>(x) + b0 * x_stride);
+    c.out = out + b0 * F_out * T;
+    hipError_t e;
+    switch (N) {
+      case 64: e = launch_stft<64, true>(c, nb, st); break;
+      case 128: e = launch_stft<128, true>(c, nb, st); break;
+      case 256: e = launch_stft<256, true>(c, nb, st); break;
+      case 512: e = launch_stft<512, true>(c, nb, st); break;
+      case 1024: e = launch_stft<1024, true>(c, nb, st); break;
       default: return set_error(SPECENH_EUNSUPPORTED, "unsupported nperseg");
     }
     if (e != hipSuccess)

@@ -55,6 +55,8 @@ SIGNATURES = {
                                             _c.c_int, _c.c_double]),
     "specenh_stft_plan_destroy": (_c.c_int, [_c.c_void_p]),
     "specenh_stft_workspace_bytes": (_c.c_size_t, [_c.c_void_p, _c.c_longlong]),
+    "specenh_stft_psd_f16": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_longlong, _c.c_longlong,
+                                        _c.c_longlong, _c.c_void_p, _c.c_int, _c.c_void_p]),
     "specenh_stft_psd": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_longlong, _c.c_longlong,
                                     _c.c_longlong, _c.c_void_p, _c.c_int, _c.c_void_p,
                                     _c.c_void_p]),

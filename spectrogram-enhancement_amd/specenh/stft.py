@@ -147,6 +147,15 @@ def get_plan(device: torch.device, nperseg: int, noverlap: int, window="hann", f
 
 def _launch(plan: StftPlan, x: torch.Tensor, out: torch.Tensor, flags: int):
     L = _lib.lib()
+    if x.dtype == torch.float16 and plan.key.nperseg > 1024:
+        x = x.float()  # the fp16-sample kernel covers nperseg <= 1024
+    if x.dtype == torch.float16:  # fp16 samples widened on load: no conversion pass
+        _lib.check(L.specenh_stft_psd_f16(plan.handle, ctypes.c_void_p(x.data_ptr()), x.shape[0],
+                                          x.shape[1], x.stride(0),
+                                          ctypes.c_void_p(out.data_ptr()), flags,
+                                          ctypes.c_void_p(_lib.current_stream_handle(x.device))),
+                   "stft_psd_f16")
+        return
     ws = plan.workspace(x.shape[0], x.device)
     _lib.check(L.specenh_stft_psd(plan.handle, ctypes.c_void_p(x.data_ptr()), x.shape[0],
                                   x.shape[1], x.stride(0), ctypes.c_void_p(out.data_ptr()), flags,
@@ -165,7 +174,7 @@ def _check_input(x: torch.Tensor) -> torch.Tensor:
         x = x.unsqueeze(0)
     if x.dim() != 2:
         raise ValueError("x must be [batch, length]")
-    if x.dtype != torch.float32:
+    if x.dtype not in (torch.float32, torch.float16):
         x = x.float()
     if x.stride(1) != 1:
         x = x.contiguous()
@@ -176,7 +185,8 @@ def stft_psd(x: torch.Tensor, nperseg: int, noverlap: int, window="hann", fs: fl
              scaling="density", detrend="linear", eps: float = 1e-11, log: bool = False,
              normalize: bool = False, drop_nyquist: bool = False,
              out: torch.Tensor | None = None) -> torch.Tensor:
-    """Batched spectrogram of ``x[B, L]`` (fp32, on a ROCm device) -> ``[B, F, T]`` fp32.
+    """Batched spectrogram of ``x[B, L]`` (fp32 or fp16 samples, on a ROCm device) ->
+    ``[B, F, T]`` fp32 (fp16 samples are widened on load; the arithmetic is fp32).
 
     ``F = nperseg//2 + 1`` (``nperseg//2`` with ``drop_nyquist``),
     ``T = (L - nperseg)//(nperseg - noverlap) + 1``.

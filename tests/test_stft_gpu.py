@@ -175,3 +175,23 @@ def test_full_c2_batch_properties(gpu_device):
     for b in (0, 1, 2047, 4095):
         truth, _, _ = ref.specgr_arrays(x[b].double().cpu().numpy(), p)
         assert np.abs(S[b].double().cpu().numpy() - truth).max() <= TOL_NORM
+
+
+@pytest.mark.parametrize("nperseg,noverlap,flags", [(256, 128, 7), (1024, 768, 7), (64, 16, 0),
+                                                    (512, 256, 1)])
+def test_fp16_samples_equal_fp32_path(gpu_device, nperseg, noverlap, flags):
+    """specenh_stft_psd_f16 (fp16 samples widened on load, the C5 stream's input) is the
+    same arithmetic as the fp32 path on the same values: bitwise-identical output, also
+    with a row stride larger than the signal length."""
+    import torch
+
+    from specenh import stft
+
+    g = torch.Generator(device="cpu").manual_seed(nperseg)
+    x = (torch.randn(6, 9000, generator=g) + torch.linspace(-1, 1, 9000)).to(torch.float16)
+    x = x.to(gpu_device)[:, : 9000 - 37]  # strided rows (x_stride > length)
+    kw = dict(nperseg=nperseg, noverlap=noverlap, window="hann", fs=5e5,
+              log=bool(flags & 1), normalize=bool(flags & 2), drop_nyquist=bool(flags & 4))
+    a = stft.stft_psd(x, **kw)
+    b = stft.stft_psd(x.float().contiguous(), **kw)
+    assert torch.equal(a, b)

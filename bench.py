@@ -210,6 +210,8 @@ def main():
     ap.add_argument("--cpu-shots", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stages", action="store_true")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the batch is split over (staggered chains; 1 = serial)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -254,10 +256,41 @@ def main():
     def stage_ae(timing=None):
         return eng.forward(A, timing=timing)
 
+    # The timed step: the batch splits into NS slices, each running the whole chain on its
+    # own HIP stream with its own autoencoder buffers. Slice h > 0 starts once slice h-1's
+    # SVD is done, so its latency-bound STFT/SVD kernels co-run with the conv layers of
+    # the slice ahead (and, with no sync between steps, the next step's head overlaps this
+    # step's tail). Every shot still goes through every stage inside the step.
+    NS = max(1, args.streams) if B % max(1, args.streams) == 0 else 1
+    Hs = B // NS
+    if NS > 1:
+        sstreams = [torch.cuda.Stream(dev) for _ in range(NS)]
+        sengs = [eng]
+        for _ in range(NS - 1):
+            e2 = ae.AutoencoderEngine(ops, (HW5, HW5, 1), compute_dtype="float16", device=dev)
+            e2.set_keras_weights(ae_weights())
+            sengs.append(e2)
+        sdone = [torch.cuda.Event() for _ in range(NS)]
+
     def step():
-        stage_stft()
-        stage_svd()
-        return stage_ae()
+        if NS == 1:
+            stage_stft()
+            stage_svd()
+            return stage_ae()
+        outs = []
+        for h in range(NS):
+            s_h = sstreams[h]
+            if h > 0:
+                s_h.wait_event(sdone[h - 1])
+            with torch.cuda.stream(s_h):
+                sl = slice(h * Hs, (h + 1) * Hs)
+                pipeline_data.specgr_batch(x16[sl], SPEC5, out=S[sl])
+                svd.denoise_batch(S[sl], out=A[sl].view(Hs, HW5, HW5))
+                sdone[h].record(s_h)
+                outs.append(sengs[h].forward(A[sl]))
+        # no join with the current stream here: step i+1's slices queue behind step i's on
+        # their own streams; the barrier (device-wide synchronize) closes the timed region
+        return outs
 
     for _ in range(args.warmup):
         step()
@@ -391,6 +424,8 @@ def main():
 
         Y = step()
         torch.cuda.synchronize()
+        if isinstance(Y, list):  # per-stream slices, in shot order
+            Y = torch.cat(Y)
         spec = ae_layers()
         params, it = [], iter(ae_weights())
         for lay in spec:
@@ -434,7 +469,7 @@ def main():
                                "fp16 forward",
                    "shots_per_step": B, "samples": L5, "stft_dtype": "fp32",
                    "svd_dtype": "fp32 (fp64 small algebra)", "ae_dtype": "fp16",
-                   "parallelism": f"shot-sharded x{world}"},
+                   "parallelism": f"shot-sharded x{world}", "streams_per_gpu": NS},
         "roofline": {k: dom[k] for k in ("bound", "achieved", "peak", "unit", "frac",
                                            "traffic")} |
                     {"kernel": f"{dom['layer']} launch of the autoencoder forward "

@@ -29,7 +29,9 @@ Rank 0 prints ONE JSON line with, besides the contract fields:
                 channel layers run on the VALU, v_dot2 314.6 TFLOP/s). traffic = measured HBM
                 bytes of that launch from profiles/pmc_traffic.json (rocprofv3 --pmc passes of
                 tools/pmc_traffic.sh at the same shapes); stages.ae_layers has every layer.
-  stages        per-stage ms of one step, and the C2 STFT-only configuration (4096 x
+  stages        per-stage ms of one slice (stages.shots_per_launch shots: the launch shape
+                of the timed step, which splits the batch over --streams HIP streams;
+                default 2), and the C2 STFT-only configuration (4096 x
                 65,536 fp32, nperseg 1024 / hop 256) with its HBM roofline.
   cpu_baseline  the same chain on the host CPU (scipy.signal.spectrogram + log/min-max,
                 numpy SVD, torch-CPU autoencoder with the same weights) on a bounded
@@ -247,22 +249,26 @@ def main():
     eng.set_keras_weights(ae_weights())
     torch.cuda.synchronize()
 
+    NS = max(1, args.streams) if B % max(1, args.streams) == 0 else 1
+    Hs = B // NS  # shots per launch in the timed step (one slice per stream)
+
+    # One slice (Hs shots) through each stage: the launch configuration of the timed step,
+    # used for the per-layer roofline and the stage breakdown, so that every launch of the
+    # run has one shape and rocprofv3's per-kernel averages match the fields below.
     def stage_stft():
-        pipeline_data.specgr_batch(x16, SPEC5, out=S)
+        pipeline_data.specgr_batch(x16[:Hs], SPEC5, out=S[:Hs])
 
     def stage_svd():  # fp32 SVD, reconstruction stored as the autoencoder's fp16 input
-        svd.denoise_batch(S, out=A.view(B, HW5, HW5))
+        svd.denoise_batch(S[:Hs], out=A[:Hs].view(Hs, HW5, HW5))
 
     def stage_ae(timing=None):
-        return eng.forward(A, timing=timing)
+        return eng.forward(A[:Hs], timing=timing)
 
     # The timed step: the batch splits into NS slices, each running the whole chain on its
     # own HIP stream with its own autoencoder buffers. Slice h > 0 starts once slice h-1's
     # SVD is done, so its latency-bound STFT/SVD kernels co-run with the conv layers of
     # the slice ahead (and, with no sync between steps, the next step's head overlaps this
     # step's tail). Every shot still goes through every stage inside the step.
-    NS = max(1, args.streams) if B % max(1, args.streams) == 0 else 1
-    Hs = B // NS
     if NS > 1:
         sstreams = [torch.cuda.Stream(dev) for _ in range(NS)]
         sengs = [eng]
@@ -328,21 +334,23 @@ def main():
     layers = []
     for name, c, ms in zip(LAYER_NAMES, ae_layer_costs(), layer_ms):
         peak_c = MFMA_PEAK_TFLOPS if c["unit"] == "mfma" else VALU_DOT2_PEAK_TFLOPS
-        t_c = c["flops"] * B / (peak_c * 1e12)
-        nb = c["bytes"] * B + c["weight_bytes"]
+        t_c = c["flops"] * Hs / (peak_c * 1e12)
+        nb = c["bytes"] * Hs + c["weight_bytes"]
         t_m = nb / (HBM_PEAK_GBPS * 1e9)
         if t_m >= t_c:
             ach = nb / (ms * 1e-3) / 1e9
             rl = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                   "frac": ach / HBM_PEAK_GBPS}
         else:
-            ach = c["flops"] * B / (ms * 1e-3) / 1e12
+            ach = c["flops"] * Hs / (ms * 1e-3) / 1e12
             rl = {"bound": c["unit"], "achieved": ach, "peak": peak_c, "unit": "TFLOP/s",
                   "frac": ach / peak_c}
         tr = pmc.get(name)
         rl.update({"layer": name, "kernel_ms": float(ms), "alg_bytes_per_launch": nb,
-                   "flops_per_launch": c["flops"] * B,
-                   "traffic": tr["hbm_bytes"] if tr else None,
+                   "flops_per_launch": c["flops"] * Hs,
+                   # PMC passes ran 4096-shot launches; these kernels' traffic is linear
+                   # in the shot count (per-image tiles), scaled to this launch
+                   "traffic": tr["hbm_bytes"] * Hs / tr.get("batch", 4096) if tr else None,
                    "traffic_kernel": tr["kernel"] if tr else None})
         layers.append(rl)
     dom = layers[int(np.argmax(layer_ms))]
@@ -361,7 +369,8 @@ def main():
             evs[3].synchronize()
             acc += [evs[i].elapsed_time(evs[i + 1]) for i in range(3)]
         acc /= reps
-        stages = {"ms": dict(zip(["stft_specgr_f16in", "svd_denoise_to_f16",
+        stages = {"shots_per_launch": Hs,
+                  "ms": dict(zip(["stft_specgr_f16in", "svd_denoise_to_f16",
                                   "ae_forward"], acc.round(4).tolist())),
                   "conv_ms_per_layer": layer_ms.round(4).tolist(),
                   "ae_layers": layers}
@@ -467,7 +476,7 @@ def main():
                                "shots -> specgr 128x128 (256 hann / hop 128) -> "
                                "denoiseSignal default -> 3-layer conv AE (16/32/64, 5x5) "
                                "fp16 forward",
-                   "shots_per_step": B, "samples": L5, "stft_dtype": "fp32",
+                   "shots_per_step": B, "shots_per_launch": Hs, "samples": L5, "stft_dtype": "fp32",
                    "svd_dtype": "fp32 (fp64 small algebra)", "ae_dtype": "fp16",
                    "parallelism": f"shot-sharded x{world}", "streams_per_gpu": NS},
         "roofline": {k: dom[k] for k in ("bound", "achieved", "peak", "unit", "frac",

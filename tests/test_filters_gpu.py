@@ -130,3 +130,21 @@ def test_label_pipeline_device_batch(gpu_device):
         np.testing.assert_array_equal(out[b], g)
         u = filters.gaussblr(torch.as_tensor(S[b], device=gpu_device)).cpu().numpy()
         np.testing.assert_allclose(u, ref.gaussblr(S[b]).astype(np.float32), rtol=0, atol=0)
+
+
+def test_gaussblr_morph_constant_and_fp32(gpu_device):
+    """Edge cases the reference hits: a constant image (rescale's 0/0 -> NaN, as numpy),
+    and float32 device input quantised in float32 (numpy would do the same for an fp32
+    array)."""
+    import torch
+
+    from specenh import filters
+
+    c = np.full((16, 40), 0.25)
+    with np.errstate(invalid="ignore"):
+        np.testing.assert_array_equal(filters.gaussblr(c), ref.gaussblr(c))
+        np.testing.assert_array_equal(filters.morph(c), ref.morph(c))
+    assert np.isnan(filters.morph(c)).all()
+    s = (np.random.default_rng(11).random((40, 70)) ** 2).astype(np.float32)
+    m = filters.morph(torch.as_tensor(s, device=gpu_device)).cpu().numpy()
+    np.testing.assert_array_equal(m, ref.morph(s).astype(np.float32))

@@ -115,12 +115,17 @@ int specenh_csd(const specenh_csd_plan* plan, const float* x, const float* y, lo
  * (spec_denoising/denoising_by_svd.ipynb:188-229):
  *   u, s, vh = np.linalg.svd(A, full_matrices=False)
  *   out = u[:, start:stop] @ diag(s[start:stop]) @ vh[start:stop, :]
- * with the notebook's clamping (start < 0 -> 0, stop > r -> r, r = min(m, n)) and
- * start >= stop -> zeros. A: device fp32, matrix b at A + b*a_stride, row-major m x n.
- * out: device fp32 [batch][m][n]. The top-K singular subspace it needs (K = stop, or
- * start when stop == r) must satisfy K <= 40 (SPECENH_EUNSUPPORTED otherwise).
- * workspace: >= specenh_svd_workspace_bytes(batch, m, n, K) bytes. */
+ * with the notebook's clamping (start < 0 -> 0, stop > r -> r, r = min(m, n)) followed by
+ * Python slicing: a negative stop counts from the end (stop + r, floored at 0), an empty
+ * slice gives zeros. A: device fp32, matrix b at A + b*a_stride, row-major m x n.
+ * out: device fp32 [batch][m][n]. Kept ranges reachable through a top-K singular subspace
+ * with K <= 40 (K = stop, or start when stop == r) use fp32-MFMA subspace iteration; any
+ * other range (wide ranges, the bottom of the spectrum) uses fp64 eigenvectors of the Gram
+ * matrix and needs min(m, n) <= 256 (SPECENH_EUNSUPPORTED otherwise).
+ * workspace: >= specenh_svd_denoise_workspace_bytes(batch, m, n, start, stop) bytes
+ * (specenh_svd_workspace_bytes(batch, m, n, K) is the same for the top-K forms). */
 size_t specenh_svd_workspace_bytes(long long batch, int m, int n, int kmax);
+size_t specenh_svd_denoise_workspace_bytes(long long batch, int m, int n, int start, int stop);
 int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long a_stride,
                         int start, int stop, float* out, void* workspace, void* stream);
 /* The same with the output written as out_dtype (SPECENH_DTYPE_F32 / _BF16 / _F16, codes
@@ -133,17 +138,18 @@ int specenh_svd_denoise_ex(const float* A, long long batch, int m, int n, long l
 /* Gavish-Donoho optimal hard-threshold modes of the same denoiser:
  *   num_sing = #{ s_i > omega(beta) * median(s) },  beta = min(m, n) / max(m, n),
  *   omega(beta) = 0.56 beta^3 - 0.95 beta^2 + 1.82 beta + 1.43   (denoising_by_svd.ipynb:155-159)
- *   SPECENH_SVD_OPTIMAL  keep components [0, num_sing - 1): denoiseSignal(A, use_optimal=True)
- *                        (:210-217, then the :224-227 clamping; num_sing <= 1 gives zeros)
- *   SPECENH_SVD_COMPUTE  keep components [1, 2 num_sing): computeSignal(A) (:161-186); the
- *                        reference raises IndexError when 2 num_sing > min(m, n):
- *                        SPECENH_ERANGE, nothing written.
- * The singular values come from the fp64 Gram matrix (Householder tridiagonalisation +
- * Sturm bisection for the two middle order statistics and the count); the kept range is
- * then reconstructed as in specenh_svd_denoise. Needs min(m, n) <= 256 and a kept range
- * ending at K <= 40 (SPECENH_EUNSUPPORTED otherwise). num_sing (device int[batch]) and
- * median_sv (device double[batch]) are optional outputs. Synchronises `stream` once (the
- * subspace width depends on the counts). */
+ *   SPECENH_SVD_OPTIMAL  keep u[:, 0:num_sing-1]: denoiseSignal(A, use_optimal=True)
+ *                        (:210-228; num_sing == 1 gives zeros, num_sing == 0 gives stop = -1,
+ *                        i.e. components [0, r-1))
+ *   SPECENH_SVD_COMPUTE  keep components [1, 2 num_sing): computeSignal(A) (:161-186); when
+ *                        2 num_sing > min(m, n) the notebook's s[idx] raises IndexError ->
+ *                        SPECENH_ERANGE (out's contents unspecified).
+ * The singular values and vectors come from the fp64 Gram matrix (Householder
+ * tridiagonalisation, Sturm bisection for the median, the count and each kept eigenvalue,
+ * inverse iteration, reflectors applied back), per matrix, with no host round trip for
+ * SPECENH_SVD_OPTIMAL (SPECENH_SVD_COMPUTE synchronises `stream` once to raise the
+ * IndexError). Needs min(m, n) <= 256. num_sing (device int[batch]) and median_sv (device
+ * double[batch]) are optional outputs. */
 #define SPECENH_SVD_OPTIMAL 0
 #define SPECENH_SVD_COMPUTE 1
 size_t specenh_svd_optimal_workspace_bytes(long long batch, int m, int n);

@@ -6,7 +6,10 @@ Restates ``spec_denoising/denoising_by_svd.ipynb`` code cell 1:
   * ``denoiseSignal``  (:188-229)  thin SVD, keep components [start, stop):
       defaults start=1, stop=r (i.e. A minus its top component);
       use_optimal: start=0, stop=num_sing-1 with num_sing = #(s > omega(beta)*median(s));
-      clamps start<0 -> 0 and stop>r -> r; start>=stop gives zeros.
+      clamps start<0 -> 0 and stop>r -> r (:224-227), then slices u[:, start:stop] with
+      Python semantics (:228): a negative stop counts from the end (stop + r, floored at 0),
+      so use_optimal with num_sing == 0 (stop = -1) keeps [0, r-1); an empty slice gives
+      zeros.
 The arithmetic is numpy -> LAPACK gesdd; here it is evaluated in float64.
 Pinned by tests/test_oracle_golden.py against the notebook's own outputs.
 """
@@ -27,8 +30,14 @@ def optimal_rank(s: np.ndarray, shape) -> int:
     return int((s > t_star).sum())
 
 
+def slice_bounds(r: int, start: int, stop: int):
+    """Python's slice s[start:stop] on a length-r axis as [lo, hi) (start already >= 0)."""
+    sl = range(r)[start:stop]
+    return sl.start, max(sl.stop, sl.start)
+
+
 def resolve_range(r: int, start=None, stop=None, use_optimal=False, s=None, shape=None):
-    """The start/stop logic of denoiseSignal (:210-227), returned as a python range."""
+    """The start/stop logic of denoiseSignal (:210-228), returned as the kept [lo, hi)."""
     if use_optimal:
         num_sing = optimal_rank(s, shape)
         start, stop = 0, num_sing - 1
@@ -41,16 +50,16 @@ def resolve_range(r: int, start=None, stop=None, use_optimal=False, s=None, shap
         start = 0
     if stop > r:
         stop = r
-    return start, stop
+    return slice_bounds(r, int(start), int(stop))
 
 
 def denoiseSignal(matrix, start=None, stop=None, use_optimal=False):
     a = np.asarray(matrix, dtype=np.float64)
     u, s, vh = np.linalg.svd(a, full_matrices=False)
-    start, stop = resolve_range(len(s), start, stop, use_optimal, s, a.shape)
-    if stop <= start:
+    lo, hi = resolve_range(len(s), start, stop, use_optimal, s, a.shape)
+    if hi <= lo:
         return np.zeros_like(a)
-    return (u[:, start:stop] * s[start:stop]) @ vh[start:stop, :]
+    return (u[:, lo:hi] * s[lo:hi]) @ vh[lo:hi, :]
 
 
 def computeSignal(matrix):

@@ -473,10 +473,17 @@ struct SsLayout {
 };
 
 // One workgroup per matrix: top-K eigenpairs of G (r x r) -> V[b] (r x K), theta[b] (K).
+// With flags, the boundary Ritz pairs of the kept range (component K-1, and cut2 when the
+// range starts inside the subspace) are checked: sqrt(theta_c) * ||G v_c - theta_c v_c|| /
+// (theta_c - theta_{c+1}) bounds the reconstruction error their angle causes (Davis-Kahan);
+// above tolv * ||X||_F the matrix is flagged for the fp64 eigen path (a cut with no
+// spectral gap, e.g. inside a noise bulk, where subspace iteration does not converge).
 template <int P>
 __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, int r, int K,
                                                               int iters, float* V,
-                                                              float* theta) {
+                                                              float* theta, int cut2,
+                                                              float tolv, int* flags) {
+  __shared__ double sRed[4];
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* sS = reinterpret_cast<double*>(smem);            // P x P
   double* sRi = sS + P * P;                                  // P x P
@@ -558,6 +565,42 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
     }
   }
   __syncthreads();
+  if (flags) {
+    auto bsum = [&](double v) {
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+      __syncthreads();
+      if ((tid & 63) == 0) sRed[tid >> 6] = v;
+      __syncthreads();
+      return (sRed[0] + sRed[1]) + (sRed[2] + sRed[3]);
+    };
+    double tr = 0.0;
+    for (int i = tid; i < r; i += SS_THREADS) tr += Gb[(long long)i * r + i];
+    tr = bsum(tr);
+    int bad = 0;
+    for (int which = 0; which < 2; ++which) {
+      const int c = which == 0 ? K - 1 : cut2;  // uniform
+      if (c < 0 || c >= K) continue;
+      const int col = sOrd[c];
+      const double th = sH[col * P + col];
+      double acc = 0.0;
+      for (int i = tid; i < r; i += SS_THREADS) {
+        double ri = 0.0;
+#pragma unroll
+        for (int d = 0; d < P; ++d)
+          ri = fma((double)sY[i * P + d] - th * (double)sZ[i * P + d], (double)sQ[d * P + col], ri);
+        acc = fma(ri, ri, acc);
+      }
+      const double res = sqrt(bsum(acc));
+      if (c + 1 >= P) {
+        if (P < r) bad = 1;  // no Ritz value past the cut to measure the gap against
+        continue;
+      }
+      const double gap = th - (double)sH[sOrd[c + 1] * P + sOrd[c + 1]];
+      if (!(sqrt(fmax(th, 0.0)) * res <= (double)tolv * gap * sqrt(fmax(tr, 0.0)))) bad = 1;
+    }
+    if (tid == 0) flags[b] = bad;
+  }
   float* Vb = V + b * (long long)r * K;  // V[:, c] = Z Q[:, ord[c]], c < K
   for (int idx = tid; idx < r * K; idx += SS_THREADS) {
     const int i = idx / K, c = idx % K;
@@ -654,8 +697,10 @@ __global__ __launch_bounds__(256) void recon_kernel(XView x, int Kr, int r, cons
 
 // fp64 Gram G = X^T X: 64x64 tile per workgroup (upper-triangle tiles, mirrored), 16 rows
 // of X per LDS stage, 4x4 outputs per thread. Products of fp32 inputs are exact in fp64.
-__global__ __launch_bounds__(256) void gram64_kernel(XView x, int K, int r, double* G, int nts) {
+__global__ __launch_bounds__(256) void gram64_kernel(XView x, int K, int r, double* G, int nts,
+                                                     const int* only) {
   __shared__ double sa[16][65], sb[16][65];
+  if (only && !only[blockIdx.y]) return;  // uniform: matrix not selected
   int t = blockIdx.x, ti = 0;
   while (t >= nts - ti) {
     t -= nts - ti;
@@ -726,30 +771,43 @@ __device__ __forceinline__ double block_sum256(double v, double* red) {
 // n <= 256, one workgroup per matrix; thread i owns column i of the trailing block):
 // d = diagonal, e = off-diagonal. Step k: v from A[k+1:, k], p = tau A22 v,
 // w = p - (tau/2)(p.v) v, A22 -= v w^T + w v^T (LAPACK dsytd2 / dlarfg arithmetic).
-__global__ __launch_bounds__(256) void tridiag_kernel(double* G, int n, double* dg, double* eg) {
+// With taug, the reflectors are kept for the eigenvector back-transform: v_k (v_k[0] = 1
+// implicit) overwrites row k right of the diagonal (never read again), tau_k -> taug[k];
+// G = Q T Q^T with Q = H_0 H_1 ... H_{n-3}.
+__global__ __launch_bounds__(256) void tridiag_kernel(double* G, int n, double* dg, double* eg,
+                                                      double* taug, const int* only) {
   __shared__ double sv[256], sw[256], red[4];
   const long long b = blockIdx.x;
+  if (only && !only[b]) return;
   double* A = G + b * (long long)n * n;
   double* d = dg + b * n;
   double* e = eg + b * n;
+  double* taub = taug ? taug + b * n : nullptr;
   const int tid = threadIdx.x;
   for (int k = 0; k + 2 < n; ++k) {
     const int len = n - k - 1;
-    const double* rowk = A + (long long)k * n + k + 1;  // = column k below the diagonal
+    double* rowk = A + (long long)k * n + k + 1;  // = column k below the diagonal
     const double xv = tid < len ? rowk[tid] : 0.0;
     const double s2 = block_sum256(tid >= 1 && tid < len ? xv * xv : 0.0, red);
     const double alpha = rowk[0];
     if (tid == 0) d[k] = A[(long long)k * n + k];
     if (s2 == 0.0) {  // uniform: already tridiagonal in this column
-      if (tid == 0) e[k] = alpha;
+      if (tid == 0) {
+        e[k] = alpha;
+        if (taub) taub[k] = 0.0;
+      }
       continue;
     }
     const double beta = -copysign(sqrt(alpha * alpha + s2), alpha);
     const double tau = (beta - alpha) / beta;
     const double scal = 1.0 / (alpha - beta);
-    if (tid == 0) e[k] = beta;
+    if (tid == 0) {
+      e[k] = beta;
+      if (taub) taub[k] = tau;
+    }
     const double vi = tid == 0 ? 1.0 : (tid < len ? xv * scal : 0.0);
     if (tid < len) sv[tid] = vi;
+    if (taub && tid >= 1 && tid < len) rowk[tid] = vi;  // rowk[0] (alpha) is read above
     __syncthreads();
     double p = 0.0;
     if (tid < len) {
@@ -855,6 +913,332 @@ __global__ __launch_bounds__(64) void optimal_rank_kernel(const double* dg, cons
   }
 }
 
+// ---------------------------------------------------------------- any kept range
+// A kept range [lo, hi) that would need more than a top-40 subspace, or the bottom of the
+// spectrum (a negative stop, use_optimal with num_sing == 0: denoising_by_svd.ipynb:216-228),
+// is reconstructed from eigenvectors of the fp64 Gram matrix: Householder tridiagonal form
+// (tridiag_kernel, reflectors kept), Sturm bisection for each selected eigenvalue, inverse
+// iteration on the tridiagonal (LU with partial pivoting, LAPACK dlagtf/dlagts arithmetic;
+// near-degenerate eigenvalues are iterated in sequence and orthogonalised against each other
+// as dstein does), the reflectors applied back, then out = X V V^T for the kept set, or
+// out = X - X V V^T for its complement, whichever set is smaller (<= r/2 vectors).
+constexpr int EIG_MAXN = 256;
+constexpr int EIG_ITERS = 4;
+
+// Kept components [lo, hi) (descending singular values) -> selected ascending eigen-indices
+// [p0, p1) u [q0, q1) and the complement flag.
+__device__ __forceinline__ void eig_select(int r, int lo, int hi, int& p0, int& p1, int& q0,
+                                           int& q1, int& comp) {
+  lo = max(lo, 0);
+  hi = min(hi, r);
+  p0 = p1 = q0 = q1 = 0;
+  comp = 0;
+  if (hi <= lo) return;
+  if (lo + (r - hi) < hi - lo) {
+    comp = 1;
+    p1 = r - hi;
+    q0 = r - lo;
+    q1 = r;
+  } else {
+    p0 = r - hi;
+    p1 = r - lo;
+  }
+}
+
+// lambda_idx (ascending, 0-based) by bisection on the Sturm count, to an absolute width of
+// a few ulps of ||T|| (what inverse iteration needs).
+__device__ double eig_bisect(const double* d, const double* e2, int n, int idx, double lo,
+                             double hi, double pivmin, double atol) {
+  for (int it = 0; it < 96; ++it) {
+    const double mid = 0.5 * (lo + hi);
+    if (hi - lo <= atol || !(mid > lo && mid < hi)) break;
+    if (sturm_count(d, e2, n, mid, pivmin) > idx) hi = mid;
+    else lo = mid;
+  }
+  return 0.5 * (lo + hi);
+}
+
+// y <- (T - lam I)^{-1} y, arrays strided by ld. dlagtf's factorisation (partial pivoting,
+// U with two super-diagonals kept in ua/ub/ud) fused with the forward application of L,
+// then back substitution with pivots below tol perturbed to +-tol (dlagts job = -1).
+__device__ void tri_inverse_solve(const double* d, const double* e, int n, double lam,
+                                  double tol, double* y, double* ua, double* ub, double* ud,
+                                  long long ld) {
+  double a = d[0] - lam, bsup = n > 1 ? e[0] : 0.0, yk = y[0];
+  for (int k = 0; k + 1 < n; ++k) {
+    const double c = e[k], an = d[k + 1] - lam, bn = k + 2 < n ? e[k + 1] : 0.0;
+    const double yn = y[(long long)(k + 1) * ld];
+    if (fabs(a) >= fabs(c)) {  // row k pivots: [a, bsup] over [c, an, bn]
+      const double mult = a != 0.0 ? c / a : 0.0;
+      ua[k * ld] = a;
+      ub[k * ld] = bsup;
+      ud[k * ld] = 0.0;
+      y[k * ld] = yk;
+      a = an - mult * bsup;
+      bsup = bn;
+      yk = yn - mult * yk;
+    } else {  // interchange: row k+1 pivots
+      const double mult = a / c;
+      ua[k * ld] = c;
+      ub[k * ld] = an;
+      ud[k * ld] = bn;
+      y[k * ld] = yn;
+      a = bsup - mult * an;
+      bsup = -mult * bn;
+      yk = yk - mult * yn;
+    }
+  }
+  ua[(long long)(n - 1) * ld] = a;
+  y[(long long)(n - 1) * ld] = yk;
+  double x1 = 0.0, x2 = 0.0;  // x[k+1], x[k+2]
+  for (int k = n - 1; k >= 0; --k) {
+    double piv = ua[k * ld];
+    if (fabs(piv) < tol) piv = piv < 0.0 ? -tol : tol;
+    const double u1 = k + 1 < n ? ub[k * ld] : 0.0, u2 = k + 2 < n ? ud[k * ld] : 0.0;
+    const double xk = (y[k * ld] - u1 * x1 - u2 * x2) / piv;
+    y[k * ld] = xk;
+    x2 = x1;
+    x1 = xk;
+  }
+}
+
+__device__ void col_normalize(double* y, int n, long long ld) {
+  double mx = 0.0;
+  for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(y[i * ld]));
+  if (!(mx > 0.0) || !isfinite(mx)) {  // degenerate solve: restart from a unit vector
+    for (int i = 0; i < n; ++i) y[i * ld] = i == 0 ? 1.0 : 0.0;
+    return;
+  }
+  double s = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double v = y[i * ld] / mx;
+    s = fma(v, v, s);
+  }
+  const double inv = 1.0 / (mx * sqrt(s));
+  for (int i = 0; i < n; ++i) y[i * ld] *= inv;
+}
+
+// One workgroup per matrix. ranges (device int[2 * batch]) gives a per-matrix kept [lo, hi),
+// else the uniform (lo, hi). Writes the selected eigenvectors of G (Q z, fp64) to
+// Z[b][i][j] (row stride ld) and kinfo[b] = {count, complement}.
+__global__ __launch_bounds__(256) void eigvec_kernel(const double* G, const double* dg,
+                                                     const double* eg, const double* taug, int n,
+                                                     int lo, int hi, const int* ranges, double* Z,
+                                                     double* fac, long long ld, int* kinfo,
+                                                     const int* only) {
+  __shared__ double sd[EIG_MAXN], se[EIG_MAXN], se2[EIG_MAXN], slam[EIG_MAXN], sv[EIG_MAXN];
+  __shared__ int sidx[EIG_MAXN], slead[EIG_MAXN];
+  __shared__ double red[4];
+  const long long b = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (only && !only[b]) return;
+  if (ranges) {
+    lo = ranges[2 * b];
+    hi = ranges[2 * b + 1];
+  }
+  int p0, p1, q0, q1, comp;
+  eig_select(n, lo, hi, p0, p1, q0, q1, comp);
+  const int np = p1 - p0, k = np + (q1 - q0);
+  if (tid == 0) {
+    kinfo[2 * b] = k;
+    kinfo[2 * b + 1] = comp;
+  }
+  if (k == 0) return;  // uniform per workgroup
+  double gl = INFINITY, gu = -INFINITY, emax = 0.0;
+  for (int i = tid; i < n; i += 256) {
+    const double di = dg[b * n + i];
+    const double el = i > 0 ? fabs(eg[b * n + i - 1]) : 0.0;
+    const double er = i + 1 < n ? fabs(eg[b * n + i]) : 0.0;
+    sd[i] = di;
+    se[i] = i + 1 < n ? eg[b * n + i] : 0.0;
+    se2[i] = er * er;
+    gl = fmin(gl, di - el - er);
+    gu = fmax(gu, di + el + er);
+    emax = fmax(emax, er * er);
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    gl = fmin(gl, __shfl_xor(gl, m));
+    gu = fmax(gu, __shfl_xor(gu, m));
+    emax = fmax(emax, __shfl_xor(emax, m));
+  }
+  __syncthreads();
+  if ((tid & 63) == 0) {
+    red[tid >> 6] = gl;
+  }
+  __syncthreads();
+  gl = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = gu;
+  __syncthreads();
+  gu = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = emax;
+  __syncthreads();
+  emax = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  const double tnorm = fmax(fabs(gl), fabs(gu)) + 1e-300;
+  const double eps = 2.220446049250313e-16;
+  gl -= 4.0 * eps * tnorm;
+  gu += 4.0 * eps * tnorm;
+  const double pivmin = 2.2250738585072014e-308 * fmax(1.0, emax);
+  // 1. eigenvalues of the selected indices (ascending)
+  for (int j = tid; j < k; j += 256) {
+    const int idx = j < np ? p0 + j : q0 + (j - np);
+    sidx[j] = idx;
+    slam[j] = eig_bisect(sd, se2, n, idx, gl, gu, pivmin, 2.0 * eps * tnorm);
+  }
+  __syncthreads();
+  // 2. clusters: consecutive indices closer than 1e-9 ||T|| share one sequential chain
+  const double ctol = 1e-9 * tnorm;
+  for (int j = tid; j < k; j += 256)
+    slead[j] = (j == 0 || sidx[j] != sidx[j - 1] + 1 || slam[j] - slam[j - 1] > ctol) ? 1 : 0;
+  __syncthreads();
+  double* Zb = Z + b * (long long)n * ld;
+  double* fa = fac + b * (long long)n * ld * 3;
+  // 3. inverse iteration; a chain leader runs its whole cluster in order (dstein)
+  const double tol = eps * tnorm;
+  for (int j0 = tid; j0 < k; j0 += 256) {
+    if (!slead[j0]) continue;
+    for (int j = j0; j < k && (j == j0 || !slead[j]); ++j) {
+      double* y = Zb + j;
+      for (int i = 0; i < n; ++i)
+        y[i * ld] = hash_unit((unsigned)i, (unsigned)(sidx[j] * 7919 + 17)) + (i == sidx[j] % n ? 0.25 : 0.0);
+      for (int it = 0; it < EIG_ITERS; ++it) {
+        for (int q = j0; q < j; ++q) {  // orthogonalise against the cluster's earlier vectors
+          const double* z = Zb + q;
+          double dot = 0.0;
+          for (int i = 0; i < n; ++i) dot = fma(z[i * ld], y[i * ld], dot);
+          for (int i = 0; i < n; ++i) y[i * ld] = fma(-dot, z[i * ld], y[i * ld]);
+        }
+        col_normalize(y, n, ld);
+        tri_inverse_solve(sd, se, n, slam[j], tol, y, fa + j, fa + ld * n + j,
+                          fa + 2 * ld * n + j, ld);
+        col_normalize(y, n, ld);
+      }
+      for (int q = j0; q < j; ++q) {  // final orthogonalisation within the cluster
+        const double* z = Zb + q;
+        double dot = 0.0;
+        for (int i = 0; i < n; ++i) dot = fma(z[i * ld], y[i * ld], dot);
+        for (int i = 0; i < n; ++i) y[i * ld] = fma(-dot, z[i * ld], y[i * ld]);
+      }
+      col_normalize(y, n, ld);
+    }
+  }
+  __syncthreads();
+  // 4. back-transform: z <- H_0 (H_1 (... H_{n-3} z)), reflector k lives in row k of G
+  const double* Gb = G + b * (long long)n * n;
+  const double* taub = taug + b * n;
+  for (int kk = n - 3; kk >= 0; --kk) {
+    const double tau = taub[kk];
+    if (tau == 0.0) continue;  // uniform
+    const int len = n - kk - 1;
+    for (int t = tid; t < len; t += 256) sv[t] = t == 0 ? 1.0 : Gb[(long long)kk * n + kk + 1 + t];
+    __syncthreads();
+    for (int j = tid; j < k; j += 256) {
+      double* z = Zb + (long long)(kk + 1) * ld + j;
+      double dot = 0.0;
+      for (int t = 0; t < len; ++t) dot = fma(sv[t], z[t * ld], dot);
+      dot *= tau;
+      for (int t = 0; t < len; ++t) z[t * ld] = fma(-dot, sv[t], z[t * ld]);
+    }
+    __syncthreads();
+  }
+}
+
+// Per-matrix kept ranges of the optimal modes from num_sing, with the notebook's slicing:
+// use_optimal keeps u[:, 0:num_sing-1] (:216-228; num_sing == 0 -> stop = -1 -> [0, r-1)),
+// computeSignal keeps [1, 2 num_sing) (:181-185; 2 num_sing > r is an IndexError, flagged).
+__global__ void optimal_ranges_kernel(const int* num, long long batch, int r, int mode,
+                                      int* ranges, int* bad) {
+  const long long b = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  const int ns = num[b];
+  int lo, hi;
+  if (mode == SPECENH_SVD_OPTIMAL) {
+    lo = 0;
+    hi = ns - 1;
+    if (hi < 0) hi = max(hi + r, 0);  // Python slice bound
+  } else {
+    lo = 1;
+    hi = 2 * ns;
+    if (ns > 0 && hi > r) {
+      atomicOr(bad, 1);
+      hi = r;
+    }
+  }
+  ranges[2 * b] = min(lo, r);
+  ranges[2 * b + 1] = min(hi, r);
+}
+
+// out = X V V^T (complement = 0) or X - X V V^T, V = the count selected columns of Z[b]
+// (fp64, cast to fp32 in LDS). Workgroup = (matrix, RB rows of X); thread i owns column i
+// of the row block (r <= 256), V streams through LDS 32 columns at a time.
+template <typename TO>
+__global__ __launch_bounds__(256) void recon_eig_kernel(XView x, int Kr, int r, const double* Z,
+                                                        long long ld, const int* kinfo, TO* out,
+                                                        long long out_bstride, long long osk,
+                                                        long long osi, const int* only) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* sX = reinterpret_cast<float*>(smem);  // RB x (r + 1)
+  float* sV = sX + RB * (r + 1);                // r x 33
+  float* sY = sV + r * 33;                      // RB x 33
+  const long long b = blockIdx.y;
+  if (only && !only[b]) return;
+  const int kc = kinfo[2 * b], comp = kinfo[2 * b + 1];
+  const int k0 = blockIdx.x * RB, tid = threadIdx.x;
+  const int rows = min(RB, Kr - k0);
+  const float* X = x.base + b * x.batch_stride;
+  if (x.si == 1) {
+    for (int idx = tid; idx < RB * r; idx += 256) {
+      const int kk = idx / r, i = idx % r;
+      sX[kk * (r + 1) + i] = kk < rows ? X[(long long)(k0 + kk) * x.sk + i] : 0.f;
+    }
+  } else {
+    for (int idx = tid; idx < RB * r; idx += 256) {
+      const int i = idx / RB, kk = idx % RB;
+      sX[kk * (r + 1) + i] = kk < rows ? X[(long long)(k0 + kk) * x.sk + (long long)i * x.si] : 0.f;
+    }
+  }
+  float acc[RB];
+#pragma unroll
+  for (int kk = 0; kk < RB; ++kk) acc[kk] = 0.f;
+  const double* Zb = Z + b * (long long)r * ld;
+  for (int c0 = 0; c0 < kc; c0 += 32) {
+    __syncthreads();  // sX staged / previous chunk consumed
+    for (int idx = tid; idx < r * 32; idx += 256) {
+      const int i = idx >> 5, c = idx & 31;
+      sV[i * 33 + c] = c0 + c < kc ? (float)Zb[(long long)i * ld + c0 + c] : 0.f;
+    }
+    __syncthreads();
+    for (int e = tid; e < RB * 32; e += 256) {
+      const int kk = e >> 5, c = e & 31;
+      float s = 0.f;
+      for (int i = 0; i < r; ++i) s = fmaf(sX[kk * (r + 1) + i], sV[i * 33 + c], s);
+      sY[kk * 33 + c] = s;
+    }
+    __syncthreads();
+    if (tid < r) {
+#pragma unroll
+      for (int kk = 0; kk < RB; ++kk) {
+        float s = acc[kk];
+#pragma unroll 8
+        for (int c = 0; c < 32; ++c) s = fmaf(sY[kk * 33 + c], sV[tid * 33 + c], s);
+        acc[kk] = s;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < r) {
+    TO* Ob = out + b * out_bstride;
+#pragma unroll
+    for (int kk = 0; kk < RB; ++kk) {
+      if (kk >= rows) break;
+      const float v = comp ? sX[kk * (r + 1) + tid] - acc[kk] : acc[kk];
+      Ob[(long long)(k0 + kk) * osk + (long long)tid * osi] = to_out<TO>(v);
+    }
+  }
+}
+
 }  // namespace specenh
 
 using namespace specenh;
@@ -886,7 +1270,7 @@ void launch_gram(const XView& xv, int Kr, int r, float* G, long long batch, hipS
 
 template <int P>
 hipError_t launch_subspace_t(const float* G, int r, int K, float* V, float* theta,
-                             long long batch, hipStream_t st) {
+                             long long batch, hipStream_t st, int cut2, int* flags) {
   const size_t lds = SsLayout<P>::bytes(r);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipError_t e = hipFuncSetAttribute((const void*)subspace_kernel<P>,
@@ -895,19 +1279,19 @@ hipError_t launch_subspace_t(const float* G, int r, int K, float* V, float* thet
   // 3 rounds when the subspace oversamples the wanted K by >= 8 columns, else 5
   const int iters = P >= K + 8 ? 3 : 5;
   hipLaunchKernelGGL(subspace_kernel<P>, dim3((unsigned)batch), dim3(SS_THREADS), lds, st, G, r,
-                     K, iters, V, theta);
+                     K, iters, V, theta, cut2, 1e-6f, flags);
   return hipGetLastError();
 }
 
 hipError_t launch_subspace(int p, const float* G, int r, int K, float* V, float* theta,
-                           long long batch, hipStream_t st) {
+                           long long batch, hipStream_t st, int cut2 = -1, int* flags = nullptr) {
   switch (p) {
-    case 8: return launch_subspace_t<8>(G, r, K, V, theta, batch, st);
-    case 16: return launch_subspace_t<16>(G, r, K, V, theta, batch, st);
-    case 24: return launch_subspace_t<24>(G, r, K, V, theta, batch, st);
-    case 32: return launch_subspace_t<32>(G, r, K, V, theta, batch, st);
-    case 40: return launch_subspace_t<40>(G, r, K, V, theta, batch, st);
-    case 48: return launch_subspace_t<48>(G, r, K, V, theta, batch, st);
+    case 8: return launch_subspace_t<8>(G, r, K, V, theta, batch, st, cut2, flags);
+    case 16: return launch_subspace_t<16>(G, r, K, V, theta, batch, st, cut2, flags);
+    case 24: return launch_subspace_t<24>(G, r, K, V, theta, batch, st, cut2, flags);
+    case 32: return launch_subspace_t<32>(G, r, K, V, theta, batch, st, cut2, flags);
+    case 40: return launch_subspace_t<40>(G, r, K, V, theta, batch, st, cut2, flags);
+    case 48: return launch_subspace_t<48>(G, r, K, V, theta, batch, st, cut2, flags);
     default: return hipErrorInvalidValue;
   }
 }
@@ -953,13 +1337,165 @@ hipError_t launch_recon(int KP, XView xb, int Kr, int r, const float* V, int K, 
 }
 
 size_t dtype_size(int dt) { return dt == SPECENH_DTYPE_F32 ? 4 : 2; }
+
+// ---- eigen path (any kept range, r <= 256): workspace per matrix and chunking
+struct EigLayout {
+  int r;
+  long long ld;  // row stride of Z / the factor arrays: >= r/2 selected vectors
+  size_t per_matrix() const {
+    return (size_t)r * r * 8 + 3 * (size_t)r * 8 + 4 * (size_t)r * ld * 8 + 4 * 4 + 8;
+  }
+  long long chunk(long long batch) const {  // matrices per pass, <= ~512 MB of workspace
+    const long long c = (long long)((512ull << 20) / per_matrix());
+    return std::max(1LL, std::min(batch, c));
+  }
+  size_t bytes(long long batch) const { return (size_t)chunk(batch) * per_matrix() + 256; }
+};
+EigLayout eig_layout(int r) { return EigLayout{r, (long long)(r / 2 + 2)}; }
+
+template <typename TO>
+hipError_t launch_recon_eig_t(XView xb, int Kr, int r, const double* Z, long long ld,
+                              const int* kinfo, void* out, long long ob, long long osk,
+                              long long osi, long long nb, hipStream_t st, const int* only) {
+  const size_t lds = (size_t)RB * (r + 1) * 4 + (size_t)r * 33 * 4 + (size_t)RB * 33 * 4;
+  hipError_t e = hipFuncSetAttribute((const void*)recon_eig_kernel<TO>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(recon_eig_kernel<TO>, dim3((Kr + RB - 1) / RB, (unsigned)nb), dim3(256), lds,
+                     st, xb, Kr, r, Z, ld, kinfo, reinterpret_cast<TO*>(out), ob, osk, osi, only);
+  return hipGetLastError();
+}
+
+hipError_t launch_recon_eig(int odt, XView xb, int Kr, int r, const double* Z, long long ld,
+                            const int* kinfo, void* out, long long ob, long long osk,
+                            long long osi, long long nb, hipStream_t st, const int* only) {
+  if (odt == SPECENH_DTYPE_F16)
+    return launch_recon_eig_t<_Float16>(xb, Kr, r, Z, ld, kinfo, out, ob, osk, osi, nb, st, only);
+  if (odt == SPECENH_DTYPE_BF16)
+    return launch_recon_eig_t<__bf16>(xb, Kr, r, Z, ld, kinfo, out, ob, osk, osi, nb, st, only);
+  return launch_recon_eig_t<float>(xb, Kr, r, Z, ld, kinfo, out, ob, osk, osi, nb, st, only);
+}
+
+// The eigen path over the whole batch, chunk by chunk (stream-ordered, no host sync).
+// Uniform kept range (lo, hi), or with opt_mode >= 0 the per-matrix optimal-threshold range
+// (num_sing / median / bad flag written to the optional outputs).
+int eig_denoise(const float* A, long long batch, int m, int n, long long a_stride, int lo,
+                int hi, int opt_mode, void* out, int odt, int* num_out, double* med_out,
+                int* bad, void* workspace, hipStream_t st, const int* only = nullptr) {
+  const int r = std::min(m, n);
+  if (r > EIG_MAXN)
+    return set_error(SPECENH_EUNSUPPORTED,
+                     "kept range needs the eigen path, which handles min(m, n) <= 256");
+  const EigLayout L = eig_layout(r);
+  const long long ch = L.chunk(batch);
+  char* w = (char*)workspace;
+  double* G64 = (double*)w;
+  double* dd = G64 + ch * (long long)r * r;
+  double* ee = dd + ch * r;
+  double* tau = ee + ch * r;
+  double* Z = tau + ch * r;
+  double* fac = Z + ch * (long long)r * L.ld;
+  int* kinfo = (int*)(fac + 3 * ch * (long long)r * L.ld);
+  int* ranges = kinfo + 2 * ch;
+  int* num = ranges + 2 * ch;
+  double* med = (double*)(((uintptr_t)(num + ch) + 7) & ~(uintptr_t)7);
+  XView xv;
+  xv.batch_stride = a_stride;
+  int Kr;
+  long long osk, osi;
+  if (m >= n) {
+    xv.sk = n; xv.si = 1; Kr = m; osk = n; osi = 1;
+  } else {
+    xv.sk = 1; xv.si = n; Kr = n; osk = 1; osi = n;
+  }
+  const long long ob = (long long)m * n;
+  const size_t osz = dtype_size(odt);
+  const int nts64 = (r + 63) / 64, ntri64 = nts64 * (nts64 + 1) / 2;
+  const double beta = (double)r / (double)std::max(m, n);
+  // omega(beta), denoising_by_svd.ipynb:155-159: sum of coef * beta**(3 - i), Python's order
+  const double omega = ((0.0 + 0.56 * std::pow(beta, 3.0)) + -0.95 * std::pow(beta, 2.0)) +
+                       1.82 * std::pow(beta, 1.0) + 1.43 * std::pow(beta, 0.0);
+  for (long long b0 = 0; b0 < batch; b0 += ch) {
+    const long long nb = std::min(ch, batch - b0);
+    xv.base = A + b0 * a_stride;
+    const int* on = only ? only + b0 : nullptr;
+    hipLaunchKernelGGL(gram64_kernel, dim3(ntri64, (unsigned)nb), dim3(256), 0, st, xv, Kr, r,
+                       G64, nts64, on);
+    hipLaunchKernelGGL(tridiag_kernel, dim3((unsigned)nb), dim3(256), 0, st, G64, r, dd, ee, tau,
+                       on);
+    const int* rg = nullptr;
+    if (opt_mode >= 0) {
+      hipLaunchKernelGGL(optimal_rank_kernel, dim3((unsigned)nb), dim3(64), 0, st, dd, ee, r,
+                         omega, num, med);
+      hipLaunchKernelGGL(optimal_ranges_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0,
+                         st, num, nb, r, opt_mode, ranges, bad);
+      if (num_out && hipMemcpyAsync(num_out + b0, num, (size_t)nb * 4, hipMemcpyDeviceToDevice,
+                                    st) != hipSuccess)
+        return set_error(SPECENH_EHIP, "num_sing copy");
+      if (med_out && hipMemcpyAsync(med_out + b0, med, (size_t)nb * 8, hipMemcpyDeviceToDevice,
+                                    st) != hipSuccess)
+        return set_error(SPECENH_EHIP, "median copy");
+      rg = ranges;
+    }
+    hipLaunchKernelGGL(eigvec_kernel, dim3((unsigned)nb), dim3(256), 0, st, G64, dd, ee, tau, r,
+                       lo, hi, rg, Z, fac, L.ld, kinfo, on);
+    if (hipGetLastError() != hipSuccess) return set_error(SPECENH_EHIP, "eigen path launch");
+    const hipError_t e = launch_recon_eig(odt, xv, Kr, r, Z, L.ld, kinfo,
+                                          static_cast<char*>(out) + (size_t)(b0 * ob) * osz, ob,
+                                          osk, osi, nb, st, on);
+    if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("recon: ") + hipGetErrorString(e));
+  }
+  return SPECENH_OK;
+}
+
+// denoising_by_svd.ipynb:224-228: clamp start < 0 and stop > r, then Python slicing
+// u[:, start:stop] (a negative stop counts from the end) -> kept [lo, hi), hi <= lo empty.
+void resolve_slice(int r, int start, int stop, int& lo, int& hi) {
+  if (start < 0) start = 0;
+  if (stop > r) stop = r;
+  lo = std::min(start, r);
+  hi = stop < 0 ? std::max(stop + r, 0) : stop;
+  if (hi < lo) hi = lo;
+}
+
+// Which path a uniform kept range takes: 0 = zeros/copy (no workspace), 1 = top-K subspace
+// (K returned), 2 = eigen path.
+int range_path(int r, int lo, int hi, int& K) {
+  K = 0;
+  if (hi <= lo || (lo == 0 && hi == r)) return 0;
+  K = hi == r ? lo : hi;
+  return (K <= PMAX - 8 && std::max(8, ((K + 7 + 7) / 8) * 8) <= std::max(8, (r / 8) * 8) &&
+          ((r / 8) * 8 >= K))
+             ? 1
+             : 2;
+}
 }  // namespace
 
 extern "C" {
 
 size_t specenh_svd_workspace_bytes(long long batch, int m, int n, int kmax) {
   const long long r = std::min(m, n);
-  return (size_t)(batch * r * r + batch * r * kmax + batch * kmax) * sizeof(float);
+  if (batch <= 0 || r <= 0) return 16;
+  if (kmax > PMAX - 8 && r <= EIG_MAXN) return eig_layout((int)r).bytes(batch);
+  // subspace path: G, V, theta; for r <= 256 also the per-matrix convergence flags and the
+  // eigen-path workspace that redoes the flagged matrices
+  size_t off = (size_t)(batch * r * r + batch * r * kmax + batch * kmax) * sizeof(float);
+  if (r > EIG_MAXN) return off;
+  off = (off + 255) / 256 * 256 + (size_t)batch * 4;
+  off = (off + 255) / 256 * 256;
+  return off + eig_layout((int)r).bytes(batch);
+}
+
+size_t specenh_svd_denoise_workspace_bytes(long long batch, int m, int n, int start, int stop) {
+  if (batch <= 0 || m <= 0 || n <= 0) return 16;
+  const int r = std::min(m, n);
+  int lo, hi, K;
+  resolve_slice(r, start, stop, lo, hi);
+  switch (range_path(r, lo, hi, K)) {
+    case 1: return specenh_svd_workspace_bytes(batch, m, n, K);
+    case 2: return r <= EIG_MAXN ? eig_layout(r).bytes(batch) : 16;
+    default: return 16;
+  }
 }
 
 int specenh_svd_denoise(const float* A, long long batch, int m, int n, long long a_stride,
@@ -979,21 +1515,18 @@ int specenh_svd_denoise_ex(const float* A, long long batch, int m, int n, long l
   if (!A || !out || !workspace) return set_error(SPECENH_EINVAL, "null pointer");
   if (a_stride < (long long)m * n) return set_error(SPECENH_EINVAL, "a_stride < m*n");
   const int r = std::min(m, n);
-  // denoising_by_svd.ipynb:224-227 clamping
-  if (start < 0) start = 0;
-  if (stop > r) stop = r;
+  int lo, hi, K;
+  resolve_slice(r, start, stop, lo, hi);  // denoising_by_svd.ipynb:224-228
   hipStream_t st = (hipStream_t)stream;
   const long long ob = (long long)m * n;
   const size_t osz = dtype_size(out_dtype);
-  if (stop <= start) {  // empty range: zeros (u[:, s:s] @ ... = 0)
+  const int path = range_path(r, lo, hi, K);
+  if (path == 0 && hi <= lo) {  // empty slice: zeros (u[:, s:s] @ ... = 0)
     if (hipMemsetAsync(out, 0, (size_t)batch * ob * osz, st) != hipSuccess)
       return set_error(SPECENH_EHIP, "memset");
     return SPECENH_OK;
   }
-  // Needed top-K subspace: complement form when stop == r.
-  const bool complement = (stop == r);
-  const int K = complement ? start : stop;
-  if (complement && start == 0) {  // whole range: out = A (u s vh reproduces A)
+  if (path == 0) {  // whole range: out = A (u s vh reproduces A)
     if (out_dtype == SPECENH_DTYPE_F32) {
       if (hipMemcpy2DAsync(out, ob * sizeof(float), A, a_stride * sizeof(float),
                            ob * sizeof(float), batch, hipMemcpyDeviceToDevice, st) != hipSuccess)
@@ -1009,16 +1542,15 @@ int specenh_svd_denoise_ex(const float* A, long long batch, int m, int n, long l
     }
     return SPECENH_OK;
   }
-  if (K > PMAX - 8 || K > r)
-    return set_error(SPECENH_EUNSUPPORTED,
-                     "GPU SVD denoiser needs a top-K subspace with K <= 40 (K = stop, or start "
-                     "when stop == r)");
-  // subspace width: K + 7 oversampling rounded up to a multiple of 8 (8 for the default
-  // K = 1), <= r (rounded down to 8)
+  if (path == 2)  // wide or bottom-of-spectrum range: fp64 eigenvectors (r <= 256)
+    return eig_denoise(A, batch, m, n, a_stride, lo, hi, -1, out, out_dtype, nullptr, nullptr,
+                       nullptr, workspace, st);
+  // Top-K subspace: [lo, hi) = V_hi V_hi^T - V_lo V_lo^T (K = hi), or X - X V_lo V_lo^T when
+  // hi == r (K = lo). Subspace width: K + 7 oversampling rounded up to a multiple of 8 (8 for
+  // the default K = 1), <= r (rounded down to 8).
+  const bool complement = (hi == r);
   int p = std::max(8, ((K + 7 + 7) / 8) * 8);
   if (p > r) p = (r / 8) * 8;
-  if (p < K || p < 8)
-    return set_error(SPECENH_EUNSUPPORTED, "matrix too small for the GPU subspace solver");
   // X orientation: Gram over the smaller dimension
   XView xv;
   xv.base = A;
@@ -1030,14 +1562,27 @@ int specenh_svd_denoise_ex(const float* A, long long batch, int m, int n, long l
   } else {
     xv.sk = 1; xv.si = n; Kr = n; osk = 1; osi = n;
   }
-  const int lo = complement ? 0 : start, hi = complement ? start : stop;
+  if (complement) {  // columns [0, lo) of the top-lo subspace, subtracted from X
+    hi = lo;
+    lo = 0;
+  }
   float* G = (float*)workspace;
   float* V = G + batch * (long long)r * r;
   float* theta = V + batch * (long long)r * K;
+  int* flags = nullptr;
+  void* eig_ws = nullptr;
+  if (r <= EIG_MAXN) {
+    size_t off = (size_t)(batch * r * r + batch * (long long)r * K + batch * K) * sizeof(float);
+    off = (off + 255) / 256 * 256;
+    flags = (int*)((char*)workspace + off);
+    off = (off + (size_t)batch * 4 + 255) / 256 * 256;
+    eig_ws = (char*)workspace + off;
+  }
   launch_gram(xv, Kr, r, G, batch, st);
   if (hipGetLastError() != hipSuccess) return set_error(SPECENH_EHIP, "gram launch");
-  const int KP = ((hi - lo > 0 ? K : 1) + 7) / 8 * 8;
-  hipError_t e = launch_subspace(p, G, r, K, V, theta, batch, st);
+  const int KP = (K + 7) / 8 * 8;
+  hipError_t e = launch_subspace(p, G, r, K, V, theta, batch, st,
+                                 (!complement && lo > 0) ? lo - 1 : -1, flags);
   if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("subspace: ") + hipGetErrorString(e));
   for (long long b0 = 0; b0 < batch; b0 += 65535) {
     const long long nb = std::min<long long>(65535, batch - b0);
@@ -1049,17 +1594,22 @@ int specenh_svd_denoise_ex(const float* A, long long batch, int m, int n, long l
     if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("recon: ") + hipGetErrorString(e));
   }
   if (hipGetLastError() != hipSuccess) return set_error(SPECENH_EHIP, "recon launch");
-  return SPECENH_OK;
+  if (!flags) return SPECENH_OK;
+  // matrices whose cut has no spectral gap: redone (overwritten) by the fp64 eigen path;
+  // every kernel of that path returns at once for the others
+  if (complement) {  // back to the kept range [start, r)
+    lo = hi;
+    hi = r;
+  }
+  return eig_denoise(A, batch, m, n, a_stride, lo, hi, -1, out, out_dtype, nullptr, nullptr,
+                     nullptr, eig_ws, st, flags);
 }
-
 
 size_t specenh_svd_optimal_workspace_bytes(long long batch, int m, int n) {
   if (batch <= 0 || m <= 0 || n <= 0) return 16;
-  const size_t r = (size_t)std::min(m, n);
-  size_t off = (size_t)batch * r * r * 8 + 2 * (size_t)batch * r * 8;  // G64, d, e
-  off += (size_t)batch * (4 + 4 + 8);                                  // num, ranges, median
-  off = (off + 255) / 256 * 256;
-  return off + specenh_svd_workspace_bytes(batch, m, n, PMAX - 8);
+  const int r = std::min(m, n);
+  if (r > EIG_MAXN) return 16;
+  return eig_layout(r).bytes(batch) + 256;  // + the IndexError flag
 }
 
 int specenh_svd_denoise_optimal(const float* A, long long batch, int m, int n,
@@ -1072,117 +1622,25 @@ int specenh_svd_denoise_optimal(const float* A, long long batch, int m, int n,
   if (!A || !out || !workspace) return set_error(SPECENH_EINVAL, "null pointer");
   if (a_stride < (long long)m * n) return set_error(SPECENH_EINVAL, "a_stride < m*n");
   const int r = std::min(m, n);
-  if (r > 256)
+  if (r > EIG_MAXN)
     return set_error(SPECENH_EUNSUPPORTED, "optimal threshold path needs min(m, n) <= 256");
   hipStream_t st = (hipStream_t)stream;
-  // workspace carve (specenh_svd_optimal_workspace_bytes)
-  char* w = (char*)workspace;
-  double* G64 = (double*)w;
-  double* dd = G64 + batch * (long long)r * r;
-  double* ee = dd + batch * (long long)r;
-  int* num = (int*)(ee + batch * (long long)r);
-  int* ranges = num + batch;
-  double* med = (double*)(ranges + 2 * batch);
-  size_t off = (size_t)batch * r * r * 8 + 2 * (size_t)batch * r * 8 + (size_t)batch * 16;
-  off = (off + 255) / 256 * 256;
-  float* G = (float*)(w + off);
-  XView xv;
-  xv.base = A;
-  xv.batch_stride = a_stride;
-  int Kr;
-  long long osk, osi;
-  if (m >= n) {
-    xv.sk = n; xv.si = 1; Kr = m; osk = n; osi = 1;
-  } else {
-    xv.sk = 1; xv.si = n; Kr = n; osk = 1; osi = n;
-  }
-  // 1-3: fp64 Gram, tridiagonal form, median and count above the threshold
-  const int nts64 = (r + 63) / 64;
-  const int ntri64 = nts64 * (nts64 + 1) / 2;
-  for (long long b0 = 0; b0 < batch; b0 += 65535) {
-    const long long nb = std::min<long long>(65535, batch - b0);
-    XView xb = xv;
-    xb.base = A + b0 * a_stride;
-    hipLaunchKernelGGL(gram64_kernel, dim3(ntri64, (unsigned)nb), dim3(256), 0, st, xb, Kr, r,
-                       G64 + b0 * (long long)r * r, nts64);
-  }
-  hipLaunchKernelGGL(tridiag_kernel, dim3((unsigned)batch), dim3(256), 0, st, G64, r, dd, ee);
-  const double beta = (double)r / (double)std::max(m, n);
-  // omega(beta), denoising_by_svd.ipynb:155-159: sum of coef * beta**(3 - i), Python's order
-  const double omega = ((0.0 + 0.56 * std::pow(beta, 3.0)) + -0.95 * std::pow(beta, 2.0)) +
-                       1.82 * std::pow(beta, 1.0) + 1.43 * std::pow(beta, 0.0);
-  hipLaunchKernelGGL(optimal_rank_kernel, dim3((unsigned)batch), dim3(64), 0, st, dd, ee, r,
-                     omega, num, med);
-  if (hipGetLastError() != hipSuccess) return set_error(SPECENH_EHIP, "optimal rank launch");
-  // 4: the kept range per matrix decides the subspace width: one host round trip
-  std::vector<int> hn((size_t)batch);
-  if (hipMemcpyAsync(hn.data(), num, (size_t)batch * sizeof(int), hipMemcpyDeviceToHost, st) !=
-          hipSuccess ||
+  // the IndexError flag sits past the eigen-path workspace
+  int* bad = (int*)((char*)workspace + eig_layout(r).bytes(batch));
+  if (mode == SPECENH_SVD_COMPUTE && hipMemsetAsync(bad, 0, sizeof(int), st) != hipSuccess)
+    return set_error(SPECENH_EHIP, "memset");
+  const int rc = eig_denoise(A, batch, m, n, a_stride, 0, 0, mode, out, SPECENH_DTYPE_F32,
+                             num_sing, median_sv, bad, workspace, st);
+  if (rc != SPECENH_OK || mode != SPECENH_SVD_COMPUTE) return rc;  // use_optimal: no host sync
+  // computeSignal raises IndexError when 2 num_sing > r (:181-185, s[idx] out of bounds):
+  // that needs the counts on the host, one stream sync.
+  int hbad = 0;
+  if (hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
-    return set_error(SPECENH_EHIP, "num_sing readback");
-  if (num_sing &&
-      hipMemcpyAsync(num_sing, num, (size_t)batch * sizeof(int), hipMemcpyDeviceToDevice, st) !=
-          hipSuccess)
-    return set_error(SPECENH_EHIP, "num_sing copy");
-  if (median_sv &&
-      hipMemcpyAsync(median_sv, med, (size_t)batch * sizeof(double), hipMemcpyDeviceToDevice,
-                     st) != hipSuccess)
-    return set_error(SPECENH_EHIP, "median copy");
-  std::vector<int> hr(2 * (size_t)batch);
-  int K = 0;
-  for (long long b = 0; b < batch; ++b) {
-    const int ns = hn[b];
-    int lo, hi;
-    if (mode == SPECENH_SVD_OPTIMAL) {  // :216-217 start = 0, stop = num_sing - 1
-      lo = 0;
-      hi = ns - 1;
-    } else {  // computeSignal :181-185: s[idx] for idx in range(1, 2 num_sing)
-      if (2 * ns - 1 > r - 1 && ns > 0)
-        return set_error(SPECENH_ERANGE, "index " + std::to_string(2 * ns - 1) +
-                                             " is out of bounds for axis 0 with size " +
-                                             std::to_string(r));
-      lo = 1;
-      hi = 2 * ns;
-    }
-    if (lo < 0) lo = 0;  // :224-227 clamping
-    if (hi > r) hi = r;
-    hr[2 * b] = lo;
-    hr[2 * b + 1] = hi;
-    if (hi > lo) K = std::max(K, hi);
-  }
-  if (K == 0) {
-    if (hipMemsetAsync(out, 0, (size_t)batch * m * n * sizeof(float), st) != hipSuccess)
-      return set_error(SPECENH_EHIP, "memset");
-    return SPECENH_OK;
-  }
-  if (K > PMAX - 8 || K > r)
-    return set_error(SPECENH_EUNSUPPORTED,
-                     "the kept range needs a top-" + std::to_string(K) +
-                         " singular subspace; the GPU subspace solver handles K <= 40");
-  if (hipMemcpy(ranges, hr.data(), hr.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
-    return set_error(SPECENH_EHIP, "ranges upload");
-  int p = std::max(8, ((K + 7 + 7) / 8) * 8);
-  if (p > r) p = (r / 8) * 8;
-  if (p < K || p < 8)
-    return set_error(SPECENH_EUNSUPPORTED, "matrix too small for the GPU subspace solver");
-  // 5: fp32 Gram, top-K subspace, per-matrix reconstruction
-  float* V = G + batch * (long long)r * r;
-  float* theta = V + batch * (long long)r * K;
-  launch_gram(xv, Kr, r, G, batch, st);
-  hipError_t e = launch_subspace(p, G, r, K, V, theta, batch, st);
-  if (e != hipSuccess)
-    return set_error(SPECENH_EHIP, std::string("subspace: ") + hipGetErrorString(e));
-  const int KP = (K + 7) / 8 * 8;
-  const long long ob = (long long)m * n;
-  for (long long b0 = 0; b0 < batch; b0 += 65535) {
-    const long long nb = std::min<long long>(65535, batch - b0);
-    XView xb = xv;
-    xb.base = A + b0 * a_stride;
-    e = launch_recon(KP, xb, Kr, r, V + b0 * (long long)r * K, K, 0, 0, 0, ranges + 2 * b0,
-                     out + b0 * ob, ob, osk, osi, nb, st);
-    if (e != hipSuccess)
-      return set_error(SPECENH_EHIP, std::string("recon: ") + hipGetErrorString(e));
-  }
+    return set_error(SPECENH_EHIP, "IndexError flag readback");
+  if (hbad)
+    return set_error(SPECENH_ERANGE, "index out of bounds for axis 0 with size " +
+                                         std::to_string(r) + " (2 * num_sing > min(m, n))");
   return SPECENH_OK;
 }
 

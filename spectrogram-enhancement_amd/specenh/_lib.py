@@ -68,6 +68,8 @@ SIGNATURES = {
                                _c.c_longlong, _c.c_longlong, _c.c_longlong, _c.c_void_p, _c.c_int,
                                _c.c_void_p]),
     "specenh_svd_workspace_bytes": (_c.c_size_t, [_c.c_longlong, _c.c_int, _c.c_int, _c.c_int]),
+    "specenh_svd_denoise_workspace_bytes": (_c.c_size_t, [_c.c_longlong, _c.c_int, _c.c_int,
+                                                          _c.c_int, _c.c_int]),
     "specenh_svd_denoise": (_c.c_int, [_c.c_void_p, _c.c_longlong, _c.c_int, _c.c_int,
                                        _c.c_longlong, _c.c_int, _c.c_int, _c.c_void_p,
                                        _c.c_void_p, _c.c_void_p]),

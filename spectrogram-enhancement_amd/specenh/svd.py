@@ -6,8 +6,9 @@
 Same names, arguments and semantics as the notebook (:155-229):
   * ``omega(beta)``          Gavish-Donoho polynomial (host scalar, as in the notebook)
   * ``denoiseSignal(matrix, start=None, stop=None, use_optimal=False)``
-        keep singular components [start, stop) — defaults start=1, stop=r; clamps
-        start<0 -> 0 and stop>r -> r; start>=stop gives zeros.
+        keep singular components u[:, start:stop] — defaults start=1, stop=r; clamps
+        start<0 -> 0 and stop>r -> r, then Python slicing (a negative stop counts from
+        the end; an empty slice gives zeros).
   * ``denoise_batch(A[B, m, n], start, stop)`` — device tensors in/out (fast path).
 
   * ``computeSignal(matrix)``  components [1, 2*num_sing) (:161-186), IndexError when
@@ -39,7 +40,8 @@ def omega(beta):
 
 
 def _resolve(r: int, start, stop):
-    """denoising_by_svd.ipynb:219-227 (non-optimal branch)."""
+    """denoising_by_svd.ipynb:219-227 (non-optimal branch): defaults and clamping. The
+    slice itself (negative stop, empty ranges) is resolved by the C-ABI like Python does."""
     if start is None:
         start = 1
     if stop is None:
@@ -81,9 +83,8 @@ def denoise_batch(A: torch.Tensor, start=None, stop=None,
     if odt is None or out.numel() != B * m * n or not out.is_contiguous() or out.device != A.device:
         raise ValueError("out must be a contiguous [B, m, n] float32/bfloat16/float16 tensor "
                          "on A's device")
-    K = max(start, stop) if stop < r else start
     L = _lib.lib()
-    ws = torch.empty(max(16, int(L.specenh_svd_workspace_bytes(B, m, n, max(K, 1)))),
+    ws = torch.empty(max(16, int(L.specenh_svd_denoise_workspace_bytes(B, m, n, start, stop))),
                      dtype=torch.uint8, device=A.device)
     _lib.check(L.specenh_svd_denoise_ex(ctypes.c_void_p(A.data_ptr()), B, m, n, A.stride(0),
                                         start, stop, ctypes.c_void_p(out.data_ptr()), odt,

@@ -111,3 +111,40 @@ def test_cv2_restatement_properties():
     assert (opened <= u).all()
     out = filters.label_pipeline(np.random.default_rng(4).random((64, 96)))
     assert out.min() == 0.0 and out.max() == 1.0
+
+
+def _ranges_fixture():
+    d = load_golden("ranges_svd")
+    out = {}
+    for k, v in d.items():
+        tag, key = k.split("__")
+        out.setdefault(tag, {})[key] = v
+    return out
+
+
+def range_args(key):
+    """'r_m4_m2' -> (-4, -2) (make_golden_svd_ranges.py's key format)."""
+    a, b = key[2:].split("_")
+    return tuple(-int(v[1:]) if v.startswith("m") else int(v) for v in (a, b))
+
+
+def test_svd_slice_semantics_match_notebook():
+    """Negative stop, num_sing == 0 under use_optimal, wide kept ranges: the oracle
+    reproduces the notebook's Python slicing (denoising_by_svd.ipynb:216-228)."""
+    for tag, e in _ranges_fixture().items():
+        A = e["A"].astype(np.float64)
+        scale = np.linalg.norm(A)
+        for key, want in e.items():
+            if key.startswith("r_"):
+                got = svd.denoiseSignal(A, *range_args(key))
+            elif key == "optimal":
+                got = svd.denoiseSignal(A, use_optimal=True)
+            elif key == "compute":
+                got = svd.computeSignal(A)
+            else:
+                continue
+            assert np.linalg.norm(got - want) <= 1e-6 * scale, (tag, key)
+        if "num_sing" in e:
+            assert svd.optimal_rank(e["s"], A.shape) == int(e["num_sing"])
+    noise = _ranges_fixture()["noise64x48"]
+    assert int(noise["num_sing"]) == 0 and np.any(noise["optimal"])  # keeps [0, r-1), not zeros

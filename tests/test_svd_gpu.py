@@ -129,12 +129,120 @@ def test_optimal_batched_c3_shape(gpu_device):
 def test_unsupported_modes_raise(gpu_device):
     from specenh import svd
 
-    big = np.random.default_rng(1).standard_normal((128, 96))
+    wide = np.random.default_rng(2).standard_normal((300, 280))
     with pytest.raises(NotImplementedError):
-        svd.denoiseSignal(big, 0, 80)   # needs a top-80 subspace (> 40)
+        svd.denoiseSignal(wide, 0, 80)        # eigen path needs min(m, n) <= 256
     with pytest.raises(NotImplementedError):
-        svd.denoiseSignal(np.random.default_rng(2).standard_normal((300, 280)),
-                          use_optimal=True)  # min(m, n) > 256 on the optimal path
+        svd.denoiseSignal(wide, use_optimal=True)
+
+
+def _ranges():
+    from test_oracle_golden import _ranges_fixture
+    return _ranges_fixture()
+
+
+def _range_err(got, want, A):
+    """||got - want||_F / ||want||_F, or relative to ||A||_F when the kept part carries
+    less than 1% of the matrix norm (fp32 reconstruction error scales with ||A||)."""
+    nw, na = np.linalg.norm(want), np.linalg.norm(A)
+    return np.linalg.norm(got - want) / max(nw, 0.01 * na, 1e-300)
+
+
+@pytest.mark.parametrize("tag", ["noise64x48", "noise40x72", "gap96x80", "gap72x100"])
+def test_slice_semantics_match_notebook(tag, gpu_device):
+    """denoising_by_svd.ipynb:216-228 with Python slicing: negative stop, empty slices,
+    wide kept ranges (K > 40, through the fp64 eigen path), use_optimal with
+    num_sing == 0 (keeps [0, r-1)) and computeSignal, vs the notebook's own outputs."""
+    import torch
+
+    from test_oracle_golden import range_args
+    from specenh import svd
+
+    e = _ranges()[tag]
+    A = e["A"]
+    A64 = A.astype(np.float64)
+    errs = {}
+    for key, want in e.items():
+        if key.startswith("r_"):
+            got = svd.denoiseSignal(A, *range_args(key))
+        elif key == "optimal":
+            got = svd.denoiseSignal(A, use_optimal=True)
+        elif key == "compute":
+            got = svd.computeSignal(A)
+        else:
+            continue
+        assert got.shape == A.shape and got.dtype == np.float64
+        errs[key] = _range_err(got, want.astype(np.float64), A64)
+        if not np.any(want):
+            assert not np.any(got), key
+    print(tag, {k: f"{v:.1e}" for k, v in errs.items()})
+    bad = {k: v for k, v in errs.items() if not v <= TOL}
+    assert not bad, bad
+    _, ns, _ = svd.optimal_batch(torch.as_tensor(A, device=gpu_device), return_rank=True)
+    assert int(ns[0]) == int(e["num_sing"])
+
+
+def test_noise_optimal_keeps_all_but_last(gpu_device):
+    """Pure noise: num_sing == 0, stop = -1: the output is A minus its smallest component
+    (not zeros), batched with a gapped matrix whose range differs."""
+    import torch
+
+    from specenh import svd
+
+    fx = _ranges()
+    A = fx["noise64x48"]["A"]
+    B = fx["gap96x80"]["A"][:64, :48].copy()
+    X = torch.as_tensor(np.stack([A, B]), device=gpu_device)
+    out, ns, _ = svd.optimal_batch(X, return_rank=True)
+    out = out.double().cpu().numpy()
+    for b, M in enumerate((A, B)):
+        M64 = M.astype(np.float64)
+        assert _range_err(out[b], ref.denoiseSignal(M64, use_optimal=True), M64) <= TOL
+    assert int(ns[0]) == 0 and int(ns[1]) > 0
+
+
+def test_c3_geometry_wide_range(gpu_device):
+    """513 x 256 (BASELINE config 3) with a K = 100 kept range: golden from the notebook."""
+    import torch
+
+    from specenh import svd
+
+    e = _ranges()["c3_513x256"]
+    A = np.stack([e["A"], e["A"][::-1].copy()])
+    out = svd.denoise_batch(torch.as_tensor(A, device=gpu_device), 0, 100).double().cpu().numpy()
+    assert _range_err(out[0], e["r_0_100"].astype(np.float64), A[0].astype(np.float64)) <= TOL
+    flipped = e["r_0_100"][::-1].astype(np.float64)  # row permutation commutes with the SVD
+    assert _range_err(out[1], flipped, A[1].astype(np.float64)) <= TOL
+
+
+@pytest.mark.parametrize("args", [(0, 100), (1, -1), (0, -3), (3, 45)])
+def test_eigen_path_half_precision_output(gpu_device, args):
+    """The eigen path's fp16/bf16 store is the fp32 result rounded once."""
+    import torch
+
+    from specenh import svd
+
+    A = torch.as_tensor(np.stack([_ranges()["gap96x80"]["A"]] * 3), device=gpu_device)
+    ref32 = svd.denoise_batch(A, *args)
+    for dt in (torch.float16, torch.bfloat16):
+        out = torch.empty(A.shape, dtype=dt, device=gpu_device)
+        svd.denoise_batch(A, *args, out=out)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref32.to(dt)), dt
+
+
+def test_rank_deficient_complement(gpu_device):
+    """Exactly degenerate eigenvalues (a rank-3 matrix: 45 zero singular values) at the
+    bottom of the spectrum: [0, r-2) through the complement of the bottom 2 (one cluster
+    iterated in sequence) and [0, 40) directly, vs float64 numpy."""
+    from specenh import svd
+
+    rng = np.random.default_rng(5)
+    A = (rng.standard_normal((64, 3)) @ rng.standard_normal((3, 48))).astype(np.float32)
+    A64 = A.astype(np.float64)
+    for args in [(0, -2), (0, 46), (1, -1), (0, 45)]:
+        got = svd.denoiseSignal(A, *args)
+        assert _range_err(got, ref.denoiseSignal(A64, *args), A64) <= TOL, args
 
 
 @pytest.mark.parametrize("shape", [(128, 128), (96, 128), (128, 40), (52, 100)])

@@ -1,7 +1,8 @@
 """ORACLE — CPU restatement of the reference's hot-path arithmetic. TEST INFRASTRUCTURE ONLY.
 
-Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg
-may import this package, and only as the checker / the timed CPU baseline. The
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` and
+accuracy legs (outside the timed region) may import this package, and only as the
+checker / the timed CPU baseline. The
 product path (``spectrogram-enhancement_amd/specenh``) never imports it: the
 HIP extension is the only implementation and fails loudly when missing.
 
@@ -18,4 +19,5 @@ Modules:
   filters      — norm / rescale / quantfilt / meansub
   strips       — patch / unpatch / reshape (patchify semantics restated)
   autoencoder  — PyTorch-CPU restatement of the Keras conv AE (unpinned)
+  checks       — AE output metrics (spread-relative output error, logit error) + tolerances
 """

@@ -346,6 +346,10 @@ class AutoencoderEngine:
                 timing.append(ev)
         return b["h"][n_ops]
 
+    def last_logits(self):
+        """fp32 pre-sigmoid output of the last forward(train=True) (device, reused buffer)."""
+        return self._buffers(self._last_train_N, True)["z"]
+
     def loss_and_grad(self, y, want_grad=True, accumulate=None):
         """BCE of the last forward(train=True) against y (device, same shape).
 

@@ -2,11 +2,15 @@
 oracle (oracle/autoencoder.py, a PyTorch-CPU restatement of the Keras model — parity
 vs Keras itself is unpinned: TensorFlow is absent, SURVEY.md §8 c).
 
-Tolerances (SURVEY.md §8 d):
+Tolerances (SURVEY.md §8 d, oracle/checks.py):
   * fp32 compute: outputs ||d||_inf / ||ref||_inf <= 1e-5; gradients per tensor
     ||d||_2 / ||ref||_2 <= 1e-5 (fp32 accumulation over up to 10^6 terms).
-  * bf16 compute (mixed_bfloat16): output PSNR >= 40 dB vs the fp32 oracle (peak 1, the
-    sigmoid range); gradient cosine similarity >= 0.99.
+  * fp16 / bf16 compute: on weights whose outputs carry a real signal (the trained fixture
+    tests/golden/ae_c4_trained.npz, or gain-scaled glorot for the reference's other
+    variants), out_rel = ||y - y_ref|| / ||y_ref - mean(y_ref)|| and
+    logit_rel = ||z - z_ref|| / ||z_ref|| within checks.TOL (fp16 2e-3, bf16 1e-2; a dropped
+    MFMA k-step moves them by >= 1.3e-2, tests/test_ae_sensitivity.py); bf16 gradient
+    cosine similarity >= 0.99.
 """
 import math
 
@@ -15,12 +19,12 @@ import pytest
 import torch
 
 from oracle import autoencoder as ora
+from oracle import checks
 
 pytestmark = pytest.mark.gpu
 
 TOL_OUT = 1e-5
 TOL_GRAD = 1e-5
-PSNR_MIN = 40.0
 
 
 def _ae():
@@ -87,9 +91,33 @@ def normwise(a, b):
     return float(np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-30))
 
 
-def psnr(a, b):
-    mse = float(np.mean((a.astype(np.float64) - b) ** 2))
-    return math.inf if mse == 0 else 10 * math.log10(1.0 / mse)
+def trained_c4(n=6, seed0=9100):
+    """The trained reference-model weights and C4-style (input, target) pairs."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_ae_weights import c4_pairs, load
+    x, y = c4_pairs(n, seed0)
+    return load(), x, y
+
+
+def set_params(eng, ws):
+    """Keras weight list -> engine + the oracle's per-layer params list."""
+    eng.set_keras_weights(ws)
+    it, params = iter(ws), []
+    for op in eng.ops:
+        params.append(None if op.kind == "pool" else {"W": next(it), "b": next(it)})
+    return params
+
+
+def lowp_errors(eng, params, x):
+    """(out_rel, logit_rel) of the engine's inference output and training-mode logits vs
+    the fp64 oracle."""
+    ref, zref = ref_forward(eng.ops, params, x)
+    got = eng.forward(upload(eng, x), train=False).cpu().numpy()
+    eng.forward(upload(eng, x), train=True)
+    z = eng.last_logits().cpu().numpy()
+    return checks.out_rel(got, ref), checks.logit_rel(z, zref), float(np.std(zref))
 
 
 def ref_model_ops(c1=16, c2=32, c3=64, k=5):
@@ -192,15 +220,20 @@ def test_reference_model_gradients_fp32(gpu_device):
     assert max(errs) <= TOL_GRAD, errs
 
 
-def test_reference_model_bf16_forward_psnr_and_gradients(gpu_device):
+def test_reference_model_bf16_relative_and_gradients(gpu_device):
+    """mixed_bfloat16 on the trained weights and C4-style data: output and logits within
+    checks.TOL of the fp64 oracle, loss within 1e-3 (the trained loss is ~0.18, not the
+    0.69 of an untrained model), gradient cosine >= 0.99 per tensor."""
     ops = ref_model_ops()
-    eng, params = make(ops, (128, 128, 1), dtype="mixed_bfloat16", seed=13)
-    rng = np.random.default_rng(6)
-    x = rng.uniform(0, 1, (4, 128, 128, 1)).astype(np.float32)
-    y = rng.uniform(0, 1, (4, 128, 128, 1)).astype(np.float32)
-    ref, ref_loss, ref_g = ref_forward(ops, params, x, grads=True, y=y)
-    got = eng.forward(upload(eng, x), train=False).cpu().numpy()
-    assert psnr(got, ref) >= PSNR_MIN
+    eng, _ = make(ops, (128, 128, 1), dtype="mixed_bfloat16")
+    ws, x, y = trained_c4(4)
+    params = set_params(eng, ws)
+    o, zr, zstd = lowp_errors(eng, params, x)
+    assert zstd > 1.0
+    tol = checks.TOL["mixed_bfloat16"]
+    assert o <= tol["out_rel"] and zr <= tol["logit_rel"], (o, zr)
+    _, ref_loss, ref_g = ref_forward(ops, params, x, grads=True, y=y)
+    assert ref_loss < 0.4
     eng.forward(upload(eng, x), train=True)
     loss = eng.loss_and_grad(upload(eng, y))
     eng.backward()
@@ -395,14 +428,76 @@ def test_backward_is_bitwise_deterministic(gpu_device):
     assert torch.equal(grads[0], grads[1])
 
 
-def test_reference_model_fp16_forward_psnr(gpu_device):
-    """C5 runs the autoencoder forward in fp16 (MFMA f16, fp32 accumulation)."""
+def test_reference_model_fp16_relative(gpu_device):
+    """C5 runs the autoencoder forward in fp16 (MFMA f16, fp32 accumulation): trained
+    weights, C4-style inputs, out_rel / logit_rel within checks.TOL['float16']."""
     ops = ref_model_ops()
-    eng, params = make(ops, (128, 128, 1), dtype="float16", seed=17)
-    x = np.random.default_rng(10).uniform(0, 1, (4, 128, 128, 1)).astype(np.float32)
-    ref, _ = ref_forward(ops, params, x)
-    got = eng.forward(upload(eng, x), train=False).cpu().numpy()
-    assert psnr(got, ref) >= PSNR_MIN
+    eng, _ = make(ops, (128, 128, 1), dtype="float16")
+    ws, x, _ = trained_c4(6)
+    params = set_params(eng, ws)
+    o, zr, zstd = lowp_errors(eng, params, x)
+    print(f"fp16 out_rel {o:.2e} logit_rel {zr:.2e}")
+    assert zstd > 1.0
+    tol = checks.TOL["float16"]
+    assert o <= tol["out_rel"] and zr <= tol["logit_rel"], (o, zr)
+
+
+def _gain_scaled(ops, seed):
+    """Glorot kernels with a relu gain (He-like variance) and random biases: outputs of an
+    untrained variant that still span the sigmoid (logit std > 0.5)."""
+    params = ora.glorot_params(oracle_spec(ops), seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    ws = []
+    for op, p in zip(ops, params):
+        if p is None:
+            continue
+        k = op.k
+        fan_in = k * k * (op.cin if op.kind == "conv" else op.cin)
+        fan_out = k * k * op.cout
+        g = math.sqrt(2.0 * (fan_in + fan_out) / (2.0 * fan_in)) * (1.6 if op.kind == "convT" else 1.0)
+        if op.act == "sigmoid":
+            g *= 6.0
+        ws += [(p["W"] * g).astype(np.float32),
+               (0.1 * rng.standard_normal(op.cout)).astype(np.float32)]
+    return ws
+
+
+def variant_ops(name):
+    """The reference's other autoencoders (all layers padding='same', MaxPool 2x2)."""
+    ae = _ae()
+    C, P = ae.ConvOp, ae.PoolOp
+    if name == "3layer_256x128":     # manual_scan_3layers.py:186-199, its real input shape
+        return ref_model_ops(), (256, 128, 1)
+    if name == "2layer_64_32_k5":    # manual_scan.py:120-124, 190-199
+        return [C("conv", 1, 64, 5, "relu"), P(), C("conv", 64, 32, 5, "relu"), P(),
+                C("convT", 32, 32, 5, "relu", stride=2), C("convT", 32, 64, 5, "relu", stride=2),
+                C("conv", 64, 1, 5, "sigmoid")], (256, 128, 1)
+    k = {"2layer_32_k7": 7, "2layer_32_k3": 3}[name]  # hyperparam_scan.py:123,153-162;
+    return [C("conv", 1, 32, k, "relu"), P(), C("conv", 32, 32, k, "relu"), P(),  # graphs.ipynb
+            C("convT", 32, 32, k, "relu", stride=2), C("convT", 32, 32, k, "relu", stride=2),
+            C("conv", 32, 1, k, "sigmoid")], (256, 128, 1)
+
+
+@pytest.mark.parametrize("dtype", ["float32", "float16", "mixed_bfloat16"])
+@pytest.mark.parametrize("name", ["3layer_256x128", "2layer_64_32_k5", "2layer_32_k7",
+                                  "2layer_32_k3"])
+def test_reference_variants(gpu_device, name, dtype):
+    """Every autoencoder the reference builds, at its (256, 128, 1) input: fp32 within
+    1e-5 (max-norm), fp16/bf16 within checks.TOL, vs the fp64 oracle."""
+    ops, hwc = variant_ops(name)
+    eng, _ = make(ops, hwc, dtype=dtype)
+    params = set_params(eng, _gain_scaled(ops, seed=len(name)))
+    x = np.random.default_rng(14).uniform(0, 1, (3,) + hwc).astype(np.float32)
+    if dtype == "float32":
+        ref, _ = ref_forward(ops, params, x)
+        got = eng.forward(upload(eng, x), train=False).cpu().numpy()
+        assert np.abs(got - ref).max() / np.abs(ref).max() <= TOL_OUT
+        return
+    o, zr, zstd = lowp_errors(eng, params, x)
+    print(f"{name} {dtype}: out_rel {o:.2e} logit_rel {zr:.2e} (logit std {zstd:.2f})")
+    assert zstd > 0.5
+    tol = checks.TOL[dtype]
+    assert o <= tol["out_rel"] and zr <= tol["logit_rel"], (o, zr)
 
 
 @pytest.mark.parametrize("dtype", ["mixed_bfloat16", "float16"])

@@ -600,22 +600,37 @@ hipError_t launch_stft(const StftArgs& a, long long batch, hipStream_t stream) {
 // The grid is persistent and no larger than the device's resident capacity, so all
 // members of a team are co-resident; tasks are pipelined: a workgroup publishes task i,
 // computes task i+1, and only then waits for task i's team (deadlock-free by induction
-// over i: every publish precedes the same workgroup's next wait). Spins are bounded: a
-// missing member sets the timeout word and the tile is normalised by what arrived.
+// over i: every publish precedes the same workgroup's next wait). Correctness does not
+// rest on co-residency (kernels on other streams or processes can break it): spins are
+// bounded, and a member that gives up stores its tile un-normalised (raw log values),
+// marks the tile in a flag array and sets the (sticky) timeout word, after which no
+// member of the launch waits any more. team_fixup_kernel, launched behind the team kernel
+// on the same stream, normalises exactly the marked tiles from the then-complete
+// granules with the same arithmetic ((v - mn) * inv): bit-identical to the in-kernel path.
 constexpr int TEAM_MAX = 64;           // one wave polls a team's granules
 constexpr int STFT_DEV_NOTEAM = 1 << 17;     // development flag: force stft_psd_kernel
 constexpr int STFT_DEV_FORCETEAM = 1 << 18;  // development flag: team even for small shots
+constexpr int STFT_DEV_GIVEUP = 1 << 19;     // test flag: every team wait gives up at once
 
-__device__ __forceinline__ void team_minmax(const unsigned long long* g, int M, int lane,
-                                            unsigned* tmo, float& mn, float& mx) {
+// Wave-wide: the team's extremes once all M granules are in (returns true), or false when
+// the wait gave up (bounded spins, or another member already timed out in this launch).
+__device__ __forceinline__ bool team_minmax(const unsigned long long* g, int M, int lane,
+                                            unsigned* tmo, float& mn, float& mx,
+                                            bool give_up) {
   unsigned long long v = 0;
-  for (unsigned spins = 0;; ++spins) {
+  bool complete = true;
+  if (give_up) {  // (test flag) exercise the raw-store + fixup path
+    if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    complete = false;
+  }
+  for (unsigned spins = 0; complete; ++spins) {
     if (lane < M) v = __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool ok = lane >= M || ((unsigned)v != 0u && (unsigned)(v >> 32) != 0u);
     if (__all(ok)) break;
     if (spins >= (1u << 20) ||
         __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
       if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      complete = false;
       break;
     }
     __builtin_amdgcn_s_sleep(2);
@@ -629,11 +644,13 @@ __device__ __forceinline__ void team_minmax(const unsigned long long* g, int M, 
   }
   mx = key2f(kmax);
   mn = key2f(~kinv);
+  return complete;
 }
 
 template <int N>
 __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_kernel(
-    StftArgs a, unsigned long long* gran, long long batch, int M, int Q, unsigned* tmo) {
+    StftArgs a, unsigned long long* gran, long long batch, int M, int Q, unsigned* tmo,
+    unsigned char* tile_flag) {
   using C = Cfg<N>;
   using Lo = Layout<N>;
   constexpr int G = C::G;
@@ -716,17 +733,21 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
       const long long sp = shot - Q;
       if (wave == 0) {
         float mn, mx;
-        team_minmax(gran + sp * M, M, lane, tmo, mn, mx);
+        const bool done = team_minmax(gran + sp * M, M, lane, tmo, mn, mx,
+                                      (a.flags & STFT_DEV_GIVEUP) != 0);
         if (lane == 0) {
           s_red[2 * C::WAVES] = mn;
           s_red[2 * C::WAVES + 1] = mx;
+          s_red[2 * C::WAVES + 2] = done ? 1.f : 0.f;
+          if (!done) tile_flag[sp * M + mem] = 1;  // raw tile: team_fixup_kernel finishes it
         }
       }
       lds_barrier();
       const float mn = s_red[2 * C::WAVES];
       const float inv = 1.0f / (s_red[2 * C::WAVES + 1] - mn);  // max == min -> NaN (0/0)
+      const bool done = s_red[2 * C::WAVES + 2] != 0.f;
       const __amdgpu_buffer_rsrc_t orr = make_rsrc(a.out + sp * plane, plane * 4);
-      tile_store<N>(a, s_tile, pvp, gl, fi, tid, orr, t0, mn, inv, true);
+      tile_store<N>(a, s_tile, pvp, gl, fi, tid, orr, t0, mn, inv, done);
     } else {
       lds_barrier();  // s_red is rewritten by the next task only after thread 0 read it
     }
@@ -736,6 +757,36 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
         pvp[i][0] = pvc[i][0];
         pvp[i][1] = pvc[i][1];
       }
+    }
+  }
+}
+
+// Normalises the tiles a team kernel stored raw (tile_flag set), from the granules, which
+// are complete once that kernel has finished. Returns at once when no wait timed out.
+__global__ __launch_bounds__(256) void team_fixup_kernel(float* out, int F_out, int T, int TF,
+                                                         const unsigned long long* gran,
+                                                         const unsigned char* tile_flag,
+                                                         long long batch, int M,
+                                                         const unsigned* tmo) {
+  if (*tmo == 0u) return;  // uniform: the common case, every tile normalised in-kernel
+  const long long plane = (long long)F_out * T;
+  for (long long task = blockIdx.x; task < batch * M; task += gridDim.x) {
+    if (!tile_flag[task]) continue;  // uniform per workgroup
+    const long long shot = task / M;
+    const int mem = (int)(task - shot * M);
+    unsigned kmax = 0u, kinv = 0u;
+    for (int j = 0; j < M; ++j) {
+      const unsigned long long v = gran[shot * M + j];
+      kmax = max(kmax, (unsigned)v);
+      kinv = max(kinv, (unsigned)(v >> 32));
+    }
+    const float mx = key2f(kmax), mn = key2f(~kinv);
+    const float inv = 1.0f / (mx - mn);
+    const int t0 = mem * TF, tw = min(TF, T - t0);
+    float* o = out + shot * plane + t0;
+    for (int e = threadIdx.x; e < F_out * tw; e += blockDim.x) {
+      const int k = e / tw, t = e - (e / tw) * tw;
+      o[(long long)k * T + t] = (o[(long long)k * T + t] - mn) * inv;
     }
   }
 }
@@ -780,15 +831,21 @@ hipError_t launch_team(const StftArgs& a, long long batch, void* workspace, hipS
   if (cap[dev] < M) return hipSuccess;
   long long Q = cap[dev] / M;
   if (Q > batch) Q = batch;
-  // workspace: [timeout word, 16 B][granules: batch x M x 8 B], zeroed every call
+  // workspace: [timeout word, 16 B][granules: batch x M x 8 B][tile flags: batch x M B],
+  // zeroed every call (specenh_stft_workspace_bytes sizes it for M = TEAM_MAX)
   unsigned* tmo = reinterpret_cast<unsigned*>(workspace);
   unsigned long long* gran =
       reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + 16);
-  const size_t zero = 16 + (((size_t)batch * M * 8 + 15) / 16) * 16;
+  unsigned char* tflag = reinterpret_cast<unsigned char*>(gran + (size_t)batch * M);
+  const size_t zero = 16 + (size_t)batch * M * 9;
   e = hipMemsetAsync(workspace, 0, zero, stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(stft_team_kernel<N>, dim3((unsigned)(Q * M)), dim3(Lo::THREADS), Lo::BYTES,
-                     stream, a, gran, batch, M, (int)Q, tmo);
+                     stream, a, gran, batch, M, (int)Q, tmo, tflag);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(team_fixup_kernel, dim3(1024), dim3(256), 0, stream, a.out, a.F_out, a.T,
+                     Lo::TF, gran, tflag, batch, M, tmo);
   e = hipGetLastError();
   *launched = e == hipSuccess;
   return e;
@@ -917,7 +974,7 @@ int specenh_stft_plan_destroy(specenh_stft_plan* plan) {
 size_t specenh_stft_workspace_bytes(const specenh_stft_plan* plan, long long batch) {
   (void)plan;
   if (batch <= 0) return 16;
-  return 16 + (size_t)batch * TEAM_MAX * 8;  // team schedule: timeout word + granules
+  return 16 + (size_t)batch * TEAM_MAX * 9;  // team schedule: timeout word, granules, flags
 }
 
 int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long batch,

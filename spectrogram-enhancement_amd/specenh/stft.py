@@ -90,13 +90,14 @@ class StftPlan:
                 w.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), key.fs, key.scaling,
                 key.detrend, key.eps), "stft_plan_create")
         self.handle = h
-        self._workspace = None
 
     def workspace(self, batch: int, device) -> torch.Tensor:
+        """A fresh workspace per call from torch's caching allocator on the current stream
+        (the team schedule's timeout word, granules and tile flags live here): two streams
+        sharing one plan never share a workspace, and a buffer returns to the pool only
+        when the stream that used it is done with it."""
         nbytes = int(_lib.lib().specenh_stft_workspace_bytes(self.handle, batch))
-        if self._workspace is None or self._workspace.numel() < nbytes:
-            self._workspace = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
-        return self._workspace
+        return torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
 
     def __del__(self):
         try:
@@ -145,7 +146,7 @@ def get_plan(device: torch.device, nperseg: int, noverlap: int, window="hann", f
     return p
 
 
-def _launch(plan: StftPlan, x: torch.Tensor, out: torch.Tensor, flags: int):
+def _launch(plan: StftPlan, x: torch.Tensor, out: torch.Tensor, flags: int, workspace=None):
     L = _lib.lib()
     if x.dtype == torch.float16 and plan.key.nperseg > 1024:
         x = x.float()  # the fp16-sample kernel covers nperseg <= 1024
@@ -156,7 +157,7 @@ def _launch(plan: StftPlan, x: torch.Tensor, out: torch.Tensor, flags: int):
                                           ctypes.c_void_p(_lib.current_stream_handle(x.device))),
                    "stft_psd_f16")
         return
-    ws = plan.workspace(x.shape[0], x.device)
+    ws = plan.workspace(x.shape[0], x.device) if workspace is None else workspace
     _lib.check(L.specenh_stft_psd(plan.handle, ctypes.c_void_p(x.data_ptr()), x.shape[0],
                                   x.shape[1], x.stride(0), ctypes.c_void_p(out.data_ptr()), flags,
                                   ctypes.c_void_p(ws.data_ptr()),

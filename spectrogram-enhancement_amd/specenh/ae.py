@@ -1,8 +1,8 @@
 """Device engine of the convolutional autoencoder (VAE/manual_scan_3layers.py:186-212).
 
 The Keras facade (specenh.keras) builds a chain of layers and hands it to
-:class:`AutoencoderEngine`, which owns every device buffer and sequences the C-ABI
-kernels of csrc/conv_ae.hip:
+:class:`AutoencoderEngine`, which owns every device buffer and sequences the kernels of
+csrc/conv_ae.hip through the ``torch.ops.specenh`` operators (specenh/ops.py):
 
 * forward   Conv2D / Conv2DTranspose = implicit-GEMM conv (+bias, relu/sigmoid fused),
             MaxPooling2D = maxpool2 with argmax;
@@ -23,7 +23,6 @@ layout directly.
 """
 from __future__ import annotations
 
-import ctypes
 import math
 from dataclasses import dataclass
 
@@ -31,6 +30,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .ops import ops
 
 F32, BF16, F16 = 0, 1, 2
 _DTYPES = {"float32": F32, "bfloat16": BF16, "bf16": BF16, "mixed_bfloat16": BF16,
@@ -38,10 +38,6 @@ _DTYPES = {"float32": F32, "bfloat16": BF16, "bf16": BF16, "mixed_bfloat16": BF1
 _TORCH = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16}
 ACT = {None: 0, "linear": 0, "relu": 1, "sigmoid": 2}
 _ALIGN = 64  # elements; keeps every layer's GEMM weights 16-byte aligned for bf16 x8 loads
-
-
-def _vp(t) -> ctypes.c_void_p:
-    return ctypes.c_void_p(0 if t is None else t.data_ptr())
 
 
 @dataclass
@@ -154,6 +150,15 @@ class AutoencoderEngine:
         self.t = 0  # Adam iterations
         self._bufs = {}
         self._loss = torch.zeros(1, dtype=torch.float64, device=dev)
+        # per-layer views into the flat buffers (the operators take tensors, not offsets)
+        lp = self.w_lp if self.dt != F32 else self.w
+        self._wv, self._bv, self._gwv, self._gbv = {}, {}, {}, {}
+        for i, op in enumerate(self.ops):
+            if isinstance(op, ConvOp):
+                self._wv[i] = lp[op.off_w:op.off_w + op.n_w]
+                self._bv[i] = self.w[op.off_b:op.off_b + op.cout]
+                self._gwv[i] = self.g[op.off_w:op.off_w + op.n_w]
+                self._gbv[i] = self.g[op.off_b:op.off_b + op.cout]
 
     # ------------------------------------------------------------------ shapes
     def _validate(self):
@@ -253,40 +258,21 @@ class AutoencoderEngine:
                 out.append(host[op.off_b:op.off_b + op.cout].copy())
         return out
 
-    def _stream(self):
-        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-
     def _refresh_lowp(self):
-        st = self._stream()
         if self.dt != F32:
-            _lib.check(self.L.specenh_cast(F32, _vp(self.w), self.dt, _vp(self.w_lp), self.n_flat,
-                                           st), "cast")
-        src = self.w_lp if self.dt != F32 else self.w
+            ops.cast_out(self.w, self.w_lp)
         for i, wd in self.w_d.items():
             op = self.ops[i]
-            _lib.check(self.L.specenh_weight_flip_transpose(
-                self.dt, ctypes.c_void_p(src.data_ptr() + op.off_w * src.element_size()), op.k,
-                op.cin, op.cout, _vp(wd), st), "flip_transpose")
-
-    def _wptr(self, op):
-        src = self.w_lp if self.dt != F32 else self.w
-        return ctypes.c_void_p(src.data_ptr() + op.off_w * src.element_size())
-
-    def _bptr(self, op, buf=None):
-        buf = self.w if buf is None else buf
-        return ctypes.c_void_p(buf.data_ptr() + op.off_b * 4)
+            ops.weight_flip_transpose_out(self._wv[i], op.k, op.cin, op.cout, wd)
 
     # ------------------------------------------------------------------ passes
-    def _conv(self, op, x, out, *, weights, geom, act, mask=None, logits=None, bias=True,
-              out_shape=None, cin=None, cout=None, pool=False, argmax=None):
-        N, IH, IW, C = x.shape
+    def _conv(self, i, x, out, *, weights, geom, act, mask=None, logits=None, bias=True,
+              out_shape=None, cout=None, pool=False, argmax=None):
+        op = self.ops[i]
         OH, OW = out_shape
         s, pt, pl, dil = geom
-        _lib.check(self.L.specenh_conv2d(
-            self.dt, _vp(x), N, IH, IW, C, weights, op.k, op.k, cout, self._bptr(op) if bias
-            else ctypes.c_void_p(0), s, pt, pl, dil, OH, OW, ACT[act], _vp(mask), _vp(logits),
-            _vp(out), int(out.dtype == torch.float32), int(pool), _vp(argmax), self._stream()),
-            "conv2d")
+        ops.conv2d_out(x, weights, self._bv[i] if bias else None, op.k, op.k, cout, s, pt, pl,
+                       dil, OH, OW, ACT[act], mask, logits, out, pool, argmax)
 
     def forward(self, x, train=False, timing=None):
         """x: device [N, H, W, C] in the compute dtype. Returns the output buffer
@@ -300,7 +286,6 @@ class AutoencoderEngine:
         b["h"][0] = x
         if train:
             self._last_train_N = N
-        st = self._stream()
         n_ops = len(self.ops)
         skip = False
         for i, op in enumerate(self.ops):
@@ -314,7 +299,7 @@ class AutoencoderEngine:
                           torch.cuda.Event(enable_timing=True))
                     ev[0].record(torch.cuda.current_stream(self.device))
                 _, H, W, _ = hin.shape
-                self._conv(op, hin, b["h"][i + 2], weights=self._wptr(op), geom=op.fwd_geom(),
+                self._conv(i, hin, b["h"][i + 2], weights=self._wv[i], geom=op.fwd_geom(),
                            act=op.act, out_shape=(H, W), cout=op.cout, pool=True,
                            argmax=b["am"][i + 1] if train else None)
                 if timing is not None:
@@ -331,14 +316,13 @@ class AutoencoderEngine:
                         am = torch.empty((N, H // 2, W // 2, C), dtype=torch.uint8,
                                          device=self.device)
                         b["am_inf"][hin.shape] = am
-                _lib.check(self.L.specenh_maxpool2_fwd(self.dt, _vp(hin), N, H, W, C, _vp(hout),
-                                                       _vp(am), st), "maxpool2_fwd")
+                ops.maxpool2_out(hin, hout, am)
                 continue
             last = i == n_ops - 1
             if timing is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record(torch.cuda.current_stream(self.device))
-            self._conv(op, hin, hout, weights=self._wptr(op), geom=op.fwd_geom(), act=op.act,
+            self._conv(i, hin, hout, weights=self._wv[i], geom=op.fwd_geom(), act=op.act,
                        logits=b["z"] if (train and last) else None,
                        out_shape=hout.shape[1:3], cout=op.cout)
             if timing is not None:
@@ -358,25 +342,19 @@ class AutoencoderEngine:
         mean is sum / y.numel()). Fills the last layer's gradient when want_grad."""
         if tuple(y.shape) != (self._last_train_N,) + self.output_shape:
             raise ValueError(f"targets must have shape (N, *{self.output_shape})")
-        inv = {v: k for k, v in _TORCH.items()}
-        if y.dtype not in inv or not y.is_contiguous():
+        if y.dtype not in _TORCH.values() or not y.is_contiguous():
             raise TypeError("targets must be contiguous float32, bfloat16 or float16")
         b = self._buffers(self._last_train_N, True)
-        z = b["z"]
         if accumulate is None:
             accumulate = self._loss
             accumulate.zero_()
-        ydt = inv[y.dtype]
-        _lib.check(self.L.specenh_bce_logits(
-            _vp(z), _vp(y), ydt, z.numel(), _vp(b["d"][-1]) if want_grad else ctypes.c_void_p(0),
-            self.dt, _vp(accumulate), self._stream()), "bce_logits")
+        ops.bce_logits_out(b["z"], y, b["d"][-1] if want_grad else None, accumulate)
         return accumulate
 
     def backward(self):
         """Gradients of the last loss_and_grad() into self.g (overwritten)."""
         N = self._last_train_N
         b = self._buffers(N, True)
-        st = self._stream()
         self.g.zero_()
         n_ops = len(self.ops)
         for i in range(n_ops - 1, -1, -1):
@@ -391,38 +369,29 @@ class AutoencoderEngine:
                     continue  # nothing upstream needs the gradient
                 _, H, W, C = d_out.shape
                 # ReLU mask of the pool's input at its argmax == (pooled output > 0)
-                _lib.check(self.L.specenh_maxpool2_bwd(
-                    self.dt, _vp(d_out), _vp(b["am"][i]), _vp(b["h"][i + 1] if prev_relu else None),
-                    N, 2 * H, 2 * W, C, _vp(b["d"][i]), st), "maxpool2_bwd")
+                ops.maxpool2_bwd_out(d_out, b["am"][i], b["h"][i + 1] if prev_relu else None,
+                                     b["d"][i])
                 continue
             if op.act == "sigmoid" and i != n_ops - 1:
                 raise NotImplementedError("sigmoid activation before the last layer")
             _, IH, IW, C = hin.shape
             OH, OW = d_out.shape[1:3]
             s, pt, pl, dil = op.fwd_geom()
-            _lib.check(self.L.specenh_conv2d_wgrad(
-                self.dt, _vp(hin), N, IH, IW, C, _vp(d_out), op.k, op.k, op.cout, s, pt, pl, dil,
-                OH, OW, ctypes.c_void_p(self.g.data_ptr() + op.off_w * 4),
-                self._bptr(op, self.g), _vp(b["ws"]), st), "conv2d_wgrad")
+            ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[i],
+                                 self._gbv[i], b["ws"])
             if i == 0:
                 continue
-            self._conv(op, d_out, b["d"][i], weights=_vp(self.w_d[i]), geom=op.dgrad_geom(),
+            self._conv(i, d_out, b["d"][i], weights=self.w_d[i], geom=op.dgrad_geom(),
                        act=None, mask=relu_mask, bias=False, out_shape=(IH, IW), cout=op.cin)
 
     def adam(self, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7, grad_scale=1.0):
         self.t += 1
         lr_t = lr * math.sqrt(1.0 - beta_2 ** self.t) / (1.0 - beta_1 ** self.t)
-        _lib.check(self.L.specenh_adam_step(
-            _vp(self.w), _vp(self.g), _vp(self.m), _vp(self.v), self.n_flat, lr_t, beta_1, beta_2,
-            epsilon, grad_scale, _vp(self.w_lp), self.dt, self._stream()), "adam_step")
-        if self.w_d:
-            src = self.w_lp if self.dt != F32 else self.w
-            st = self._stream()
-            for i, wd in self.w_d.items():
-                op = self.ops[i]
-                _lib.check(self.L.specenh_weight_flip_transpose(
-                    self.dt, ctypes.c_void_p(src.data_ptr() + op.off_w * src.element_size()),
-                    op.k, op.cin, op.cout, _vp(wd), st), "flip_transpose")
+        ops.adam_step_(self.w, self.g, self.m, self.v, lr_t, beta_1, beta_2, epsilon, grad_scale,
+                       self.w_lp)
+        for i, wd in self.w_d.items():
+            op = self.ops[i]
+            ops.weight_flip_transpose_out(self._wv[i], op.k, op.cin, op.cout, wd)
 
     def train_step(self, x, y, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7,
                    process_group=None):
@@ -455,7 +424,4 @@ class AutoencoderEngine:
             return t
         if t.dtype != torch.float32:
             raise TypeError(f"unsupported input dtype {t.dtype}")
-        out = torch.empty(t.shape, dtype=self.tdt, device=self.device)
-        _lib.check(self.L.specenh_cast(F32, _vp(t), self.dt, _vp(out), t.numel(),
-                                       self._stream()), "cast")
-        return out
+        return ops.cast(t, self.tdt)

@@ -7,7 +7,7 @@ signal2[i], t)`` from ``co2_deps`` — a module absent from the reference — an
 (``scipy/signal/_spectral_py.py`` ``_spectral_helper(x, y, mode='psd')``): per frame
 ``Pxy = conj(X) * Y * scale`` with one-sided doubling, the un-averaged form of
 ``scipy.signal.csd``. That arithmetic is what runs here (csrc/cross_spectrum.hip through
-``specenh_csd``), pinned against scipy; ae_co2's own normalisation is unknown
+``torch.ops.specenh.csd`` -> ``specenh_csd``), pinned against scipy; ae_co2's own normalisation is unknown
 ("parity unpinned"), so :func:`crosspower_amplitude` documents the choice it makes.
 """
 from __future__ import annotations
@@ -52,14 +52,16 @@ _plans: dict = {}
 _lock = threading.Lock()
 
 
-def _plan(device, nperseg, noverlap, window, fs, scaling, detrend) -> CsdPlan:
+def get_plan_key(device, nperseg, noverlap, window: str, fs, scaling: int, detrend: int) -> CsdPlan:
+    """Plan lookup from the csd operator's arguments (window by name / registered key)."""
+    from .ops import window_coefs
     nperseg, noverlap = int(nperseg), int(noverlap)
     if noverlap >= nperseg:
         raise ValueError("noverlap must be less than nperseg.")
-    w = get_window(window, nperseg)
+    w = window_coefs(window, nperseg)
     dev = device.index if device.index is not None else torch.cuda.current_device()
     key = (dev, nperseg, noverlap, hashlib.sha1(w.tobytes()).hexdigest(), float(fs),
-           _norm_scaling(scaling), _norm_detrend(detrend))
+           int(scaling), int(detrend))
     with _lock:
         p = _plans.get(key)
         if p is None:
@@ -94,24 +96,18 @@ def cross_spectrogram_batch(x: torch.Tensor, y: torch.Tensor, fs: float = 1.0, w
     pairs ``x, y[B, L]``, with scipy's ``_spectral_helper(x, y, mode='psd')`` semantics
     (scipy.signal.csd's defaults: hann, 50 % overlap, constant detrend, density).
     Returns ``(f, t, Pxy)``; ``f``/``t`` are float64 numpy arrays bit-equal to scipy's."""
+    from .ops import ops, window_key
     x, y, squeeze = _as_pairs(x, y)
     if noverlap is None:
         noverlap = int(nperseg) // 2
-    plan = _plan(x.device, nperseg, noverlap, window, fs, scaling, detrend)
-    B, L = x.shape
-    T = frame_count(L, nperseg, noverlap)
-    F = int(nperseg) // 2 + 1
-    if amplitude:
-        out = torch.empty((B, F, T), dtype=torch.float32, device=x.device)
-    else:
-        out = torch.empty((B, F, T), dtype=torch.complex64, device=x.device)
-    for b0 in range(0, B, 65535):
-        b1 = min(B, b0 + 65535)
-        _lib.check(_lib.lib().specenh_csd(
-            plan.handle, ctypes.c_void_p(x[b0:b1].data_ptr()), ctypes.c_void_p(y[b0:b1].data_ptr()),
-            b1 - b0, L, x.stride(0), y.stride(0), ctypes.c_void_p(out[b0:b1].data_ptr()),
-            CSD_AMPLITUDE if amplitude else CSD_COMPLEX,
-            ctypes.c_void_p(_lib.current_stream_handle(x.device))), "csd")
+    nperseg, noverlap = int(nperseg), int(noverlap)
+    if noverlap >= nperseg:
+        raise ValueError("noverlap must be less than nperseg.")
+    L = x.shape[1]
+    frame_count(L, nperseg, noverlap)  # ValueError for a signal shorter than nperseg
+    out = ops.csd(x, y, nperseg, noverlap, window_key(window, nperseg), float(fs),
+                  _norm_scaling(scaling), _norm_detrend(detrend),
+                  CSD_AMPLITUDE if amplitude else CSD_COMPLEX)
     f = frequencies(int(nperseg), fs)
     t = times(L, int(nperseg), int(noverlap), fs)
     return f, t, (out[0] if squeeze else out)

@@ -1,5 +1,5 @@
 """GPU label filters: norm / rescale / meansub / quantfilt / gaussblr / morph of
-spec_denoising/pipeline_data.py (:38-72) through the C-ABI (csrc/filters.hip), and the
+spec_denoising/pipeline_data.py (:38-72) through ``torch.ops.specenh`` (csrc/filters.hip), and the
 whole label chain of its main loop (:101-110) as ``label_pipeline``. The reference-named functions live in
 ``specenh.pipeline_data``; this module holds the device paths.
 
@@ -11,8 +11,6 @@ N-D numpy inputs keep the reference's whole-array semantics: norm / rescale over
 elements, quantfilt per column of axis 0, meansub over axis 1 with one global rescale.
 """
 from __future__ import annotations
-
-import ctypes
 
 import numpy as np
 import torch
@@ -29,41 +27,21 @@ def _device():
 
 
 def _run(kind, t: torch.Tensor, arg):
-    """t: contiguous device tensor [B, rows, cols] float32/float64."""
+    """t: device tensor [B, rows, cols] float32/float64 -> torch.ops.specenh.<filter>."""
+    from .ops import ops
     if t.device.type != "cuda":
         raise RuntimeError("specenh.filters runs on the GPU only (no CPU fallback)")
     if t.dtype not in _DT:
         t = t.double()
     t = t.contiguous()
-    B, rows, cols = t.shape
-    out = torch.empty_like(t)
-    L = _lib.lib()
-    st = ctypes.c_void_p(_lib.current_stream_handle(t.device))
-    if kind in ("gaussblr", "morph"):
-        ws = torch.empty(max(16, int(L.specenh_u8filter_workspace_bytes(B, rows, cols))),
-                         dtype=torch.uint8, device=t.device)
-        if kind == "gaussblr":
-            kw, kh = arg
-            rc = L.specenh_gaussblr(_DT[t.dtype], ctypes.c_void_p(t.data_ptr()), B, rows, cols,
-                                    rows * cols, int(kw), int(kh), 0.0,
-                                    ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
-                                    st)
-        else:
-            rc = L.specenh_morph(_DT[t.dtype], ctypes.c_void_p(t.data_ptr()), B, rows, cols,
-                                 rows * cols, ctypes.c_void_p(out.data_ptr()),
-                                 ctypes.c_void_p(ws.data_ptr()), st)
-        _lib.check(rc, kind)
-    elif kind == "quantfilt":
-        _lib.check(L.specenh_quantfilt(_DT[t.dtype], ctypes.c_void_p(t.data_ptr()), B, rows, cols,
-                                       rows * cols, float(arg), ctypes.c_void_p(out.data_ptr()),
-                                       st), "quantfilt")
-    else:
-        ws = torch.empty(max(16, int(L.specenh_filter_workspace_bytes(B, rows))),
-                         dtype=torch.uint8, device=t.device)
-        _lib.check(L.specenh_filter(arg, _DT[t.dtype], ctypes.c_void_p(t.data_ptr()), B, rows,
-                                    cols, rows * cols, ctypes.c_void_p(out.data_ptr()),
-                                    ctypes.c_void_p(ws.data_ptr()), st), kind)
-    return out
+    if kind == "gaussblr":
+        kw, kh = arg
+        return ops.gaussblr(t, int(kw), int(kh), 0.0)
+    if kind == "morph":
+        return ops.morph(t)
+    if kind == "quantfilt":
+        return ops.quantfilt(t, float(arg))
+    return ops.label_filter(t, int(arg))
 
 
 def _apply(kind, src, arg, to2d, back):

@@ -1,0 +1,529 @@
+"""``torch.ops.specenh.*``: every entry point of the C-ABI (include/specenh.h) as a PyTorch
+operator.
+
+The Python API that keeps the reference's names (``pipeline_data``, ``svd``, ``keras``,
+``strips``, ``cross``, ``filters``) reaches the HIP kernels only through these operators:
+
+    reference call site -> specenh.<module> -> torch.ops.specenh.<op> -> C-ABI -> HIP
+
+Each operator is defined with an explicit schema on a ``torch.library.Library`` (its
+dispatch costs ~2.5 us a call, a sixth of ``torch.library.custom_op``'s), implemented for
+the CUDA (= HIP on ROCm) dispatch key only — a CPU tensor raises NotImplementedError, there
+is no fallback — and has a fake (meta) kernel, so shapes propagate through FakeTensor /
+``torch.compile`` tracing. Operators ending in ``_out`` write caller-owned buffers (the
+autoencoder engine reuses its activations across calls); the others allocate.
+``tests/test_ops_gpu.py`` runs ``torch.library.opcheck`` on each.
+
+Every launch goes on the current HIP stream of the tensors' device.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import threading
+
+import numpy as np
+import torch
+
+from . import _lib
+
+F32, BF16, F16, F64 = 0, 1, 2, 3
+_CODE = {torch.float32: F32, torch.bfloat16: BF16, torch.float16: F16, torch.float64: F64}
+
+
+def _vp(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _st(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _code(t: torch.Tensor, allowed=(F32, BF16, F16)) -> int:
+    c = _CODE.get(t.dtype)
+    if c is None or c not in allowed:
+        raise TypeError(f"unsupported dtype {t.dtype}")
+    return c
+
+
+def _need(t: torch.Tensor, name: str):
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+_LIB = torch.library.Library("specenh", "DEF")
+
+
+def _op(schema: str, impl, fake):
+    name = schema.split("(", 1)[0]
+    _LIB.define(schema)
+    _LIB.impl(name, impl, "CUDA")
+    torch.library.register_fake(f"specenh::{name}", fake, lib=_LIB)
+
+
+# ---------------------------------------------------------------- windows / plans
+_windows: dict = {}
+_wlock = threading.Lock()
+
+
+def window_key(window, nperseg: int) -> str:
+    """A string naming a window for the STFT / CSD operators: scipy window names pass
+    through; tuples and coefficient arrays are registered under their sha1 digest."""
+    if isinstance(window, str):
+        return window
+    from .stft import get_window
+    w = np.ascontiguousarray(get_window(window, int(nperseg)), dtype=np.float64)
+    key = "sha1:" + hashlib.sha1(w.tobytes()).hexdigest()
+    with _wlock:
+        _windows.setdefault(key, w)
+    return key
+
+
+def window_coefs(key: str, nperseg: int) -> np.ndarray:
+    if key.startswith("sha1:"):
+        w = _windows.get(key)
+        if w is None or w.shape[0] != nperseg:
+            raise ValueError(f"unknown window {key!r} (register it with ops.window_key)")
+        return w
+    from .stft import get_window
+    return get_window(key, int(nperseg))
+
+
+# ---------------------------------------------------------------- STFT-PSD
+def _stft_shape(x, nperseg, noverlap, flags):
+    T = (x.shape[-1] - nperseg) // (nperseg - noverlap) + 1
+    F = nperseg // 2 + (0 if flags & _lib.STFT_DROP_NYQUIST else 1)
+    return x.shape[0], F, T
+
+
+def _stft_out(x, nperseg, noverlap, window, fs, scaling, detrend, eps, flags, out):
+    from . import stft
+    if x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("x must be [batch, length] with unit stride along length")
+    if x.dtype not in (torch.float32, torch.float16):
+        raise TypeError("x must be float32 or float16")
+    if tuple(out.shape) != _stft_shape(x, nperseg, noverlap, flags) or \
+            out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("out must be contiguous float32 [batch, F, T]")
+    plan = stft.get_plan_key(x.device, nperseg, noverlap, window, fs, scaling, detrend, eps)
+    L = _lib.lib()
+    if x.dtype == torch.float16 and nperseg > 1024:
+        x = x.float()  # the fp16-sample kernel covers nperseg <= 1024
+    if x.dtype == torch.float16:  # fp16 samples widened on load: no conversion pass
+        _lib.check(L.specenh_stft_psd_f16(plan.handle, _vp(x), x.shape[0], x.shape[1],
+                                          x.stride(0), _vp(out), flags, _st(x)), "stft_psd_f16")
+        return
+    ws = plan.workspace(x.shape[0], x.device)
+    _lib.check(L.specenh_stft_psd(plan.handle, _vp(x), x.shape[0], x.shape[1], x.stride(0),
+                                  _vp(out), flags, _vp(ws), _st(x)), "stft_psd")
+
+
+def _stft(x, nperseg, noverlap, window, fs, scaling, detrend, eps, flags):
+    out = torch.empty(_stft_shape(x, nperseg, noverlap, flags), dtype=torch.float32,
+                      device=x.device)
+    _stft_out(x, nperseg, noverlap, window, fs, scaling, detrend, eps, flags, out)
+    return out
+
+
+_STFT_ARGS = "int nperseg, int noverlap, str window, float fs, int scaling, int detrend, " \
+             "float eps, int flags"
+_op(f"stft_psd(Tensor x, {_STFT_ARGS}) -> Tensor", _stft,
+    lambda x, nperseg, noverlap, window, fs, scaling, detrend, eps, flags:
+    x.new_empty(_stft_shape(x, nperseg, noverlap, flags), dtype=torch.float32))
+_op(f"stft_psd_out(Tensor x, {_STFT_ARGS}, Tensor(a!) out) -> ()", _stft_out,
+    lambda *a: None)
+
+
+# ---------------------------------------------------------------- cross spectrum
+def _csd(x, y, nperseg, noverlap, window, fs, scaling, detrend, mode):
+    from . import cross
+    if x.shape != y.shape or x.dim() != 2 or x.dtype != torch.float32 or y.dtype != torch.float32:
+        raise ValueError("x and y must be float32 [batch, length] of the same shape")
+    if x.stride(1) != 1 or y.stride(1) != 1:
+        raise ValueError("x and y need unit stride along length")
+    plan = cross.get_plan_key(x.device, nperseg, noverlap, window, fs, scaling, detrend)
+    B, L = x.shape
+    T = (L - nperseg) // (nperseg - noverlap) + 1
+    F = nperseg // 2 + 1
+    out = torch.empty((B, F, T), dtype=torch.float32 if mode == 1 else torch.complex64,
+                      device=x.device)
+    for b0 in range(0, B, 65535):
+        b1 = min(B, b0 + 65535)
+        _lib.check(_lib.lib().specenh_csd(
+            plan.handle, _vp(x[b0:b1]), _vp(y[b0:b1]), b1 - b0, L, x.stride(0), y.stride(0),
+            _vp(out[b0:b1]), int(mode), _st(x)), "csd")
+    return out
+
+
+def _csd_fake(x, y, nperseg, noverlap, window, fs, scaling, detrend, mode):
+    T = (x.shape[1] - nperseg) // (nperseg - noverlap) + 1
+    return x.new_empty((x.shape[0], nperseg // 2 + 1, T),
+                       dtype=torch.float32 if mode == 1 else torch.complex64)
+
+
+_op("csd(Tensor x, Tensor y, int nperseg, int noverlap, str window, float fs, int scaling, "
+    "int detrend, int mode) -> Tensor", _csd, _csd_fake)
+
+
+# ---------------------------------------------------------------- SVD denoiser
+def _svd_check(A):
+    if A.dim() != 3 or A.dtype != torch.float32 or A.stride(2) != 1 or A.stride(1) != A.shape[2]:
+        raise ValueError("A must be float32 [batch, m, n] with row-major matrices")
+
+
+def _svd_out(A, start, stop, out):
+    _svd_check(A)
+    B, m, n = A.shape
+    if out.shape != A.shape or not out.is_contiguous() or out.device != A.device:
+        raise ValueError("out must be a contiguous [B, m, n] tensor on A's device")
+    L = _lib.lib()
+    ws = torch.empty(max(16, int(L.specenh_svd_denoise_workspace_bytes(B, m, n, start, stop))),
+                     dtype=torch.uint8, device=A.device)
+    _lib.check(L.specenh_svd_denoise_ex(_vp(A), B, m, n, A.stride(0), start, stop, _vp(out),
+                                        _code(out), _vp(ws), _st(A)), "svd_denoise")
+
+
+def _svd(A, start, stop, out_dtype):
+    out = torch.empty(A.shape, dtype=out_dtype, device=A.device)
+    _svd_out(A, start, stop, out)
+    return out
+
+
+def _svd_opt(A, mode):
+    _svd_check(A)
+    B, m, n = A.shape
+    L = _lib.lib()
+    out = torch.empty(A.shape, dtype=torch.float32, device=A.device)
+    ws = torch.empty(max(16, int(L.specenh_svd_optimal_workspace_bytes(B, m, n))),
+                     dtype=torch.uint8, device=A.device)
+    ns = torch.empty(B, dtype=torch.int32, device=A.device)
+    med = torch.empty(B, dtype=torch.float64, device=A.device)
+    _lib.check(L.specenh_svd_denoise_optimal(_vp(A), B, m, n, A.stride(0), int(mode), _vp(out),
+                                             _vp(ns), _vp(med), _vp(ws), _st(A)),
+               "svd_denoise_optimal")
+    return out, ns, med
+
+
+_op("svd_denoise(Tensor A, int start, int stop, ScalarType out_dtype) -> Tensor", _svd,
+    lambda A, start, stop, out_dtype: A.new_empty(A.shape, dtype=out_dtype))
+_op("svd_denoise_out(Tensor A, int start, int stop, Tensor(a!) out) -> ()", _svd_out,
+    lambda *a: None)
+_op("svd_denoise_optimal(Tensor A, int mode) -> (Tensor, Tensor, Tensor)", _svd_opt,
+    lambda A, mode: (A.new_empty(A.shape), A.new_empty((A.shape[0],), dtype=torch.int32),
+                     A.new_empty((A.shape[0],), dtype=torch.float64)))
+
+
+# ---------------------------------------------------------------- convolutions
+def _conv_out(x, w, bias, kh, kw, cout, stride, pad_t, pad_l, in_dil, oh, ow, act, mask,
+              logits, out, pool, argmax):
+    if x.dim() != 4:
+        raise ValueError("x must be NHWC [N, H, W, C]")
+    _need(x, "x")
+    _need(out, "out")
+    N, IH, IW, C = x.shape
+    dt = _code(x)
+    if w.dtype != x.dtype or w.numel() != cout * kh * kw * C:
+        raise ValueError("w must be the [CO][KH][KW][C] GEMM weights in x's dtype")
+    _need(w, "w")
+    oshape = (N, oh // 2, ow // 2, cout) if pool else (N, oh, ow, cout)
+    if tuple(out.shape) != oshape or out.dtype not in (x.dtype, torch.float32):
+        raise ValueError(f"out must be {oshape} in x's dtype or float32")
+    if bias is not None and (bias.dtype != torch.float32 or bias.numel() != cout):
+        raise ValueError("bias must be float32 [CO]")
+    if mask is not None and (mask.dtype != x.dtype or mask.numel() != N * oh * ow * cout):
+        raise ValueError("mask must match the output (compute dtype)")
+    if logits is not None and (logits.dtype != torch.float32 or
+                               logits.numel() != N * oh * ow * cout):
+        raise ValueError("logits must be float32 [N, OH, OW, CO]")
+    if argmax is not None and (argmax.dtype != torch.uint8 or tuple(argmax.shape) != oshape):
+        raise ValueError("argmax must be uint8 like the pooled output")
+    out_f32 = int(out.dtype == torch.float32)
+    _lib.check(_lib.lib().specenh_conv2d(
+        dt, _vp(x), N, IH, IW, C, _vp(w), kh, kw, cout, _vp(bias), stride, pad_t, pad_l, in_dil,
+        oh, ow, act, _vp(mask), _vp(logits), _vp(out), out_f32, int(pool), _vp(argmax), _st(x)),
+        "conv2d")
+
+
+def _conv(x, w, bias, kh, kw, cout, stride, pad_t, pad_l, in_dil, oh, ow, act):
+    out = torch.empty((x.shape[0], oh, ow, cout), dtype=x.dtype, device=x.device)
+    _conv_out(x, w, bias, kh, kw, cout, stride, pad_t, pad_l, in_dil, oh, ow, act, None, None,
+              out, False, None)
+    return out
+
+
+_CONV_ARGS = "int kh, int kw, int cout, int stride, int pad_t, int pad_l, int in_dil, int oh, " \
+             "int ow, int act"
+_op(f"conv2d(Tensor x, Tensor w, Tensor? bias, {_CONV_ARGS}) -> Tensor", _conv,
+    lambda x, w, bias, kh, kw, cout, stride, pad_t, pad_l, in_dil, oh, ow, act:
+    x.new_empty((x.shape[0], oh, ow, cout)))
+_op(f"conv2d_out(Tensor x, Tensor w, Tensor? bias, {_CONV_ARGS}, Tensor? mask, "
+    "Tensor(a!)? logits, Tensor(b!) out, bool pool, Tensor(c!)? argmax) -> ()", _conv_out,
+    lambda *a: None)
+
+
+def wgrad_workspace(x, dout, kh, kw):
+    N, _, _, C = x.shape
+    _, OH, OW, CO = dout.shape
+    n = int(_lib.lib().specenh_conv2d_wgrad_workspace_bytes(N, OH, OW, kh, kw, C, CO))
+    return torch.empty(max(16, n), dtype=torch.uint8, device=x.device)
+
+
+def _wgrad_out(x, dout, kh, kw, stride, pad_t, pad_l, in_dil, dw, dbias, workspace):
+    _need(x, "x")
+    _need(dout, "dout")
+    N, IH, IW, C = x.shape
+    _, OH, OW, CO = dout.shape
+    if dout.dtype != x.dtype or dout.shape[0] != N:
+        raise ValueError("dout must be [N, OH, OW, CO] in x's dtype")
+    if dw.dtype != torch.float32 or dw.numel() != CO * kh * kw * C or not dw.is_contiguous():
+        raise ValueError("dw must be contiguous float32 [CO][KH][KW][C]")
+    if dbias is not None and (dbias.dtype != torch.float32 or dbias.numel() != CO):
+        raise ValueError("dbias must be float32 [CO]")
+    need = int(_lib.lib().specenh_conv2d_wgrad_workspace_bytes(N, OH, OW, kh, kw, C, CO))
+    if workspace.numel() < need:
+        raise ValueError(f"workspace needs {need} bytes")
+    _lib.check(_lib.lib().specenh_conv2d_wgrad(
+        _code(x), _vp(x), N, IH, IW, C, _vp(dout), kh, kw, CO, stride, pad_t, pad_l, in_dil, OH,
+        OW, _vp(dw), _vp(dbias), _vp(workspace), _st(x)), "conv2d_wgrad")
+
+
+def _wgrad(x, dout, kh, kw, stride, pad_t, pad_l, in_dil):
+    C, CO = x.shape[3], dout.shape[3]
+    dw = torch.zeros((CO, kh, kw, C), dtype=torch.float32, device=x.device)
+    db = torch.zeros((CO,), dtype=torch.float32, device=x.device)
+    _wgrad_out(x, dout, kh, kw, stride, pad_t, pad_l, in_dil, dw, db,
+               wgrad_workspace(x, dout, kh, kw))
+    return dw, db
+
+
+_WG_ARGS = "int kh, int kw, int stride, int pad_t, int pad_l, int in_dil"
+_op(f"conv2d_wgrad(Tensor x, Tensor dout, {_WG_ARGS}) -> (Tensor, Tensor)", _wgrad,
+    lambda x, dout, kh, kw, stride, pad_t, pad_l, in_dil:
+    (x.new_empty((dout.shape[3], kh, kw, x.shape[3]), dtype=torch.float32),
+     x.new_empty((dout.shape[3],), dtype=torch.float32)))
+_op(f"conv2d_wgrad_out(Tensor x, Tensor dout, {_WG_ARGS}, Tensor(a!) dw, Tensor(b!)? dbias, "
+    "Tensor(c!) workspace) -> ()", _wgrad_out, lambda *a: None)
+
+
+# ---------------------------------------------------------------- pooling, loss, optimizer
+def _pool_out(x, out, argmax):
+    _need(x, "x")
+    N, H, W, C = x.shape
+    if tuple(out.shape) != (N, H // 2, W // 2, C) or out.dtype != x.dtype:
+        raise ValueError("out must be [N, H/2, W/2, C] in x's dtype")
+    if argmax.dtype != torch.uint8 or argmax.shape != out.shape:
+        raise ValueError("argmax must be uint8 like out")
+    _lib.check(_lib.lib().specenh_maxpool2_fwd(_code(x), _vp(x), N, H, W, C, _vp(out),
+                                               _vp(argmax), _st(x)), "maxpool2_fwd")
+
+
+def _pool(x):
+    N, H, W, C = x.shape
+    out = torch.empty((N, H // 2, W // 2, C), dtype=x.dtype, device=x.device)
+    am = torch.empty(out.shape, dtype=torch.uint8, device=x.device)
+    _pool_out(x, out, am)
+    return out, am
+
+
+def _pool_bwd_out(dy, argmax, pooled, dx):
+    _need(dy, "dy")
+    N, H2, W2, C = dy.shape
+    if tuple(dx.shape) != (N, 2 * H2, 2 * W2, C) or dx.dtype != dy.dtype:
+        raise ValueError("dx must be [N, 2H, 2W, C] in dy's dtype")
+    _lib.check(_lib.lib().specenh_maxpool2_bwd(_code(dy), _vp(dy), _vp(argmax), _vp(pooled), N,
+                                               2 * H2, 2 * W2, C, _vp(dx), _st(dy)),
+               "maxpool2_bwd")
+
+
+def _pool_bwd(dy, argmax, pooled):
+    N, H2, W2, C = dy.shape
+    dx = torch.empty((N, 2 * H2, 2 * W2, C), dtype=dy.dtype, device=dy.device)
+    _pool_bwd_out(dy, argmax, pooled, dx)
+    return dx
+
+
+_op("maxpool2(Tensor x) -> (Tensor, Tensor)", _pool,
+    lambda x: (x.new_empty((x.shape[0], x.shape[1] // 2, x.shape[2] // 2, x.shape[3])),
+               x.new_empty((x.shape[0], x.shape[1] // 2, x.shape[2] // 2, x.shape[3]),
+                           dtype=torch.uint8)))
+_op("maxpool2_out(Tensor x, Tensor(a!) out, Tensor(b!) argmax) -> ()", _pool_out,
+    lambda *a: None)
+_op("maxpool2_bwd(Tensor dy, Tensor argmax, Tensor? pooled) -> Tensor", _pool_bwd,
+    lambda dy, argmax, pooled: dy.new_empty((dy.shape[0], 2 * dy.shape[1], 2 * dy.shape[2],
+                                             dy.shape[3])))
+_op("maxpool2_bwd_out(Tensor dy, Tensor argmax, Tensor? pooled, Tensor(a!) dx) -> ()",
+    _pool_bwd_out, lambda *a: None)
+
+
+def _bce_out(z, target, grad, loss_sum):
+    if z.dtype != torch.float32 or target.numel() != z.numel():
+        raise ValueError("z must be float32 and target the same size")
+    _need(z, "z")
+    _need(target, "target")
+    if loss_sum.dtype != torch.float64 or loss_sum.numel() != 1:
+        raise ValueError("loss_sum must be a float64 [1] accumulator")
+    if grad is not None and grad.numel() != z.numel():
+        raise ValueError("grad must have z's size")
+    _lib.check(_lib.lib().specenh_bce_logits(
+        _vp(z), _vp(target), _code(target), z.numel(), _vp(grad),
+        _code(grad) if grad is not None else F32, _vp(loss_sum), _st(z)), "bce_logits")
+
+
+def _bce(z, target, grad_dtype):
+    loss = torch.zeros(1, dtype=torch.float64, device=z.device)
+    grad = torch.empty(z.shape, dtype=grad_dtype, device=z.device)
+    _bce_out(z, target, grad, loss)
+    return loss, grad
+
+
+_op("bce_logits(Tensor z, Tensor target, ScalarType grad_dtype) -> (Tensor, Tensor)", _bce,
+    lambda z, target, grad_dtype: (z.new_empty((1,), dtype=torch.float64),
+                                   z.new_empty(z.shape, dtype=grad_dtype)))
+_op("bce_logits_out(Tensor z, Tensor target, Tensor(a!)? grad, Tensor(b!) loss_sum) -> ()",
+    _bce_out, lambda *a: None)
+
+
+def _adam(w, g, m, v, lr_t, beta_1, beta_2, epsilon, grad_scale, w_lowp):
+    n = w.numel()
+    for t, nm in ((g, "g"), (m, "m"), (v, "v")):
+        if t.numel() != n or t.dtype != torch.float32:
+            raise ValueError(f"{nm} must be float32 like w")
+    if w_lowp is not None and w_lowp.numel() != n:
+        raise ValueError("w_lowp must have w's size")
+    _lib.check(_lib.lib().specenh_adam_step(
+        _vp(w), _vp(g), _vp(m), _vp(v), n, lr_t, beta_1, beta_2, epsilon, grad_scale,
+        _vp(w_lowp), _code(w_lowp) if w_lowp is not None else F32, _st(w)), "adam_step")
+
+
+_op("adam_step_(Tensor(a!) w, Tensor g, Tensor(b!) m, Tensor(c!) v, float lr_t, float beta_1, "
+    "float beta_2, float epsilon, float grad_scale, Tensor(d!)? w_lowp) -> ()", _adam,
+    lambda *a: None)
+
+
+def _flip_out(bt, k, ci, co, out):
+    if bt.numel() != co * k * k * ci or out.numel() != bt.numel() or out.dtype != bt.dtype:
+        raise ValueError("bt / out sizes")
+    _lib.check(_lib.lib().specenh_weight_flip_transpose(_code(bt), _vp(bt), k, ci, co, _vp(out),
+                                                        _st(bt)), "flip_transpose")
+
+
+def _flip(bt, k, ci, co):
+    out = torch.empty((ci, k, k, co), dtype=bt.dtype, device=bt.device)
+    _flip_out(bt, k, ci, co, out)
+    return out
+
+
+_op("weight_flip_transpose(Tensor bt, int k, int ci, int co) -> Tensor", _flip,
+    lambda bt, k, ci, co: bt.new_empty((ci, k, k, co)))
+_op("weight_flip_transpose_out(Tensor bt, int k, int ci, int co, Tensor(a!) out) -> ()",
+    _flip_out, lambda *a: None)
+
+
+def _cast_out(x, out):
+    if out.numel() != x.numel():
+        raise ValueError("out must have x's size")
+    _need(x, "x")
+    _need(out, "out")
+    _lib.check(_lib.lib().specenh_cast(_code(x), _vp(x), _code(out), _vp(out), x.numel(), _st(x)),
+               "cast")
+
+
+def _cast(x, dtype):
+    out = torch.empty(x.shape, dtype=dtype, device=x.device)
+    _cast_out(x, out)
+    return out
+
+
+_op("cast(Tensor x, ScalarType dtype) -> Tensor", _cast,
+    lambda x, dtype: x.new_empty(x.shape, dtype=dtype))
+_op("cast_out(Tensor x, Tensor(a!) out) -> ()", _cast_out, lambda *a: None)
+
+
+# ---------------------------------------------------------------- label filters
+def _batch3(S):
+    if S.dim() != 3:
+        raise ValueError("S must be [batch, rows, cols]")
+    _need(S, "S")
+    return S.shape
+
+
+def _filter(S, op):
+    B, rows, cols = _batch3(S)
+    L = _lib.lib()
+    out = torch.empty_like(S)
+    ws = torch.empty(max(16, int(L.specenh_filter_workspace_bytes(B, rows))), dtype=torch.uint8,
+                     device=S.device)
+    _lib.check(L.specenh_filter(int(op), _code(S, (F32, F64)), _vp(S), B, rows, cols, rows * cols,
+                                _vp(out), _vp(ws), _st(S)), "filter")
+    return out
+
+
+def _quantfilt(S, thr):
+    B, rows, cols = _batch3(S)
+    out = torch.empty_like(S)
+    _lib.check(_lib.lib().specenh_quantfilt(_code(S, (F32, F64)), _vp(S), B, rows, cols,
+                                            rows * cols, float(thr), _vp(out), _st(S)), "quantfilt")
+    return out
+
+
+def _u8ws(S):
+    B, rows, cols = S.shape
+    n = int(_lib.lib().specenh_u8filter_workspace_bytes(B, rows, cols))
+    return torch.empty(max(16, n), dtype=torch.uint8, device=S.device)
+
+
+def _gaussblr(S, kw, kh, sigma):
+    B, rows, cols = _batch3(S)
+    out = torch.empty_like(S)
+    _lib.check(_lib.lib().specenh_gaussblr(_code(S, (F32, F64)), _vp(S), B, rows, cols,
+                                           rows * cols, int(kw), int(kh), float(sigma), _vp(out),
+                                           _vp(_u8ws(S)), _st(S)), "gaussblr")
+    return out
+
+
+def _morph(S):
+    B, rows, cols = _batch3(S)
+    out = torch.empty_like(S)
+    _lib.check(_lib.lib().specenh_morph(_code(S, (F32, F64)), _vp(S), B, rows, cols, rows * cols,
+                                        _vp(out), _vp(_u8ws(S)), _st(S)), "morph")
+    return out
+
+
+_op("label_filter(Tensor S, int op) -> Tensor", _filter, lambda S, op: torch.empty_like(S))
+_op("quantfilt(Tensor S, float thr) -> Tensor", _quantfilt, lambda S, thr: torch.empty_like(S))
+_op("gaussblr(Tensor S, int kw, int kh, float sigma) -> Tensor", _gaussblr,
+    lambda S, kw, kh, sigma: torch.empty_like(S))
+_op("morph(Tensor S) -> Tensor", _morph, lambda S: torch.empty_like(S))
+
+
+# ---------------------------------------------------------------- strip glue
+def _pack(S, rows, width, n_strips, dtype):
+    if S.dim() != 3 or S.dtype != torch.float32 or S.stride(2) != 1 or S.stride(1) != S.shape[2]:
+        raise ValueError("S must be float32 [batch, F, T] with row-major spectrograms")
+    B, F, T = S.shape
+    out = torch.empty((B * n_strips, rows, width, 1), dtype=dtype, device=S.device)
+    _lib.check(_lib.lib().specenh_strips_pack(
+        _code(out), _vp(S), B, F, T, S.stride(0), rows, width, n_strips, _vp(out), _st(S)),
+        "strips_pack")
+    return out
+
+
+def _unpack(strips, rows, width, n_strips):
+    _need(strips, "strips")
+    if strips.shape[0] % n_strips or tuple(strips.shape[1:3]) != (rows, width):
+        raise ValueError(f"strips must be [k*{n_strips}, {rows}, {width}(, 1)]")
+    B = strips.shape[0] // n_strips
+    out = torch.empty((B, rows, n_strips * width), dtype=torch.float32, device=strips.device)
+    _lib.check(_lib.lib().specenh_strips_unpack(_code(strips), _vp(strips), B, rows, width,
+                                                n_strips, _vp(out), _st(strips)), "strips_unpack")
+    return out
+
+
+_op("strips_pack(Tensor S, int rows, int width, int n_strips, ScalarType dtype) -> Tensor", _pack,
+    lambda S, rows, width, n_strips, dtype:
+    S.new_empty((S.shape[0] * n_strips, rows, width, 1), dtype=dtype))
+_op("strips_unpack(Tensor strips, int rows, int width, int n_strips) -> Tensor", _unpack,
+    lambda strips, rows, width, n_strips:
+    strips.new_empty((strips.shape[0] // n_strips, rows, n_strips * width), dtype=torch.float32))
+
+ops = torch.ops.specenh

@@ -1,10 +1,10 @@
-"""Batched STFT-PSD on the GPU: plan cache + the ``specenh::stft_psd`` torch op.
+"""Batched STFT-PSD on the GPU: plan cache + the tensor API over ``torch.ops.specenh.stft_psd``.
 
 Tensor-in / tensor-out fast path behind ``pipeline_data.specgr`` (SURVEY.md §8(b)
-B1/B2). The arithmetic is the HIP kernel in csrc/stft_psd.hip reached through the
-C-ABI ``specenh_stft_psd`` (include/specenh.h); this module only validates
-arguments, builds/caches plans (window + twiddle tables resident on the device)
-and passes pointers + the current HIP stream.
+B1/B2). The arithmetic is the HIP kernel in csrc/stft_psd.hip, reached through the
+operator ``torch.ops.specenh.stft_psd[_out]`` (specenh/ops.py) and the C-ABI
+``specenh_stft_psd`` (include/specenh.h); this module validates arguments and
+builds/caches plans (window + twiddle tables resident on the device).
 
 Semantics follow scipy.signal.spectrogram as called by
 spec_denoising/pipeline_data.py:32 (mode='psd', one-sided, no boundary padding),
@@ -131,38 +131,53 @@ def _norm_scaling(scaling) -> int:
 
 def get_plan(device: torch.device, nperseg: int, noverlap: int, window="hann", fs: float = 1.0,
              scaling="density", detrend="linear", eps: float = 1e-11) -> StftPlan:
+    from .ops import window_key
+    return get_plan_key(device, nperseg, noverlap, window_key(window, nperseg), fs,
+                        _norm_scaling(scaling), _norm_detrend(detrend), eps)
+
+
+_fast: dict = {}
+
+
+def get_plan_key(device: torch.device, nperseg: int, noverlap: int, window: str, fs: float,
+                 scaling: int, detrend: int, eps: float) -> StftPlan:
+    """Plan lookup from the operator's arguments (window by name / registered key)."""
+    dev = device.index if device.index is not None else torch.cuda.current_device()
+    fk = (dev, nperseg, noverlap, window, fs, scaling, detrend, eps)
+    p = _fast.get(fk)
+    if p is not None:
+        return p
+    from .ops import window_coefs
     nperseg = int(nperseg)
     noverlap = int(noverlap)
     if noverlap >= nperseg:
         raise ValueError("noverlap must be less than nperseg.")
-    w = get_window(window, nperseg)
-    dev = device.index if device.index is not None else torch.cuda.current_device()
+    w = window_coefs(window, nperseg)
     key = PlanKey(dev, nperseg, noverlap, hashlib.sha1(w.tobytes()).hexdigest(), float(fs),
-                  _norm_scaling(scaling), _norm_detrend(detrend), float(eps))
+                  int(scaling), int(detrend), float(eps))
     with _plans_lock:
         p = _plans.get(key)
         if p is None:
             p = _plans[key] = StftPlan(key, w)
+        _fast[fk] = p
     return p
 
 
 def _launch(plan: StftPlan, x: torch.Tensor, out: torch.Tensor, flags: int, workspace=None):
+    """Direct C-ABI launch on a plan (tests use it for the development flags and an explicit
+    workspace); the API below goes through torch.ops.specenh.stft_psd_out."""
     L = _lib.lib()
-    if x.dtype == torch.float16 and plan.key.nperseg > 1024:
-        x = x.float()  # the fp16-sample kernel covers nperseg <= 1024
-    if x.dtype == torch.float16:  # fp16 samples widened on load: no conversion pass
+    st = ctypes.c_void_p(_lib.current_stream_handle(x.device))
+    if x.dtype == torch.float16:
         _lib.check(L.specenh_stft_psd_f16(plan.handle, ctypes.c_void_p(x.data_ptr()), x.shape[0],
                                           x.shape[1], x.stride(0),
-                                          ctypes.c_void_p(out.data_ptr()), flags,
-                                          ctypes.c_void_p(_lib.current_stream_handle(x.device))),
+                                          ctypes.c_void_p(out.data_ptr()), flags, st),
                    "stft_psd_f16")
         return
     ws = plan.workspace(x.shape[0], x.device) if workspace is None else workspace
     _lib.check(L.specenh_stft_psd(plan.handle, ctypes.c_void_p(x.data_ptr()), x.shape[0],
                                   x.shape[1], x.stride(0), ctypes.c_void_p(out.data_ptr()), flags,
-                                  ctypes.c_void_p(ws.data_ptr()),
-                                  ctypes.c_void_p(_lib.current_stream_handle(x.device))),
-               "stft_psd")
+                                  ctypes.c_void_p(ws.data_ptr()), st), "stft_psd")
 
 
 def _check_input(x: torch.Tensor) -> torch.Tensor:
@@ -193,9 +208,12 @@ def stft_psd(x: torch.Tensor, nperseg: int, noverlap: int, window="hann", fs: fl
     ``T = (L - nperseg)//(nperseg - noverlap) + 1``.
     ``normalize`` implies ``log`` (the specgr chain of pipeline_data.py:33-35).
     """
+    from .ops import ops, window_key
     squeeze = x.dim() == 1
     x = _check_input(x)
-    plan = get_plan(x.device, nperseg, noverlap, window, fs, scaling, detrend, eps)
+    nperseg, noverlap = int(nperseg), int(noverlap)
+    if noverlap >= nperseg:
+        raise ValueError("noverlap must be less than nperseg.")
     T = frame_count(x.shape[1], nperseg, noverlap)
     F = nperseg // 2 + (0 if drop_nyquist else 1)
     flags = ((_lib.STFT_LOG if log else 0) | (_lib.STFT_NORMALIZE if normalize else 0)
@@ -204,32 +222,6 @@ def stft_psd(x: torch.Tensor, nperseg: int, noverlap: int, window="hann", fs: fl
         out = torch.empty((x.shape[0], F, T), dtype=torch.float32, device=x.device)
     elif out.shape != (x.shape[0], F, T) or out.dtype != torch.float32 or not out.is_contiguous():
         raise ValueError(f"out must be contiguous float32 of shape {(x.shape[0], F, T)}")
-    _launch(plan, x, out, flags)
+    ops.stft_psd_out(x, nperseg, noverlap, window_key(window, nperseg), float(fs),
+                     _norm_scaling(scaling), _norm_detrend(detrend), float(eps), flags, out)
     return out[0] if squeeze else out
-
-
-# ---------------------------------------------------------------- torch op
-@torch.library.custom_op("specenh::stft_psd", mutates_args=())
-def stft_psd_op(x: torch.Tensor, nperseg: int, noverlap: int, window: list[float], fs: float,
-                scaling: int, detrend: int, eps: float, flags: int) -> torch.Tensor:
-    """Registered op form (window passed as explicit coefficients, codes as ints)."""
-    w = np.asarray(window, dtype=np.float64)
-    xx = _check_input(x)
-    dev = xx.device
-    inv_det = {v: k for k, v in _lib.DETREND.items() if isinstance(k, str) and len(k) > 1}
-    inv_det[0] = False
-    inv_sc = {v: k for k, v in _lib.SCALING.items()}
-    plan = get_plan(dev, nperseg, noverlap, w, fs, inv_sc[scaling], inv_det[detrend], eps)
-    T = frame_count(xx.shape[1], nperseg, noverlap)
-    F = nperseg // 2 + (0 if flags & _lib.STFT_DROP_NYQUIST else 1)
-    out = torch.empty((xx.shape[0], F, T), dtype=torch.float32, device=dev)
-    _launch(plan, xx, out, flags)
-    return out
-
-
-@stft_psd_op.register_fake
-def _(x, nperseg, noverlap, window, fs, scaling, detrend, eps, flags):
-    B = x.shape[0] if x.dim() == 2 else 1
-    T = (x.shape[-1] - nperseg) // (nperseg - noverlap) + 1
-    F = nperseg // 2 + (0 if flags & _lib.STFT_DROP_NYQUIST else 1)
-    return x.new_empty((B, F, T), dtype=torch.float32)

@@ -6,25 +6,18 @@ manual_scan.py, hyperparam_scan.py, graphs.ipynb):
     reshape(arr)  (N, 256, 128) -> (N, 256, 128, 1)
 
 numpy in -> numpy float64 out like the reference (patchify views, ``np.empty`` float64);
-the copies run on the GPU (csrc/strips.hip). ``patch_batch`` / ``unpatch_batch`` are the
+the copies run on the GPU (csrc/strips.hip via ``torch.ops.specenh.strips_pack/unpack``). ``patch_batch`` / ``unpatch_batch`` are the
 device fast path: fp32 spectrograms [B, F, T] -> AE input [B*30, 256, 128, 1] already in
 the AE's compute dtype (bf16 or fp32), and back.
 """
 from __future__ import annotations
 
-import ctypes
-
 import numpy as np
 import torch
 
-from . import _lib
 
 ROWS, WIDTH, N_STRIPS = 256, 128, 30
 _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
-
-
-def _stream(dev):
-    return ctypes.c_void_p(_lib.current_stream_handle(dev))
 
 
 def patch_batch(S: torch.Tensor, dtype=torch.float32, rows=ROWS, width=WIDTH,
@@ -39,12 +32,11 @@ def patch_batch(S: torch.Tensor, dtype=torch.float32, rows=ROWS, width=WIDTH,
         raise TypeError("spectrograms must be float32")
     if not (S.stride(2) == 1 and S.stride(1) == S.shape[2]):
         S = S.contiguous()
-    B, F, T = S.shape
+    from .ops import ops
+    res = ops.strips_pack(S, rows, width, n_strips, dtype)
     if out is None:
-        out = torch.empty((B * n_strips, rows, width, 1), dtype=dtype, device=S.device)
-    _lib.check(_lib.lib().specenh_strips_pack(
-        _DT[dtype], ctypes.c_void_p(S.data_ptr()), B, F, T, S.stride(0), rows, width, n_strips,
-        ctypes.c_void_p(out.data_ptr()), _stream(S.device)), "strips_pack")
+        return res
+    out.copy_(res)
     return out
 
 
@@ -56,12 +48,11 @@ def unpatch_batch(strips: torch.Tensor, rows=ROWS, width=WIDTH, n_strips=N_STRIP
     strips = strips.contiguous()
     if strips.shape[0] % n_strips or tuple(strips.shape[1:3]) != (rows, width):
         raise ValueError(f"strips must be [k*{n_strips}, {rows}, {width}(, 1)]")
-    B = strips.shape[0] // n_strips
+    from .ops import ops
+    res = ops.strips_unpack(strips, rows, width, n_strips)
     if out is None:
-        out = torch.empty((B, rows, n_strips * width), dtype=torch.float32, device=strips.device)
-    _lib.check(_lib.lib().specenh_strips_unpack(
-        _DT[strips.dtype], ctypes.c_void_p(strips.data_ptr()), B, rows, width, n_strips,
-        ctypes.c_void_p(out.data_ptr()), _stream(strips.device)), "strips_unpack")
+        return res
+    out.copy_(res)
     return out
 
 

@@ -15,16 +15,14 @@ Same names, arguments and semantics as the notebook (:155-229):
         2*num_sing > min(m, n) like the notebook
   * ``optimal_batch(A[B, m, n], mode)`` — use_optimal / computeSignal on device tensors.
 
-The arithmetic runs on the GPU (csrc/svd_denoise.hip through the C-ABI
-``specenh_svd_denoise`` / ``specenh_svd_denoise_optimal``): fp32-MFMA Gram matrix, top-K
-subspace iteration with fp64 CholeskyQR2 + Rayleigh-Ritz, reconstruction ``A V V^T``; the
-optimal threshold's median and count come from the fp64 Gram's eigenvalues (Householder
-tridiagonalisation + Sturm bisection). numpy inputs come back as float64 numpy arrays like
-the reference.
+The arithmetic runs on the GPU (csrc/svd_denoise.hip, reached through
+``torch.ops.specenh.svd_denoise_out`` / ``svd_denoise_optimal`` and the C-ABI): fp32-MFMA
+Gram matrix, top-K subspace iteration with fp64 CholeskyQR2 + Rayleigh-Ritz,
+reconstruction ``A V V^T``; wide or bottom-of-spectrum ranges and the optimal threshold use
+fp64 eigenvectors of the Gram matrix (Householder tridiagonalisation, Sturm bisection,
+inverse iteration). numpy inputs come back as float64 numpy arrays like the reference.
 """
 from __future__ import annotations
-
-import ctypes
 
 import numpy as np
 import torch
@@ -83,14 +81,8 @@ def denoise_batch(A: torch.Tensor, start=None, stop=None,
     if odt is None or out.numel() != B * m * n or not out.is_contiguous() or out.device != A.device:
         raise ValueError("out must be a contiguous [B, m, n] float32/bfloat16/float16 tensor "
                          "on A's device")
-    L = _lib.lib()
-    ws = torch.empty(max(16, int(L.specenh_svd_denoise_workspace_bytes(B, m, n, start, stop))),
-                     dtype=torch.uint8, device=A.device)
-    _lib.check(L.specenh_svd_denoise_ex(ctypes.c_void_p(A.data_ptr()), B, m, n, A.stride(0),
-                                        start, stop, ctypes.c_void_p(out.data_ptr()), odt,
-                                        ctypes.c_void_p(ws.data_ptr()),
-                                        ctypes.c_void_p(_lib.current_stream_handle(A.device))),
-               "svd_denoise")
+    from .ops import ops
+    ops.svd_denoise_out(A, start, stop, out.view(B, m, n))
     return out[0] if squeeze else out
 
 
@@ -111,18 +103,12 @@ def optimal_batch(A: torch.Tensor, mode: int = _lib.SVD_OPTIMAL, out: torch.Tens
     if not (A.stride(2) == 1 and A.stride(1) == A.shape[2]):
         A = A.contiguous()
     B, m, n = A.shape
+    from .ops import ops
+    res_, ns, med = ops.svd_denoise_optimal(A, int(mode))
     if out is None:
-        out = torch.empty((B, m, n), dtype=torch.float32, device=A.device)
-    L = _lib.lib()
-    ws = torch.empty(max(16, int(L.specenh_svd_optimal_workspace_bytes(B, m, n))),
-                     dtype=torch.uint8, device=A.device)
-    ns = torch.empty(B, dtype=torch.int32, device=A.device)
-    med = torch.empty(B, dtype=torch.float64, device=A.device)
-    _lib.check(L.specenh_svd_denoise_optimal(
-        ctypes.c_void_p(A.data_ptr()), B, m, n, A.stride(0), int(mode),
-        ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ns.data_ptr()),
-        ctypes.c_void_p(med.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
-        ctypes.c_void_p(_lib.current_stream_handle(A.device))), "svd_denoise_optimal")
+        out = res_
+    else:
+        out.copy_(res_)
     res = out[0] if squeeze else out
     return (res, ns, med) if return_rank else res
 

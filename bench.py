@@ -209,6 +209,29 @@ def cpu_baseline(n_shots: int) -> dict:
                       f"worker processes x 1 thread, {dt:.2f} s wall"}
 
 
+# ------------------------------------------------------------------ multi-GPU plumbing
+def shard(world: int, rank: int, batch: int) -> dict:
+    """Weak scaling: every rank owns `batch` shots of its own, the global
+    shot ids [rank * batch, (rank + 1) * batch), synthesised from a per-rank seed. Shots are
+    independent, so there is no collective in the data path."""
+    return {"seed": 1000 + rank, "first_shot": rank * batch, "shots": batch}
+
+
+def max_over_ranks(elapsed: float, dist=None, device=None) -> float:
+    """The slowest rank's wall time of the timed region (the job is done when it is)."""
+    if dist is None:
+        return elapsed
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def throughput(world: int, batch: int, steps: int, elapsed: float) -> float:
+    """Whole-job spectrograms/s: every rank's shots of every timed step / the max time."""
+    return world * batch * steps / elapsed
+
+
 # ------------------------------------------------------------------ GPU
 def main():
     ap = argparse.ArgumentParser()
@@ -239,12 +262,15 @@ def main():
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    # launched by torch.distributed.run (any world size, 1 included): RCCL process group
+    use_dist = world > 1 or ("MASTER_ADDR" in os.environ and "RANK" in os.environ)
+    if use_dist:
         dist.init_process_group("nccl", device_id=dev)
     L = _lib.lib()
 
     B = args.batch
-    x16 = plasma_chirps_torch(B, L5, seed=1000 + rank, device=dev).to(torch.float16)
+    mine = shard(world, rank, B)
+    x16 = plasma_chirps_torch(B, L5, seed=mine["seed"], device=dev).to(torch.float16)
     S = torch.empty((B, HW5, HW5), dtype=torch.float32, device=dev)
     A = torch.empty((B, HW5, HW5, 1), dtype=torch.float16, device=dev)
     ops = []
@@ -309,7 +335,7 @@ def main():
         step()
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -318,11 +344,7 @@ def main():
     for _ in range(args.steps):
         step()
     barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0, dist if use_dist else None, dev)
 
     # ---- dominant kernel: conv_fwd_kernel, every conv launch bracketed by HIP events on
     # the stream it is launched on ----
@@ -466,16 +488,15 @@ def main():
                     "shots": 8, "reference": "fp64 CPU chain: scipy-semantics specgr -> numpy "
                                              "SVD denoiseSignal -> fp64 autoencoder restatement"}
 
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
     if rank != 0:
         return
 
-    total = world * B * args.steps
     res = {
         "metric": METRIC,
-        "value": total / elapsed,
+        "value": throughput(world, B, args.steps, elapsed),
         "unit": "spectrograms/s",
         "n_gpus": world,
         "steps": args.steps,

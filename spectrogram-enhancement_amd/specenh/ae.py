@@ -351,8 +351,32 @@ class AutoencoderEngine:
         ops.bce_logits_out(b["z"], y, b["d"][-1] if want_grad else None, accumulate)
         return accumulate
 
-    def backward(self):
-        """Gradients of the last loss_and_grad() into self.g (overwritten)."""
+    def grad_bucket_split(self):
+        """(op index j, flat offset): the gradients of layers >= j (the decoder: from the first
+        Conv2DTranspose, else the second half of the convolutions) occupy self.g[offset:] and
+        are final once backward() has run layer j's weight gradient — a data-parallel step
+        all-reduces that bucket while the encoder's backward still runs."""
+        convs = [i for i, op in enumerate(self.ops) if isinstance(op, ConvOp)]
+        dec = [i for i in convs if self.ops[i].kind == "convT"]
+        j = dec[0] if dec else convs[len(convs) // 2]
+        return j, self.ops[j].off_w
+
+    def sync_state(self, group=None, src=0):
+        """Broadcast the master weights, the Adam moments and the step count from rank
+        ``src`` (data-parallel start: ranks may have initialised differently), then refresh
+        the low-precision and flipped weight copies."""
+        import torch.distributed as dist
+        for t in (self.w, self.m, self.v):
+            dist.broadcast(t, src, group=group)
+        tt = torch.tensor([self.t], dtype=torch.float64, device=self.device)
+        dist.broadcast(tt, src, group=group)
+        self.t = int(tt.item())
+        self._refresh_lowp()
+
+    def backward(self, on_layer_done=None):
+        """Gradients of the last loss_and_grad() into self.g (overwritten).
+        ``on_layer_done(i)`` (optional) is called once layer i's weight gradient is enqueued
+        (layers in reverse order): self.g[ops[i].off_w:] is then final on this stream."""
         N = self._last_train_N
         b = self._buffers(N, True)
         self.g.zero_()
@@ -379,6 +403,8 @@ class AutoencoderEngine:
             s, pt, pl, dil = op.fwd_geom()
             ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[i],
                                  self._gbv[i], b["ws"])
+            if on_layer_done is not None:
+                on_layer_done(i)
             if i == 0:
                 continue
             self._conv(i, d_out, b["d"][i], weights=self.w_d[i], geom=op.dgrad_geom(),
@@ -399,16 +425,13 @@ class AutoencoderEngine:
         device fp64 loss sum of this rank (divide by y.numel() for the mean).
 
         With ``process_group`` (an initialised torch.distributed group, RCCL on the GPU)
-        the flat gradient buffer is SUM-all-reduced in one call and Adam scales it by
-        1/world_size: every rank then applies the identical update."""
+        the flat gradient buffer is SUM-all-reduced and Adam scales it by 1/world_size:
+        every rank then applies the identical update. The decoder's
+        bucket is all-reduced asynchronously while the encoder's backward runs
+        (dp_backward)."""
         self.forward(x, train=True)
         loss = self.loss_and_grad(y)
-        self.backward()
-        scale = 1.0
-        if process_group is not None:
-            import torch.distributed as dist
-            dist.all_reduce(self.g, op=dist.ReduceOp.SUM, group=process_group)
-            scale = 1.0 / dist.get_world_size(process_group)
+        scale = dp_backward(self, process_group)
         self.adam(lr, beta_1, beta_2, epsilon, grad_scale=scale)
         return loss
 
@@ -425,3 +448,33 @@ class AutoencoderEngine:
         if t.dtype != torch.float32:
             raise TypeError(f"unsupported input dtype {t.dtype}")
         return ops.cast(t, self.tdt)
+
+
+def dp_backward(eng, group=None, dist=None) -> float:
+    """eng.backward() with the data-parallel gradient exchange: two
+    buckets of the ONE flat gradient buffer, SUM-all-reduced over ``group``. The decoder
+    bucket (eng.grad_bucket_split) goes out asynchronously as soon as its weight gradients
+    are enqueued and overlaps the encoder's backward; the encoder bucket follows when
+    backward ends; both are awaited before returning. Returns Adam's grad_scale
+    (1/world_size), or 1.0 (plain backward) without a process group."""
+    if dist is None:
+        import torch.distributed as tdist
+        dist = tdist if (tdist.is_available() and tdist.is_initialized()) else None
+    if dist is None:
+        eng.backward()
+        return 1.0
+    j, off = eng.grad_bucket_split()
+    works = []
+
+    def ready(i):
+        if i == j:
+            works.append(dist.all_reduce(eng.g[off:], group=group, async_op=True))
+
+    eng.backward(on_layer_done=ready)
+    if not works:  # layer j never reported (cannot happen for a conv layer): whole buffer
+        off = eng.g.numel()
+    if off > 0:
+        works.append(dist.all_reduce(eng.g[:off], group=group, async_op=True))
+    for w in works:
+        w.wait()
+    return 1.0 / dist.get_world_size(group)

@@ -60,8 +60,10 @@ def _to_op(layer):
 
 
 def _dist():
+    """torch.distributed when a process group is initialised (any world size: a 1-rank RCCL
+    group still runs the exchange), else None."""
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         return dist
     return None
 
@@ -192,10 +194,14 @@ class Model:
         self.stop_training = False
         hwc = int(np.prod(self.output_shape[1:]))
         acc = torch.zeros(1, dtype=torch.float64, device=eng.device)
+        if dist:  # every rank starts from rank 0's weights and optimizer state
+            eng.sync_state(group)
         for epoch in range(initial_epoch, epochs):
             t0 = time.time()
             order = utils.rng().permutation(n) if shuffle else np.arange(n)
             order_d = torch.from_numpy(order).to(eng.device)
+            if dist and shuffle:  # one epoch permutation for all ranks: rank 0's
+                dist.broadcast(order_d, 0, group=group)
             acc.zero_()
             seen = 0
             for s in range(0, n, batch_size):
@@ -209,11 +215,7 @@ class Model:
                 yb = yd.index_select(0, idx)
                 eng.forward(xb, train=True)
                 eng.loss_and_grad(yb, accumulate=acc)
-                eng.backward()
-                scale = 1.0
-                if dist:
-                    dist.all_reduce(eng.g, group=group)
-                    scale = 1.0 / world
+                scale = _ae.dp_backward(eng, group, dist)  # bucketed RCCL all-reduce under DP
                 eng.adam(opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon,
                          grad_scale=scale)
                 seen += bs

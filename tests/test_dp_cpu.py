@@ -1,11 +1,14 @@
 """Data-parallel fit() on CPU with gloo, world_size 2.
 
-Model.fit under torch.distributed takes each global batch, gives every rank its slice,
-SUM-all-reduces the ONE flat gradient buffer, scales it by 1/world inside Adam and
-all-reduces the epoch loss. These tests run that orchestration with a test-only engine:
-the oracle's autograd on CPU behind the engine interface (the HIP engine needs a GPU).
-Two gloo ranks must then end with the weights and history a single process gets on the
-same global batches.
+Model.fit under torch.distributed broadcasts rank 0's weights and optimizer state, uses
+rank 0's epoch permutation on every rank, takes each global batch, gives every rank its
+slice, SUM-all-reduces the ONE flat gradient buffer in two buckets (the decoder's
+asynchronously, overlapping the encoder's backward; specenh.ae.dp_backward), scales it by
+1/world inside Adam and all-reduces the epoch loss. These tests run that orchestration with
+a test-only engine: the oracle's autograd on CPU behind the engine interface (the HIP
+engine under a real RCCL group is tests/test_dp_gpu.py). Two gloo ranks must then end with
+the weights and history a single process gets on the same global batches, and unseeded
+ranks (different initial weights) must still end identical.
 """
 import math
 import os
@@ -73,8 +76,24 @@ class OracleEngine:
         accumulate += per.sum().detach()
         return accumulate
 
-    def backward(self):
+    def backward(self, on_layer_done=None):
         self.g = torch.cat([t.grad.reshape(-1) for t in self._tensors()])
+        if on_layer_done is not None:
+            for i in reversed(range(len(self.spec))):
+                if self.spec[i][0] != "pool":
+                    on_layer_done(i)
+
+    def grad_bucket_split(self):
+        convs = [i for i, s in enumerate(self.spec) if s[0] != "pool"]
+        dec = [i for i in convs if self.spec[i][0] == "convT"]
+        j = dec[0] if dec else convs[len(convs) // 2]
+        off = sum(p["W"].numel() + p["b"].numel() for p in self.params[:j] if p is not None)
+        return j, off
+
+    def sync_state(self, group=None, src=0):
+        with torch.no_grad():
+            for t in self._tensors() + [self.m, self.v]:
+                dist.broadcast(t, src, group=group)
 
     def adam(self, lr, b1, b2, eps, grad_scale=1.0):
         self.t += 1
@@ -91,10 +110,11 @@ class OracleEngine:
                 off += n
 
 
-def _build():
+def _build(seed=0):
     from specenh.keras import layers, utils
     from specenh.keras.models import Model
-    utils.set_random_seed(0)
+    if seed is not None:
+        utils.set_random_seed(seed)
     inp = layers.Input(shape=(16, 16, 1))
     x = layers.Conv2D(4, 3, activation="relu", padding="same")(inp)
     x = layers.MaxPooling2D((2, 2), padding="same")(x)
@@ -112,7 +132,7 @@ def _data():
     return x, y
 
 
-def _fit(out_q=None, rank=0, world=1, port=0):
+def _fit(out_q=None, rank=0, world=1, port=0, seed=0):
     from specenh import ae
     if world > 1:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -121,11 +141,12 @@ def _fit(out_q=None, rank=0, world=1, port=0):
     real_engine = ae.AutoencoderEngine
     ae.AutoencoderEngine = OracleEngine  # test-only: CPU autograd behind the engine API
     try:
-        m = _build()
+        m = _build(seed)
         x, y = _data()
+        w0 = [w.copy() for w in m.get_weights()]
         hist = m.fit(x, y, epochs=2, batch_size=8, shuffle=True, validation_data=(x[:8], y[:8]),
                      verbose=0)
-        res = ([w.copy() for w in m.get_weights()], dict(hist.history))
+        res = ([w.copy() for w in m.get_weights()], dict(hist.history), w0)
     finally:
         ae.AutoencoderEngine = real_engine
         if world > 1:
@@ -141,20 +162,25 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_dp_fit_world2_matches_single_process():
-    ref_w, ref_h = _fit()
+def _run_world2(seed):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_fit, args=(q, r, 2, port)) for r in range(2)]
+    procs = [ctx.Process(target=_fit, args=(q, r, 2, port, seed)) for r in range(2)]
     for p in procs:
         p.start()
     results = dict(q.get(timeout=300) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return results
+
+
+def test_dp_fit_world2_matches_single_process():
+    ref_w, ref_h, _ = _fit()
+    results = _run_world2(0)
     for rank in (0, 1):
-        w, h = results[rank]
+        w, h, _ = results[rank]
         for a, b in zip(w, ref_w):
             np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-7)
         for key in ("loss", "val_loss"):
@@ -162,3 +188,15 @@ def test_dp_fit_world2_matches_single_process():
     # every rank applied the identical update
     for a, b in zip(results[0][0], results[1][0]):
         np.testing.assert_array_equal(a, b)
+
+
+def test_dp_fit_unseeded_ranks_stay_in_lockstep():
+    """No set_random_seed on any rank (the reference scripts never seed): the ranks start
+    from different glorot weights, fit() broadcasts rank 0's, and they end identical."""
+    results = _run_world2(None)
+    w0_0, w0_1 = results[0][2], results[1][2]
+    assert any(not np.array_equal(a, b) for a, b in zip(w0_0, w0_1))
+    for a, b in zip(results[0][0], results[1][0]):
+        np.testing.assert_array_equal(a, b)
+    h = results[0][1]
+    assert h["loss"][-1] < h["loss"][0]

@@ -113,13 +113,15 @@ def ae_flops_per_sample(h=HW5, w=HW5):
 VALU_DOT2_PEAK_TFLOPS = 314.6         # v_dot2_f32_f16: 4 FLOP/lane/instr, 128 lanes/clk/CU
 LAYER_NAMES = ["conv1+pool", "conv2+pool", "conv3+pool", "convT1", "convT2", "convT3",
                "conv_out"]
+LAYER_NAMES_TAIL = LAYER_NAMES[:5] + ["convT3+conv_out"]
 
 
-def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4):
-    """Per launch of the fused forward (conv+pool fused): useful FLOPs and algorithmic HBM
-    bytes per sample (activations read once + written once), the weights read once per
-    launch, and the unit that bounds the arithmetic (the narrow 1-in / 1-out channel
-    layers run on the VALU)."""
+def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4, tail=False):
+    """Per launch of the fused forward (conv+pool fused; with ``tail`` the last
+    Conv2DTranspose + Conv2D(1) are one launch, csrc/decoder_tail.hip): useful FLOPs and
+    algorithmic HBM bytes per sample (activations read once + written once), the weights
+    read once per launch, and the units that do the arithmetic (the narrow 1-in / 1-out
+    channel layers run on the VALU). ``mfma_flops`` is the part on the matrix cores."""
     lays = ae_layers()
     res, hh, ww, i = [], h, w, 0
     while i < len(lays):
@@ -131,10 +133,18 @@ def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4):
         last = i + (2 if pool else 1) >= len(lays)
         nbytes = hh * ww * cin * act_bytes + sh * sw * cout * (out_bytes if last else act_bytes)
         unit = "valu" if (cin == 1 or cout == 1) else "mfma"
-        res.append({"flops": 2 * macs, "bytes": nbytes, "weight_bytes": k * k * cin * cout *
-                    act_bytes + 4 * cout, "unit": unit})
+        res.append({"flops": 2 * macs, "mfma_flops": 2 * macs if unit == "mfma" else 0,
+                    "bytes": nbytes, "weight_bytes": k * k * cin * cout * act_bytes + 4 * cout,
+                    "unit": unit})
         hh, ww = sh, sw
         i += 2 if pool else 1
+    if tail:  # convT3 (MFMA) + conv_out (VALU): the 16-channel map is not HBM traffic
+        a, b = res[-2], res[-1]
+        res = res[:-2] + [{"flops": a["flops"] + b["flops"], "mfma_flops": a["mfma_flops"],
+                           "bytes": (h // 2) * (w // 2) * AE_FILTERS[1] * act_bytes +
+                           h * w * out_bytes,
+                           "weight_bytes": a["weight_bytes"] + b["weight_bytes"],
+                           "unit": "mfma+valu"}]
     return res
 
 
@@ -357,13 +367,15 @@ def main():
         stage_ae(timing)
         torch.cuda.synchronize()
         conv_ms.append([a.elapsed_time(b) for a, b in timing])
-    conv_ms = np.array(conv_ms)                       # [reps, 7]
+    conv_ms = np.array(conv_ms)                       # [reps, launches]
     layer_ms = np.median(conv_ms, axis=0)
     pmc = load_pmc_traffic()
     layers = []
-    for name, c, ms in zip(LAYER_NAMES, ae_layer_costs(), layer_ms):
-        peak_c = MFMA_PEAK_TFLOPS if c["unit"] == "mfma" else VALU_DOT2_PEAK_TFLOPS
-        t_c = c["flops"] * Hs / (peak_c * 1e12)
+    names = LAYER_NAMES_TAIL if eng.tail else LAYER_NAMES
+    for name, c, ms in zip(names, ae_layer_costs(tail=eng.tail), layer_ms):
+        # compute floor: MFMA FLOPs at the dense fp16 MFMA peak + VALU FLOPs at the dot2 peak
+        t_c = c["mfma_flops"] * Hs / (MFMA_PEAK_TFLOPS * 1e12) + \
+            (c["flops"] - c["mfma_flops"]) * Hs / (VALU_DOT2_PEAK_TFLOPS * 1e12)
         nb = c["bytes"] * Hs + c["weight_bytes"]
         t_m = nb / (HBM_PEAK_GBPS * 1e9)
         if t_m >= t_c:
@@ -371,12 +383,16 @@ def main():
             rl = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                   "frac": ach / HBM_PEAK_GBPS}
         else:
+            # the FLOP-mix peak: this launch's FLOPs over its compute floor (= the MFMA peak
+            # for a pure-MFMA layer, the dot2 peak for a pure-VALU one)
+            peak_c = c["flops"] * Hs / t_c / 1e12
             ach = c["flops"] * Hs / (ms * 1e-3) / 1e12
-            rl = {"bound": c["unit"], "achieved": ach, "peak": peak_c, "unit": "TFLOP/s",
-                  "frac": ach / peak_c}
+            rl = {"bound": "mfma" if c["mfma_flops"] else "valu", "achieved": ach,
+                  "peak": peak_c, "unit": "TFLOP/s", "frac": ach / peak_c}
         tr = pmc.get(name)
         rl.update({"layer": name, "kernel_ms": float(ms), "alg_bytes_per_launch": nb,
                    "flops_per_launch": c["flops"] * Hs,
+                   "mfma_flops_per_launch": c["mfma_flops"] * Hs,
                    # PMC passes ran 4096-shot launches; these kernels' traffic is linear
                    # in the shot count (per-image tiles), scaled to this launch
                    "traffic": tr["hbm_bytes"] * Hs / tr.get("batch", 4096) if tr else None,

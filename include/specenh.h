@@ -232,6 +232,19 @@ int specenh_weight_flip_transpose(int dtype, const void* bt, int k, int ci, int 
 int specenh_cast(int src_dtype, const void* src, int dst_dtype, void* dst, long long n,
                  void* stream);
 
+/* The model's last two layers fused for inference (manual_scan_3layers.py:197-199):
+ *   Conv2DTranspose(CO, kt, strides=2, activation="relu", padding="same") on x [N][H][W][C]
+ *   -> Conv2D(1, ko, activation="sigmoid", padding="same") -> out fp32 [N][2H][2W]
+ * with wt_gemm / bt and wo_gemm / bo the two layers' specenh_conv2d weights (GEMM layout,
+ * dtype) and fp32 biases (device pointers). The CO-channel map between the layers stays
+ * in LDS; it is rounded to dtype after the ReLU exactly as the two-launch path stores it.
+ * dtype BF16 / F16; C = 32, CO = 16, kt = ko = 5 (the reference model), otherwise
+ * SPECENH_EUNSUPPORTED (use the two specenh_conv2d launches). */
+int specenh_convt_conv_out(int dtype, const void* x, int N, int H, int W, int C,
+                           const void* wt_gemm, const float* bt, int CO, int kt,
+                           const void* wo_gemm, const float* bo, int ko, float* out,
+                           void* stream);
+
 /* ---------------------------------------------------------------- label filters
  * The image-filter helpers of spec_denoising/pipeline_data.py:38-61 (the training-label
  * chain) on a batch of spectrograms, each a rows x cols row-major block at

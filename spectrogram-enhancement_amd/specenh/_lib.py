@@ -92,6 +92,10 @@ SIGNATURES = {
                                         _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p,
                                         _c.c_void_p]),
     "specenh_conv2d_wgrad_workspace_bytes": (_c.c_size_t, [_c.c_int] * 7),
+    "specenh_convt_conv_out": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                          _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int,
+                                          _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p,
+                                          _c.c_void_p]),
     "specenh_maxpool2_fwd": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
                                         _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p]),
     "specenh_maxpool2_bwd": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p,

@@ -24,13 +24,14 @@ layout directly.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
 import torch
 
 from . import _lib
-from .ops import ops
+from .ops import ops, tail_supported
 
 F32, BF16, F16 = 0, 1, 2
 _DTYPES = {"float32": F32, "bfloat16": BF16, "bf16": BF16, "mixed_bfloat16": BF16,
@@ -147,6 +148,17 @@ class AutoencoderEngine:
                       if self.dt != F32 and isinstance(op, ConvOp) and op.kind == "conv"
                       and isinstance(self.ops[i + 1], PoolOp) and op.k <= 5
                       and (op.cin in (1, 16) or op.cin % 32 == 0)}
+        # inference: the last Conv2DTranspose(relu) + Conv2D(1, sigmoid) as one launch
+        # (csrc/decoder_tail.hip); its 16-channel map never reaches HBM
+        last2 = self.ops[-2:] if len(self.ops) >= 2 else []
+        self.tail = (len(last2) == 2 and all(isinstance(o, ConvOp) for o in last2)
+                     and last2[0].kind == "convT" and last2[0].act == "relu"
+                     and last2[0].stride == 2 and last2[1].kind == "conv"
+                     and last2[1].cout == 1 and last2[1].act == "sigmoid"
+                     and last2[1].padding == "same"
+                     and tail_supported(self.tdt, last2[0].cin, last2[0].cout, last2[0].k,
+                                        last2[1].k)
+                     and os.environ.get("SPECENH_NO_TAIL_FUSION", "0") in ("", "0"))
         self.t = 0  # Adam iterations
         self._bufs = {}
         self._loss = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -210,7 +222,8 @@ class AutoencoderEngine:
             H, W, C = shp[i]
             last = i == len(self.ops)
             dtype = torch.float32 if (last and not train) else self.tdt
-            if (i - 1) not in self.fused:  # a fused conv's full-resolution output is never stored
+            tail_map = self.tail and not train and i == len(self.ops) - 1
+            if (i - 1) not in self.fused and not tail_map:  # never-stored fused outputs
                 b["h"][i] = torch.empty((N, H, W, C), dtype=dtype, device=dev)
             if train:
                 b["d"][i] = torch.empty((N, H, W, C), dtype=self.tdt, device=dev)
@@ -322,6 +335,14 @@ class AutoencoderEngine:
             if timing is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record(torch.cuda.current_stream(self.device))
+            if self.tail and not train and i == n_ops - 2:  # fused decoder tail, then done
+                o2 = self.ops[i + 1]
+                ops.convt_conv_out_out(hin, self._wv[i], self._bv[i], op.cout, op.k,
+                                       self._wv[i + 1], self._bv[i + 1], o2.k, b["h"][n_ops])
+                if timing is not None:
+                    ev[1].record(torch.cuda.current_stream(self.device))
+                    timing.append(ev)
+                break
             self._conv(i, hin, hout, weights=self._wv[i], geom=op.fwd_geom(), act=op.act,
                        logits=b["z"] if (train and last) else None,
                        out_shape=hout.shape[1:3], cout=op.cout)

@@ -305,6 +305,43 @@ _op(f"conv2d_wgrad_out(Tensor x, Tensor dout, {_WG_ARGS}, Tensor(a!) dw, Tensor(
     "Tensor(c!) workspace) -> ()", _wgrad_out, lambda *a: None)
 
 
+def _tail_out(x, wt, bt, cout, kt, wo, bo, ko, out):
+    _need(x, "x")
+    _need(out, "out")
+    N, H, W, C = x.shape
+    if wt.dtype != x.dtype or wo.dtype != x.dtype or wt.numel() != cout * kt * kt * C or \
+            wo.numel() != ko * ko * cout:
+        raise ValueError("wt / wo must be the two layers' GEMM weights in x's dtype")
+    if bt.dtype != torch.float32 or bt.numel() != cout or bo.dtype != torch.float32 or \
+            bo.numel() != 1:
+        raise ValueError("biases must be float32 [CO] and [1]")
+    if out.dtype != torch.float32 or out.numel() != N * 4 * H * W:
+        raise ValueError("out must be float32 [N, 2H, 2W(, 1)]")
+    _lib.check(_lib.lib().specenh_convt_conv_out(
+        _code(x), _vp(x), N, H, W, C, _vp(wt), _vp(bt), cout, kt, _vp(wo), _vp(bo), ko, _vp(out),
+        _st(x)), "convt_conv_out")
+
+
+def _tail(x, wt, bt, cout, kt, wo, bo, ko):
+    N, H, W, _ = x.shape
+    out = torch.empty((N, 2 * H, 2 * W, 1), dtype=torch.float32, device=x.device)
+    _tail_out(x, wt, bt, cout, kt, wo, bo, ko, out)
+    return out
+
+
+_op("convt_conv_out(Tensor x, Tensor wt, Tensor bt, int cout, int kt, Tensor wo, Tensor bo, "
+    "int ko) -> Tensor", _tail,
+    lambda x, wt, bt, cout, kt, wo, bo, ko:
+    x.new_empty((x.shape[0], 2 * x.shape[1], 2 * x.shape[2], 1), dtype=torch.float32))
+_op("convt_conv_out_out(Tensor x, Tensor wt, Tensor bt, int cout, int kt, Tensor wo, Tensor bo, "
+    "int ko, Tensor(a!) out) -> ()", _tail_out, lambda *a: None)
+
+
+def tail_supported(dtype: torch.dtype, cin: int, cout: int, kt: int, ko: int) -> bool:
+    """specenh_convt_conv_out's configurations (the reference model's last two layers)."""
+    return dtype in (torch.float16, torch.bfloat16) and (cin, cout, kt, ko) == (32, 16, 5, 5)
+
+
 # ---------------------------------------------------------------- pooling, loss, optimizer
 def _pool_out(x, out, argmax):
     _need(x, "x")

@@ -1,0 +1,58 @@
+"""The fused decoder tail (csrc/decoder_tail.hip: Conv2DTranspose(16, 5, strides=2, relu) +
+Conv2D(1, 5, sigmoid) in one launch, the 16-channel map kept in LDS) against the two-launch
+path and the fp64 oracle: same map rounding, so the outputs agree to fp32 accumulation-order
+differences (the map may differ by one fp16 ulp where the two MFMA orders round apart)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import autoencoder as ora
+from oracle import checks
+
+pytestmark = pytest.mark.gpu
+
+
+def _tail_model(dtype, hw, seed):
+    from specenh import ae
+    C = ae.ConvOp
+    ops_ = [C("conv", 1, 32, 3, "relu"), C("convT", 32, 16, 5, "relu", stride=2),
+            C("conv", 16, 1, 5, "sigmoid")]
+    eng = ae.AutoencoderEngine(ops_, hw + (1,), compute_dtype=dtype, device="cuda")
+    rng = np.random.default_rng(seed)
+    ws = [(0.5 * rng.standard_normal((3, 3, 1, 32))).astype(np.float32),
+          (0.1 * rng.standard_normal(32)).astype(np.float32),
+          (0.08 * rng.standard_normal((5, 5, 16, 32))).astype(np.float32),
+          (0.1 * rng.standard_normal(16)).astype(np.float32),
+          (0.25 * rng.standard_normal((5, 5, 16, 1))).astype(np.float32),
+          (0.1 * rng.standard_normal(1)).astype(np.float32)]
+    eng.set_keras_weights(ws)
+    return eng, ops_, ws
+
+
+@pytest.mark.parametrize("dtype", ["float16", "mixed_bfloat16"])
+@pytest.mark.parametrize("hw", [(64, 64), (20, 28), (9, 33), (1, 1)])
+def test_fused_tail_matches_two_launches_and_oracle(gpu_device, dtype, hw, monkeypatch):
+    eng, ops_, ws = _tail_model(dtype, hw, seed=hw[0] * 7 + hw[1])
+    assert eng.tail
+    x = np.random.default_rng(1).uniform(0, 1, (5,) + hw + (1,)).astype(np.float32)
+    xd = eng.to_compute(torch.from_numpy(x))
+    fused = eng.forward(xd).clone()
+    monkeypatch.setenv("SPECENH_NO_TAIL_FUSION", "1")
+    from specenh import ae
+    plain_eng = ae.AutoencoderEngine(ops_, hw + (1,), compute_dtype=dtype, device="cuda")
+    assert not plain_eng.tail
+    plain_eng.set_keras_weights(ws)
+    plain = plain_eng.forward(xd).clone()
+    torch.cuda.synchronize()
+    assert fused.shape == plain.shape == (5, 2 * hw[0], 2 * hw[1], 1)
+    d = (fused - plain).abs().max().item()
+    assert d <= 2e-3, d
+    spec = [("conv", 1, 32, 3, "relu"), ("convT", 32, 16, 5, "relu"),
+            ("conv", 16, 1, 5, "sigmoid")]
+    it = iter(ws)
+    params = [{"W": torch.tensor(next(it), dtype=torch.float64),
+               "b": torch.tensor(next(it), dtype=torch.float64)} for _ in spec]
+    with torch.no_grad():
+        ref = ora.forward(spec, params, torch.tensor(x, dtype=torch.float64)).numpy()
+    err = checks.out_rel(fused.cpu().numpy(), ref)
+    assert err <= checks.TOL[dtype]["out_rel"], err

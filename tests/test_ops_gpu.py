@@ -29,6 +29,9 @@ def _cases(dev):
     z, t = r(300, lo=-3, hi=3), r(300)
     w, gr, m, v = r(1000, lo=-1), r(1000, lo=-1), r(1000, lo=-1), r(1000)
     F64 = r(2, 32, 40, dtype=torch.float64)
+    xt = r(2, 20, 12, 32, dtype=torch.float16)
+    wt, bc16 = r(16 * 25 * 32, dtype=torch.float16, lo=-0.1, hi=0.1), r(16, lo=-0.1, hi=0.1)
+    wo, bo = r(25 * 16, dtype=torch.float16, lo=-0.2, hi=0.2), r(1)
     Sp = r(1, 256, 3845)
     ops = torch.ops.specenh
     return [
@@ -52,6 +55,9 @@ def _cases(dev):
         (ops.conv2d_wgrad_out, (xc, dout, 3, 3, 1, 1, 1, 1, torch.zeros(8, 3, 3, 4, device=dev),
                                 torch.zeros(8, device=dev),
                                 torch.empty(1 << 20, dtype=torch.uint8, device=dev))),
+        (ops.convt_conv_out, (xt, wt, bc16, 16, 5, wo, bo, 5)),
+        (ops.convt_conv_out_out, (xt, wt, bc16, 16, 5, wo, bo, 5,
+                                  torch.empty(2, 40, 24, 1, device=dev))),
         (ops.maxpool2, (pin,)),
         (ops.maxpool2_out, (pin, torch.empty_like(pooled), torch.empty_like(am))),
         (ops.maxpool2_bwd, (pooled.clone(), am, pooled)),

@@ -219,6 +219,97 @@ def cpu_baseline(n_shots: int) -> dict:
                       f"worker processes x 1 thread, {dt:.2f} s wall"}
 
 
+# ------------------------------------------------------------------ C3 / C4 stages
+FP32_MFMA_PEAK_TFLOPS = 157.3        # v_mfma_f32_16x16x4_f32 / 32x32x2 (= the FP32 vector rate)
+
+
+def c3_matrices(dev, B=4096, m=513, n=256, k=16, seed=3):
+    """B gapped m x n fp32 matrices: 16 components 10 * 0.8^i along random orthonormal
+    directions (QR of Gaussian matrices) + Gaussian noise (singular values ~0.003-0.017)."""
+    import torch
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    A = torch.empty((B, m, n), dtype=torch.float32, device=dev)
+    s_sig = 10.0 * 0.8 ** torch.arange(k, device=dev, dtype=torch.float32)
+    for b0 in range(0, B, 512):
+        b1 = min(B, b0 + 512)
+        U = torch.linalg.qr(torch.randn((b1 - b0, m, k), generator=g, device=dev)).Q
+        V = torch.linalg.qr(torch.randn((b1 - b0, n, k), generator=g, device=dev)).Q
+        A[b0:b1] = (U * s_sig) @ V.transpose(1, 2) + \
+            (0.01 / m ** 0.5) * torch.randn((b1 - b0, m, n), generator=g, device=dev)
+        del U, V
+    return A
+
+
+def svd_c3_stage(dev, B=4096, m=513, n=256, k=16, reps=5):
+    """BASELINE config 3: denoiseSignal on 4096 gapped 513 x 256 fp32 matrices, rank-16
+    (start 0, stop 16) and the default (1, r). Matrices: 16 signal components 10 * 0.8^i
+    along random orthonormal directions + Gaussian noise of
+    singular values ~0.003-0.017 (SURVEY.md §8 d: the gap sits at the cut; orthonormal
+    directions from a QR of Gaussian matrices, so the signal spectrum is exact). Roofline
+    (SURVEY §8 d C3): 2mn^2 + 4mnk = 75.6 MFLOP per matrix at the fp32 MFMA peak; HBM floor
+    8mn bytes (read A, write the reconstruction)."""
+    import torch
+    from specenh import svd
+    A = c3_matrices(dev, B, m, n, k)
+    out = torch.empty_like(A)
+    st = torch.cuda.current_stream(dev)
+    res = {"workload": f"{B} x {m} x {n} fp32 gapped matrices (rank 16 + noise)"}
+    flop = 2.0 * m * n * n + 4.0 * m * n * k
+    for name, (lo, hi) in {"rank16": (0, 16), "default": (None, None)}.items():
+        for _ in range(2):
+            svd.denoise_batch(A, lo, hi, out=out)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            svd.denoise_batch(A, lo, hi, out=out)
+        e1.record(st)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        fl = flop if name == "rank16" else 2.0 * m * n * n + 4.0 * m * n  # K = 1
+        ach = fl * B / (ms * 1e-3) / 1e12
+        res[name] = {"ms": ms, "matrices_per_s": B / (ms * 1e-3),
+                     "roofline": {"bound": "mfma_fp32", "achieved": ach,
+                                  "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                  "frac": ach / FP32_MFMA_PEAK_TFLOPS,
+                                  "flops_per_matrix": fl,
+                                  "hbm_floor_ms": 8.0 * m * n * B / (HBM_PEAK_GBPS * 1e9) * 1e3}}
+    del A, out
+    return res
+
+
+def ae_train_c4_stage(dev, ops, batch=128, steps=20):
+    """BASELINE config 4's step on one GPU: Keras fit() of the 3-layer model on 128 x 128 x 1
+    inputs, mixed_bfloat16 (bf16 MFMA, fp32 master weights + Adam), batch 128: forward, BCE
+    from logits, backward (dgrad + deterministic wgrad), Adam. 1.494 GFLOP per sample
+    (SURVEY §8 d C4: forward x 3) at the dense bf16 MFMA peak."""
+    import torch
+    from specenh import ae
+    eng = ae.AutoencoderEngine(ops, (HW5, HW5, 1), compute_dtype="mixed_bfloat16", device=dev)
+    eng.set_keras_weights(ae_weights())
+    g = torch.Generator(device=dev)
+    g.manual_seed(4)
+    x = eng.to_compute(torch.rand((batch, HW5, HW5, 1), generator=g, device=dev))
+    y = eng.to_compute(torch.rand((batch, HW5, HW5, 1), generator=g, device=dev))
+    for _ in range(3):
+        eng.train_step(x, y)
+    st = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(steps):
+        eng.train_step(x, y)
+    e1.record(st)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    fl = 3.0 * ae_flops_per_sample() * batch
+    ach = fl / (ms * 1e-3) / 1e12
+    return {"workload": f"fit step, batch {batch}, 128x128x1, mixed_bfloat16, Adam",
+            "ms_per_step": ms, "samples_per_s": batch / (ms * 1e-3),
+            "roofline": {"bound": "mfma", "achieved": ach, "peak": MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": ach / MFMA_PEAK_TFLOPS,
+                         "flops_per_step": fl}}
+
+
 # ------------------------------------------------------------------ multi-GPU plumbing
 def shard(world: int, rank: int, batch: int) -> dict:
     """Weak scaling: every rank owns `batch` shots of its own, the global
@@ -468,6 +559,8 @@ def main():
                          "frac": achc / HBM_PEAK_GBPS, "alg_bytes_per_launch": algc,
                          "traffic": None}}
         del x2, oc
+        stages["svd_c3"] = svd_c3_stage(dev)
+        stages["ae_train_c4"] = ae_train_c4_stage(dev, ops)
 
     # ---- accuracy vs the fp64 CPU chain on sample shots ----
     accuracy = None

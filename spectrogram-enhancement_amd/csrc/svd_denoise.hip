@@ -476,13 +476,16 @@ struct SsLayout {
 // With flags, the boundary Ritz pairs of the kept range (component K-1, and cut2 when the
 // range starts inside the subspace) are checked: sqrt(theta_c) * ||G v_c - theta_c v_c|| /
 // (theta_c - theta_{c+1}) bounds the reconstruction error their angle causes (Davis-Kahan);
-// above tolv * ||X||_F the matrix is flagged for the fp64 eigen path (a cut with no
-// spectral gap, e.g. inside a noise bulk, where subspace iteration does not converge).
+// above tolv * ||X||_F (tolv = 5e-6: half the 1e-5 parity contract, and above the fp32
+// floor of the residual itself on gapped inputs) the matrix is flagged for the fp64 eigen
+// path (a cut with no spectral gap, e.g. inside a noise bulk, where subspace iteration does
+// not converge).
 template <int P>
 __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, int r, int K,
                                                               int iters, float* V,
                                                               float* theta, int cut2,
-                                                              float tolv, int* flags) {
+                                                              float tolv, int* flags, int seed,
+                                                              const int* only) {
   __shared__ double sRed[4];
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* sS = reinterpret_cast<double*>(smem);            // P x P
@@ -504,7 +507,9 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
     if constexpr (P == 8) gemm_GZ8(Gb, r, z, y, sT);
     else gemm_GZ<P>(Gb, r, z, y);
   };
-  for (int idx = tid; idx < r * P; idx += SS_THREADS) sZ[idx] = hash_unit(idx / P, idx % P);
+  if (only && !only[b]) return;  // (second pass: only the matrices the first one flagged)
+  for (int idx = tid; idx < r * P; idx += SS_THREADS)
+    sZ[idx] = hash_unit(idx / P + 7919u * seed, idx % P);
   __syncthreads();
   GZ(sZ, sY);
   __syncthreads();
@@ -619,8 +624,7 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
 //   out = Y[:, lo:hi] V[:, lo:hi]^T     (RB x r)      phase 2 (complement: X_blk - ...)
 constexpr int RB = 32;
 
-// ranges (optional, device int[2 * batch]): a per-matrix [lo, hi) replacing the uniform
-// one (always the direct, non-complement form); hi <= lo gives zeros.
+// only (optional, device int[batch]): reconstruct only the matrices with only[b] != 0.
 template <typename TO>
 __device__ __forceinline__ TO to_out(float v) { return (TO)v; }
 
@@ -629,7 +633,7 @@ __device__ __forceinline__ TO to_out(float v) { return (TO)v; }
 template <int KP, typename TO>
 __global__ __launch_bounds__(256) void recon_kernel(XView x, int Kr, int r, const float* V,
                                                     int K, int lo, int hi, int complement,
-                                                    const int* ranges, TO* out,
+                                                    const int* only, TO* out,
                                                     long long out_bstride, long long osk,
                                                     long long osi) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -637,11 +641,7 @@ __global__ __launch_bounds__(256) void recon_kernel(XView x, int Kr, int r, cons
   float* sX = sV + r * KP;                      // RB x (r + 1)
   float* sY = sX + RB * (r + 1);                // RB x KP
   const long long b = blockIdx.y;
-  if (ranges) {
-    lo = ranges[2 * b];
-    hi = ranges[2 * b + 1];
-    complement = 0;
-  }
+  if (only && !only[b]) return;
   const int k0 = blockIdx.x * RB;
   const int tid = threadIdx.x;
   const float* X = x.base + b * x.batch_stride;
@@ -1270,35 +1270,36 @@ void launch_gram(const XView& xv, int Kr, int r, float* G, long long batch, hipS
 
 template <int P>
 hipError_t launch_subspace_t(const float* G, int r, int K, float* V, float* theta,
-                             long long batch, hipStream_t st, int cut2, int* flags) {
+                             long long batch, hipStream_t st, int cut2, int* flags, int seed,
+                             const int* only) {
   const size_t lds = SsLayout<P>::bytes(r);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipError_t e = hipFuncSetAttribute((const void*)subspace_kernel<P>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   // 3 rounds when the subspace oversamples the wanted K by >= 8 columns, else 5
-  const int iters = P >= K + 8 ? 3 : 5;
+  // (a second pass over flagged matrices starts elsewhere and iterates 4x longer)
+  const int iters = (P >= K + 8 ? 3 : 5) * (seed ? 4 : 1);
   hipLaunchKernelGGL(subspace_kernel<P>, dim3((unsigned)batch), dim3(SS_THREADS), lds, st, G, r,
-                     K, iters, V, theta, cut2, 1e-6f, flags);
+                     K, iters, V, theta, cut2, 5e-6f, flags, seed, only);
   return hipGetLastError();
 }
 
 hipError_t launch_subspace(int p, const float* G, int r, int K, float* V, float* theta,
-                           long long batch, hipStream_t st, int cut2 = -1, int* flags = nullptr) {
+                           long long batch, hipStream_t st, int cut2 = -1, int* flags = nullptr,
+                           int seed = 0, const int* only = nullptr) {
   switch (p) {
-    case 8: return launch_subspace_t<8>(G, r, K, V, theta, batch, st, cut2, flags);
-    case 16: return launch_subspace_t<16>(G, r, K, V, theta, batch, st, cut2, flags);
-    case 24: return launch_subspace_t<24>(G, r, K, V, theta, batch, st, cut2, flags);
-    case 32: return launch_subspace_t<32>(G, r, K, V, theta, batch, st, cut2, flags);
-    case 40: return launch_subspace_t<40>(G, r, K, V, theta, batch, st, cut2, flags);
-    case 48: return launch_subspace_t<48>(G, r, K, V, theta, batch, st, cut2, flags);
+#define SPECENH_SS(n) \
+    case n: return launch_subspace_t<n>(G, r, K, V, theta, batch, st, cut2, flags, seed, only);
+    SPECENH_SS(8) SPECENH_SS(16) SPECENH_SS(24) SPECENH_SS(32) SPECENH_SS(40) SPECENH_SS(48)
+#undef SPECENH_SS
     default: return hipErrorInvalidValue;
   }
 }
 
 template <int KP, typename TO>
 hipError_t launch_recon_t(XView xb, int Kr, int r, const float* V, int K, int lo, int hi,
-                          int comp, const int* ranges, void* out, long long ob, long long osk,
+                          int comp, const int* only, void* out, long long ob, long long osk,
                           long long osi, long long nb, hipStream_t st) {
   const size_t lds = (size_t)r * KP * 4 + (size_t)RB * (r + 1) * 4 + (size_t)RB * KP * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
@@ -1306,19 +1307,19 @@ hipError_t launch_recon_t(XView xb, int Kr, int r, const float* V, int K, int lo
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((recon_kernel<KP, TO>), dim3((Kr + RB - 1) / RB, (unsigned)nb), dim3(256),
-                     lds, st, xb, Kr, r, V, K, lo, hi, comp, ranges, reinterpret_cast<TO*>(out),
+                     lds, st, xb, Kr, r, V, K, lo, hi, comp, only, reinterpret_cast<TO*>(out),
                      ob, osk, osi);
   return hipGetLastError();
 }
 
 template <typename TO>
 hipError_t launch_recon_k(int KP, XView xb, int Kr, int r, const float* V, int K, int lo,
-                          int hi, int comp, const int* ranges, void* out, long long ob,
+                          int hi, int comp, const int* only, void* out, long long ob,
                           long long osk, long long osi, long long nb, hipStream_t st) {
   switch (KP) {
 #define SPECENH_RC(n)                                                                          \
   case n:                                                                                      \
-    return launch_recon_t<n, TO>(xb, Kr, r, V, K, lo, hi, comp, ranges, out, ob, osk, osi, nb, \
+    return launch_recon_t<n, TO>(xb, Kr, r, V, K, lo, hi, comp, only, out, ob, osk, osi, nb, \
                                  st);
     SPECENH_RC(8) SPECENH_RC(16) SPECENH_RC(24) SPECENH_RC(32) SPECENH_RC(40) SPECENH_RC(48)
 #undef SPECENH_RC
@@ -1327,13 +1328,13 @@ hipError_t launch_recon_k(int KP, XView xb, int Kr, int r, const float* V, int K
 }
 
 hipError_t launch_recon(int KP, XView xb, int Kr, int r, const float* V, int K, int lo, int hi,
-                        int comp, const int* ranges, void* out, long long ob, long long osk,
+                        int comp, const int* only, void* out, long long ob, long long osk,
                         long long osi, long long nb, hipStream_t st, int odt = SPECENH_DTYPE_F32) {
   if (odt == SPECENH_DTYPE_F16)
-    return launch_recon_k<_Float16>(KP, xb, Kr, r, V, K, lo, hi, comp, ranges, out, ob, osk, osi, nb, st);
+    return launch_recon_k<_Float16>(KP, xb, Kr, r, V, K, lo, hi, comp, only, out, ob, osk, osi, nb, st);
   if (odt == SPECENH_DTYPE_BF16)
-    return launch_recon_k<__bf16>(KP, xb, Kr, r, V, K, lo, hi, comp, ranges, out, ob, osk, osi, nb, st);
-  return launch_recon_k<float>(KP, xb, Kr, r, V, K, lo, hi, comp, ranges, out, ob, osk, osi, nb, st);
+    return launch_recon_k<__bf16>(KP, xb, Kr, r, V, K, lo, hi, comp, only, out, ob, osk, osi, nb, st);
+  return launch_recon_k<float>(KP, xb, Kr, r, V, K, lo, hi, comp, only, out, ob, osk, osi, nb, st);
 }
 
 size_t dtype_size(int dt) { return dt == SPECENH_DTYPE_F32 ? 4 : 2; }
@@ -1477,11 +1478,11 @@ size_t specenh_svd_workspace_bytes(long long batch, int m, int n, int kmax) {
   const long long r = std::min(m, n);
   if (batch <= 0 || r <= 0) return 16;
   if (kmax > PMAX - 8 && r <= EIG_MAXN) return eig_layout((int)r).bytes(batch);
-  // subspace path: G, V, theta; for r <= 256 also the per-matrix convergence flags and the
-  // eigen-path workspace that redoes the flagged matrices
+  // subspace path: G, V, theta; for r <= 256 also the per-matrix convergence flags of the
+  // two subspace passes and the eigen-path workspace that redoes what stays flagged
   size_t off = (size_t)(batch * r * r + batch * r * kmax + batch * kmax) * sizeof(float);
   if (r > EIG_MAXN) return off;
-  off = (off + 255) / 256 * 256 + (size_t)batch * 4;
+  off = (off + 255) / 256 * 256 + 2 * (size_t)batch * 4;
   off = (off + 255) / 256 * 256;
   return off + eig_layout((int)r).bytes(batch);
 }
@@ -1569,13 +1570,15 @@ int specenh_svd_denoise_ex(const float* A, long long batch, int m, int n, long l
   float* G = (float*)workspace;
   float* V = G + batch * (long long)r * r;
   float* theta = V + batch * (long long)r * K;
-  int* flags = nullptr;
+  int* flags = nullptr;   // first subspace pass: cut without a converged gap
+  int* flags2 = nullptr;  // still so after the second pass
   void* eig_ws = nullptr;
   if (r <= EIG_MAXN) {
     size_t off = (size_t)(batch * r * r + batch * (long long)r * K + batch * K) * sizeof(float);
     off = (off + 255) / 256 * 256;
     flags = (int*)((char*)workspace + off);
-    off = (off + (size_t)batch * 4 + 255) / 256 * 256;
+    flags2 = flags + batch;
+    off = (off + 2 * (size_t)batch * 4 + 255) / 256 * 256;
     eig_ws = (char*)workspace + off;
   }
   launch_gram(xv, Kr, r, G, batch, st);
@@ -1595,14 +1598,29 @@ int specenh_svd_denoise_ex(const float* A, long long batch, int m, int n, long l
   }
   if (hipGetLastError() != hipSuccess) return set_error(SPECENH_EHIP, "recon launch");
   if (!flags) return SPECENH_OK;
-  // matrices whose cut has no spectral gap: redone (overwritten) by the fp64 eigen path;
-  // every kernel of that path returns at once for the others
+  // Flagged matrices: a second subspace pass (other start vectors, 4x the rounds) catches
+  // an unlucky start; what is still flagged has no spectral gap at the cut and is redone by
+  // the fp64 eigen path. Every kernel of both returns at once for unflagged matrices.
+  if (hipMemsetAsync(flags2, 0, (size_t)batch * 4, st) != hipSuccess)
+    return set_error(SPECENH_EHIP, "memset");
+  e = launch_subspace(p, G, r, K, V, theta, batch, st, (!complement && lo > 0) ? lo - 1 : -1,
+                      flags2, 1, flags);
+  if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("subspace: ") + hipGetErrorString(e));
+  for (long long b0 = 0; b0 < batch; b0 += 65535) {
+    const long long nb = std::min<long long>(65535, batch - b0);
+    XView xb = xv;
+    xb.base = A + b0 * a_stride;
+    e = launch_recon(KP, xb, Kr, r, V + b0 * (long long)r * K, K, lo, hi, complement ? 1 : 0,
+                     flags + b0, static_cast<char*>(out) + (size_t)(b0 * ob) * osz, ob, osk, osi,
+                     nb, st, out_dtype);
+    if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("recon: ") + hipGetErrorString(e));
+  }
   if (complement) {  // back to the kept range [start, r)
     lo = hi;
     hi = r;
   }
   return eig_denoise(A, batch, m, n, a_stride, lo, hi, -1, out, out_dtype, nullptr, nullptr,
-                     nullptr, eig_ws, st, flags);
+                     nullptr, eig_ws, st, flags2);
 }
 
 size_t specenh_svd_optimal_workspace_bytes(long long batch, int m, int n) {

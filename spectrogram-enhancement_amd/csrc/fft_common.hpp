@@ -93,39 +93,41 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 w) {
   return make_float2(fmaf(a.x, w.x, -a.y * w.y), fmaf(a.x, w.y, a.y * w.x));
 }
 
-// d * W_M^j with compile-time (j, M): trivial rotations are free.
-template <int M, int J>
-__device__ __forceinline__ float2 twiddle_const(float2 d) {
-  constexpr int j = J % M;
-  if constexpr (j == 0) {
-    return d;
-  } else if constexpr (4 * j == M) {  // -i
-    return make_float2(d.y, -d.x);
-  } else if constexpr (2 * j == M) {  // -1
-    return make_float2(-d.x, -d.y);
-  } else if constexpr (4 * j == 3 * M) {  // +i
-    return make_float2(-d.y, d.x);
-  } else if constexpr (8 * j == M) {  // (1 - i)/sqrt2
-    constexpr float h = 0.70710678118654752440f;
-    return make_float2((d.x + d.y) * h, (d.y - d.x) * h);
-  } else if constexpr (8 * j == 3 * M) {  // (-1 - i)/sqrt2
-    constexpr float h = 0.70710678118654752440f;
-    return make_float2((d.y - d.x) * h, -(d.x + d.y) * h);
-  } else {
-    constexpr Twiddles<M> tw{};
-    return cmul(d, make_float2(tw.re[j], tw.im[j]));
-  }
-}
+// ------------------------------------------------------------ complex arithmetic
+// A complex value as a two-float vector {re, im}. The library is built without packed
+// fp32 codegen (build.py: on CDNA4 a v_pk_*_f32 issues as two scalar ops and only adds
+// register-pair moves), so these are plain scalar VALU ops; rotations by -i are free
+// (operand renaming).
+typedef float f2v __attribute__((ext_vector_type(2)));
 
-// In-register radix-2 DIF butterflies of one stage (span H), unrolled by recursion.
+namespace pk {
+__device__ __forceinline__ f2v add(f2v a, f2v b) { return a + b; }
+__device__ __forceinline__ f2v sub(f2v a, f2v b) { return a - b; }
+// -i (a - b) = (a.y - b.y, b.x - a.x)
+__device__ __forceinline__ f2v sub_mi(f2v a, f2v b) { return f2v{a.y - b.y, b.x - a.x}; }
+__device__ __forceinline__ f2v cmul(f2v d, f2v w) {
+  return f2v{fmaf(d.x, w.x, -d.y * w.y), fmaf(d.x, w.y, d.y * w.x)};
+}
+}  // namespace pk
+
+// In-register radix-2 DIF butterflies of one stage (span H), unrolled by recursion; the
+// difference's twiddle W_{2H}^K is a compile-time constant (1 and -i cost nothing extra).
 template <int R, int H, int S, int K>
 struct DifStage {
-  __device__ __forceinline__ static void run(float2 (&v)[R]) {
+  __device__ __forceinline__ static void run(f2v (&v)[R]) {
     if constexpr (S < R) {
       if constexpr (K < H) {
-        float2 a = v[S + K], b = v[S + K + H];
-        v[S + K] = cadd(a, b);
-        v[S + K + H] = twiddle_const<2 * H, K>(csub(a, b));
+        constexpr int M = 2 * H;
+        const f2v a = v[S + K], b = v[S + K + H];
+        v[S + K] = pk::add(a, b);
+        if constexpr (K == 0) {
+          v[S + K + H] = pk::sub(a, b);
+        } else if constexpr (4 * K == M) {
+          v[S + K + H] = pk::sub_mi(a, b);
+        } else {
+          constexpr Twiddles<M> tw{};
+          v[S + K + H] = pk::cmul(pk::sub(a, b), f2v{tw.re[K], tw.im[K]});
+        }
         DifStage<R, H, S, K + 1>::run(v);
       } else {
         DifStage<R, H, S + 2 * H, 0>::run(v);
@@ -136,7 +138,7 @@ struct DifStage {
 
 template <int R, int H>
 struct DifAll {
-  __device__ __forceinline__ static void run(float2 (&v)[R]) {
+  __device__ __forceinline__ static void run(f2v (&v)[R]) {
     if constexpr (H >= 1) {
       DifStage<R, H, 0, 0>::run(v);
       DifAll<R, H / 2>::run(v);
@@ -148,7 +150,7 @@ struct DifAll {
 // output bin bitrev(r) (log2 R bits) — callers fold that permutation into their
 // store addresses at compile time.
 template <int R>
-__device__ __forceinline__ void fft_dif(float2 (&v)[R]) {
+__device__ __forceinline__ void fft_dif(f2v (&v)[R]) {
   DifAll<R, R / 2>::run(v);
 }
 

@@ -33,6 +33,10 @@
 #include <vector>
 
 #include "fft_common.hpp"
+
+#ifndef SPECENH_STFT_PF_EARLY
+#define SPECENH_STFT_PF_EARLY 0
+#endif
 #include "specenh.h"
 
 // Development-only flag bit (not part of the public header): skip the output store,
@@ -69,22 +73,27 @@ struct StftArgs {
   int F_out;
   const float* window;
   const float2* twiddle;  // per-pass [r-1][k] tables (TwOff<N>)
-  const double* dc_coef;  // c_n: DC bin of the detrended, windowed frame = <x, c> (fp64)
+  // DC bin of the detrended, windowed frame = <x, c> in fp64 with
+  // c_n = w_n - dc_alpha - dc_beta (n - (N-1)/2), w the fp32 window (see pair_spectrum)
+  double dc_alpha;
+  double dc_beta;
 };
 
 // Per-N decomposition: G lanes per FFT, WAVES per workgroup, Stockham radices.
 template <int N>
 struct Cfg;
-// G lanes own one FFT (two frames); WAVES per workgroup (one workgroup per CU: the
-// LDS footprint is sized for that); R1 x R2 (x R3) Stockham radices; PF = prefetch the
-// next tile's samples into registers while the current tile computes.
-template <> struct Cfg<64>   { static constexpr int G = 8,  WAVES = 8, R1 = 8,  R2 = 8,  R3 = 1, PF = 1; };
-template <> struct Cfg<128>  { static constexpr int G = 8,  WAVES = 8, R1 = 16, R2 = 8,  R3 = 1, PF = 1; };
-template <> struct Cfg<256>  { static constexpr int G = 16, WAVES = 8, R1 = 16, R2 = 16, R3 = 1, PF = 1; };
-template <> struct Cfg<512>  { static constexpr int G = 16, WAVES = 8, R1 = 32, R2 = 16, R3 = 1, PF = 1; };
-template <> struct Cfg<1024> { static constexpr int G = 32, WAVES = 8, R1 = 32, R2 = 32, R3 = 1, PF = 1; };
-template <> struct Cfg<2048> { static constexpr int G = 64, WAVES = 4, R1 = 32, R2 = 8,  R3 = 8, PF = 1; };
-template <> struct Cfg<4096> { static constexpr int G = 64, WAVES = 2, R1 = 32, R2 = 16, R3 = 8, PF = 0; };
+// G lanes own one FFT (two frames); WAVES per workgroup; OCC = resident workgroups per CU
+// the LDS and register budgets are sized for; R1 x R2 (x R3) Stockham radices; PF =
+// prefetch the next tile's samples into registers while the current tile computes.
+// N = 1024 (C2): 4-wave workgroups, 3 per CU (168 VGPRs, 47 KB LDS each), so one
+// workgroup's barriers, team wait and store burst overlap two others' FFTs.
+template <> struct Cfg<64>   { static constexpr int G = 8,  WAVES = 8, OCC = 1, R1 = 8,  R2 = 8,  R3 = 1, PF = 1; };
+template <> struct Cfg<128>  { static constexpr int G = 8,  WAVES = 8, OCC = 1, R1 = 16, R2 = 8,  R3 = 1, PF = 1; };
+template <> struct Cfg<256>  { static constexpr int G = 16, WAVES = 8, OCC = 1, R1 = 16, R2 = 16, R3 = 1, PF = 1; };
+template <> struct Cfg<512>  { static constexpr int G = 16, WAVES = 8, OCC = 1, R1 = 32, R2 = 16, R3 = 1, PF = 1; };
+template <> struct Cfg<1024> { static constexpr int G = 32, WAVES = 4, OCC = 3, R1 = 32, R2 = 32, R3 = 1, PF = 1; };
+template <> struct Cfg<2048> { static constexpr int G = 64, WAVES = 4, OCC = 1, R1 = 32, R2 = 8,  R3 = 8, PF = 1; };
+template <> struct Cfg<4096> { static constexpr int G = 64, WAVES = 2, OCC = 1, R1 = 32, R2 = 16, R3 = 8, PF = 0; };
 
 // Stockham pass p >= 2 of radix R at stride NS uses twiddles W_N^{r k N/(NS R)} for
 // r in [1, R), k in [0, NS); stored as a [r-1][k] table so the lanes of a group read
@@ -97,32 +106,37 @@ struct TwOff {
   static constexpr int TOTAL = P3 + (C::R3 > 1 ? (C::R3 - 1) * C::R1 * C::R2 : 0);
 };
 
+constexpr int align16(int b) { return (b + 15) / 16 * 16; }
+
 template <int N>
 struct Layout {
   using C = Cfg<N>;
   static constexpr int G = C::G;
   static constexpr int THREADS = 64 * C::WAVES;
-  static constexpr int WPE = C::WAVES >= 8 ? C::WAVES / 4 : 1;  // waves per SIMD
+  static constexpr int WPE = C::OCC * C::WAVES >= 4 ? C::OCC * C::WAVES / 4 : 1;  // waves/SIMD
   static constexpr int FFTS = C::WAVES * (64 / G);  // concurrent FFTs per workgroup
   static constexpr int TF = 2 * FFTS;                // frames per tile (power of two)
   static constexpr int LOG_TF = ilog2(TF);
   static constexpr int TS = TF + 1;                  // tile row stride (odd: conflict-free)
   static constexpr int NBINS = N / 2 + 1;
   static constexpr int IB = (NBINS + G - 1) / G;     // bins per lane in the epilogue
-  static constexpr int BUF = N + N / 32;             // padded complex entries per FFT
-  static constexpr int BUF_BYTES = FFTS * BUF * 8;
+  // per-FFT exchange buffer: N padded FLOATS (real and imaginary parts take turns)
+  static constexpr int BUF = N + N / 32;
+  static constexpr int BUF_BYTES = FFTS * BUF * 4;
   static constexpr int TILE_BYTES = NBINS * TS * 4;  // aliases the FFT buffers
   static constexpr int TWN = TwOff<N>::TOTAL;
   // byte offsets into dynamic LDS (all multiples of 16)
-  static constexpr int OFF_DC = 0;
-  static constexpr int OFF_TW = OFF_DC + N * 8;
-  static constexpr int OFF_WIN = OFF_TW + ((TWN * 8 + 15) / 16) * 16;
-  static constexpr int OFF_BUF = OFF_WIN + N * 4;
-  static constexpr int OFF_RED = OFF_BUF + (BUF_BYTES > TILE_BYTES ? BUF_BYTES : TILE_BYTES);
-  static constexpr int BYTES = OFF_RED + 4 * C::WAVES * 4;
-  static_assert(BYTES <= 160 * 1024, "LDS budget");
+  static constexpr int OFF_TW = 0;
+  static constexpr int OFF_WIN = OFF_TW + align16(TWN * 8);
+  static constexpr int OFF_BUF = OFF_WIN + align16(N * 4);
+  // + 16 B: the mirror read of lane 0 (see pair_spectrum) may touch one float past the
+  // last FFT buffer
+  static constexpr int OFF_RED = OFF_BUF + align16((BUF_BYTES > TILE_BYTES ? BUF_BYTES : TILE_BYTES) + 16);
+  static constexpr int BYTES = OFF_RED + 4 * C::WAVES * 4;  // [2*WAVES] + team {mn, mx, done}
+  static_assert(BYTES * C::OCC <= 160 * 1024, "LDS budget");
   static_assert(C::R1 * C::R2 * C::R3 == N, "radix product");
   static_assert((TF & (TF - 1)) == 0, "tile width must be a power of two");
+  static_assert(4 * C::WAVES >= 2 * C::WAVES + 3, "reduction scratch");
 };
 
 __device__ __forceinline__ int pad(int e) { return e + (e >> 5); }
@@ -184,35 +198,51 @@ __device__ __forceinline__ T group_sum(T v) {
   return v;
 }
 
-// Stockham pass NS>1 through the LDS buffer (all butterflies of the lane read first,
-// then written back in place: legal because the whole FFT lives in one wave).
+// Split exchange through one per-FFT float buffer: the register array `w` of one stage
+// (element (i, r) holds FFT index WI(i, r)) becomes the next stage's `v` (element (i, r)
+// = FFT index RI(i, r)); real parts first, then imaginary parts, so the buffer is N
+// floats instead of N complex values. Wave-local (the FFT lives in one wave).
+template <int WB, int WR, int RB, int RR, class WI, class RI>
+__device__ __forceinline__ void split_exchange(float* buf, const f2v (&w)[WB][WR], f2v (&v)[RB][RR],
+                                               WI wi, RI ri) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < WB; ++i)
+#pragma unroll
+      for (int r = 0; r < WR; ++r) buf[pad(wi(i, r))] = w[i][r][h];
+    wave_lds_sync();
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+#pragma unroll
+      for (int r = 0; r < RR; ++r) v[i][r][h] = buf[pad(ri(i, r))];
+    wave_lds_sync();
+  }
+}
+
+// Stockham pass of radix R at stride NS on registers loaded by split_exchange from FFT
+// indices b + r*N/R (b = gl + i*G): twiddles from the LDS table, then the in-register DIF.
+// Element (i, r) then holds FFT index stockham_out<N, G, R, NS>(gl, i, r).
 template <int N, int G, int R, int NS>
-__device__ __forceinline__ void stockham_pass(float2* buf, const float2* tw /* [R-1][NS] */,
-                                              int gl) {
-  constexpr int NB = N / R;
-  constexpr int BPL = NB / G;
-  constexpr int LOGR = ilog2(R);
-  static_assert(BPL >= 1 && NB % G == 0, "butterflies per lane");
-  float2 v[BPL][R];
+__device__ __forceinline__ int stockham_out(int gl, int i, int r) {
+  const int b = gl + i * G;
+  return (b / NS) * NS * R + b % NS + bitrev(r, ilog2(R)) * NS;
+}
+template <int N, int G, int R, int NS>
+__device__ __forceinline__ void stockham_compute(f2v (&v)[(N / R) / G][R], const f2v* tw, int gl) {
+  constexpr int BPL = (N / R) / G;
 #pragma unroll
   for (int i = 0; i < BPL; ++i) {
-    const int b = gl + i * G;
+    const int k = (gl + i * G) % NS;
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[i][r] = buf[pad(b + r * NB)];
-  }
-  wave_lds_sync();
-#pragma unroll
-  for (int i = 0; i < BPL; ++i) {
-    const int b = gl + i * G;
-    const int k = b % NS;
-#pragma unroll
-    for (int r = 1; r < R; ++r) v[i][r] = cmul(v[i][r], tw[(r - 1) * NS + k]);
+    for (int r = 1; r < R; ++r) {
+      v[i][r] = pk::cmul(v[i][r], tw[(r - 1) * NS + k]);
+      // twiddles in chunks of 8: the scheduler would otherwise hoist all R-1 table reads
+      // (2 VGPRs each) ahead of the multiplies
+      if (r % 8 == 7) __builtin_amdgcn_sched_barrier(0);
+    }
     fft_dif<R>(v[i]);
-    const int base = (b / NS) * NS * R + k;
-#pragma unroll
-    for (int r = 0; r < R; ++r) buf[pad(base + bitrev(r, LOGR) * NS)] = v[i][r];
   }
-  wave_lds_sync();
 }
 
 // acc += (double)x * c, as one opaque statement: hipcc otherwise converts all N/G
@@ -220,9 +250,7 @@ __device__ __forceinline__ void stockham_pass(float2* buf, const float2* tw /* [
 // v_cvt_f64_f32 -> v_fma_f64 is an ordinary VALU RAW dependency (interlocked).
 __device__ __forceinline__ void dc_fma(double& acc, float x, double c) {
   double t;
-  asm volatile("v_cvt_f64_f32 %1, %2\n\tv_fma_f64 %0, %1, %3, %0"
-               : "+v"(acc), "=&v"(t)
-               : "v"(x), "v"(c));
+  asm("v_cvt_f64_f32 %1, %2\n\tv_fma_f64 %0, %1, %3, %0" : "+v"(acc), "=&v"(t) : "v"(x), "v"(c));
 }
 
 // Raw samples of one FFT pair as this lane holds them: x[.][r] = (frame a, frame b)
@@ -231,7 +259,7 @@ template <int N>
 struct PairSamples {
   static constexpr int R1 = Cfg<N>::R1;
   static constexpr int BPL1 = (N / R1) / Cfg<N>::G;
-  float2 x[BPL1][R1];
+  f2v x[BPL1][R1];  // {frame a, frame b} sample pairs
 };
 
 // Shot-local buffer descriptor (wave-uniform base, 32-bit offsets): every sample load
@@ -261,25 +289,30 @@ __device__ __forceinline__ void load_pair(PairSamples<N>& s, __amdgpu_buffer_rsr
       if constexpr (XH) {
         const unsigned short ha = __builtin_amdgcn_raw_buffer_load_b16(xr, oa + o, 0, 0);
         const unsigned short hb = __builtin_amdgcn_raw_buffer_load_b16(xr, ob + o, 0, 0);
-        s.x[i][r] = make_float2((float)__builtin_bit_cast(_Float16, ha),
-                                (float)__builtin_bit_cast(_Float16, hb));
+        s.x[i][r] = f2v{(float)__builtin_bit_cast(_Float16, ha),
+                        (float)__builtin_bit_cast(_Float16, hb)};
       } else {
-        s.x[i][r] = make_float2(
-            __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, oa + o, 0, 0)),
-            __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ob + o, 0, 0)));
+        s.x[i][r] = f2v{__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, oa + o, 0, 0)),
+                        __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ob + o, 0, 0))};
       }
     }
 }
 
-// Detrend + window + all FFT passes for one pair; leaves Z (natural order) in `buf`
-// and returns the fp64 DC bins of both frames.
+// One FFT pair end to end: detrend + window + all FFT passes (split exchanges through the
+// lane group's float buffer `buf`), then the two frames' separation, PSD (+ log2 / ln) of
+// bins gl + i*G into pv[i] = (frame a, frame b) and the running min/max. DC bins come
+// from the fp64 path. With `prefetch`, the next tile's samples are loaded into `nxt` while
+// this pair computes (`in` and `nxt` may be the same set: `in` is consumed first).
 template <int N, bool XH = false>
-__device__ __forceinline__ void fft_pair(const StftArgs& a, PairSamples<N>& in, bool va,
-                                         bool vb, const float2* s_tw, const float* s_win,
-                                         const double* s_dc, float2* buf, int gl, double& dca,
-                                         double& dcb, __amdgpu_buffer_rsrc_t xr, int fa_next,
-                                         bool prefetch) {
+__device__ __forceinline__ void pair_spectrum(const StftArgs& a, const PairSamples<N>& in,
+                                              PairSamples<N>& nxt, const f2v* s_tw,
+                                              const float* s_win, float* buf, int gl,
+                                              double dc_base, __amdgpu_buffer_rsrc_t xr,
+                                              int fa_next, bool prefetch, bool want_log,
+                                              bool log2_out, f2v (&pv)[Layout<N>::IB],
+                                              float& lmin, float& lmax) {
   using C = Cfg<N>;
+  using Lo = Layout<N>;
   constexpr int G = C::G;
   constexpr int R1 = C::R1;
   constexpr int NB1 = N / R1;
@@ -287,41 +320,40 @@ __device__ __forceinline__ void fft_pair(const StftArgs& a, PairSamples<N>& in, 
   constexpr int LOGR1 = ilog2(R1);
   constexpr float kmid = 0.5f * float(N - 1);
   constexpr float invN = 1.0f / float(N);
+  constexpr int IB = Lo::IB;
+  constexpr bool PF_EARLY = SPECENH_STFT_PF_EARLY;
 
   // DC bin in fp64: X_0 = sum_n w_n y_n = <x, c> with c = w - mean(w) - kc*sum(w kc)/sum(kc^2)
   // (c is orthogonal to constants and ramps, so the detrend cancellation happens exactly
   // in the coefficients, not in the data). After detrending X_0 is tiny by construction;
   // in fp32 it would sit at the rounding floor eps*||w y|| and, being the usual
   // spectrogram minimum under 'spectrum' scaling, would shift every normalised value.
-  float2 v[BPL1][R1];
-  float s0a = 0.f, s0b = 0.f, s1a = 0.f, s1b = 0.f;
+  // c_n = (w_n - dc_base) - beta * j is formed here from the fp32 window (dc_base =
+  // alpha + beta * (gl - kmid) per lane): no coefficient table in LDS.
+  f2v s0 = {0.f, 0.f}, s1 = {0.f, 0.f};  // per frame (a, b): sum x, sum j x
   // 4 independent fp64 partial sums per frame: a single chain of R1 dependent
   // v_fma_f64 would be latency-bound.
   constexpr int NDC = 4;
   double pda[NDC] = {}, pdb[NDC] = {};
-  const double* dcp = s_dc + gl;
+  const float* win = s_win + gl;
 #pragma unroll
   for (int i = 0; i < BPL1; ++i)
 #pragma unroll
     for (int r = 0; r < R1; ++r) {
       const int j = i * G + r * NB1;
-      const float xa_n = in.x[i][r].x, xb_n = in.x[i][r].y;
-      v[i][r] = in.x[i][r];
-      s0a += xa_n;
-      s0b += xb_n;
-      s1a = fmaf(float(j), xa_n, s1a);
-      s1b = fmaf(float(j), xb_n, s1b);
-      const double c = dcp[j];
-      dc_fma(pda[(i * R1 + r) % NDC], xa_n, c);
-      dc_fma(pdb[(i * R1 + r) % NDC], xb_n, c);
+      const f2v xv = in.x[i][r];
+      s0 += xv;
+      s1 = __builtin_elementwise_fma(f2v{float(j), float(j)}, xv, s1);
+      const double c = __builtin_fma(-a.dc_beta, double(j), (double)win[j] - dc_base);
+      dc_fma(pda[(i * R1 + r) % NDC], xv.x, c);
+      dc_fma(pdb[(i * R1 + r) % NDC], xv.y, c);
+      if ((i * R1 + r) % 8 == 7) __builtin_amdgcn_sched_barrier(0);
     }
-  dca = (pda[0] + pda[1]) + (pda[2] + pda[3]);
-  dcb = (pdb[0] + pdb[1]) + (pdb[2] + pdb[3]);
-  // `in` is consumed: refill it with the next tile's samples now, so their HBM latency
-  // hides under this pair's FFT (the fences keep the loads after the reads above).
-  __builtin_amdgcn_sched_barrier(0);
-  if (prefetch) load_pair<N, XH>(in, xr, a.hop, fa_next, a.T, gl);
-  __builtin_amdgcn_sched_barrier(0);
+  // memory clobber: the windowing below re-reads win[j] from LDS instead of keeping the
+  // N/G values read above live across the detrend sums (CSE would add N/G VGPRs)
+  asm volatile("" ::: "memory");
+  double dca = (pda[0] + pda[1]) + (pda[2] + pda[3]);
+  double dcb = (pdb[0] + pdb[1]) + (pdb[2] + pdb[3]);
   dca = group_sum<G>(dca);
   dcb = group_sum<G>(dcb);
 
@@ -331,76 +363,118 @@ __device__ __forceinline__ void fft_pair(const StftArgs& a, PairSamples<N>& in, 
   // Only the DC bin is sensitive to the fp32 rounding of the fitted line (a coherent
   // error times sum(w)); it is taken from the fp64 path above instead.
   const float kc0 = float(gl) - kmid;
-  float A_a = 0.f, A_b = 0.f, B_a = 0.f, B_b = 0.f;  // y = x - A - B*j
+  f2v A = {0.f, 0.f}, nB = {0.f, 0.f};  // y = x - A - B*j (nB = -B)
   if (a.detrend != SPECENH_DETREND_NONE) {
-    s1a = fmaf(kc0, s0a, s1a);  // lane sums of kc*x
-    s1b = fmaf(kc0, s0b, s1b);
-    s0a = group_sum<G>(s0a);
-    s0b = group_sum<G>(s0b);
-    A_a = s0a * invN;
-    A_b = s0b * invN;
+    s1 = __builtin_elementwise_fma(f2v{kc0, kc0}, s0, s1);  // lane sums of kc*x
+    s0 = f2v{group_sum<G>(s0.x), group_sum<G>(s0.y)};
+    A = s0 * invN;
     if (a.detrend == SPECENH_DETREND_LINEAR) {
-      s1a = group_sum<G>(s1a);
-      s1b = group_sum<G>(s1b);
-      const float sa = s1a * a.inv_kk, sb = s1b * a.inv_kk;
-      A_a = fmaf(sa, kc0, A_a);
-      A_b = fmaf(sb, kc0, A_b);
-      B_a = sa;
-      B_b = sb;
+      const f2v sl = f2v{group_sum<G>(s1.x), group_sum<G>(s1.y)} * a.inv_kk;
+      A = __builtin_elementwise_fma(sl, f2v{kc0, kc0}, A);
+      nB = -sl;
     }
   }
-  const float* win = s_win + gl;
+  f2v v1[BPL1][R1];
 #pragma unroll
   for (int i = 0; i < BPL1; ++i) {
-    const int b = gl + i * G;
 #pragma unroll
     for (int r = 0; r < R1; ++r) {
       const int j = i * G + r * NB1;
-      const float w = win[j];
-      const float ya = fmaf(-B_a, float(j), v[i][r].x - A_a);
-      const float yb = fmaf(-B_b, float(j), v[i][r].y - A_b);
-      v[i][r] = make_float2(w * ya, w * yb);
+      const f2v y = __builtin_elementwise_fma(nB, f2v{float(j), float(j)}, in.x[i][r] - A);
+      v1[i][r] = y * win[j];
     }
-    fft_dif<R1>(v[i]);
-#pragma unroll
-    for (int r = 0; r < R1; ++r) buf[pad(b * R1 + bitrev(r, LOGR1))] = v[i][r];
+    fft_dif<R1>(v1[i]);
   }
-  wave_lds_sync();
-  stockham_pass<N, G, C::R2, R1>(buf, s_tw + TwOff<N>::P2, gl);
-  if constexpr (C::R3 > 1) stockham_pass<N, G, C::R3, R1 * C::R2>(buf, s_tw + TwOff<N>::P3, gl);
-}
+  // `in` is consumed; the next tile's samples are loaded once the Stockham passes are
+  // done (below): issued earlier, the 64 in-flight sample registers on top of a pass's
+  // 64 data registers spill under the 168-VGPR budget of Cfg<1024>::OCC = 3
 
-// Separate the two frames of this lane group's FFT pair (Z in `buf`), PSD (+log2 / ln) of
-// bins gl + i*G in registers, running min/max. DC bins come from the fp64 path.
-template <int N>
-__device__ __forceinline__ void pair_psd(const StftArgs& a, const float2* buf, int gl, double dca,
-                                         double dcb, bool want_log, bool log2_out,
-                                         float (&pv)[Layout<N>::IB][2], float& lmin, float& lmax) {
-  using Lo = Layout<N>;
-  constexpr int G = Cfg<N>::G;
-  constexpr int IB = Lo::IB;
+  // `prefetch` is compile-time per configuration and unconditional at run time: a
+  // conditional load would keep the consumed samples live (the "not loaded" path) when
+  // `nxt` is `in`. Past the last tile the clamped frames / repeated shot are re-read.
+  auto issue_prefetch = [&]() {  // fences keep the loads after the FFT's reads of `in`
+    __builtin_amdgcn_sched_barrier(0);
+    if (prefetch) load_pair<N, XH>(nxt, xr, a.hop, fa_next, a.T, gl);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // ---- Stockham passes 2 (and 3) ----
+  constexpr int R2 = C::R2, R3 = C::R3;
+  if constexpr (PF_EARLY) issue_prefetch();
+  f2v v2[(N / R2) / G][R2];
+  split_exchange(buf, v1, v2, [&](int i, int r) { return (gl + i * G) * R1 + bitrev(r, LOGR1); },
+                 [&](int i, int r) { return gl + i * G + r * (N / R2); });
+  stockham_compute<N, G, R2, R1>(v2, s_tw + TwOff<N>::P2, gl);
+
+  // ---- final split exchange: Z[k] and Z[N - k] for bins k = gl + i*G ----
+  // Mirror-bin index pad((N - k) & (N - 1)). For G a multiple of 32 it is affine in i:
+  // zmb - (G + G/32) i, so all IB reads share one address register (otherwise the
+  // compiler hoists IB lane-dependent addresses out of the tile loop and spills them).
+  // Lane gl == 0 at i == 0 reads one slot past its FFT buffer (still inside the LDS
+  // allocation, Layout::OFF_RED): that value is bin 0's, which the fp64 DC path replaces.
+  const int zmb = N + N / 32 - gl + ((-gl) >> 5);
+  auto kk_of = [&](int i) {  // bins k > N/2 (only at i == IB-1) duplicate bin gl
+    const int k = gl + i * G;
+    return (i == IB - 1 && k >= Lo::NBINS) ? gl : k;
+  };
+  auto mi_of = [&](int i) {
+    const int k = gl + i * G;
+    const bool dup = i == IB - 1 && k >= Lo::NBINS;
+    if constexpr (G % 32 == 0) return dup ? zmb : zmb - (G + G / 32) * i;
+    return pad((N - kk_of(i)) & (N - 1));
+  };
+  // The two frames' powers accumulate across the real and imaginary halves of the
+  // exchange: q = ((Re Z_k + Re Z_m)^2 + (Im Z_k - Im Z_m)^2,
+  //                (Re Z_k - Re Z_m)^2 + (Im Z_k + Im Z_m)^2) = 4 (|A_k|^2, |B_k|^2)
+  // (m = N - k), so only IB pairs stay live between the halves, not 2 IB complex values.
+  f2v q[IB];
+  auto final_exchange = [&](const auto& vf, auto out_index) {
+    constexpr int FB = sizeof(vf) / sizeof(vf[0]);
+    constexpr int FR = sizeof(vf[0]) / sizeof(vf[0][0]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int i = 0; i < FB; ++i)
+#pragma unroll
+        for (int r = 0; r < FR; ++r) buf[pad(out_index(i, r))] = vf[i][r][h];
+      wave_lds_sync();
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        const float zk = buf[pad(kk_of(i))], zm = buf[mi_of(i)];
+        const f2v t = h == 0 ? f2v{zk + zm, zk - zm} : f2v{zk - zm, zk + zm};
+        q[i] = h == 0 ? t * t : __builtin_elementwise_fma(t, t, q[i]);
+      }
+      wave_lds_sync();
+    }
+  };
+  if constexpr (R3 > 1) {
+    f2v v3[(N / R3) / G][R3];
+    split_exchange(buf, v2, v3,
+                   [&](int i, int r) { return stockham_out<N, G, R2, R1>(gl, i, r); },
+                   [&](int i, int r) { return gl + i * G + r * (N / R3); });
+    stockham_compute<N, G, R3, R1 * R2>(v3, s_tw + TwOff<N>::P3, gl);
+    if constexpr (!PF_EARLY) issue_prefetch();
+    final_exchange(v3, [&](int i, int r) { return stockham_out<N, G, R3, R1 * R2>(gl, i, r); });
+  } else {
+    if constexpr (!PF_EARLY) issue_prefetch();
+    final_exchange(v2, [&](int i, int r) { return stockham_out<N, G, R2, R1>(gl, i, r); });
+  }
+
+  // ---- separate the two frames, PSD (+log2/ln), running min/max ----
   const float scale_mid = 0.5f * a.scale, scale_end = 0.25f * a.scale;
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
     // bins k = gl + i*G: only i == 0 holds k = 0 (gl == 0), only i == IB-1 can hold
     // k = N/2 and k > N/2 (clamped to a duplicate of bin gl), all compile-time known.
-    const int k = gl + i * G;
-    const int kk = (i == IB - 1 && k >= Lo::NBINS) ? gl : k;
-    const float2 zk = buf[pad(kk)];
-    const float2 zm = buf[pad((N - kk) & (N - 1))];
-    const float ar = zk.x + zm.x, ai = zk.y - zm.y;
-    const float br = zk.x - zm.x, bi = zk.y + zm.y;
-    float qa = fmaf(ar, ar, ai * ai);
-    float qb = fmaf(br, br, bi * bi);
+    const int kk = kk_of(i);
     float sc = scale_mid;
     if (i == IB - 1 && (N / 2) % G == 0) sc = (kk == N / 2) ? scale_end : scale_mid;
     float pa, pb;
     if (want_log) {
-      pa = __log2f(fmaf(qa, sc, a.eps));
-      pb = __log2f(fmaf(qb, sc, a.eps));
+      pa = __log2f(fmaf(q[i].x, sc, a.eps));
+      pb = __log2f(fmaf(q[i].y, sc, a.eps));
     } else {
-      pa = qa * sc;
-      pb = qb * sc;
+      pa = q[i].x * sc;
+      pb = q[i].y * sc;
     }
     if (i == 0) {  // DC of both frames from the fp64 path (lane gl == 0 only)
       const float da = (float)(dca * dca * (double)a.scale);
@@ -416,58 +490,79 @@ __device__ __forceinline__ void pair_psd(const StftArgs& a, const float2* buf, i
     }
     lmin = fmin3(lmin, pa, pb);
     lmax = fmax3(lmax, pa, pb);
-    pv[i][0] = pa;
-    pv[i][1] = pb;
+    pv[i] = f2v{pa, pb};
   }
 }
 
 // The workgroup's (bins x TF frames) tile through LDS (it aliases the FFT buffers) and out
 // as frequency-row segments out[k][t0 : t0 + tfv]; with `norm` each value is rescaled
-// (v - mn) * inv on the way. Starts and ends with a workgroup LDS barrier.
+// (v - mn) * inv on the way. Ends with a workgroup LDS barrier; starts with one unless
+// the caller has just passed one after every wave finished reading its FFT buffer.
 template <int N>
 __device__ __forceinline__ void tile_store(const StftArgs& a, float* s_tile,
-                                           const float (&pv)[Layout<N>::IB][2], int gl, int fi,
+                                           const f2v (&pv)[Layout<N>::IB], int gl, int fi,
                                            int tid, __amdgpu_buffer_rsrc_t orr, int t0, float mn,
-                                           float inv, bool norm) {
+                                           float inv, bool norm, bool lead_barrier = true) {
   using Lo = Layout<N>;
   constexpr int G = Cfg<N>::G;
   constexpr int IB = Lo::IB;
-  lds_barrier();  // every group is done with its FFT buffer: reuse as the tile
+  if (lead_barrier) lds_barrier();  // every group is done with its FFT buffer: reuse as the tile
   const int fl = 2 * fi;
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
     const int k = gl + i * G;
     if (k < Lo::NBINS) {
-      s_tile[k * Lo::TS + fl] = norm ? (pv[i][0] - mn) * inv : pv[i][0];
-      s_tile[k * Lo::TS + fl + 1] = norm ? (pv[i][1] - mn) * inv : pv[i][1];
+      const f2v t = norm ? (pv[i] - mn) * inv : pv[i];
+      s_tile[k * Lo::TS + fl] = t.x;
+      s_tile[k * Lo::TS + fl + 1] = t.y;
     }
   }
   lds_barrier();
   // ---- store frequency-row segments: out[shot][k][t0 : t0+tfv] ----
+  // Branch-free: rows k >= F_out land past the end of the shot's buffer descriptor
+  // (num_records = F_out * T * 4) and frames past T get an offset beyond it, so the
+  // hardware drops exactly those stores (the host keeps a plane below 2^30 bytes).
   // Compile-time trip count: the compiler can then count these stores in its partial
   // vmcnt waits for the prefetched samples instead of draining everything.
   const int tfv = min(Lo::TF, a.T - t0);
   if (!(a.flags & SPECENH_STFT_DEV_NOSTORE)) {
     constexpr int ST = (Lo::NBINS * Lo::TF + Lo::THREADS - 1) / Lo::THREADS;
     constexpr int ROWS_PER_IT = Lo::THREADS >> Lo::LOG_TF;
+    constexpr int GRP = 12;  // LDS reads issued ahead of their stores
     const int k0 = tid >> Lo::LOG_TF;
     const int f = tid & (Lo::TF - 1);
     // one VGPR offset for all stores of this tile; the row step is a scalar soffset
-    const int voff = (k0 * a.T + t0 + f) * 4;
+    const int voff = f < tfv ? (k0 * a.T + t0 + f) * 4 : (1 << 30);
     const int sstep = ROWS_PER_IT * a.T * 4;
-    int soff = 0;
-    asm volatile("" : "+s"(soff));  // opaque: keeps the 33 offsets from being hoisted
-                                    // out of the tile loop into (spilled) SGPRs
+    const float* src = s_tile + k0 * Lo::TS + f;
 #pragma unroll
-    for (int it = 0; it < ST; ++it) {
-      const int k = k0 + it * ROWS_PER_IT;
-      if (k < a.F_out && f < tfv)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s_tile[k * Lo::TS + f]), orr,
-                                              voff, soff, 0);
-      soff += sstep;
+    for (int g0 = 0; g0 < ST; g0 += GRP) {
+      float v[GRP];
+#pragma unroll
+      for (int u = 0; u < GRP; ++u) {
+        const int it = g0 + u;
+        if (it < ST && it * ROWS_PER_IT < Lo::NBINS) {
+          if ((it + 1) * ROWS_PER_IT <= Lo::NBINS)
+            v[u] = src[it * ROWS_PER_IT * Lo::TS];
+          else  // last, partial row group: rows past the tile re-read its last row (their
+                // stores fall past the descriptor's end anyway)
+            v[u] = s_tile[min(k0 + it * ROWS_PER_IT, Lo::NBINS - 1) * Lo::TS + f];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < GRP; ++u)
+        if (g0 + u < ST && (g0 + u) * ROWS_PER_IT < Lo::NBINS)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[u]), orr, voff,
+                                                (g0 + u) * sstep, 0);
     }
   }
   lds_barrier();  // tile (= FFT buffers) free for the next tile's FFTs
+}
+
+// Per-lane base of the DC coefficients: alpha + beta * (gl - (N-1)/2).
+template <int N>
+__device__ __forceinline__ double dc_lane_base(const StftArgs& a, int gl) {
+  return a.dc_alpha + a.dc_beta * (double(gl) - 0.5 * double(N - 1));
 }
 
 // One workgroup per spectrogram (shot): loops over tiles of TF frames. Tables are
@@ -486,25 +581,21 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
   constexpr int G = C::G;
   constexpr int IB = Lo::IB;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* s_dc = reinterpret_cast<double*>(smem + Lo::OFF_DC);
-  float2* s_tw = reinterpret_cast<float2*>(smem + Lo::OFF_TW);
+  f2v* s_tw = reinterpret_cast<f2v*>(smem + Lo::OFF_TW);
   float* s_win = reinterpret_cast<float*>(smem + Lo::OFF_WIN);
   float* s_tile = reinterpret_cast<float*>(smem + Lo::OFF_BUF);
   float* s_red = reinterpret_cast<float*>(smem + Lo::OFF_RED);
 
   const int tid = threadIdx.x;
   const long long shot = blockIdx.x;
-  for (int i = tid; i < Lo::TWN; i += Lo::THREADS) s_tw[i] = a.twiddle[i];
-  for (int i = tid; i < N; i += Lo::THREADS) {
-    s_win[i] = a.window[i];
-    s_dc[i] = a.dc_coef[i];
-  }
+  for (int i = tid; i < Lo::TWN; i += Lo::THREADS) s_tw[i] = f2v{a.twiddle[i].x, a.twiddle[i].y};
+  for (int i = tid; i < N; i += Lo::THREADS) s_win[i] = a.window[i];
 
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int gl = lane % G;                          // lane within the FFT group
   const int fi = wave * (64 / G) + lane / G;        // FFT index within the tile
-  float2* buf = reinterpret_cast<float2*>(smem + Lo::OFF_BUF) + fi * Lo::BUF;
+  float* buf = reinterpret_cast<float*>(smem + Lo::OFF_BUF) + fi * Lo::BUF;
   constexpr int ES = XH ? 2 : 4;
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(
       reinterpret_cast<const char*>(a.x) + shot * a.x_stride * ES, a.x_stride * ES);
@@ -513,24 +604,20 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
   const int ntiles = (a.T + Lo::TF - 1) / Lo::TF;
   float* o_shot = a.out + shot * (long long)a.F_out * a.T;
   float lmin = INFINITY, lmax = -INFINITY;
+  const double dcb = dc_lane_base<N>(a, gl);
 
   const __amdgpu_buffer_rsrc_t orr = make_rsrc(o_shot, (long long)a.F_out * a.T * 4);
-  PairSamples<N> nxt;
-  if constexpr (C::PF) load_pair<N, XH>(nxt, xr, a.hop, 2 * fi, a.T, gl);
+  PairSamples<N> s0;
+  if constexpr (C::PF) load_pair<N, XH>(s0, xr, a.hop, 2 * fi, a.T, gl);
   __syncthreads();
 
   for (int tile = 0; tile < ntiles; ++tile) {
     const int t0 = tile * Lo::TF;
-    const int fa = t0 + 2 * fi;
-    const bool va = true, vb = true;  // tail frames are clamped duplicates (load_pair)
-    if constexpr (!C::PF) load_pair<N, XH>(nxt, xr, a.hop, fa, a.T, gl);
-    double dca, dcb;
-    fft_pair<N, XH>(a, nxt, va, vb, s_tw, s_win, s_dc, buf, gl, dca, dcb, xr, fa + Lo::TF,
-                C::PF && tile + 1 < ntiles);
-
-    // ---- separate the two frames, PSD (+log2/ln), running min/max; values in registers ----
-    float pv[IB][2];
-    pair_psd<N>(a, buf, gl, dca, dcb, want_log, log2_out, pv, lmin, lmax);
+    const int fa = t0 + 2 * fi;  // tail frames are clamped duplicates (load_pair)
+    if constexpr (!C::PF) load_pair<N, XH>(s0, xr, a.hop, fa, a.T, gl);
+    f2v pv[IB];
+    pair_spectrum<N, XH>(a, s0, s0, s_tw, s_win, buf, gl, dcb, xr, fa + Lo::TF, C::PF != 0,
+                         want_log, log2_out, pv, lmin, lmax);
     tile_store<N>(a, s_tile, pv, gl, fi, tid, orr, t0, 0.f, 1.f, false);
   }
 
@@ -611,6 +698,7 @@ constexpr int TEAM_MAX = 64;           // one wave polls a team's granules
 constexpr int STFT_DEV_NOTEAM = 1 << 17;     // development flag: force stft_psd_kernel
 constexpr int STFT_DEV_FORCETEAM = 1 << 18;  // development flag: team even for small shots
 constexpr int STFT_DEV_GIVEUP = 1 << 19;     // test flag: every team wait gives up at once
+constexpr int STFT_DEV_NOWAIT = 1 << 20;     // profiling flag: skip the team wait (wrong output)
 
 // Wave-wide: the team's extremes once all M granules are in (returns true), or false when
 // the wait gave up (bounded spins, or another member already timed out in this launch).
@@ -650,63 +738,63 @@ __device__ __forceinline__ bool team_minmax(const unsigned long long* g, int M, 
 template <int N>
 __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_kernel(
     StftArgs a, unsigned long long* gran, long long batch, int M, int Q, unsigned* tmo,
-    unsigned char* tile_flag) {
+    unsigned char* tile_flag, int xcd_teams) {
   using C = Cfg<N>;
   using Lo = Layout<N>;
   constexpr int G = C::G;
   constexpr int IB = Lo::IB;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* s_dc = reinterpret_cast<double*>(smem + Lo::OFF_DC);
-  float2* s_tw = reinterpret_cast<float2*>(smem + Lo::OFF_TW);
+  f2v* s_tw = reinterpret_cast<f2v*>(smem + Lo::OFF_TW);
   float* s_win = reinterpret_cast<float*>(smem + Lo::OFF_WIN);
   float* s_tile = reinterpret_cast<float*>(smem + Lo::OFF_BUF);
-  float* s_red = reinterpret_cast<float*>(smem + Lo::OFF_RED);  // [2*WAVES] + team {mn, mx}
+  float* s_red = reinterpret_cast<float*>(smem + Lo::OFF_RED);  // [2*WAVES] + team {mn, mx, done}
 
   if ((int)blockIdx.x >= Q * M) return;  // whole workgroup: spare slots of the grid
   const int tid = threadIdx.x;
-  const int q = blockIdx.x / M, mem = blockIdx.x - (blockIdx.x / M) * M;
-  for (int i = tid; i < Lo::TWN; i += Lo::THREADS) s_tw[i] = a.twiddle[i];
-  for (int i = tid; i < N; i += Lo::THREADS) {
-    s_win[i] = a.window[i];
-    s_dc[i] = a.dc_coef[i];
-  }
+  // xcd_teams: a team's members are blocks b, b + 8, b + 16, ... (dealt to one XCD), so the
+  // row segments two neighbouring members write into one 32-B sector meet in one L2, and
+  // the frames their sample windows share are read once (a speed choice only: nothing
+  // here depends on where the blocks actually run)
+  const int b = blockIdx.x;
+  const int s8 = xcd_teams ? (b >> 3) : b;
+  const int q = xcd_teams ? (s8 / M) * 8 + (b & 7) : s8 / M;
+  const int mem = s8 - (s8 / M) * M;
+  for (int i = tid; i < Lo::TWN; i += Lo::THREADS) s_tw[i] = f2v{a.twiddle[i].x, a.twiddle[i].y};
+  for (int i = tid; i < N; i += Lo::THREADS) s_win[i] = a.window[i];
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int gl = lane % G;
   const int fi = wave * (64 / G) + lane / G;
-  float2* buf = reinterpret_cast<float2*>(smem + Lo::OFF_BUF) + fi * Lo::BUF;
+  float* buf = reinterpret_cast<float*>(smem + Lo::OFF_BUF) + fi * Lo::BUF;
   const int t0 = mem * Lo::TF;  // this member's tile: frames [t0, t0 + TF)
   const int fa = t0 + 2 * fi;
   const long long ntask = (batch - q + Q - 1) / Q;  // shots q, q + Q, ... < batch
   const long long plane = (long long)a.F_out * a.T;
   const long long xbytes = a.x_stride * 4;
+  const double dcb = dc_lane_base<N>(a, gl);
 
-  PairSamples<N> nxt;
-  load_pair<N>(nxt, make_rsrc(a.x + q * a.x_stride, xbytes), a.hop, fa, a.T, gl);
-  float pvp[IB][2];
-#pragma unroll
-  for (int i = 0; i < IB; ++i) pvp[i][0] = pvp[i][1] = 0.f;
+  PairSamples<N> s0;
+  load_pair<N>(s0, make_rsrc(a.x + q * a.x_stride, xbytes), a.hop, fa, a.T, gl);
   __syncthreads();
 
-  for (long long it = 0; it <= ntask; ++it) {
+  // Per task: the tile's spectrum (next task's samples prefetched meanwhile), publish the
+  // tile's extremes, wait for the team's, store the normalised tile. No software
+  // pipelining across tasks: the other resident workgroups of the CU (Cfg::OCC) fill
+  // the waits.
+  for (long long it = 0; it < ntask; ++it) {
     const long long shot = q + it * Q;
-    const bool cur = it < ntask;
-    float pvc[IB][2];
+    const bool pf = it + 1 < ntask;
+    const __amdgpu_buffer_rsrc_t xn = make_rsrc(a.x + (pf ? shot + Q : shot) * a.x_stride, xbytes);
+    f2v pv[IB];
+    float dmin = INFINITY, dmax = -INFINITY;  // (pair_spectrum's running extremes: unused)
+    pair_spectrum<N>(a, s0, s0, s_tw, s_win, buf, gl, dcb, xn, fa, true, true, true, pv, dmin, dmax);
+    // the tile's extremes from the held values themselves (the v_min3/v_max3 running
+    // pair came out wrong in this kernel's schedule: measured on gfx950)
     float lmin = INFINITY, lmax = -INFINITY;
-    if (cur) {
-      const bool pf = it + 1 < ntask;
-      const __amdgpu_buffer_rsrc_t xn = make_rsrc(a.x + (pf ? shot + Q : shot) * a.x_stride, xbytes);
-      double dca, dcb;
-      fft_pair<N>(a, nxt, true, true, s_tw, s_win, s_dc, buf, gl, dca, dcb, xn, fa, pf);
-      float dmin = INFINITY, dmax = -INFINITY;  // (pair_psd's running extremes: unused)
-      pair_psd<N>(a, buf, gl, dca, dcb, true, true, pvc, dmin, dmax);
-      // the tile's extremes from the held values themselves (the v_min3/v_max3 running
-      // pair in pair_psd came out wrong in this kernel's schedule: measured on gfx950)
 #pragma unroll
-      for (int i = 0; i < IB; ++i) {
-        lmin = fminf(lmin, fminf(pvc[i][0], pvc[i][1]));
-        lmax = fmaxf(lmax, fmaxf(pvc[i][0], pvc[i][1]));
-      }
+    for (int i = 0; i < IB; ++i) {
+      lmin = fminf(lmin, fminf(pv[i].x, pv[i].y));
+      lmax = fmaxf(lmax, fmaxf(pv[i].x, pv[i].y));
     }
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
@@ -718,7 +806,7 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
       s_red[C::WAVES + wave] = lmax;
     }
     lds_barrier();  // s_red complete; every lane is done reading its FFT buffer
-    if (cur && tid == 0) {
+    if (tid == 0) {
       float mn = s_red[0], mx = s_red[C::WAVES];
 #pragma unroll
       for (int w = 1; w < C::WAVES; ++w) {
@@ -729,35 +817,24 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
           ((unsigned long long)(~f2key(mn)) << 32) | (unsigned long long)f2key(mx);
       __hip_atomic_store(gran + shot * M + mem, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (it > 0) {  // the previous task's tile: team extremes, normalise, store
-      const long long sp = shot - Q;
-      if (wave == 0) {
-        float mn, mx;
-        const bool done = team_minmax(gran + sp * M, M, lane, tmo, mn, mx,
-                                      (a.flags & STFT_DEV_GIVEUP) != 0);
-        if (lane == 0) {
-          s_red[2 * C::WAVES] = mn;
-          s_red[2 * C::WAVES + 1] = mx;
-          s_red[2 * C::WAVES + 2] = done ? 1.f : 0.f;
-          if (!done) tile_flag[sp * M + mem] = 1;  // raw tile: team_fixup_kernel finishes it
-        }
-      }
-      lds_barrier();
-      const float mn = s_red[2 * C::WAVES];
-      const float inv = 1.0f / (s_red[2 * C::WAVES + 1] - mn);  // max == min -> NaN (0/0)
-      const bool done = s_red[2 * C::WAVES + 2] != 0.f;
-      const __amdgpu_buffer_rsrc_t orr = make_rsrc(a.out + sp * plane, plane * 4);
-      tile_store<N>(a, s_tile, pvp, gl, fi, tid, orr, t0, mn, inv, done);
-    } else {
-      lds_barrier();  // s_red is rewritten by the next task only after thread 0 read it
-    }
-    if (cur) {
-#pragma unroll
-      for (int i = 0; i < IB; ++i) {
-        pvp[i][0] = pvc[i][0];
-        pvp[i][1] = pvc[i][1];
+    if (wave == 0) {
+      float mn = 0.f, mx = 1.f;
+      const bool done = (a.flags & STFT_DEV_NOWAIT) ||
+                        team_minmax(gran + shot * M, M, lane, tmo, mn, mx,
+                                    (a.flags & STFT_DEV_GIVEUP) != 0);
+      if (lane == 0) {
+        s_red[2 * C::WAVES] = mn;
+        s_red[2 * C::WAVES + 1] = mx;
+        s_red[2 * C::WAVES + 2] = done ? 1.f : 0.f;
+        if (!done) tile_flag[shot * M + mem] = 1;  // raw tile: team_fixup_kernel finishes it
       }
     }
+    lds_barrier();
+    const float mn = s_red[2 * C::WAVES];
+    const float inv = 1.0f / (s_red[2 * C::WAVES + 1] - mn);  // max == min -> NaN (0/0)
+    const bool done = s_red[2 * C::WAVES + 2] != 0.f;
+    const __amdgpu_buffer_rsrc_t orr = make_rsrc(a.out + shot * plane, plane * 4);
+    tile_store<N>(a, s_tile, pv, gl, fi, tid, orr, t0, mn, inv, done, false);
   }
 }
 
@@ -831,6 +908,8 @@ hipError_t launch_team(const StftArgs& a, long long batch, void* workspace, hipS
   if (cap[dev] < M) return hipSuccess;
   long long Q = cap[dev] / M;
   if (Q > batch) Q = batch;
+  const int xcd_teams = Q >= 8;
+  if (xcd_teams) Q &= ~7ll;  // Q / 8 teams per XCD
   // workspace: [timeout word, 16 B][granules: batch x M x 8 B][tile flags: batch x M B],
   // zeroed every call (specenh_stft_workspace_bytes sizes it for M = TEAM_MAX)
   unsigned* tmo = reinterpret_cast<unsigned*>(workspace);
@@ -841,7 +920,7 @@ hipError_t launch_team(const StftArgs& a, long long batch, void* workspace, hipS
   e = hipMemsetAsync(workspace, 0, zero, stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(stft_team_kernel<N>, dim3((unsigned)(Q * M)), dim3(Lo::THREADS), Lo::BYTES,
-                     stream, a, gran, batch, M, (int)Q, tmo, tflag);
+                     stream, a, gran, batch, M, (int)Q, tmo, tflag, xcd_teams);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(team_fixup_kernel, dim3(1024), dim3(256), 0, stream, a.out, a.F_out, a.T,
@@ -862,7 +941,7 @@ struct specenh_stft_plan {
   int device;
   float* d_window;
   float2* d_twiddle;
-  double* d_dc;
+  double dc_alpha, dc_beta;  // DC coefficients from the fp32 window (StftArgs)
 };
 
 extern "C" {
@@ -900,22 +979,20 @@ int specenh_stft_plan_create(specenh_stft_plan** plan, int nperseg, int noverlap
     s2 += window_host[i] * window_host[i];
     win[i] = float(window_host[i]);
   }
-  // DC coefficients c_n (fp64): the detrend folded into the window (see kernel).
-  std::vector<double> dc(N);
+  // DC coefficients c_n = w_n - alpha - beta (n - kmid) (fp64): the detrend folded into
+  // the window the kernel applies (the fp32 one), so c stays orthogonal to constants and
+  // ramps to fp64 precision (see pair_spectrum).
+  double dc_alpha = 0, dc_beta = 0;
   {
     const double kmid = 0.5 * (N - 1);
-    double sk2 = 0, swk = 0;
+    double sk2 = 0, swk = 0, sw = 0;
     for (int i = 0; i < N; ++i) {
       sk2 += (i - kmid) * (i - kmid);
-      swk += window_host[i] * (i - kmid);
+      swk += double(win[i]) * (i - kmid);
+      sw += double(win[i]);
     }
-    const double wbar = s1 / N;
-    for (int i = 0; i < N; ++i) {
-      double c = window_host[i];
-      if (detrend != SPECENH_DETREND_NONE) c -= wbar;
-      if (detrend == SPECENH_DETREND_LINEAR) c -= (i - kmid) * (swk / sk2);
-      dc[i] = c;
-    }
+    if (detrend != SPECENH_DETREND_NONE) dc_alpha = sw / N;
+    if (detrend == SPECENH_DETREND_LINEAR) dc_beta = swk / sk2;
   }
   std::vector<float2> tw;
   auto add_pass = [&](int R, int NS) {  // [r-1][k] = W_N^{r k N/(NS R)}
@@ -944,17 +1021,16 @@ int specenh_stft_plan_create(specenh_stft_plan** plan, int nperseg, int noverlap
   p->scaling = scaling;
   p->detrend = detrend;
   p->scale = scaling == SPECENH_SCALING_DENSITY ? 1.0 / (fs * s2) : 1.0 / (s1 * s1);
+  p->dc_alpha = dc_alpha;
+  p->dc_beta = dc_beta;
   hipError_t e = hipGetDevice(&p->device);
   if (e == hipSuccess) e = hipMalloc(&p->d_window, N * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&p->d_twiddle, tw.size() * sizeof(float2));
-  if (e == hipSuccess) e = hipMalloc(&p->d_dc, N * sizeof(double));
-  if (e == hipSuccess) e = hipMemcpy(p->d_dc, dc.data(), N * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_window, win.data(), N * sizeof(float), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_twiddle, tw.data(), tw.size() * sizeof(float2), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     (void)hipFree(p->d_window);
     (void)hipFree(p->d_twiddle);
-    (void)hipFree(p->d_dc);
     delete p;
     return set_error(SPECENH_EHIP, std::string("plan allocation: ") + hipGetErrorString(e));
   }
@@ -966,7 +1042,6 @@ int specenh_stft_plan_destroy(specenh_stft_plan* plan) {
   if (!plan) return SPECENH_OK;
   (void)hipFree(plan->d_window);
   (void)hipFree(plan->d_twiddle);
-  (void)hipFree(plan->d_dc);
   delete plan;
   return SPECENH_OK;
 }
@@ -989,6 +1064,8 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
   if (T < 0) return (int)T;
   if (x_stride < length) return set_error(SPECENH_EINVAL, "x_stride < length");
   if (T > (1ll << 30)) return set_error(SPECENH_EINVAL, "too many frames");
+  if ((long long)(N / 2 + 1) * T * 4 >= (1ll << 30))
+    return set_error(SPECENH_EUNSUPPORTED, "one spectrogram must stay below 1 GiB");
   hipStream_t st = (hipStream_t)stream;
   StftArgs a{};
   a.x = x;
@@ -1004,7 +1081,8 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
   a.F_out = (flags & SPECENH_STFT_DROP_NYQUIST) ? N / 2 : N / 2 + 1;
   a.window = plan->d_window;
   a.twiddle = plan->d_twiddle;
-  a.dc_coef = plan->d_dc;
+  a.dc_alpha = plan->dc_alpha;
+  a.dc_beta = plan->dc_beta;
   const long long F_out = a.F_out;
   // team schedule for large spectrograms (C2: 518 KB each); small ones (C5: 64 KB) are
   // re-read from L2 by the sweep for less than the team's hand-off costs (measured)
@@ -1059,6 +1137,8 @@ int specenh_stft_psd_f16(const specenh_stft_plan* plan, const void* x, long long
   if (T < 0) return (int)T;
   if (x_stride < length) return set_error(SPECENH_EINVAL, "x_stride < length");
   if (T > (1ll << 30)) return set_error(SPECENH_EINVAL, "too many frames");
+  if ((long long)(N / 2 + 1) * T * 4 >= (1ll << 30))
+    return set_error(SPECENH_EUNSUPPORTED, "one spectrogram must stay below 1 GiB");
   if (N > 1024) return set_error(SPECENH_EUNSUPPORTED, "fp16 samples need nperseg <= 1024");
   StftArgs a{};
   a.x = reinterpret_cast<const float*>(x);  // reinterpreted as fp16 by stft_psd_kernel<N, true>
@@ -1073,7 +1153,8 @@ int specenh_stft_psd_f16(const specenh_stft_plan* plan, const void* x, long long
   a.F_out = (flags & SPECENH_STFT_DROP_NYQUIST) ? N / 2 : N / 2 + 1;
   a.window = plan->d_window;
   a.twiddle = plan->d_twiddle;
-  a.dc_coef = plan->d_dc;
+  a.dc_alpha = plan->dc_alpha;
+  a.dc_beta = plan->dc_beta;
   hipStream_t st = (hipStream_t)stream;
   const long long F_out = a.F_out;
   for (long long b0 = 0; b0 < batch; b0 += 1 << 30) {

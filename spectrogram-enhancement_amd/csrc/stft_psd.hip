@@ -34,6 +34,13 @@
 
 #include "fft_common.hpp"
 
+#ifndef SPECENH_C1024_WAVES
+#define SPECENH_C1024_WAVES 4
+#define SPECENH_C1024_OCC 3
+#endif
+#ifndef SPECENH_STFT_PF_AFTER_WAIT
+#define SPECENH_STFT_PF_AFTER_WAIT 1
+#endif
 #ifndef SPECENH_STFT_PF_EARLY
 #define SPECENH_STFT_PF_EARLY 0
 #endif
@@ -42,6 +49,8 @@
 // Development-only flag bit (not part of the public header): skip the output store,
 // to separate compute from store cost when profiling.
 #define SPECENH_STFT_DEV_NOSTORE (1 << 16)
+// Profiling only: every prefetch re-reads frames 0-1 of its shot (L2 hits, no HBM reads).
+#define SPECENH_STFT_DEV_NOLOAD (1 << 21)
 
 namespace specenh {
 
@@ -77,6 +86,7 @@ struct StftArgs {
   // c_n = w_n - dc_alpha - dc_beta (n - (N-1)/2), w the fp32 window (see pair_spectrum)
   double dc_alpha;
   double dc_beta;
+  const double* dc_coef;  // the same c_n as a table (fp64), staged in LDS when it fits
 };
 
 // Per-N decomposition: G lanes per FFT, WAVES per workgroup, Stockham radices.
@@ -91,7 +101,7 @@ template <> struct Cfg<64>   { static constexpr int G = 8,  WAVES = 8, OCC = 1, 
 template <> struct Cfg<128>  { static constexpr int G = 8,  WAVES = 8, OCC = 1, R1 = 16, R2 = 8,  R3 = 1, PF = 1; };
 template <> struct Cfg<256>  { static constexpr int G = 16, WAVES = 8, OCC = 1, R1 = 16, R2 = 16, R3 = 1, PF = 1; };
 template <> struct Cfg<512>  { static constexpr int G = 16, WAVES = 8, OCC = 1, R1 = 32, R2 = 16, R3 = 1, PF = 1; };
-template <> struct Cfg<1024> { static constexpr int G = 32, WAVES = 4, OCC = 3, R1 = 32, R2 = 32, R3 = 1, PF = 1; };
+template <> struct Cfg<1024> { static constexpr int G = 32, WAVES = SPECENH_C1024_WAVES, OCC = SPECENH_C1024_OCC, R1 = 32, R2 = 32, R3 = 1, PF = 1; };
 template <> struct Cfg<2048> { static constexpr int G = 64, WAVES = 4, OCC = 1, R1 = 32, R2 = 8,  R3 = 8, PF = 1; };
 template <> struct Cfg<4096> { static constexpr int G = 64, WAVES = 2, OCC = 1, R1 = 32, R2 = 16, R3 = 8, PF = 0; };
 
@@ -107,6 +117,7 @@ struct TwOff {
 };
 
 constexpr int align16(int b) { return (b + 15) / 16 * 16; }
+constexpr int lds_granules(int b) { return (b + 2047) / 2048 * 2048; }
 
 template <int N>
 struct Layout {
@@ -117,7 +128,13 @@ struct Layout {
   static constexpr int FFTS = C::WAVES * (64 / G);  // concurrent FFTs per workgroup
   static constexpr int TF = 2 * FFTS;                // frames per tile (power of two)
   static constexpr int LOG_TF = ilog2(TF);
-  static constexpr int TS = TF + 1;                  // tile row stride (odd: conflict-free)
+  // Tile rows: odd stride TF + 1 (conflict-free 4-B writes), or for G = 32 unpadded
+  // (TS = TF) with an XOR swizzle of the frame index, element (k, f) at
+  // k TS + (f ^ swz(k)), swz(k) = ((k / (64/TF)) & (TF/2 - 1)) << 1: each lane's two
+  // frames go out as one 8-B write, writes (rows gl + 32 i) and row reads (64/TF rows x
+  // TF frames per wave) are conflict-free, and the tile is no larger than the FFT buffers.
+  static constexpr bool TILE_SWZ = G == 32 && (TF == 16 || TF == 32);
+  static constexpr int TS = TILE_SWZ ? TF : TF + 1;
   static constexpr int NBINS = N / 2 + 1;
   static constexpr int IB = (NBINS + G - 1) / G;     // bins per lane in the epilogue
   // per-FFT exchange buffer: N padded FLOATS (real and imaginary parts take turns)
@@ -125,21 +142,37 @@ struct Layout {
   static constexpr int BUF_BYTES = FFTS * BUF * 4;
   static constexpr int TILE_BYTES = NBINS * TS * 4;  // aliases the FFT buffers
   static constexpr int TWN = TwOff<N>::TOTAL;
+  // + 16 B: the mirror read of lane 0 (see pair_spectrum) may touch one float past the
+  // last FFT buffer
+  static constexpr int REGION = align16((BUF_BYTES > TILE_BYTES ? BUF_BYTES : TILE_BYTES) + 16);
+  static constexpr int RED_BYTES = 4 * C::WAVES * 4;  // [2*WAVES] + team {mn, mx, done}
+  static constexpr int BASE_BYTES = align16(TWN * 8) + align16(N * 4) + REGION + RED_BYTES;
+  // the fp64 DC coefficient table goes to LDS when OCC workgroups still fit with it;
+  // otherwise pair_spectrum forms the coefficients from the window (3 more fp64 ops/sample)
+  // (budget in 2-KB allocation granules: a table that only fits to the byte cost one
+  // resident workgroup per CU when measured, 1.44 -> 1.79 ms at C2)
+  static constexpr bool DC_TABLE = lds_granules(BASE_BYTES + N * 8) * C::OCC <= 160 * 1024;
   // byte offsets into dynamic LDS (all multiples of 16)
   static constexpr int OFF_TW = 0;
   static constexpr int OFF_WIN = OFF_TW + align16(TWN * 8);
-  static constexpr int OFF_BUF = OFF_WIN + align16(N * 4);
-  // + 16 B: the mirror read of lane 0 (see pair_spectrum) may touch one float past the
-  // last FFT buffer
-  static constexpr int OFF_RED = OFF_BUF + align16((BUF_BYTES > TILE_BYTES ? BUF_BYTES : TILE_BYTES) + 16);
-  static constexpr int BYTES = OFF_RED + 4 * C::WAVES * 4;  // [2*WAVES] + team {mn, mx, done}
-  static_assert(BYTES * C::OCC <= 160 * 1024, "LDS budget");
+  static constexpr int OFF_DC = OFF_WIN + align16(N * 4);
+  static constexpr int OFF_BUF = OFF_DC + (DC_TABLE ? N * 8 : 0);
+  static constexpr int OFF_RED = OFF_BUF + REGION;
+  static constexpr int BYTES = OFF_RED + RED_BYTES;
+  static_assert(lds_granules(BYTES) * C::OCC <= 160 * 1024, "LDS budget");
   static_assert(C::R1 * C::R2 * C::R3 == N, "radix product");
   static_assert((TF & (TF - 1)) == 0, "tile width must be a power of two");
   static_assert(4 * C::WAVES >= 2 * C::WAVES + 3, "reduction scratch");
 };
 
 __device__ __forceinline__ int pad(int e) { return e + (e >> 5); }
+
+template <int N>
+__device__ __forceinline__ int tile_swz(int k) {
+  using Lo = Layout<N>;
+  if constexpr (Lo::TILE_SWZ) return ((k / (64 / Lo::TF)) & (Lo::TF / 2 - 1)) << 1;
+  return 0;
+}
 
 // min/max of three floats as one instruction each (plain fminf/fmaxf get NaN-quieting
 // canonicalisation v_max ops on every operand). Operands are finite here or NaN only
@@ -281,19 +314,26 @@ __device__ __forceinline__ void load_pair(PairSamples<N>& s, __amdgpu_buffer_rsr
   // they cannot move the min/max and need no masking; they are never stored.
   const int oa = ((fa < T ? fa : T - 1) * hop + gl) * ES;
   const int ob = ((fa + 1 < T ? fa + 1 : T - 1) * hop + gl) * ES;
+  // The per-register offset o goes in the scalar soffset operand (an SGPR constant): as a
+  // VGPR add it would cost one VALU op per load (the compiler does not fold it into the
+  // instruction's immediate offset).
+  // (opaque base: the N/G constants are re-formed by SALU adds here rather than hoisted
+  // out of the tile loop into N/G live SGPRs)
+  int sbase = 0;
+  asm volatile("" : "+s"(sbase));
 #pragma unroll
   for (int i = 0; i < PairSamples<N>::BPL1; ++i)
 #pragma unroll
     for (int r = 0; r < PairSamples<N>::R1; ++r) {
-      const int o = (i * G + r * NB1) * ES;
+      const int o = sbase + (i * G + r * NB1) * ES;
       if constexpr (XH) {
-        const unsigned short ha = __builtin_amdgcn_raw_buffer_load_b16(xr, oa + o, 0, 0);
-        const unsigned short hb = __builtin_amdgcn_raw_buffer_load_b16(xr, ob + o, 0, 0);
+        const unsigned short ha = __builtin_amdgcn_raw_buffer_load_b16(xr, oa, o, 0);
+        const unsigned short hb = __builtin_amdgcn_raw_buffer_load_b16(xr, ob, o, 0);
         s.x[i][r] = f2v{(float)__builtin_bit_cast(_Float16, ha),
                         (float)__builtin_bit_cast(_Float16, hb)};
       } else {
-        s.x[i][r] = f2v{__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, oa + o, 0, 0)),
-                        __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ob + o, 0, 0))};
+        s.x[i][r] = f2v{__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, oa, o, 0)),
+                        __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ob, o, 0))};
       }
     }
 }
@@ -306,7 +346,8 @@ __device__ __forceinline__ void load_pair(PairSamples<N>& s, __amdgpu_buffer_rsr
 template <int N, bool XH = false>
 __device__ __forceinline__ void pair_spectrum(const StftArgs& a, const PairSamples<N>& in,
                                               PairSamples<N>& nxt, const f2v* s_tw,
-                                              const float* s_win, float* buf, int gl,
+                                              const float* s_win, const double* s_dc,
+                                              float* buf, int gl,
                                               double dc_base, __amdgpu_buffer_rsrc_t xr,
                                               int fa_next, bool prefetch, bool want_log,
                                               bool log2_out, f2v (&pv)[Layout<N>::IB],
@@ -328,8 +369,9 @@ __device__ __forceinline__ void pair_spectrum(const StftArgs& a, const PairSampl
   // in the coefficients, not in the data). After detrending X_0 is tiny by construction;
   // in fp32 it would sit at the rounding floor eps*||w y|| and, being the usual
   // spectrogram minimum under 'spectrum' scaling, would shift every normalised value.
-  // c_n = (w_n - dc_base) - beta * j is formed here from the fp32 window (dc_base =
-  // alpha + beta * (gl - kmid) per lane): no coefficient table in LDS.
+  // c_n comes from the LDS table (Layout::DC_TABLE) or is formed here from the fp32
+  // window as c_n = (w_n - dc_base) - beta * j (dc_base = alpha + beta * (gl - kmid) per
+  // lane); both are the same fp64 coefficients up to fp64 rounding.
   f2v s0 = {0.f, 0.f}, s1 = {0.f, 0.f};  // per frame (a, b): sum x, sum j x
   // 4 independent fp64 partial sums per frame: a single chain of R1 dependent
   // v_fma_f64 would be latency-bound.
@@ -344,7 +386,11 @@ __device__ __forceinline__ void pair_spectrum(const StftArgs& a, const PairSampl
       const f2v xv = in.x[i][r];
       s0 += xv;
       s1 = __builtin_elementwise_fma(f2v{float(j), float(j)}, xv, s1);
-      const double c = __builtin_fma(-a.dc_beta, double(j), (double)win[j] - dc_base);
+      double c;
+      if constexpr (Lo::DC_TABLE)
+        c = s_dc[gl + j];
+      else
+        c = __builtin_fma(-a.dc_beta, double(j), (double)win[j] - dc_base);
       dc_fma(pda[(i * R1 + r) % NDC], xv.x, c);
       dc_fma(pdb[(i * R1 + r) % NDC], xv.y, c);
       if ((i * R1 + r) % 8 == 7) __builtin_amdgcn_sched_barrier(0);
@@ -394,7 +440,8 @@ __device__ __forceinline__ void pair_spectrum(const StftArgs& a, const PairSampl
   // `nxt` is `in`. Past the last tile the clamped frames / repeated shot are re-read.
   auto issue_prefetch = [&]() {  // fences keep the loads after the FFT's reads of `in`
     __builtin_amdgcn_sched_barrier(0);
-    if (prefetch) load_pair<N, XH>(nxt, xr, a.hop, fa_next, a.T, gl);
+    if (prefetch)
+      load_pair<N, XH>(nxt, xr, a.hop, (a.flags & SPECENH_STFT_DEV_NOLOAD) ? 0 : fa_next, a.T, gl);
     __builtin_amdgcn_sched_barrier(0);
   };
   // ---- Stockham passes 2 (and 3) ----
@@ -494,69 +541,99 @@ __device__ __forceinline__ void pair_spectrum(const StftArgs& a, const PairSampl
   }
 }
 
-// The workgroup's (bins x TF frames) tile through LDS (it aliases the FFT buffers) and out
-// as frequency-row segments out[k][t0 : t0 + tfv]; with `norm` each value is rescaled
-// (v - mn) * inv on the way. Ends with a workgroup LDS barrier; starts with one unless
-// the caller has just passed one after every wave finished reading its FFT buffer.
+// The workgroup's (bins x TF frames) tile through LDS (it aliases the FFT buffers): each
+// lane group writes its bins for its two frames (raw, or rescaled (v - mn) * inv with
+// `norm`); no barriers here.
 template <int N>
-__device__ __forceinline__ void tile_store(const StftArgs& a, float* s_tile,
-                                           const f2v (&pv)[Layout<N>::IB], int gl, int fi,
-                                           int tid, __amdgpu_buffer_rsrc_t orr, int t0, float mn,
-                                           float inv, bool norm, bool lead_barrier = true) {
+__device__ __forceinline__ void tile_write(float* s_tile, const f2v (&pv)[Layout<N>::IB], int gl,
+                                           int fi, float mn, float inv, bool norm) {
   using Lo = Layout<N>;
   constexpr int G = Cfg<N>::G;
   constexpr int IB = Lo::IB;
-  if (lead_barrier) lds_barrier();  // every group is done with its FFT buffer: reuse as the tile
   const int fl = 2 * fi;
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
     const int k = gl + i * G;
     if (k < Lo::NBINS) {
       const f2v t = norm ? (pv[i] - mn) * inv : pv[i];
-      s_tile[k * Lo::TS + fl] = t.x;
-      s_tile[k * Lo::TS + fl + 1] = t.y;
-    }
-  }
-  lds_barrier();
-  // ---- store frequency-row segments: out[shot][k][t0 : t0+tfv] ----
-  // Branch-free: rows k >= F_out land past the end of the shot's buffer descriptor
-  // (num_records = F_out * T * 4) and frames past T get an offset beyond it, so the
-  // hardware drops exactly those stores (the host keeps a plane below 2^30 bytes).
-  // Compile-time trip count: the compiler can then count these stores in its partial
-  // vmcnt waits for the prefetched samples instead of draining everything.
-  const int tfv = min(Lo::TF, a.T - t0);
-  if (!(a.flags & SPECENH_STFT_DEV_NOSTORE)) {
-    constexpr int ST = (Lo::NBINS * Lo::TF + Lo::THREADS - 1) / Lo::THREADS;
-    constexpr int ROWS_PER_IT = Lo::THREADS >> Lo::LOG_TF;
-    constexpr int GRP = 12;  // LDS reads issued ahead of their stores
-    const int k0 = tid >> Lo::LOG_TF;
-    const int f = tid & (Lo::TF - 1);
-    // one VGPR offset for all stores of this tile; the row step is a scalar soffset
-    const int voff = f < tfv ? (k0 * a.T + t0 + f) * 4 : (1 << 30);
-    const int sstep = ROWS_PER_IT * a.T * 4;
-    const float* src = s_tile + k0 * Lo::TS + f;
-#pragma unroll
-    for (int g0 = 0; g0 < ST; g0 += GRP) {
-      float v[GRP];
-#pragma unroll
-      for (int u = 0; u < GRP; ++u) {
-        const int it = g0 + u;
-        if (it < ST && it * ROWS_PER_IT < Lo::NBINS) {
-          if ((it + 1) * ROWS_PER_IT <= Lo::NBINS)
-            v[u] = src[it * ROWS_PER_IT * Lo::TS];
-          else  // last, partial row group: rows past the tile re-read its last row (their
-                // stores fall past the descriptor's end anyway)
-            v[u] = s_tile[min(k0 + it * ROWS_PER_IT, Lo::NBINS - 1) * Lo::TS + f];
-        }
+      if constexpr (Lo::TILE_SWZ) {
+        *reinterpret_cast<f2v*>(s_tile + k * Lo::TS + (fl ^ tile_swz<N>(k))) = t;
+      } else {
+        s_tile[k * Lo::TS + fl] = t.x;
+        s_tile[k * Lo::TS + fl + 1] = t.y;
       }
-#pragma unroll
-      for (int u = 0; u < GRP; ++u)
-        if (g0 + u < ST && (g0 + u) * ROWS_PER_IT < Lo::NBINS)
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[u]), orr, voff,
-                                                (g0 + u) * sstep, 0);
     }
   }
-  lds_barrier();  // tile (= FFT buffers) free for the next tile's FFTs
+}
+
+// The tile out as frequency-row segments out[k][t0 : t0 + tfv]; with `norm` each value is
+// rescaled (v - mn) * inv on the way (the same arithmetic as tile_write's). No barriers.
+// Branch-free: rows k >= F_out land past the end of the shot's buffer descriptor
+// (num_records = F_out * T * 4) and frames past T get an offset beyond it, so the
+// hardware drops exactly those stores (the host keeps a plane below 2^30 bytes).
+// Compile-time trip count: the compiler can then count these stores in its partial
+// vmcnt waits for the prefetched samples instead of draining everything.
+template <int N>
+__device__ __forceinline__ void tile_emit(const StftArgs& a, const float* s_tile, int tid,
+                                          __amdgpu_buffer_rsrc_t orr, int t0, float mn, float inv,
+                                          bool norm) {
+  using Lo = Layout<N>;
+  const int tfv = min(Lo::TF, a.T - t0);
+  if (a.flags & SPECENH_STFT_DEV_NOSTORE) return;
+  constexpr int ST = (Lo::NBINS * Lo::TF + Lo::THREADS - 1) / Lo::THREADS;
+  constexpr int ROWS_PER_IT = Lo::THREADS >> Lo::LOG_TF;
+  constexpr int GRP = 12;  // LDS reads issued ahead of their stores
+  const int k0 = tid >> Lo::LOG_TF;
+  const int f = tid & (Lo::TF - 1);
+  // one VGPR offset for all stores of this tile; the row step is a scalar soffset
+  const int voff = f < tfv ? (k0 * a.T + t0 + f) * 4 : (1 << 30);
+  const int sstep = ROWS_PER_IT * a.T * 4;
+  // With the swizzled tile, rows k0 + it * ROWS_PER_IT take two swizzle values that
+  // alternate with `it` (the row step moves the swizzle key by half its range).
+  constexpr int SWZ_STEP =
+      Lo::TILE_SWZ ? ((ROWS_PER_IT / (64 / Lo::TF)) & (Lo::TF / 2 - 1)) << 1 : 0;
+  static_assert(!Lo::TILE_SWZ || ((2 * (ROWS_PER_IT / (64 / Lo::TF))) % (Lo::TF / 2)) == 0,
+                "swizzle must alternate over row groups");
+  const float* src0 = s_tile + k0 * Lo::TS + (f ^ tile_swz<N>(k0));
+  const float* src1 = s_tile + k0 * Lo::TS + (f ^ (tile_swz<N>(k0) ^ SWZ_STEP));
+#pragma unroll
+  for (int g0 = 0; g0 < ST; g0 += GRP) {
+    float v[GRP];
+#pragma unroll
+    for (int u = 0; u < GRP; ++u) {
+      const int it = g0 + u;
+      if (it < ST && it * ROWS_PER_IT < Lo::NBINS) {
+        if ((it + 1) * ROWS_PER_IT <= Lo::NBINS) {
+          v[u] = ((it & 1) ? src1 : src0)[it * ROWS_PER_IT * Lo::TS];
+        } else {  // last, partial row group: rows past the tile re-read its last row (their
+                  // stores fall past the descriptor's end anyway)
+          const int k = min(k0 + it * ROWS_PER_IT, Lo::NBINS - 1);
+          v[u] = s_tile[k * Lo::TS + (f ^ tile_swz<N>(k))];
+        }
+        if (norm) v[u] = (v[u] - mn) * inv;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < GRP; ++u)
+      if (g0 + u < ST && (g0 + u) * ROWS_PER_IT < Lo::NBINS)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[u]), orr, voff, (g0 + u) * sstep,
+                                              0);
+  }
+}
+
+// tile_write + tile_emit between workgroup LDS barriers: starts with one (every group is
+// done with its FFT buffer) unless the caller has just passed one, ends with one (the
+// tile = FFT buffers free for the next tile's FFTs).
+template <int N>
+__device__ __forceinline__ void tile_store(const StftArgs& a, float* s_tile,
+                                           const f2v (&pv)[Layout<N>::IB], int gl, int fi,
+                                           int tid, __amdgpu_buffer_rsrc_t orr, int t0, float mn,
+                                           float inv, bool norm, bool lead_barrier = true) {
+  if (lead_barrier) lds_barrier();
+  tile_write<N>(s_tile, pv, gl, fi, mn, inv, norm);
+  lds_barrier();
+  tile_emit<N>(a, s_tile, tid, orr, t0, 0.f, 1.f, false);
+  lds_barrier();
 }
 
 // Per-lane base of the DC coefficients: alpha + beta * (gl - (N-1)/2).
@@ -590,6 +667,9 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
   const long long shot = blockIdx.x;
   for (int i = tid; i < Lo::TWN; i += Lo::THREADS) s_tw[i] = f2v{a.twiddle[i].x, a.twiddle[i].y};
   for (int i = tid; i < N; i += Lo::THREADS) s_win[i] = a.window[i];
+  double* s_dc = reinterpret_cast<double*>(smem + Lo::OFF_DC);
+  if constexpr (Lo::DC_TABLE)
+    for (int i = tid; i < N; i += Lo::THREADS) s_dc[i] = a.dc_coef[i];
 
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -616,7 +696,7 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
     const int fa = t0 + 2 * fi;  // tail frames are clamped duplicates (load_pair)
     if constexpr (!C::PF) load_pair<N, XH>(s0, xr, a.hop, fa, a.T, gl);
     f2v pv[IB];
-    pair_spectrum<N, XH>(a, s0, s0, s_tw, s_win, buf, gl, dcb, xr, fa + Lo::TF, C::PF != 0,
+    pair_spectrum<N, XH>(a, s0, s0, s_tw, s_win, s_dc, buf, gl, dcb, xr, fa + Lo::TF, C::PF != 0,
                          want_log, log2_out, pv, lmin, lmax);
     tile_store<N>(a, s_tile, pv, gl, fi, tid, orr, t0, 0.f, 1.f, false);
   }
@@ -712,7 +792,9 @@ __device__ __forceinline__ bool team_minmax(const unsigned long long* g, int M, 
     complete = false;
   }
   for (unsigned spins = 0; complete; ++spins) {
-    if (lane < M) v = __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int ln = lane;  // opaque: the per-lane 64-bit address is re-formed here each poll
+    asm volatile("" : "+v"(ln));  // instead of being hoisted out of the task loop (spilled)
+    if (lane < M) v = __hip_atomic_load(g + ln, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool ok = lane >= M || ((unsigned)v != 0u && (unsigned)(v >> 32) != 0u);
     if (__all(ok)) break;
     if (spins >= (1u << 20) ||
@@ -735,7 +817,9 @@ __device__ __forceinline__ bool team_minmax(const unsigned long long* g, int M, 
   return complete;
 }
 
-template <int N>
+// MODE (compile time, so each schedule keeps its own register allocation): 0 = plain
+// PSD, 1 = log PSD (independent tiles: no granules, no waits), 2 = NORMALIZE (teams).
+template <int N, int MODE>
 __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_kernel(
     StftArgs a, unsigned long long* gran, long long batch, int M, int Q, unsigned* tmo,
     unsigned char* tile_flag, int xcd_teams) {
@@ -761,6 +845,9 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
   const int mem = s8 - (s8 / M) * M;
   for (int i = tid; i < Lo::TWN; i += Lo::THREADS) s_tw[i] = f2v{a.twiddle[i].x, a.twiddle[i].y};
   for (int i = tid; i < N; i += Lo::THREADS) s_win[i] = a.window[i];
+  double* s_dc = reinterpret_cast<double*>(smem + Lo::OFF_DC);
+  if constexpr (Lo::DC_TABLE)
+    for (int i = tid; i < N; i += Lo::THREADS) s_dc[i] = a.dc_coef[i];
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int gl = lane % G;
@@ -772,6 +859,10 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
   const long long plane = (long long)a.F_out * a.T;
   const long long xbytes = a.x_stride * 4;
   const double dcb = dc_lane_base<N>(a, gl);
+  // Without NORMALIZE the tiles are independent: the same persistent tile-parallel
+  // schedule, no granules and no waits (log or plain PSD values stored as computed).
+  constexpr bool normalize = MODE == 2;
+  constexpr bool want_log = MODE >= 1;
 
   PairSamples<N> s0;
   load_pair<N>(s0, make_rsrc(a.x + q * a.x_stride, xbytes), a.hop, fa, a.T, gl);
@@ -787,7 +878,17 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
     const __amdgpu_buffer_rsrc_t xn = make_rsrc(a.x + (pf ? shot + Q : shot) * a.x_stride, xbytes);
     f2v pv[IB];
     float dmin = INFINITY, dmax = -INFINITY;  // (pair_spectrum's running extremes: unused)
-    pair_spectrum<N>(a, s0, s0, s_tw, s_win, buf, gl, dcb, xn, fa, true, true, true, pv, dmin, dmax);
+    // NORMALIZE: the next task's samples are requested after the team wait, not inside
+    // pair_spectrum: vmcnt is in order, so the wave polling the granules would otherwise
+    // first wait for its whole prefetch to land while the workgroup idles at the barrier
+    constexpr bool pf_inside = !normalize || !SPECENH_STFT_PF_AFTER_WAIT;
+    pair_spectrum<N>(a, s0, s0, s_tw, s_win, s_dc, buf, gl, dcb, xn, fa, pf_inside, want_log, normalize,
+                     pv, dmin, dmax);
+    const __amdgpu_buffer_rsrc_t orr = make_rsrc(a.out + shot * plane, plane * 4);
+    if constexpr (!normalize) {
+      tile_store<N>(a, s_tile, pv, gl, fi, tid, orr, t0, 0.f, 1.f, false);
+      continue;
+    }
     // the tile's extremes from the held values themselves (the v_min3/v_max3 running
     // pair came out wrong in this kernel's schedule: measured on gfx950)
     float lmin = INFINITY, lmax = -INFINITY;
@@ -806,6 +907,8 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
       s_red[C::WAVES + wave] = lmax;
     }
     lds_barrier();  // s_red complete; every lane is done reading its FFT buffer
+    // the raw tile goes to LDS now (normalised on its way out), overlapping the team wait
+    tile_write<N>(s_tile, pv, gl, fi, 0.f, 1.f, false);
     if (tid == 0) {
       float mn = s_red[0], mx = s_red[C::WAVES];
 #pragma unroll
@@ -830,11 +933,16 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
       }
     }
     lds_barrier();
+    if constexpr (!pf_inside) {
+      __builtin_amdgcn_sched_barrier(0);
+      load_pair<N>(s0, xn, a.hop, (a.flags & SPECENH_STFT_DEV_NOLOAD) ? 0 : fa, a.T, gl);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     const float mn = s_red[2 * C::WAVES];
     const float inv = 1.0f / (s_red[2 * C::WAVES + 1] - mn);  // max == min -> NaN (0/0)
     const bool done = s_red[2 * C::WAVES + 2] != 0.f;
-    const __amdgpu_buffer_rsrc_t orr = make_rsrc(a.out + shot * plane, plane * 4);
-    tile_store<N>(a, s_tile, pv, gl, fi, tid, orr, t0, mn, inv, done, false);
+    tile_emit<N>(a, s_tile, tid, orr, t0, mn, inv, done);
+    lds_barrier();  // tile (= FFT buffers) free for the next task's FFTs
   }
 }
 
@@ -870,9 +978,9 @@ __global__ __launch_bounds__(256) void team_fixup_kernel(float* out, int F_out, 
 
 // Launch the team schedule when it applies (NORMALIZE, workspace given, team size <=
 // TEAM_MAX and <= the resident capacity). *launched = false: the caller falls back.
-template <int N>
-hipError_t launch_team(const StftArgs& a, long long batch, void* workspace, hipStream_t stream,
-                       bool* launched) {
+template <int N, int MODE>
+hipError_t launch_team_mode(const StftArgs& a, long long batch, void* workspace, hipStream_t stream,
+                            bool* launched) {
   using Lo = Layout<N>;
   *launched = false;
   const int M = (a.T + Lo::TF - 1) / Lo::TF;
@@ -883,11 +991,11 @@ hipError_t launch_team(const StftArgs& a, long long batch, void* workspace, hipS
   if (e != hipSuccess) return e;
   if (dev < 0 || dev >= 64) return hipSuccess;
   if (cap[dev] == 0) {
-    e = hipFuncSetAttribute((const void*)stft_team_kernel<N>,
+    e = hipFuncSetAttribute((const void*)stft_team_kernel<N, MODE>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, Lo::BYTES);
     if (e != hipSuccess) return e;
     int per_cu = 0, cus = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)stft_team_kernel<N>,
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)stft_team_kernel<N, MODE>,
                                                      Lo::THREADS, Lo::BYTES);
     if (e != hipSuccess) return e;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -896,7 +1004,7 @@ hipError_t launch_team(const StftArgs& a, long long batch, void* workspace, hipS
     // here): bound it by the register file (512 VGPR+AGPR per lane and SIMD, 8-register
     // granules, 4 SIMDs per CU) and by LDS as well
     hipFuncAttributes fa{};
-    e = hipFuncGetAttributes(&fa, (const void*)stft_team_kernel<N>);
+    e = hipFuncGetAttributes(&fa, (const void*)stft_team_kernel<N, MODE>);
     if (e != hipSuccess) return e;
     const int regs = ((fa.numRegs + 7) / 8) * 8;
     const int waves_per_simd = regs > 0 ? std::min(8, 512 / regs) : 8;
@@ -910,24 +1018,41 @@ hipError_t launch_team(const StftArgs& a, long long batch, void* workspace, hipS
   if (Q > batch) Q = batch;
   const int xcd_teams = Q >= 8;
   if (xcd_teams) Q &= ~7ll;  // Q / 8 teams per XCD
-  // workspace: [timeout word, 16 B][granules: batch x M x 8 B][tile flags: batch x M B],
-  // zeroed every call (specenh_stft_workspace_bytes sizes it for M = TEAM_MAX)
-  unsigned* tmo = reinterpret_cast<unsigned*>(workspace);
-  unsigned long long* gran =
-      reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + 16);
-  unsigned char* tflag = reinterpret_cast<unsigned char*>(gran + (size_t)batch * M);
-  const size_t zero = 16 + (size_t)batch * M * 9;
-  e = hipMemsetAsync(workspace, 0, zero, stream);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(stft_team_kernel<N>, dim3((unsigned)(Q * M)), dim3(Lo::THREADS), Lo::BYTES,
+  constexpr bool normalize = MODE == 2;
+  unsigned* tmo = nullptr;
+  unsigned long long* gran = nullptr;
+  unsigned char* tflag = nullptr;
+  if constexpr (normalize) {
+    // workspace: [timeout word, 16 B][granules: batch x M x 8 B][tile flags: batch x M B],
+    // zeroed every call (specenh_stft_workspace_bytes sizes it for M = TEAM_MAX)
+    tmo = reinterpret_cast<unsigned*>(workspace);
+    gran = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + 16);
+    tflag = reinterpret_cast<unsigned char*>(gran + (size_t)batch * M);
+    const size_t zero = 16 + (size_t)batch * M * 9;
+    e = hipMemsetAsync(workspace, 0, zero, stream);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((stft_team_kernel<N, MODE>), dim3((unsigned)(Q * M)), dim3(Lo::THREADS), Lo::BYTES,
                      stream, a, gran, batch, M, (int)Q, tmo, tflag, xcd_teams);
   e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || !normalize) {
+    *launched = e == hipSuccess;
+    return e;
+  }
   hipLaunchKernelGGL(team_fixup_kernel, dim3(1024), dim3(256), 0, stream, a.out, a.F_out, a.T,
                      Lo::TF, gran, tflag, batch, M, tmo);
   e = hipGetLastError();
   *launched = e == hipSuccess;
   return e;
+}
+
+template <int N>
+hipError_t launch_team(const StftArgs& a, long long batch, void* workspace, hipStream_t stream,
+                       bool* launched) {
+  if (a.flags & SPECENH_STFT_NORMALIZE)
+    return launch_team_mode<N, 2>(a, batch, workspace, stream, launched);
+  if (a.flags & SPECENH_STFT_LOG) return launch_team_mode<N, 1>(a, batch, workspace, stream, launched);
+  return launch_team_mode<N, 0>(a, batch, workspace, stream, launched);
 }
 
 }  // namespace specenh
@@ -942,6 +1067,7 @@ struct specenh_stft_plan {
   float* d_window;
   float2* d_twiddle;
   double dc_alpha, dc_beta;  // DC coefficients from the fp32 window (StftArgs)
+  double* d_dc;              // c_n = w_n - alpha - beta (n - kmid), fp64
 };
 
 extern "C" {
@@ -1026,11 +1152,18 @@ int specenh_stft_plan_create(specenh_stft_plan** plan, int nperseg, int noverlap
   hipError_t e = hipGetDevice(&p->device);
   if (e == hipSuccess) e = hipMalloc(&p->d_window, N * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&p->d_twiddle, tw.size() * sizeof(float2));
+  if (e == hipSuccess) e = hipMalloc(&p->d_dc, N * sizeof(double));
+  if (e == hipSuccess) {
+    std::vector<double> dc(N);
+    for (int i = 0; i < N; ++i) dc[i] = (double(win[i]) - dc_alpha) - dc_beta * (i - 0.5 * (N - 1));
+    e = hipMemcpy(p->d_dc, dc.data(), N * sizeof(double), hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) e = hipMemcpy(p->d_window, win.data(), N * sizeof(float), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_twiddle, tw.data(), tw.size() * sizeof(float2), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     (void)hipFree(p->d_window);
     (void)hipFree(p->d_twiddle);
+    (void)hipFree(p->d_dc);
     delete p;
     return set_error(SPECENH_EHIP, std::string("plan allocation: ") + hipGetErrorString(e));
   }
@@ -1042,6 +1175,7 @@ int specenh_stft_plan_destroy(specenh_stft_plan* plan) {
   if (!plan) return SPECENH_OK;
   (void)hipFree(plan->d_window);
   (void)hipFree(plan->d_twiddle);
+  (void)hipFree(plan->d_dc);
   delete plan;
   return SPECENH_OK;
 }
@@ -1083,12 +1217,14 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
   a.twiddle = plan->d_twiddle;
   a.dc_alpha = plan->dc_alpha;
   a.dc_beta = plan->dc_beta;
+  a.dc_coef = plan->d_dc;
   const long long F_out = a.F_out;
-  // team schedule for large spectrograms (C2: 518 KB each); small ones (C5: 64 KB) are
-  // re-read from L2 by the sweep for less than the team's hand-off costs (measured)
+  // team (tile-parallel) schedule for large spectrograms (C2: 518 KB each); small ones (C5:
+  // 64 KB) are re-read from L2 by the sweep for less than the team's hand-off costs
+  // (measured). Without NORMALIZE it needs no workspace.
   const bool team = (F_out * T * 4 >= (256ll << 10)) || (flags & STFT_DEV_FORCETEAM);
-  if ((flags & SPECENH_STFT_NORMALIZE) && workspace && !(flags & STFT_DEV_NOTEAM) && team &&
-      batch <= (1ll << 30)) {
+  const bool norm = (flags & SPECENH_STFT_NORMALIZE) != 0;
+  if ((workspace || !norm) && !(flags & STFT_DEV_NOTEAM) && team && batch <= (1ll << 30)) {
     bool launched = false;
     hipError_t e = hipSuccess;
     switch (N) {
@@ -1155,6 +1291,7 @@ int specenh_stft_psd_f16(const specenh_stft_plan* plan, const void* x, long long
   a.twiddle = plan->d_twiddle;
   a.dc_alpha = plan->dc_alpha;
   a.dc_beta = plan->dc_beta;
+  a.dc_coef = plan->d_dc;
   hipStream_t st = (hipStream_t)stream;
   const long long F_out = a.F_out;
   for (long long b0 = 0; b0 < batch; b0 += 1 << 30) {

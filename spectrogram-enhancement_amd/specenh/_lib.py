@@ -15,7 +15,9 @@ import threading
 
 import torch  # noqa: F401  (must precede the dlopen below; see module docstring)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libspecenh.so")
+# SPECENH_LIB: development A/B builds only (tools/build_variant.sh); default = in-tree build
+LIB_PATH = os.environ.get("SPECENH_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                         "libspecenh.so")
 
 SPECENH_OK = 0
 SPECENH_EINVAL = -1

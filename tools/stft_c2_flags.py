@@ -13,7 +13,7 @@ B = 4096
 x = plasma_chirps_torch(B, 65536, seed=1, device="cuda")
 plan = stft.get_plan(x.device, 1024, 768, "hamm", 500000.0, "density", "linear", 1e-11)
 out = torch.empty((B, 512, 253), device="cuda")
-NOSTORE, NOTEAM, NOWAIT = 1 << 16, 1 << 17, 1 << 20
+NOSTORE, NOTEAM, NOWAIT, NOLOAD = 1 << 16, 1 << 17, 1 << 20, 1 << 21
 
 
 def timed(flags, reps=10):
@@ -30,5 +30,7 @@ def timed(flags, reps=10):
 
 for name, fl in (("team", 7), ("team_nostore", 7 | NOSTORE), ("team_nowait", 7 | NOWAIT),
                  ("team_nostore_nowait", 7 | NOSTORE | NOWAIT), ("sweep", 7 | NOTEAM),
-                 ("psd_nonorm_nostore", 5 | NOSTORE | NOTEAM), ("psd_nonorm", 5 | NOTEAM)):
+                 ("psd_nonorm_nostore", 5 | NOSTORE | NOTEAM), ("psd_nonorm", 5 | NOTEAM),
+                 ("team_nonorm", 5), ("team_noload", 7 | NOLOAD),
+                 ("team_noload_nostore_nowait", 7 | NOLOAD | NOSTORE | NOWAIT)):
     print(f"{name:22s} {timed(fl):.4f} ms", flush=True)

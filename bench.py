@@ -528,7 +528,7 @@ def main():
         stages["stft_c2"] = {
             "workload": "4096 x 65536 fp32, nperseg 1024 hop 256 hamm, linear, density, "
                         "log + min-max + drop Nyquist -> 4096 x 512 x 253",
-            "spectrograms_per_s": B2 / (k_ms * 1e-3), "kernel": "stft_psd_kernel<1024>",
+            "spectrograms_per_s": B2 / (k_ms * 1e-3), "kernel": "stft_team_kernel<1024, 2>",
             "kernel_ms": k_ms, "roofline": {"bound": "hbm", "achieved": ach2,
                                             "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                             "frac": ach2 / HBM_PEAK_GBPS,

@@ -1,7 +1,8 @@
 """Run one autoencoder layer's forward launch repeatedly (for rocprofv3 PMC passes).
 
     python tools/conv_one.py LAYER [--batch 4096] [--reps 20] [--dtype float16]
-LAYER: l1 l2 l3 ct1 ct2 ct3 last (the C5 model at 128x128) or all
+LAYER: l1 l2 l3 ct1 ct2 ct3 last (the C5 model at 128x128), tail (convT3 + conv_out, the
+fused decoder tail) or all
 """
 import argparse
 import os
@@ -19,7 +20,7 @@ from specenh import ae  # noqa: E402
 LAYERS = {"l1": ("conv", 1, 16, 128, True), "l2": ("conv", 16, 32, 64, True),
           "l3": ("conv", 32, 64, 32, True), "ct1": ("convT", 64, 64, 16, False),
           "ct2": ("convT", 64, 32, 32, False), "ct3": ("convT", 32, 16, 64, False),
-          "last": ("conv", 16, 1, 128, False)}
+          "last": ("conv", 16, 1, 128, False), "tail": ("convT", 32, 16, 64, False)}
 
 
 def main():
@@ -36,6 +37,8 @@ def main():
                          stride=2 if kind == "convT" else 1)]
         if pool:  # pool + a 1x1 tail so the pool is fused as in the model
             ops += [ae.PoolOp(), ae.ConvOp("conv", cout, 16, 1, "relu")]
+        elif name == "tail":  # the model's last two layers: fused into one launch
+            ops += [ae.ConvOp("conv", cout, 1, 5, "sigmoid")]
         elif kind == "convT":  # a 1x1 tail: the layer writes T activations as in the model
             ops += [ae.ConvOp("conv", cout, 16, 1, "relu")]
         eng = ae.AutoencoderEngine(ops, (H, H, cin), compute_dtype=a.dtype, device="cuda:0")

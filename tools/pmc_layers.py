@@ -13,10 +13,13 @@ import os
 import statistics
 import sys
 
-LAYERS = {"ct1": "convT1", "ct2": "convT2", "ct3": "convT3", "last": "conv_out", "stft_c2": "stft_c2"}
+LAYERS = {"l1": "conv1+pool", "l2": "conv2+pool", "l3": "conv3+pool", "ct1": "convT1",
+          "ct2": "convT2", "ct3": "convT3", "last": "conv_out", "tail": "convT3+conv_out",
+          "stft_c2": "stft_c2"}
 # the layer's own kernel (tools/conv_one.py adds a 1x1 tail conv after the convT layers)
-KERNEL = {"ct1": "Li4ELi64ELb0", "ct2": "Li2ELi64ELb0", "ct3": "Li1ELi32ELb0",
-          "last": "conv_co1", "stft_c2": "stft"}
+KERNEL = {"l1": "conv_c1_kernel", "l2": "Li2ELi16ELb1", "l3": "Li4ELi32ELb1",
+          "ct1": "Li4ELi64ELb0", "ct2": "Li2ELi64ELb0", "ct3": "Li1ELi32ELb0",
+          "last": "conv_co1", "tail": "convt_conv_out", "stft_c2": "stft_team"}
 
 
 def one(path, must="", skip=("cast", "flip", "Fill", "fill", "copy", "at::native", "rocclr")):

@@ -7,7 +7,7 @@ R=$(pwd)
 OUT=$R/gpurun_out/pmc_traffic
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-for L in ct1 ct2 ct3 last; do
+for L in l1 l2 l3 ct1 ct2 ct3 last tail; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $OUT/${L}_$C -o p -- python3 $R/tools/conv_one.py $L --reps 3 > $OUT/${L}_$C.log 2>&1 || exit 1
   done

@@ -160,6 +160,27 @@ __device__ __forceinline__ void set_elem(V8<T>& v, int j, T x) {
   }
 }
 
+// Two floats rounded to T (round to nearest even) and packed into one 32-bit word, element
+// a in the low half: v_cvt_pk_bf16_f32 / two v_cvt_f16_f32 + v_pack_b32_f16 (no mask ops).
+template <typename T>
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  if constexpr (__is_same(T, __bf16)) {
+    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, b2{(__bf16)a, (__bf16)b});
+  } else {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, h2{(_Float16)a, (_Float16)b});
+  }
+}
+
+// max(a, b) without the NaN-quieting canonicalisation fmaxf gets (operands are
+// accumulators: finite unless the inputs hold NaN/Inf)
+__device__ __forceinline__ float vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // 8 GEMM-K elements k .. k+7 of one output pixel (by, bx = top-left of its window, nb =
 // n*IH). Out-of-range rows have by far below zero.
 template <typename T>
@@ -418,20 +439,23 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 // output line is completed by two phase stores microseconds apart, and the half-written
 // line is evicted in between (2-2.6x the algorithmic write traffic). The
 // two row phases of a tile run on one XCD back to back and share its input lines in L2.
-template <int CC, int NT, bool PAIR>
-struct PatchLds {
-  static constexpr int patch = 20 * 20 * Patch<CC>::PST;
-  static constexpr int stage = 16 * 16 * (32 * NT + 8);  // 16 rows x 16 pixel pairs, padded
-  static constexpr int elems = PAIR && stage > patch ? stage : patch;
-};
 
+// waves per SIMD the register budget is sized for (4 -> 128 VGPRs, 3 -> 168, 2 -> 256)
+#ifndef SPECENH_PATCH_WPE
+#define SPECENH_PATCH_WPE(PAIR, NT, CC) \
+  ((PAIR && NT == 1) || (CC == 16 && NT == 2) ? 4 : ((CC == 32 && NT == 4) || CC == 64 ? 3 : 1))
+#endif
 template <typename T, int NT, int CC, bool POOL, bool PAIR = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((PAIR && NT == 1) || (CC == 16 && NT == 2) ? 4 : (CC == 32 && NT == 4 ? 3 : 1))))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SPECENH_PATCH_WPE(PAIR, NT, CC))))
 void conv_patch_kernel(ConvArgs a) {
   constexpr int TILE = 16;
   constexpr int PST = Patch<CC>::PST;
   constexpr int MT = 4;  // output rows per wave
-  __shared__ __attribute__((aligned(16))) T sP[PatchLds<CC, NT, PAIR>::elems];
+  // the patch (and PAIR's output stage) in dynamic LDS sized by the launch for the actual
+  // patch (patch_lds_bytes): a Conv2DTranspose's 4 phases share an 18 x 18 patch, not 20 x 20
+  // (CC = 64: 52 KB -> 3 workgroups per CU instead of 2)
+  extern __shared__ __attribute__((aligned(16))) unsigned char sP_raw[];
+  T* const sP = reinterpret_cast<T*>(sP_raw);
   __shared__ int sTap[MAXPH][32];  // patch offset of tap t (elements), -1 past the last tap
   __shared__ int sCol[MAXPH][32];  // weight column of tap t at ci = 0
 
@@ -626,10 +650,13 @@ void conv_patch_kernel(ConvArgs a) {
             const uint4 q = *reinterpret_cast<const uint4*>(sP + rbase[i] + aoff);  // ds_read_b128
             pv[i].w[0] = q.x; pv[i].w[1] = q.y; pv[i].w[2] = q.z; pv[i].w[3] = q.w;
           }
-          if (2 * st + 1 >= ntap) {  // last step of an odd tap count: no second tap
+          if (__builtin_expect(2 * st + 1 >= ntap, 0)) {  // last step of an odd tap count:
+            // no second tap (a wave-uniform branch: the zeroing stays out of the other steps)
+            if (second) {
 #pragma unroll
-            for (int i = 0; i < MT; ++i)
-              if (second) zero8(pv[i]);
+              for (int i = 0; i < MT; ++i) zero8(pv[i]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
           }
 #pragma unroll
           for (int i = 0; i < MT; ++i)
@@ -729,6 +756,34 @@ void conv_patch_kernel(ConvArgs a) {
       // 2x2 windows: rows (2ip, 2ip+1) of this wave in registers, columns (px, px^1) across
       // the lane pair; values compared as stored (rounded to T), first max wins
       const int PHo = g.OH / 2, PWo = g.OW / 2;
+      if (!a.argmax && (g.CO & 3) == 0 && a.act <= 1) {
+        // inference: the pooled value only. x -> round_T(act(x + b)) is monotone, so the
+        // max of the four stored values is that map of the max accumulator: max first
+        // (in-lane rows, then the lane pair), one bias add / ReLU / rounding per output.
+        const bool relu = a.act == 1;
+#pragma unroll
+        for (int ip = 0; ip < 2; ++ip) {
+          const int oy = oy0 + wave * MT + 2 * ip;
+          const int py = oy / 2, pxo = ox / 2;
+          const bool store = (px & 1) == 0 && py < PHo && pxo < PWo;
+#pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            float m[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float m1 = vmax(acc[2 * ip][j][r], acc[2 * ip + 1][j][r]);
+              float v = vmax(m1, __shfl_xor(m1, 1)) + bv[j][r];
+              m[r] = relu ? vmax(v, 0.f) : v;
+            }
+            const int ch0 = n0 + 16 * j + 4 * kgrp;
+            if (store && ch0 < g.CO) {
+              const long long o = (((long long)n * PHo + py) * PWo + pxo) * g.CO + ch0;
+              *reinterpret_cast<uint2*>(reinterpret_cast<T*>(a.out) + o) =
+                  uint2{pack2<T>(m[0], m[1]), pack2<T>(m[2], m[3])};
+            }
+          }
+        }
+      } else
 #pragma unroll
       for (int ip = 0; ip < 2; ++ip) {
         const int oy = oy0 + wave * MT + 2 * ip;
@@ -835,14 +890,13 @@ void conv_patch_kernel(ConvArgs a) {
         for (int j = 0; j < NT; ++j) {
           const int ch0 = n0 + 16 * j + 4 * kgrp;
           if (ch0 >= CO) continue;
-          V8<T> pk;
-          zero8(pk);
+          float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float v = acc[i][j][r] + bv[j][r];
-            set_elem(pk, r, from_f<T>(relu ? fmaxf(v, 0.f) : v));
+            const float x = acc[i][j][r] + bv[j][r];
+            v[r] = relu ? vmax(x, 0.f) : x;
           }
-          *reinterpret_cast<uint2*>(out + o + ch0) = uint2{pk.w[0], pk.w[1]};
+          *reinterpret_cast<uint2*>(out + o + ch0) = uint2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
         }
       }
     } else {
@@ -1195,6 +1249,22 @@ int check_sizes(long long N, long long IH, long long IW, long long C, long long 
   return SPECENH_OK;
 }
 
+// dynamic LDS of conv_patch_kernel<T, NT, CC, *, PAIR>: the staged patch (largest phase, or
+// the shared patch of all phases) and, for PAIR, the output stage it aliases
+template <typename T, int CC>
+size_t patch_lds_bytes(const ConvArgs& a, int nph, int NT, bool pair) {
+  size_t px = 0;
+  if (a.ph_shared) {
+    px = (size_t)a.PH * a.PW;
+  } else {
+    for (int i = 0; i < nph; ++i)
+      px = std::max(px, (size_t)(16 + a.g[i].KH - 1) * (16 + a.g[i].KW - 1));
+  }
+  size_t elems = px * Patch<CC>::PST;
+  if (pair) elems = std::max(elems, (size_t)16 * 16 * (32 * NT + 8));
+  return (elems * sizeof(T) + 15) / 16 * 16;
+}
+
 template <typename T, int CC>
 int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   // all phases of a dilated conv in one workgroup when they share a tile grid and the
@@ -1239,7 +1309,8 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   }
   if (pair) {
     const dim3 grid2((tiles + 7) / 8 * 16, 1, 1);
-#define SPECENH_PAIR(NT) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC, false, true>), grid2, dim3(256), 0, st, a)
+    const size_t lds = patch_lds_bytes<T, CC>(a, nph, nt, true);
+#define SPECENH_PAIR(NT) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC, false, true>), grid2, dim3(256), lds, st, a)
     if (nt == 1) SPECENH_PAIR(1);
     else if (nt == 2) SPECENH_PAIR(2);
     else if (nt == 3) SPECENH_PAIR(3);
@@ -1248,7 +1319,8 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "conv launch");
   }
   const dim3 grid(tiles, (unsigned)((CO + 16 * nt - 1) / (16 * nt)), a.ph_shared ? 1 : nph);
-#define SPECENH_PATCH(NT, P) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC, P>), grid, dim3(256), 0, st, a)
+  const size_t lds = patch_lds_bytes<T, CC>(a, nph, nt, false);
+#define SPECENH_PATCH(NT, P) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC, P>), grid, dim3(256), lds, st, a)
   if (a.pool) {
     if (nt == 1) SPECENH_PATCH(1, true);
     else if (nt == 2) SPECENH_PATCH(2, true);

@@ -1067,21 +1067,338 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   if (do_bias && n0 + tid < g.CO) a.bpart[((long long)ph * a.Z + z) * g.CO + n0 + tid] = bacc;
 }
 
-// dst[e] += sum_{z < nz} part[z * n + e], always in the same order (bit-reproducible).
-__global__ void ordered_sum_kernel(const float* __restrict__ part, int nz, long long n,
-                                   float* __restrict__ dst) {
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
-       e += (long long)gridDim.x * blockDim.x) {
-    float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
-    int z = 0;
-    for (; z + 4 <= nz; z += 4) {
-      t0 += part[(long long)z * n + e];
-      t1 += part[(long long)(z + 1) * n + e];
-      t2 += part[(long long)(z + 2) * n + e];
-      t3 += part[(long long)(z + 3) * n + e];
+// ------------------------------------------------------------------ weight gradient, C % 16 == 0
+// dW[co][(tap, ci)] = sum_p dOut[p][co] * in[p + tap][ci] as MFMA 16x16x32 with the 32 pixels
+// as the reduction: A = dOut^T (16 co x 32 px), B = input window (32 px x 16 ci). A workgroup
+// owns one phase, 16 input channels, 16*NTW output channels and a run of 16x16 output tiles;
+// per tile the dOut tile ([pixel][co]) and the input patch ([pixel][16 ci]) are staged in LDS
+// as plain NHWC rows (16-B copies) and the fragments come out with ds_read_b64_tr_b16
+// (the transpose is free), so one staged dOut fragment feeds every tap: wave w owns taps
+// w, w+4, ... (<= 7 of 25) and keeps 7 x NTW accumulators; the bias gradient is one more
+// MFMA per co-block against a ones fragment. Partial sums per pixel run (blockIdx.x) go to
+// part[z] and are reduced in a fixed order (ordered_sum_kernel): bit-reproducible.
+struct WgradTrArgs {
+  Geo g[MAXPH];
+  int Z;     // tile runs per phase (blockIdx.x)
+  int ncog;  // co groups of 16 * NTW (blockIdx.y = chunk * ncog + cog)
+  const void* in;
+  const void* dout;  // [N][OHs][OWs][CO]
+  float* part;       // [Z][CO][Kf]
+  float* bpart;      // [nphase][Z][CO] or null
+};
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// rows q = 0..3 of a 4 x 16 block of 16-bit elements, transposed across a 16-lane group
+__device__ __forceinline__ s16x4 lds_tr16(const void* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(const_cast<void*>(p)));
+}
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma_s16(s16x8 a, s16x8 b, f32x4 acc) {
+  if constexpr (__is_same(T, __bf16))
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), acc, 0, 0, 0);
+}
+
+// C1 (one input channel, the first Conv2D): the B tile is an im2col block built in LDS per tile
+// ([256 pixels][32 taps], taps >= KH*KW zero, tap 31 = 1 so column 31 of D is the bias
+// gradient); waves w take k-block w & 1 over pixel groups of parity w >> 1 and pairs of waves
+// are summed in a fixed order at the end. The next tile's global data is prefetched into
+// registers while the current tile computes.
+template <typename T, int NTW, bool C1>
+__global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
+  constexpr int CH = 16;             // input channels per workgroup: one k-block per tap
+  constexpr int COT = 16 * NTW;      // output channels per workgroup
+  constexpr int DST = COT + 8;       // dOut tile row stride (elements; 16-B multiple, 2-way max)
+  constexpr int PST = C1 ? 40 : CH + 8;  // B rows: im2col taps (C1) or patch pixel channels
+  constexpr int MAXT = C1 ? 1 : 7;   // taps (k-blocks) per wave
+  constexpr int PROWS = C1 ? 256 : 400;
+  constexpr int NDV = COT / 8;       // dOut uint4 per thread (256 pixels x COT channels)
+  constexpr int NPV = C1 ? 2 : 4;    // patch elements (C1: T) / uint4 per thread
+  __shared__ __attribute__((aligned(16))) T sD[256 * DST];
+  __shared__ __attribute__((aligned(16))) T sP[PROWS * PST];
+  __shared__ __attribute__((aligned(16))) T sIn[C1 ? 20 * 20 : 8];
+  const int ph = blockIdx.z;
+  const Geo& g = a.g[ph];
+  const int chunk = blockIdx.y / a.ncog, cog = blockIdx.y - (blockIdx.y / a.ncog) * a.ncog;
+  const int c0 = chunk * CH, co0 = cog * COT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntx = (g.OW + 15) / 16, nty = (g.OH + 15) / 16;
+  const long long ntiles = (long long)g.N * nty * ntx;
+  const long long t_begin = blockIdx.x * ntiles / a.Z, t_end = (blockIdx.x + 1) * ntiles / a.Z;
+  const int ntap = g.KH * g.KW;
+  const int PW = 16 + g.KW - 1, PH = 16 + g.KH - 1;
+  const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
+  const T* __restrict__ dout = reinterpret_cast<const T*>(a.dout);
+  const bool co_vec = (g.CO & 7) == 0, co_one = g.CO == 1;
+
+  f32x4 acc[MAXT][NTW];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 bacc[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) bacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = !C1 && a.bpart && chunk == 0 && wave == 0;
+  s16x8 ones;
+  const short one = __builtin_bit_cast(short, from_f<T>(1.f));
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = one;
+
+  // tr-read lane roles: group g4 = lane >> 4 owns MFMA K-elements 8 g4 .. 8 g4 + 7 = pixels
+  // (row 2 pg + (g4 >> 1), columns 8 (g4 & 1) .. + 7) of pixel group pg; lane 4q + p of the
+  // group addresses row q (pixel column + q, + 4 for the upper half) and elements 4p .. 4p+3
+  const int g4 = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int prow = g4 >> 1, pcol = 8 * (g4 & 1) + q;
+
+  // ---- per-thread prefetch registers of one tile ----
+  uint4 rd[NDV];
+  T rd1;               // CO == 1: this thread's pixel
+  uint4 rp[C1 ? 1 : NPV];
+  T rp1[C1 ? NPV : 1];
+  auto tile_org = [&](long long tile, int& n, int& oyt, int& oxt) {
+    n = (int)(tile / (nty * ntx));
+    const int trem = (int)(tile - (long long)n * nty * ntx);
+    oyt = (trem / ntx) * 16;
+    oxt = (trem - (trem / ntx) * ntx) * 16;
+  };
+  auto fetch = [&](long long tile) {
+    int n, oyt, oxt;
+    tile_org(tile, n, oyt, oxt);
+    if (co_vec) {
+#pragma unroll
+      for (int u = 0; u < NDV; ++u) {
+        const int e = tid + 256 * u;
+        const int pix = e / NDV, v = e - (e / NDV) * NDV;
+        const int oy = oyt + (pix >> 4), ox = oxt + (pix & 15);
+        const int co = co0 + 8 * v;
+        rd[u] = uint4{0u, 0u, 0u, 0u};
+        if (oy < g.OH && ox < g.OW && co < g.CO)
+          rd[u] = *reinterpret_cast<const uint4*>(
+              dout + (((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0) * g.CO + co);
+      }
+    } else if (co_one) {
+      const int oy = oyt + (tid >> 4), ox = oxt + (tid & 15);
+      rd1 = from_f<T>(0.f);
+      if (oy < g.OH && ox < g.OW)
+        rd1 = dout[((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0];
     }
-    for (; z < nz; ++z) t0 += part[(long long)z * n + e];
-    dst[e] += (t0 + t1) + (t2 + t3);
+#pragma unroll
+    for (int u = 0; u < NPV; ++u) {
+      const int e = tid + 256 * u;
+      if constexpr (C1) {
+        const int py = e / PW, px = e - (e / PW) * PW;
+        const int iy = oyt - g.pad_t + py, ix = oxt - g.pad_l + px;
+        rp1[u] = from_f<T>(0.f);
+        if (e < PH * PW && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW)
+          rp1[u] = in[((long long)n * g.IH + iy) * g.IW + ix];
+      } else {
+        const int pix = e >> 1, v = e & 1;
+        const int py = pix / PW, px = pix - (pix / PW) * PW;
+        const int iy = oyt - g.pad_t + py, ix = oxt - g.pad_l + px;
+        rp[u] = uint4{0u, 0u, 0u, 0u};
+        if (pix < PH * PW && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW)
+          rp[u] = *reinterpret_cast<const uint4*>(in + (((long long)n * g.IH + iy) * g.IW + ix) * g.C + c0 + 8 * v);
+      }
+    }
+  };
+  auto stage = [&](long long tile) {
+    if (co_vec) {
+#pragma unroll
+      for (int u = 0; u < NDV; ++u) {
+        const int e = tid + 256 * u;
+        const int pix = e / NDV, v = e - (e / NDV) * NDV;
+        *reinterpret_cast<uint4*>(sD + pix * DST + 8 * v) = rd[u];
+      }
+    } else if (co_one) {
+      const uint32_t w0 = __builtin_bit_cast(unsigned short, rd1);
+#pragma unroll
+      for (int v = 0; v < COT / 8; ++v)
+        *reinterpret_cast<uint4*>(sD + tid * DST + 8 * v) = uint4{v == 0 ? w0 : 0u, 0u, 0u, 0u};
+    } else {  // other narrow CO: element-wise, not prefetched
+      int n, oyt, oxt;
+      tile_org(tile, n, oyt, oxt);
+      for (int e = tid; e < 256 * COT; e += 256) {
+        const int pix = e / COT, c = e - (e / COT) * COT;
+        const int oy = oyt + (pix >> 4), ox = oxt + (pix & 15);
+        T val = from_f<T>(0.f);
+        if (oy < g.OH && ox < g.OW && co0 + c < g.CO)
+          val = dout[(((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0) * g.CO + co0 + c];
+        sD[pix * DST + c] = val;
+      }
+    }
+    if constexpr (C1) {
+#pragma unroll
+      for (int u = 0; u < NPV; ++u) {
+        const int e = tid + 256 * u;
+        if (e < PH * PW) sIn[e] = rp1[u];
+      }
+      lds_sync();
+      // im2col row of this thread's pixel: taps (ky, kx) -> column ky*KW + kx; 31 = ones
+      const int r = tid >> 4, c = tid & 15;
+#pragma unroll
+      for (int t4 = 0; t4 < 8; ++t4) {
+        uint32_t w[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          uint32_t pk = 0u;
+#pragma unroll
+          for (int e2 = 0; e2 < 2; ++e2) {
+            const int t = 4 * t4 + 2 * h + e2;
+            unsigned short b = 0;
+            if (t == 31) {
+              b = (unsigned short)one;
+            } else if (t < ntap) {
+              const int jy = t / g.KW, jx = t - (t / g.KW) * g.KW;
+              b = __builtin_bit_cast(unsigned short, sIn[(r + jy) * PW + c + jx]);
+            }
+            pk |= (uint32_t)b << (16 * e2);
+          }
+          w[h] = pk;
+        }
+        *reinterpret_cast<uint2*>(sP + tid * PST + 4 * t4) = uint2{w[0], w[1]};
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < NPV; ++u) {
+        const int e = tid + 256 * u;
+        const int pix = e >> 1, v = e & 1;
+        if (pix < PH * PW) *reinterpret_cast<uint4*>(sP + pix * PST + 8 * v) = rp[u];
+      }
+    }
+  };
+
+  if (t_begin < t_end) fetch(t_begin);
+  for (long long tile = t_begin; tile < t_end; ++tile) {
+    lds_sync();  // the previous tile's fragment reads are done
+    stage(tile);
+    lds_sync();
+    if (tile + 1 < t_end) fetch(tile + 1);  // in flight while this tile computes
+    if constexpr (C1) {
+      // wave w: k-block kb = w & 1 (taps 16 kb .. 16 kb + 15), pixel groups of parity w >> 1
+      const int kb = wave & 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pg = 2 * i + (wave >> 1);
+        const int r = 2 * pg + prow;
+        const T* da = sD + (r * 16 + pcol) * DST + 4 * pp;
+        const T* pb = sP + (r * 16 + pcol) * PST + 16 * kb + 4 * pp;
+        const s16x4 blo = lds_tr16(pb), bhi = lds_tr16(pb + 4 * PST);
+        const s16x8 bf = s16x8{blo[0], blo[1], blo[2], blo[3], bhi[0], bhi[1], bhi[2], bhi[3]};
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          const s16x4 lo = lds_tr16(da + 16 * j), hi = lds_tr16(da + 4 * DST + 16 * j);
+          const s16x8 af = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          acc[0][j] = mfma_s16<T>(af, bf, acc[0][j]);
+        }
+      }
+    } else {
+      for (int pg = 0; pg < 8; ++pg) {
+        const int r = 2 * pg + prow;
+        s16x8 af[NTW];
+        const T* da = sD + (r * 16 + pcol) * DST + 4 * pp;
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          const s16x4 lo = lds_tr16(da + 16 * j), hi = lds_tr16(da + 4 * DST + 16 * j);
+          af[j] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int tt = 0; tt < MAXT; ++tt) {
+          const int t = wave + 4 * tt;
+          if (t >= ntap) break;  // wave-uniform
+          const int jy = t / g.KW, jx = t - (t / g.KW) * g.KW;
+          const T* pb = sP + ((r + jy) * PW + pcol + jx) * PST + 4 * pp;
+          const s16x4 lo = lds_tr16(pb), hi = lds_tr16(pb + 4 * PST);
+          const s16x8 bf = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int j = 0; j < NTW; ++j) acc[tt][j] = mfma_s16<T>(af[j], bf, acc[tt][j]);
+        }
+        if (do_bias) {
+#pragma unroll
+          for (int j = 0; j < NTW; ++j) bacc[j] = mfma_s16<T>(af[j], ones, bacc[j]);
+        }
+      }
+    }
+  }
+  // ---- partial sums: D[co][n], lane column n = lane & 15, rows co = 4 (lane >> 4) + r ----
+  const long long z = blockIdx.x;
+  if constexpr (C1) {
+    // waves 2, 3 hand their sums to waves 0, 1 (same k-block): fixed-order pair sums
+    float* red = reinterpret_cast<float*>(sD);
+    lds_sync();
+    if (wave >= 2) {
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) red[(((wave - 2) * NTW + j) * 4 + rr) * 64 + lane] = acc[0][j][rr];
+    }
+    lds_sync();
+    if (wave < 2) {
+      const int t = 16 * wave + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const float v = acc[0][j][rr] + red[((wave * NTW + j) * 4 + rr) * 64 + lane];
+          const int co = co0 + 16 * j + 4 * (lane >> 4) + rr;
+          if (co >= g.CO) continue;
+          if (t < ntap) a.part[(z * g.CO + co) * g.Kf + wcol(g, t, 0)] = v;
+          else if (t == 31 && a.bpart) a.bpart[((long long)ph * a.Z + z) * g.CO + co] = v;
+        }
+    }
+    return;
+  }
+  const int ci = c0 + (lane & 15);
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) {
+    const int t = wave + 4 * tt;
+    if (t >= ntap) break;
+    const int col = wcol(g, t, ci);
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int co = co0 + 16 * j + 4 * (lane >> 4) + rr;
+        if (co < g.CO) a.part[(z * g.CO + co) * g.Kf + col] = acc[tt][j][rr];
+      }
+  }
+  if (do_bias && (lane & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int co = co0 + 16 * j + 4 * (lane >> 4) + rr;
+        if (co < g.CO) a.bpart[((long long)ph * a.Z + z) * g.CO + co] = bacc[j][rr];
+      }
+  }
+}
+
+// dst[e] += sum_{z < nz} part[z * n + e], always in the same order (bit-reproducible): a
+// workgroup owns 16 consecutive e; its 16 z-lanes each sum z = zl, zl + 16, ... in order,
+// then lane zl = 0 adds the 16 lane sums in order. Launch with (n + 15) / 16 workgroups.
+__global__ __launch_bounds__(256) void ordered_sum_kernel(const float* __restrict__ part, int nz,
+                                                          long long n, float* __restrict__ dst) {
+  __shared__ float red[16][17];
+  const int el = threadIdx.x & 15, zl = threadIdx.x >> 4;
+  const long long e = blockIdx.x * 16LL + el;
+  float t = 0.f;
+  if (e < n)
+    for (int z = zl; z < nz; z += 16) t += part[(long long)z * n + e];
+  red[zl][el] = t;
+  __syncthreads();
+  if (zl == 0 && e < n) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][el];
+    dst[e] += s;
   }
 }
 
@@ -1387,6 +1704,11 @@ struct WgradPlan {
   unsigned gx, gy;
 };
 
+// tile runs of the MFMA path (wgrad_tr_kernel): at most this many partial slices
+// (small weight tensors may take more runs: a layer with one workgroup per run would
+// otherwise leave one workgroup per CU, latency-bound)
+inline int wgrad_tr_zmax(long long CO, long long Kf) { return CO * Kf <= 8192 ? 2048 : 256; }
+
 WgradPlan wgrad_plan(int Kf, int CO) {
   WgradPlan p{};
   p.nt = std::min(4, (CO + 15) / 16);
@@ -1397,8 +1719,63 @@ WgradPlan wgrad_plan(int Kf, int CO) {
   return p;
 }
 
+// the MFMA path: bf16/f16, every phase stride 1 with C % 16 == 0 and <= 28 taps in a 20 x 20
+// patch (SPECENH_WGRAD_GENERIC=1 forces the generic gather kernel)
+template <typename T>
+bool wgrad_tr_applies(const WgradArgs& a, int nph) {
+  if constexpr (__is_same(T, float)) return false;
+  if (getenv_flag("SPECENH_WGRAD_GENERIC")) return false;
+  for (int i = 0; i < nph; ++i) {
+    const Geo& g = a.g[i];
+    if ((g.C % 16 != 0 && g.C != 1) || g.stride != 1 || g.KH * g.KW > 28 || g.KH > 5 || g.KW > 5)
+      return false;
+    if (g.C == 1 && g.KH * g.KW > 31) return false;  // im2col columns 0..30 (+ the ones column)
+  }
+  return true;
+}
+
+template <typename T>
+int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream_t st) {
+  const Geo& g0 = w.g[0];
+  WgradTrArgs a{};
+  // (C == 1: workspace sized like the MFMA path, see specenh_conv2d_wgrad_workspace_bytes)
+  for (int i = 0; i < nph; ++i) a.g[i] = w.g[i];
+  a.in = w.in;
+  a.dout = w.dout;
+  a.part = w.part;
+  a.bpart = w.bpart;
+  const int nt = std::min(4, (g0.CO + 15) / 16);
+  const int ntw = nt >= 2 ? 2 : 1;
+  a.ncog = (g0.CO + 16 * ntw - 1) / (16 * ntw);
+  const bool c1 = g0.C == 1;
+  const int nchunk = c1 ? 1 : g0.C / 16;
+  long long tiles = 1;
+  for (int i = 0; i < nph; ++i)
+    tiles = std::max(tiles, (long long)w.g[i].N * ((w.g[i].OH + 15) / 16) * ((w.g[i].OW + 15) / 16));
+  // ~4096 workgroups, at least 4 tiles each
+  long long z = 4096 / std::max(1LL, (long long)nchunk * a.ncog * nph);
+  z = std::min<long long>(z, std::max(1LL, tiles / 4));
+  a.Z = (int)std::max(1LL, std::min<long long>(z, wgrad_tr_zmax(g0.CO, g0.Kf)));
+  const dim3 grid((unsigned)a.Z, (unsigned)(nchunk * a.ncog), (unsigned)nph);
+  if (c1) {
+    if (ntw == 1) hipLaunchKernelGGL((wgrad_tr_kernel<T, 1, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_tr_kernel<T, 2, true>), grid, dim3(256), 0, st, a);
+  } else {
+    if (ntw == 1) hipLaunchKernelGGL((wgrad_tr_kernel<T, 1, false>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_tr_kernel<T, 2, false>), grid, dim3(256), 0, st, a);
+  }
+  const long long n = (long long)g0.CO * g0.Kf;
+  hipLaunchKernelGGL(ordered_sum_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, st, a.part, a.Z, n, dw);
+  if (db)
+    hipLaunchKernelGGL(ordered_sum_kernel, dim3((unsigned)((g0.CO + 15) / 16)), dim3(256), 0, st, a.bpart, nph * a.Z,
+                       (long long)g0.CO, db);
+  return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
+}
+
 template <typename T>
 int launch_wgrad(WgradArgs& a, int nph, float* dw, float* db, hipStream_t st) {
+  if constexpr (!__is_same(T, float))
+    if (wgrad_tr_applies<T>(a, nph)) return launch_wgrad_tr<T>(a, nph, dw, db, st);
   const Geo& g0 = a.g[0];
   const WgradPlan p = wgrad_plan(g0.Kf, g0.CO);
   constexpr int BP = Tile<T>::BK;
@@ -1419,9 +1796,9 @@ int launch_wgrad(WgradArgs& a, int nph, float* dw, float* db, hipStream_t st) {
   else SPECENH_WG(4);
 #undef SPECENH_WG
   const long long n = (long long)g0.CO * g0.Kf;
-  hipLaunchKernelGGL(ordered_sum_kernel, dim3(grid1d(n)), dim3(256), 0, st, a.part, p.Z, n, dw);
+  hipLaunchKernelGGL(ordered_sum_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, st, a.part, p.Z, n, dw);
   if (db)
-    hipLaunchKernelGGL(ordered_sum_kernel, dim3(1), dim3(256), 0, st, a.bpart, nph * p.Z,
+    hipLaunchKernelGGL(ordered_sum_kernel, dim3((unsigned)((g0.CO + 15) / 16)), dim3(256), 0, st, a.bpart, nph * p.Z,
                        (long long)g0.CO, db);
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
 }
@@ -1468,7 +1845,11 @@ size_t specenh_conv2d_wgrad_workspace_bytes(int N, int OH, int OW, int KH, int K
                                             int CO) {
   if (N <= 0 || OH <= 0 || OW <= 0 || KH <= 0 || KW <= 0 || C <= 0 || CO <= 0) return 0;
   const WgradPlan p = wgrad_plan(KH * KW * C, CO);
-  return ((size_t)p.Z * CO * KH * KW * C + (size_t)MAXPH * p.Z * CO) * sizeof(float);
+  // room for the generic plan's slices and, when C % 16 == 0, the MFMA path's
+  const size_t Z = (C % 16 == 0 || C == 1)
+                       ? std::max<size_t>(p.Z, wgrad_tr_zmax(CO, (long long)KH * KW * C))
+                       : (size_t)p.Z;
+  return (Z * CO * KH * KW * C + (size_t)MAXPH * Z * CO) * sizeof(float);
 }
 
 int specenh_conv2d_wgrad(int dtype, const void* in, int N, int IH, int IW, int C, const void* dout,
@@ -1489,7 +1870,10 @@ int specenh_conv2d_wgrad(int dtype, const void* in, int N, int IH, int IW, int C
   a.in = in;
   a.dout = dout;
   a.part = (float*)workspace;
-  a.bpart = dbias ? a.part + (size_t)p.Z * CO * KH * KW * C : nullptr;
+  const size_t Zws = (C % 16 == 0 || C == 1)
+                         ? std::max<size_t>(p.Z, wgrad_tr_zmax(CO, (long long)KH * KW * C))
+                         : (size_t)p.Z;
+  a.bpart = dbias ? a.part + Zws * CO * KH * KW * C : nullptr;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == SPECENH_DTYPE_F32) return launch_wgrad<float>(a, nph, dw, dbias, st);
   if (dtype == SPECENH_DTYPE_BF16) return launch_wgrad<__bf16>(a, nph, dw, dbias, st);

@@ -12,10 +12,12 @@ arrays like the reference (computed in fp32 on the device; tolerance in
 DESIGN.md). ``specgr_batch`` is the tensor-in/tensor-out fast path that keeps
 data on the device.
 
-The image-filter helpers ``norm/rescale/quantfilt/meansub`` (:38-61), the
+The image-filter helpers ``norm/rescale/quantfilt/meansub/gaussblr/morph`` (:38-72), the
 label-generator chain, run as HIP kernels too (csrc/filters.hip):
 numpy inputs come back as float64 numpy, device tensors stay on the device.
-``gaussblr``/``morph`` need OpenCV semantics (cv2 is absent here): not built.
+``gaussblr``/``morph`` restate OpenCV's GaussianBlur / MORPH_CLOSE+OPEN on the uint8
+quantisation (cv2 itself is absent here: their parity rests on that restatement and the
+filter goldens).
 """
 from __future__ import annotations
 

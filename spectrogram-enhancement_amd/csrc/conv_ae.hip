@@ -44,7 +44,7 @@ int set_error(int code, const std::string& msg);  // stft_psd.hip
 int launch_conv_narrow(int dtype, const void* in, int N, int IH, int IW, int C, const void* w,
                        int KH, int KW, int CO, const float* bias, int pad_t, int pad_l, int OH,
                        int OW, int act, void* out, int out_f32, float* logits, int pool,
-                       unsigned char* argmax, hipStream_t st);  // conv_narrow.hip
+                       unsigned char* argmax, const void* mask, hipStream_t st);  // conv_narrow.hip
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -445,9 +445,15 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 #define SPECENH_PATCH_WPE(PAIR, NT, CC) \
   ((PAIR && NT == 1) || (CC == 16 && NT == 2) ? 4 : ((CC == 32 && NT == 4) || CC == 64 ? 3 : 1))
 #endif
-template <typename T, int NT, int CC, bool POOL, bool PAIR = false>
+// S2 (stride-2 conv, CC == 16, one phase: the input gradient of a Conv2DTranspose): the
+// 35 x 35 input patch of a 16 x 16 output tile is staged de-interleaved into its four
+// (row, column) parity sub-patches of 18 x 18, so tap (jy, jx) of output pixel (y, x) is
+// pixel (y + jy/2, x + jx/2) of sub-patch (jy&1, jx&1): the lanes' fragment reads stay
+// unit-stride and the k-step loop is the stride-1 one.
+template <typename T, int NT, int CC, bool POOL, bool PAIR = false, bool S2 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SPECENH_PATCH_WPE(PAIR, NT, CC))))
 void conv_patch_kernel(ConvArgs a) {
+  static_assert(!S2 || (CC == 16 && !POOL && !PAIR), "stride-2 patches: CC 16, plain epilogue");
   constexpr int TILE = 16;
   constexpr int PST = Patch<CC>::PST;
   constexpr int MT = 4;  // output rows per wave
@@ -478,8 +484,10 @@ void conv_patch_kernel(ConvArgs a) {
   const int ty = trem / ntx, tx = trem - (trem / ntx) * ntx;
   const int oy0 = ty * TILE, ox0 = tx * TILE;
   const int upt = shared ? a.upt : g0.pad_t, upl = shared ? a.upl : g0.pad_l;
-  const int PH = shared ? a.PH : TILE + g0.KH - 1, PW = shared ? a.PW : TILE + g0.KW - 1;
-  const int iy0 = oy0 - upt, ix0 = ox0 - upl;
+  const int PH = shared ? a.PH : (S2 ? 2 * TILE - 2 : TILE - 1) + g0.KH;
+  const int PW = shared ? a.PW : (S2 ? 2 * TILE - 2 : TILE - 1) + g0.KW;
+  const int SPH = S2 ? (PH + 1) / 2 : PH, SPW = S2 ? (PW + 1) / 2 : PW;  // S2 sub-patches
+  const int iy0 = (S2 ? 2 : 1) * oy0 - upt, ix0 = (S2 ? 2 : 1) * ox0 - upl;
   const int n0 = blockIdx.y * 16 * NT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kgrp = lane >> 4, px = lane & 15;
@@ -497,7 +505,7 @@ void conv_patch_kernel(ConvArgs a) {
 
   int rbase[MT];  // this lane's pixel (row i of the wave, column px) in the patch
 #pragma unroll
-  for (int i = 0; i < MT; ++i) rbase[i] = ((wave * MT + i) * PW + px) * PST;
+  for (int i = 0; i < MT; ++i) rbase[i] = ((wave * MT + i) * SPW + px) * PST;
 
   auto stage = [&](int c) {
     if constexpr (CC == 1) {
@@ -515,14 +523,29 @@ void conv_patch_kernel(ConvArgs a) {
       const int pwinv = (65536 + PW - 1) / PW;
       const int IHl = g0.IH, IWl = g0.IW, Cl = g0.C;
       const T* __restrict__ inb = in + n * IHl * IWl * Cl + c * CC;
-      for (int e = tid; e < PH * PW * GP; e += 256) {
-        const int pix = e / GP, cg = e - (e / GP) * GP;
-        const int py = (pix * pwinv) >> 16, pxx = pix - py * PW;
-        const int iy = iy0 + py, ix = ix0 + pxx;
-        const bool ok = (unsigned)iy < (unsigned)IHl && (unsigned)ix < (unsigned)IWl;
-        const uint4 v = ok ? *reinterpret_cast<const uint4*>(inb + (iy * IWl + ix) * Cl + 8 * cg)
-                           : uint4{0u, 0u, 0u, 0u};
-        *reinterpret_cast<uint4*>(sP + pix * PST + 8 * cg) = v;
+      // batches of NB loads in flight per thread (a load-wait-store loop would pay the full
+      // memory latency once per element); out-of-image pixels load a valid address and are
+      // zeroed, so the loads are unconditional
+      constexpr int NB = (SPECENH_PATCH_WPE(PAIR, NT, CC) >= 4 || NT >= 4) ? 4 : 8;  // VGPR budget
+      const int total = PH * PW * GP;
+      for (int e0 = tid; e0 < total; e0 += NB * 256) {
+        uint4 v[NB];
+        int dst[NB];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          const int e = min(e0 + 256 * k, total - 1);
+          const int pix = e / GP, cg = e - (e / GP) * GP;
+          const int py = (pix * pwinv) >> 16, pxx = pix - py * PW;
+          const int iy = iy0 + py, ix = ix0 + pxx;
+          const bool ok = (unsigned)iy < (unsigned)IHl && (unsigned)ix < (unsigned)IWl;
+          v[k] = *reinterpret_cast<const uint4*>(inb + (ok ? (iy * IWl + ix) * Cl : 0) + 8 * cg);
+          if (!ok) v[k] = uint4{0u, 0u, 0u, 0u};
+          const int spix = S2 ? ((py & 1) * 2 + (pxx & 1)) * SPH * SPW + (py >> 1) * SPW + (pxx >> 1) : pix;
+          dst[k] = spix * PST + 8 * cg;
+        }
+#pragma unroll
+        for (int k = 0; k < NB; ++k)
+          if (e0 + 256 * k < total) *reinterpret_cast<uint4*>(sP + dst[k]) = v[k];
       }
     }
   };
@@ -615,14 +638,17 @@ void conv_patch_kernel(ConvArgs a) {
         const T* wl[NT];
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          wl[j] = W + (long long)min(n0 + 16 * j + px, g.CO - 1) * Kfl + 8 * (kgrp & 1);
+          wl[j] = W + (long long)min(n0 + 16 * j + px, g.CO - 1) * Kfl + c * CC + 8 * (kgrp & 1);
         auto wcol_t = [&](int t) {
           const int jy = (t * kwinv) >> 16, jx = t - jy * KWl;
           return ((ky0 + ks * jy) * KWf + kx0 + ks * jx) * Cl;
         };
         auto aoff_t = [&](int t) {
           const int jy = (t * kwinv) >> 16, jx = t - jy * KWl;
-          return ((jy + dy) * PW + jx + dx) * PST;
+          if constexpr (S2)
+            return (((jy & 1) * 2 + (jx & 1)) * SPH * SPW + (jy >> 1) * SPW + (jx >> 1)) * PST;
+          else
+            return ((jy + dy) * PW + jx + dx) * PST;
         };
         auto wcol_of = [&](int st) {
           const int c0 = wcol_t(2 * st), c1 = wcol_t(min(2 * st + 1, ntap - 1));
@@ -875,12 +901,14 @@ void conv_patch_kernel(ConvArgs a) {
               *reinterpret_cast<const uint4*>(sP + (r * 16 + q) * PS + 8 * (c - q * QV));
         }
       }
-    } else if (!a.mask && !a.logits && !a.out_f32 && (g.CO & 3) == 0 && a.act <= 1) {
-      // the inference/activation-store path: 32-bit offsets, branch-free ReLU, 8-byte stores
+    } else if (!a.logits && !a.out_f32 && (g.CO & 3) == 0 && a.act <= 1) {
+      // the inference/activation-store path: 32-bit offsets, branch-free ReLU, 8-byte stores;
+      // the backward pass's ReLU mask as 8-byte loads at the same offsets (act(0) = 0 here)
       const bool relu = a.act == 1;
       const int CO = g.CO, OWs = g.OWs;
       const int pbase = (n * g.OHs + g.oy0) * OWs + g.ox0 + ox * g.oxs;
       T* __restrict__ out = reinterpret_cast<T*>(a.out);
+      const T* __restrict__ mk = reinterpret_cast<const T*>(a.mask);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const int oy = oy0 + wave * MT + i;
@@ -895,6 +923,15 @@ void conv_patch_kernel(ConvArgs a) {
           for (int r = 0; r < 4; ++r) {
             const float x = acc[i][j][r] + bv[j][r];
             v[r] = relu ? vmax(x, 0.f) : x;
+          }
+          if (mk) {
+            const uint2 m = *reinterpret_cast<const uint2*>(mk + o + ch0);
+            const uint32_t mw[2] = {m.x, m.y};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const T mv = __builtin_bit_cast(T, (unsigned short)(mw[r >> 1] >> (16 * (r & 1))));
+              v[r] = to_f(mv) > 0.f ? v[r] : 0.f;
+            }
           }
           *reinterpret_cast<uint2*>(out + o + ch0) = uint2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
         }
@@ -1085,6 +1122,7 @@ struct WgradTrArgs {
   const void* dout;  // [N][OHs][OWs][CO]
   float* part;       // [Z][CO][Kf]
   float* bpart;      // [nphase][Z][CO] or null
+  int upt, upl, PH, PW;  // phase-shared launches (wgrad_trp_kernel): the union patch
 };
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -1381,25 +1419,216 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
   }
 }
 
-// dst[e] += sum_{z < nz} part[z * n + e], always in the same order (bit-reproducible): a
-// workgroup owns 16 consecutive e; its 16 z-lanes each sum z = zl, zl + 16, ... in order,
-// then lane zl = 0 adds the 16 lane sums in order. Launch with (n + 15) / 16 workgroups.
-__global__ __launch_bounds__(256) void ordered_sum_kernel(const float* __restrict__ part, int nz,
-                                                          long long n, float* __restrict__ dst) {
-  __shared__ float red[16][17];
-  const int el = threadIdx.x & 15, zl = threadIdx.x >> 4;
-  const long long e = blockIdx.x * 16LL + el;
-  float t = 0.f;
-  if (e < n)
-    for (int z = zl; z < nz; z += 16) t += part[(long long)z * n + e];
-  red[zl][el] = t;
-  __syncthreads();
-  if (zl == 0 && e < n) {
-    float s = 0.f;
+// Conv2DTranspose stride 2 (four output phases (oy0, ox0) = (p >> 1, p & 1) over one tile
+// grid): a workgroup owns a 16 x 16 phase tile of ALL four phases, i.e. the 32 x 32 dOut
+// region, staged de-interleaved per phase ([phase][256 pixels][16 co], the wgrad_tr_kernel
+// layout), and ONE union input patch serves every phase's taps. The (phase, tap) blocks
+// (25 for a 5 x 5 kernel) are split into contiguous runs of <= 7 per wave, so a wave reloads
+// its dOut fragment only when the run crosses into the next phase; wave w also owns the
+// bias gradient of phase w (bpart[w][z]). Same fixed-order partial sums as wgrad_tr_kernel.
+template <typename T>
+__global__ __launch_bounds__(256) void wgrad_trp_kernel(WgradTrArgs a) {
+  constexpr int CH = 16, COT = 16, DST = COT + 8, PST = CH + 8, MAXT = 7;
+  __shared__ __attribute__((aligned(16))) T sD[4 * 256 * DST];
+  __shared__ __attribute__((aligned(16))) T sP[400 * PST];
+  const Geo& g0 = a.g[0];
+  const int chunk = blockIdx.y / a.ncog, cog = blockIdx.y - (blockIdx.y / a.ncog) * a.ncog;
+  const int c0 = chunk * CH, co0 = cog * COT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntx = (g0.OW + 15) / 16, nty = (g0.OH + 15) / 16;
+  const long long ntiles = (long long)g0.N * nty * ntx;
+  const long long t_begin = blockIdx.x * ntiles / a.Z, t_end = (blockIdx.x + 1) * ntiles / a.Z;
+  const int PW = a.PW, PH = a.PH;
+  const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
+  const T* __restrict__ dout = reinterpret_cast<const T*>(a.dout);
+  const int CO = g0.CO, OHs = g0.OHs, OWs = g0.OWs;
+
+  // this wave's run of (phase, tap) blocks: u in [ub, ue) over the phases' taps in order
+  int U = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) s += red[k][el];
-    dst[e] += s;
+  for (int p = 0; p < 4; ++p) U += a.g[p].KH * a.g[p].KW;
+  const int ub = wave * U / 4, ue = (wave + 1) * U / 4;
+  int aoff[MAXT], boff[MAXT], tph[MAXT], ttap[MAXT];
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) {
+    int u = ub + tt, p = 0;
+    while (p < 3 && u >= a.g[p].KH * a.g[p].KW) { u -= a.g[p].KH * a.g[p].KW; ++p; }
+    const Geo& g = a.g[p];
+    const int jy = u / max(g.KW, 1), jx = u - (u / max(g.KW, 1)) * g.KW;
+    tph[tt] = p;
+    ttap[tt] = u;
+    aoff[tt] = p * 256 * DST;
+    boff[tt] = ((a.upt - g.pad_t + jy) * PW + a.upl - g.pad_l + jx) * PST;
   }
+
+  f32x4 acc[MAXT];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 bacc = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = a.bpart && chunk == 0;
+  s16x8 ones;
+  const short one = __builtin_bit_cast(short, from_f<T>(1.f));
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = one;
+  const int g4 = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int prow = g4 >> 1, pcol = 8 * (g4 & 1) + q;
+
+  uint4 rd[8];  // 32 x 32 dOut pixels x 16 co: 2048 uint4
+  uint4 rp[4];  // <= 20 x 20 patch pixels x 16 ci: 800 uint4
+  auto tile_org = [&](long long tile, int& n, int& oyt, int& oxt) {
+    n = (int)(tile / (nty * ntx));
+    const int trem = (int)(tile - (long long)n * nty * ntx);
+    oyt = (trem / ntx) * 16;
+    oxt = (trem - (trem / ntx) * ntx) * 16;
+  };
+  auto fetch = [&](long long tile) {
+    int n, oyt, oxt;
+    tile_org(tile, n, oyt, oxt);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u;
+      const int pix = e >> 1, v = e & 1;
+      const int y = 2 * oyt + (pix >> 5), x = 2 * oxt + (pix & 31);
+      rd[u] = uint4{0u, 0u, 0u, 0u};
+      if (y < OHs && x < OWs)
+        rd[u] = *reinterpret_cast<const uint4*>(dout + (((long long)n * OHs + y) * OWs + x) * CO + co0 + 8 * v);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u;
+      const int pix = e >> 1, v = e & 1;
+      const int py = pix / PW, px = pix - (pix / PW) * PW;
+      const int iy = oyt - a.upt + py, ix = oxt - a.upl + px;
+      rp[u] = uint4{0u, 0u, 0u, 0u};
+      if (pix < PH * PW && (unsigned)iy < (unsigned)g0.IH && (unsigned)ix < (unsigned)g0.IW)
+        rp[u] = *reinterpret_cast<const uint4*>(in + (((long long)n * g0.IH + iy) * g0.IW + ix) * g0.C + c0 + 8 * v);
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u;
+      const int pix = e >> 1, v = e & 1;
+      const int y = pix >> 5, x = pix & 31;
+      const int p = 2 * (y & 1) + (x & 1);
+      *reinterpret_cast<uint4*>(sD + (p * 256 + (y >> 1) * 16 + (x >> 1)) * DST + 8 * v) = rd[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u;
+      const int pix = e >> 1, v = e & 1;
+      if (pix < PH * PW) *reinterpret_cast<uint4*>(sP + pix * PST + 8 * v) = rp[u];
+    }
+  };
+  auto afrag = [&](const T* da) {
+    const s16x4 lo = lds_tr16(da), hi = lds_tr16(da + 4 * DST);
+    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+
+  if (t_begin < t_end) fetch(t_begin);
+  for (long long tile = t_begin; tile < t_end; ++tile) {
+    lds_sync();
+    stage();
+    lds_sync();
+    if (tile + 1 < t_end) fetch(tile + 1);
+#pragma unroll 1
+    for (int pg = 0; pg < 8; ++pg) {
+      const int r = 2 * pg + prow;
+      const int pix = r * 16 + pcol, ppix = r * PW + pcol;
+      s16x8 af = afrag(sD + aoff[0] + pix * DST + 4 * pp);
+#pragma unroll
+      for (int tt = 0; tt < MAXT; ++tt) {
+        if (ub + tt >= ue) break;  // wave-uniform
+        if (tt > 0 && tph[tt] != tph[tt - 1]) af = afrag(sD + aoff[tt] + pix * DST + 4 * pp);
+        const T* pb = sP + ppix * PST + boff[tt] + 4 * pp;
+        const s16x4 lo = lds_tr16(pb), hi = lds_tr16(pb + 4 * PST);
+        const s16x8 bf = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[tt] = mfma_s16<T>(af, bf, acc[tt]);
+      }
+      if (do_bias) bacc = mfma_s16<T>(afrag(sD + wave * 256 * DST + pix * DST + 4 * pp), ones, bacc);
+    }
+  }
+  const long long z = blockIdx.x;
+  const int ci = c0 + (lane & 15);
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) {
+    if (ub + tt >= ue) break;
+    const int col = wcol(a.g[tph[tt]], ttap[tt], ci);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int co = co0 + 4 * (lane >> 4) + rr;
+      if (co < CO) a.part[(z * CO + co) * g0.Kf + col] = acc[tt][rr];
+    }
+  }
+  if (do_bias && (lane & 15) == 0) {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int co = co0 + 4 * (lane >> 4) + rr;
+      if (co < CO) a.bpart[((long long)wave * a.Z + z) * CO + co] = bacc[rr];
+    }
+  }
+}
+
+// dst[e] += sum_{z < nz} part[z * n + e], always in the same order (bit-reproducible). One
+// launch carries two such sums (the weight and the bias gradient): blocks [0, nb0) do job 0.
+// A workgroup owns EW consecutive e (EW = 16, 4 or 1, fixed per job so that a small n still
+// spreads over enough workgroups) and ZL = 256 / EW z-lanes; lane zl sums z = zl, zl + ZL,
+// ... in order (8 loads in flight), then the lane sums meet in a fixed pairwise tree.
+struct SumJob {
+  const float* part;
+  float* dst;
+  long long n;
+  int nz, ew;
+};
+
+__global__ __launch_bounds__(256) void ordered_sum_kernel(SumJob j0, SumJob j1, unsigned nb0) {
+  __shared__ float red[256];
+  const bool second = blockIdx.x >= nb0;
+  const SumJob j = second ? j1 : j0;
+  const long long blk = second ? blockIdx.x - nb0 : blockIdx.x;
+  const int EW = j.ew, ZL = 256 / EW;
+  const int el = threadIdx.x % EW, zl = threadIdx.x / EW;
+  const long long e = blk * EW + el;
+  float t = 0.f;
+  if (e < j.n) {
+    const float* p = j.part + e;
+    int z = zl;
+    for (; z + 7 * ZL < j.nz; z += 8 * ZL) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = p[(long long)(z + k * ZL) * j.n];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t += v[k];
+    }
+    for (; z < j.nz; z += ZL) t += p[(long long)z * j.n];
+  }
+  red[threadIdx.x] = t;
+  __syncthreads();
+  for (int w = ZL / 2; w >= 1; w >>= 1) {
+    if (zl < w) red[threadIdx.x] += red[threadIdx.x + w * EW];
+    __syncthreads();
+  }
+  if (zl == 0 && e < j.n) j.dst[e] += red[threadIdx.x];
+}
+
+// the sums of one weight-gradient launch: dw over nz slices, db (if any) over nzb slices
+inline SumJob sum_job(const float* part, int nz, long long n, float* dst) {
+  SumJob j{part, dst, n, nz, 16};
+  if ((n + 15) / 16 < 256) j.ew = (n + 3) / 4 >= 128 ? 4 : 1;
+  return j;
+}
+inline unsigned sum_blocks(const SumJob& j) { return (unsigned)((j.n + j.ew - 1) / j.ew); }
+inline void launch_ordered_sums(const float* part, int nz, long long n, float* dw, const float* bpart,
+                                int nzb, long long nb, float* db, hipStream_t st) {
+  const SumJob j0 = sum_job(part, nz, n, dw);
+  SumJob j1{};
+  unsigned blocks = sum_blocks(j0);
+  if (db) {
+    j1 = sum_job(bpart, nzb, nb, db);
+    blocks += sum_blocks(j1);
+  }
+  hipLaunchKernelGGL(ordered_sum_kernel, dim3(blocks), dim3(256), 0, st, j0, j1, sum_blocks(j0));
 }
 
 // ------------------------------------------------------------------ elementwise
@@ -1582,6 +1811,15 @@ size_t patch_lds_bytes(const ConvArgs& a, int nph, int NT, bool pair) {
   return (elems * sizeof(T) + 15) / 16 * 16;
 }
 
+// output-channel blocks of 16 per workgroup: all of them (up to 4) unless that leaves fewer
+// than 2 workgroups per CU (a small batch at 16 x 16 output: 128 tiles), then narrower
+// blocks over more workgroups (each re-stages the patch, an L2 hit)
+inline int patch_nt(int CO, unsigned tiles) {
+  int nt = std::min(4, (CO + 15) / 16);
+  while (nt > 1 && (unsigned long long)tiles * ((CO + 16 * nt - 1) / (16 * nt)) < 512) nt = (nt + 1) / 2;
+  return nt;
+}
+
 template <typename T, int CC>
 int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   // all phases of a dilated conv in one workgroup when they share a tile grid and the
@@ -1615,7 +1853,7 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   for (int i = 0; i < nph; ++i)
     tiles = std::max(tiles, (unsigned)(a.g[i].N * ((a.g[i].OH + 15) / 16) * ((a.g[i].OW + 15) / 16)));
   const int CO = a.g[0].CO;
-  const int nt = std::min(4, (CO + 15) / 16);
+  const int nt = patch_nt(CO, tiles);
   // Conv2DTranspose stride 2: (tile, row phase) workgroups with whole-row stores
   bool pair = a.ph_shared && nph == 4 && !a.pool && !a.mask && !a.logits && !a.out_f32 &&
               CO == 16 * nt && getenv_flag("SPECENH_CONVT_PAIR");
@@ -1653,8 +1891,30 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "conv launch");
 }
 
-// which LDS-patch chunking applies (0 = none: use the generic gather kernel)
+// stride-2 conv (Conv2DTranspose input gradient) over de-interleaved 16-channel patches
+template <typename T>
+int launch_patch_s2(const ConvArgs& a, hipStream_t st) {
+  const Geo& g = a.g[0];
+  const unsigned tiles = (unsigned)(g.N * ((g.OH + 15) / 16) * ((g.OW + 15) / 16));
+  const int nt = patch_nt(g.CO, tiles);
+  const int sph = (30 + g.KH + 1) / 2, spw = (30 + g.KW + 1) / 2;
+  const size_t lds = ((size_t)4 * sph * spw * Patch<16>::PST * sizeof(T) + 15) / 16 * 16;
+  const dim3 grid(tiles, (unsigned)((g.CO + 16 * nt - 1) / (16 * nt)), 1);
+#define SPECENH_S2(NT) hipLaunchKernelGGL((conv_patch_kernel<T, NT, 16, false, false, true>), grid, dim3(256), lds, st, a)
+  if (nt == 1) SPECENH_S2(1);
+  else if (nt == 2) SPECENH_S2(2);
+  else if (nt == 3) SPECENH_S2(3);
+  else SPECENH_S2(4);
+#undef SPECENH_S2
+  return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "conv launch");
+}
+
+// which LDS-patch chunking applies (0 = none: use the generic gather kernel; -2: the
+// stride-2 16-channel patch kernel)
 int patch_cc(const ConvArgs& a, int nph) {
+  if (nph == 1 && a.g[0].stride == 2 && a.g[0].C % 16 == 0 && a.g[0].KH <= 5 && a.g[0].KW <= 5 &&
+      !a.pool && !getenv_flag("SPECENH_CONV_NO_S2"))
+    return -2;
   if (nph != 1 && nph != 4) return 0;
   for (int i = 0; i < nph; ++i) {
     const Geo& g = a.g[i];
@@ -1673,6 +1933,7 @@ int launch_fwd(const ConvArgs& a, int nph, hipStream_t st) {
   if constexpr (!__is_same(T, float)) {
     if (!getenv_flag("SPECENH_CONV_NO_PATCH")) {
       switch (patch_cc(a, nph)) {
+        case -2: return launch_patch_s2<T>(a, st);
         case 64: return launch_patch<T, 64>(a, nph, st);
         case 32: return launch_patch<T, 32>(a, nph, st);
         case 16: return launch_patch<T, 16>(a, nph, st);
@@ -1756,6 +2017,38 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
   long long z = 4096 / std::max(1LL, (long long)nchunk * a.ncog * nph);
   z = std::min<long long>(z, std::max(1LL, tiles / 4));
   a.Z = (int)std::max(1LL, std::min<long long>(z, wgrad_tr_zmax(g0.CO, g0.Kf)));
+  // Conv2DTranspose stride 2: all four phases per workgroup over one union patch
+  if (!c1 && nph == 4 && g0.CO % 16 == 0 && !getenv_flag("SPECENH_WGRAD_PERPHASE")) {
+    bool ok = true;
+    int upt = -1 << 20, upl = -1 << 20, lo_y = 1 << 20, hi_y = -(1 << 20), lo_x = 1 << 20,
+        hi_x = -(1 << 20), U = 0;
+    for (int i = 0; i < nph; ++i) {
+      const Geo& g = w.g[i];
+      ok = ok && g.OH == g0.OH && g.OW == g0.OW && g.oys == 2 && g.oxs == 2 && g.oy0 == i / 2 &&
+           g.ox0 == i % 2 && g.OHs == 2 * g.OH && g.OWs == 2 * g.OW;
+      upt = std::max(upt, g.pad_t);
+      upl = std::max(upl, g.pad_l);
+      lo_y = std::min(lo_y, -g.pad_t);
+      hi_y = std::max(hi_y, 15 - g.pad_t + g.KH - 1);
+      lo_x = std::min(lo_x, -g.pad_l);
+      hi_x = std::max(hi_x, 15 - g.pad_l + g.KW - 1);
+      U += g.KH * g.KW;
+    }
+    if (ok && hi_y - lo_y + 1 <= 20 && hi_x - lo_x + 1 <= 20 && U <= 28) {
+      a.upt = upt;
+      a.upl = upl;
+      a.PH = hi_y - lo_y + 1;
+      a.PW = hi_x - lo_x + 1;
+      a.ncog = g0.CO / 16;
+      long long zp = 4096 / std::max(1LL, (long long)nchunk * a.ncog);
+      zp = std::min<long long>(zp, std::max(1LL, tiles / 4));
+      a.Z = (int)std::max(1LL, std::min<long long>(zp, wgrad_tr_zmax(g0.CO, g0.Kf)));
+      hipLaunchKernelGGL(wgrad_trp_kernel<T>, dim3((unsigned)a.Z, (unsigned)(nchunk * a.ncog)), dim3(256), 0,
+                         st, a);
+      launch_ordered_sums(a.part, a.Z, (long long)g0.CO * g0.Kf, dw, a.bpart, nph * a.Z, g0.CO, db, st);
+      return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
+    }
+  }
   const dim3 grid((unsigned)a.Z, (unsigned)(nchunk * a.ncog), (unsigned)nph);
   if (c1) {
     if (ntw == 1) hipLaunchKernelGGL((wgrad_tr_kernel<T, 1, true>), grid, dim3(256), 0, st, a);
@@ -1764,11 +2057,7 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
     if (ntw == 1) hipLaunchKernelGGL((wgrad_tr_kernel<T, 1, false>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((wgrad_tr_kernel<T, 2, false>), grid, dim3(256), 0, st, a);
   }
-  const long long n = (long long)g0.CO * g0.Kf;
-  hipLaunchKernelGGL(ordered_sum_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, st, a.part, a.Z, n, dw);
-  if (db)
-    hipLaunchKernelGGL(ordered_sum_kernel, dim3((unsigned)((g0.CO + 15) / 16)), dim3(256), 0, st, a.bpart, nph * a.Z,
-                       (long long)g0.CO, db);
+  launch_ordered_sums(a.part, a.Z, (long long)g0.CO * g0.Kf, dw, a.bpart, nph * a.Z, g0.CO, db, st);
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
 }
 
@@ -1795,11 +2084,7 @@ int launch_wgrad(WgradArgs& a, int nph, float* dw, float* db, hipStream_t st) {
   else if (p.nt == 3) SPECENH_WG(3);
   else SPECENH_WG(4);
 #undef SPECENH_WG
-  const long long n = (long long)g0.CO * g0.Kf;
-  hipLaunchKernelGGL(ordered_sum_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, st, a.part, p.Z, n, dw);
-  if (db)
-    hipLaunchKernelGGL(ordered_sum_kernel, dim3((unsigned)((g0.CO + 15) / 16)), dim3(256), 0, st, a.bpart, nph * p.Z,
-                       (long long)g0.CO, db);
+  launch_ordered_sums(a.part, p.Z, (long long)g0.CO * g0.Kf, dw, a.bpart, nph * p.Z, g0.CO, db, st);
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
 }
 
@@ -1831,9 +2116,9 @@ int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, cons
     return set_error(SPECENH_EUNSUPPORTED, "fused max-pool: plain conv with even output only");
   hipStream_t st = (hipStream_t)stream;
   // 1 input or 1 output channel: direct VALU convolution (conv_narrow.hip)
-  if (stride == 1 && in_dil == 1 && !mask && !getenv_flag("SPECENH_CONV_NO_NARROW")) {
+  if (stride == 1 && in_dil == 1 && !getenv_flag("SPECENH_CONV_NO_NARROW")) {
     const int r = launch_conv_narrow(dtype, in, N, IH, IW, C, w_gemm, KH, KW, CO, bias, pad_t,
-                                     pad_l, OH, OW, act, out, out_f32, logits, pool2, argmax, st);
+                                     pad_l, OH, OW, act, out, out_f32, logits, pool2, argmax, mask, st);
     if (r != 0) return r < 0 ? r : SPECENH_OK;
   }
   if (dtype == SPECENH_DTYPE_F32) return launch_fwd<float>(a, nph, st);

@@ -20,6 +20,7 @@
 // Accumulation is fp32 in both (products of two 16-bit values are exact in fp32).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <string>
 
@@ -42,6 +43,8 @@ struct NarrowArgs {
   int N, IH, IW, C, OH, OW, CO;
   int pad_t, pad_l;
   int act, out_f32;
+  const void* mask;  // conv_c1_kernel, no pool: out = 0 where mask <= 0 (backward of a ReLU)
+  int band_steps;  // conv_co1_kernel: TR-row steps per workgroup (blockIdx.y = band)
 };
 
 __device__ __forceinline__ float act_f(float v, int act) {
@@ -96,12 +99,23 @@ __global__ __launch_bounds__(256) void conv_c1_kernel(NarrowArgs a) {
   const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
   const T* __restrict__ W = reinterpret_cast<const T*>(a.w);
 
-  for (int e = tid; e < PH * PST; e += 256) {
-    const int py = e / PST, px = e - (e / PST) * PST;
-    const int iy = iy0 + py, ix = ix0 + px;
-    const bool ok = px < C1_TILE + K - 1 && (unsigned)iy < (unsigned)a.IH &&
-                    (unsigned)ix < (unsigned)a.IW;
-    sP[e] = ok ? in[((long long)n * a.IH + iy) * a.IW + ix] : (T)0.f;
+  {
+    // every load of the patch in flight at once (unconditional, from a clamped address)
+    constexpr int NE = (PH * PST + 255) / 256;
+    T v[NE];
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      const int e = tid + 256 * k;
+      const int py = e / PST, px = e - (e / PST) * PST;
+      const int iy = iy0 + py, ix = ix0 + px;
+      const bool ok = e < PH * PST && px < C1_TILE + K - 1 && (unsigned)iy < (unsigned)a.IH &&
+                      (unsigned)ix < (unsigned)a.IW;
+      v[k] = in[ok ? ((long long)n * a.IH + iy) * a.IW + ix : 0];
+      if (!ok) v[k] = (T)0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < NE; ++k)
+      if (tid + 256 * k < PH * PST) sP[tid + 256 * k] = v[k];
   }
   for (int e = tid; e < 16 * NQ4; e += 256) {
     const int cl = e / NQ4, q = e - (e / NQ4) * NQ4;
@@ -235,7 +249,26 @@ __global__ __launch_bounds__(256) void conv_c1_kernel(NarrowArgs a) {
       for (int dx = 0; dx < 2; ++dx) {
         if (!okpix[dy][dx]) continue;
         T* dst = reinterpret_cast<T*>(a.out) + opix[dy][dx];
-        const uint32_t* w8 = pk[dy][dx];
+        uint32_t* w8 = pk[dy][dx];
+        if (a.mask) {
+          const T* mk = reinterpret_cast<const T*>(a.mask) + opix[dy][dx];
+          uint32_t m8[8];
+          if (nco == 16 && (a.CO & 7) == 0) {
+            const uint4 m0 = reinterpret_cast<const uint4*>(mk)[0], m1 = reinterpret_cast<const uint4*>(mk)[1];
+            m8[0] = m0.x; m8[1] = m0.y; m8[2] = m0.z; m8[3] = m0.w;
+            m8[4] = m1.x; m8[5] = m1.y; m8[6] = m1.z; m8[7] = m1.w;
+          } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) m8[i] = 0u;
+            for (int cl = 0; cl < nco; ++cl) m8[cl >> 1] |= tbits(mk[cl]) << (16 * (cl & 1));
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const uint32_t lo = (float)from_bits<T>(m8[i] & 0xffffu) > 0.f ? 0x0000ffffu : 0u;
+            const uint32_t hi = (float)from_bits<T>(m8[i] >> 16) > 0.f ? 0xffff0000u : 0u;
+            w8[i] &= lo | hi;
+          }
+        }
         if (nco == 16 && (a.CO & 7) == 0) {
           reinterpret_cast<uint4*>(dst)[0] = uint4{w8[0], w8[1], w8[2], w8[3]};
           reinterpret_cast<uint4*>(dst)[1] = uint4{w8[4], w8[5], w8[6], w8[7]};
@@ -247,8 +280,10 @@ __global__ __launch_bounds__(256) void conv_c1_kernel(NarrowArgs a) {
 }
 
 // ------------------------------------------------------------------ CO == 1
-// One workgroup streams a 128-column strip of one image top to bottom, TR output rows per
-// step. The input rows live in an LDS ring of TR + K - 1 rows: each step reads only its TR
+// One workgroup streams a band of a 128-column strip of one image top to bottom (bands of
+// band_steps x TR output rows, so that a batch of 128 x 128 images still spreads over the
+// whole chip; a band re-reads the K - 1 halo rows above it), TR output rows per step. The
+// input rows live in an LDS ring of TR + K - 1 rows: each step reads only its TR
 // new rows from HBM (no halo re-reads), and they are loaded into registers one step ahead,
 // while the current rows compute.
 template <int C>
@@ -287,7 +322,8 @@ __global__ __launch_bounds__(256) void conv_co1_kernel(NarrowArgs a) {
   const int n = blockIdx.x / ntx;
   const int ox0 = (blockIdx.x - n * ntx) * TW;
   const int ix0 = ox0 - a.pad_l;
-  const int nsteps = (a.OH + TR - 1) / TR;
+  const int step0 = blockIdx.y * a.band_steps;
+  const int nsteps = min((a.OH + TR - 1) / TR, step0 + a.band_steps);
   const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
   const T* __restrict__ img = in + (long long)n * a.IH * a.IW * C;
 
@@ -310,7 +346,7 @@ __global__ __launch_bounds__(256) void conv_co1_kernel(NarrowArgs a) {
   // prologue: the first step's RN rows
   for (int e = tid; e < RN * ROWP; e += 256) {
     const int rr = e / ROWP, pe = e - rr * ROWP;
-    const int iy = -a.pad_t + rr;
+    const int iy = step0 * TR - a.pad_t + rr;
     put(iy, pe, fetch(iy, pe));
   }
   for (int e = tid; e < K * K * CW; e += 256)
@@ -319,7 +355,7 @@ __global__ __launch_bounds__(256) void conv_co1_kernel(NarrowArgs a) {
 
   const int g = tid % (TW / P), r = tid / (TW / P);
   const float bb = a.bias ? a.bias[0] : 0.f;
-  for (int step = 0; step < nsteps; ++step) {
+  for (int step = step0; step < nsteps; ++step) {
     // next step's TR new rows into registers (their latency hides under this step)
     const int ny0 = (step + 1) * TR - a.pad_t + K - 1;  // first new input row of step + 1
     uint4 nx[Rg::PPT];
@@ -425,8 +461,15 @@ int launch_co1(const NarrowArgs& a, hipStream_t st) {
     attr = true;
   }
   const long long strips = (long long)a.N * ((a.OW + Co1<C>::TW - 1) / Co1<C>::TW);
-  hipLaunchKernelGGL((conv_co1_kernel<T, C, K>), dim3((unsigned)strips), dim3(256), Rg::LDS, st,
-                     a);
+  // bands: ~1024 workgroups (every CU busy) unless the halo re-reads would exceed ~25%
+  const int steps = (a.OH + Co1<C>::TR - 1) / Co1<C>::TR;
+  const int min_steps = std::max(1, (4 * (K - 1) + Co1<C>::TR - 1) / Co1<C>::TR);
+  long long bands = std::max(1LL, std::min<long long>(steps, (1024 + strips - 1) / strips));
+  NarrowArgs b = a;
+  b.band_steps = std::max<int>(min_steps, (int)((steps + bands - 1) / bands));
+  bands = (steps + b.band_steps - 1) / b.band_steps;
+  hipLaunchKernelGGL((conv_co1_kernel<T, C, K>), dim3((unsigned)strips, (unsigned)bands), dim3(256),
+                     Rg::LDS, st, b);
   return hipGetLastError() == hipSuccess ? 1 : set_error(SPECENH_EHIP, "conv_co1 launch");
 }
 
@@ -442,6 +485,7 @@ int launch_c1(const NarrowArgs& a, bool pool, hipStream_t st) {
 
 template <typename T>
 int dispatch(const NarrowArgs& a, int K, bool pool, hipStream_t st) {
+  if (a.mask && (a.C != 1 || pool || a.out_f32 || a.act == SPECENH_ACT_SIGMOID)) return 0;  // act(0) = 0
   if (a.C == 1) {
     if (a.logits) return 0;
     switch (K) {
@@ -475,17 +519,18 @@ int dispatch(const NarrowArgs& a, int K, bool pool, hipStream_t st) {
 }  // namespace
 
 // Narrow-channel direct convolution (C == 1, or CO == 1 with C in {16, 32}), bf16/f16,
-// stride 1, undilated, square odd kernel <= 7, no ReLU mask. Returns 1 when launched, 0
+// stride 1, undilated, square odd kernel <= 7 (a ReLU mask only for C == 1 without pooling
+// or fp32 output). Returns 1 when launched, 0
 // when the shape is not covered (the caller takes the MFMA path), < 0 on error.
 int launch_conv_narrow(int dtype, const void* in, int N, int IH, int IW, int C, const void* w,
                        int KH, int KW, int CO, const float* bias, int pad_t, int pad_l, int OH,
                        int OW, int act, void* out, int out_f32, float* logits, int pool,
-                       unsigned char* argmax, hipStream_t st) {
+                       unsigned char* argmax, const void* mask, hipStream_t st) {
   if (dtype == SPECENH_DTYPE_F32 || KH != KW || (KH & 1) == 0 || KH > 7) return 0;
   if (C != 1 && CO != 1) return 0;
   if (pool && ((OH & 1) || (OW & 1))) return 0;
   NarrowArgs a{in, w, bias, out, logits, argmax, N, IH, IW, C, OH, OW, CO,
-               pad_t, pad_l, act, out_f32};
+               pad_t, pad_l, act, out_f32, mask, 0};
   if (dtype == SPECENH_DTYPE_BF16) return dispatch<__bf16>(a, KH, pool != 0, st);
   return dispatch<_Float16>(a, KH, pool != 0, st);
 }

@@ -1,7 +1,8 @@
 """Weight / bias gradients of the 16-bit conv layers (specenh_conv2d_wgrad) on the GPU.
 
-The MFMA path (csrc/conv_ae.hip wgrad_tr_kernel: C % 16 == 0 or C == 1 via an LDS im2col
-block, transposed LDS fragment reads)
+The MFMA paths (csrc/conv_ae.hip wgrad_tr_kernel: C % 16 == 0 or C == 1 via an LDS im2col
+block, transposed LDS fragment reads; wgrad_trp_kernel: the four Conv2DTranspose phases per
+workgroup, SPECENH_WGRAD_PERPHASE=1 forces one phase per workgroup)
 and the generic gather kernel (SPECENH_WGRAD_GENERIC=1) are both checked against the
 float64 im2col product dW = dZ^T A of the header's gather formula (test_ae_mapping.igemm)
 on the same bf16 / f16-rounded operands: products are exact in the fp32 accumulators, so
@@ -36,10 +37,14 @@ def _reference(x, dz, op):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("kind,cin,cout,k,H,W,N", CASES)
-@pytest.mark.parametrize("path", ["mfma", "generic"])
+@pytest.mark.parametrize("path", ["mfma", "mfma_perphase", "generic"])
 def test_wgrad_matches_im2col(gpu_device, monkeypatch, dtype, kind, cin, cout, k, H, W, N, path):
     if path == "generic":
         monkeypatch.setenv("SPECENH_WGRAD_GENERIC", "1")
+    elif path == "mfma_perphase":
+        if kind != "convT":
+            pytest.skip("phase-shared launches are Conv2DTranspose only")
+        monkeypatch.setenv("SPECENH_WGRAD_PERPHASE", "1")
     op = ae.ConvOp(kind, cin, cout, k, "relu", stride=2 if kind == "convT" else 1)
     OH, OW = op.out_hw(H, W)
     rng = np.random.default_rng(cin * 131 + cout * 7 + k + H)
@@ -55,7 +60,10 @@ def test_wgrad_matches_im2col(gpu_device, monkeypatch, dtype, kind, cin, cout, k
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_wgrad_mfma_is_bitwise_deterministic(gpu_device, dtype):
+@pytest.mark.parametrize("perphase", [False, True])
+def test_wgrad_mfma_is_bitwise_deterministic(gpu_device, monkeypatch, dtype, perphase):
+    if perphase:
+        monkeypatch.setenv("SPECENH_WGRAD_PERPHASE", "1")
     op = ae.ConvOp("convT", 32, 16, 5, "relu", stride=2)
     rng = np.random.default_rng(5)
     x = torch.tensor(rng.standard_normal((4, 32, 32, 32)), dtype=dtype, device=gpu_device)

@@ -45,6 +45,10 @@ int launch_conv_narrow(int dtype, const void* in, int N, int IH, int IW, int C, 
                        int KH, int KW, int CO, const float* bias, int pad_t, int pad_l, int OH,
                        int OW, int act, void* out, int out_f32, float* logits, int pool,
                        unsigned char* argmax, const void* mask, hipStream_t st);  // conv_narrow.hip
+int launch_conv_c1_mfma(int dtype, const void* in, int N, int IH, int IW, int C, const void* w,
+                        int KH, int KW, int CO, const float* bias, int pad_t, int pad_l, int OH,
+                        int OW, int act, void* out, int out_f32, float* logits, int pool,
+                        unsigned char* argmax, const void* mask, hipStream_t st);  // conv_c1_mfma.hip
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -1570,6 +1574,139 @@ __global__ __launch_bounds__(256) void wgrad_trp_kernel(WgradTrArgs a) {
   }
 }
 
+// One output channel, 16 input channels (the last Conv2D, VAE/manual_scan_3layers.py:199):
+//   dW[jy][jx][ci] = sum_p dOut[p] in[p + (jy, jx) - pad][ci]
+//                  = sum_q in[q + (jy, 0) - pad][ci] * dOut[q - (0, jx)]       (q = p + (0, jx))
+// so with the pixels q of a tile (16 rows x 24 columns) as the MFMA reduction, A = the input
+// patch shifted by jy (rows = ci, ds_read_b64_tr_b16 from [pixel][ci] rows) and B = dOut
+// shifted by jx (columns = jx): one MFMA per (32 pixels, jy) yields all KW taps of a kernel
+// row, 5x fewer MFMAs than one per tap with 15 of 16 rows idle. The KW shifted copies of
+// the 16 x 16 dOut tile live in LDS with their zero margins written once. A workgroup is
+// ONE wave over a run of tiles (no barriers beyond the wave's own LDS ordering), the next
+// tile prefetched in registers; the bias gradient is the lanes' fp32 sums of dOut, reduced
+// in a fixed order. Partial sums per run go to part[z] / bpart[z] (ordered_sum_kernel).
+template <typename T>
+__global__ __launch_bounds__(64) void wgrad_co1_kernel(WgradTrArgs a) {
+  constexpr int QC = 24;       // q columns per tile row (16 + KW - 1 <= 20, 3 groups of 8)
+  constexpr int PSTC = 24;     // patch pixel stride (16 ci + 8: tr reads 2-way at most)
+  constexpr int PR = 20;       // patch rows (16 + KH - 1, KH <= 5)
+  constexpr int NPV = (PR * QC * 2 + 63) / 64;  // patch uint4 per lane (15)
+  __shared__ __attribute__((aligned(16))) T sP[PR * QC * PSTC];
+  __shared__ __attribute__((aligned(16))) T sB[5 * 16 * QC];
+  const Geo& g = a.g[0];
+  const int lane = threadIdx.x;
+  const int KH = g.KH, KW = g.KW;
+  const int ntx = (g.OW + 15) / 16, nty = (g.OH + 15) / 16;
+  const long long ntiles = (long long)g.N * nty * ntx;
+  const long long t_begin = blockIdx.x * ntiles / a.Z, t_end = (blockIdx.x + 1) * ntiles / a.Z;
+  const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
+  const T* __restrict__ dout = reinterpret_cast<const T*>(a.dout);
+
+  // zero margins of the shifted dOut copies (columns outside [s, s + 16) stay zero)
+  for (int e = lane; e < 5 * 16 * QC / 8; e += 64)
+    reinterpret_cast<uint4*>(sB)[e] = uint4{0u, 0u, 0u, 0u};
+
+  f32x4 acc[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+
+  const int g4 = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, n16 = lane & 15;
+  const int sft = min(n16, KW - 1);  // B column jx (columns >= KW are never stored)
+
+  uint4 rp[NPV];
+  uint2 rd;
+  auto tile_org = [&](long long tile, int& n, int& oyt, int& oxt) {
+    n = (int)(tile / (nty * ntx));
+    const int trem = (int)(tile - (long long)n * nty * ntx);
+    oyt = (trem / ntx) * 16;
+    oxt = (trem - (trem / ntx) * ntx) * 16;
+  };
+  auto fetch = [&](long long tile) {
+    int n, oyt, oxt;
+    tile_org(tile, n, oyt, oxt);
+    {  // dOut: lane = (row lane >> 2, columns 4 (lane & 3) .. + 3)
+      const int oy = oyt + (lane >> 2), ox = oxt + 4 * (lane & 3);
+      const bool full = oy < g.OH && ox + 3 < g.OW && (g.OW & 3) == 0;
+      const long long o = ((long long)n * g.OH + min(oy, g.OH - 1)) * g.OW;
+      if (full) {
+        rd = *reinterpret_cast<const uint2*>(dout + o + ox);
+      } else {
+        uint32_t w[2] = {0u, 0u};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (oy < g.OH && ox + k < g.OW)
+            w[k >> 1] |= (uint32_t)__builtin_bit_cast(unsigned short, dout[o + ox + k]) << (16 * (k & 1));
+        rd = uint2{w[0], w[1]};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NPV; ++u) {
+      const int e = min(lane + 64 * u, PR * QC * 2 - 1);
+      const int pix = e >> 1, v = e & 1;
+      const int py = pix / QC, px = pix - (pix / QC) * QC;
+      const int iy = oyt - g.pad_t + py, ix = oxt - g.pad_l + px;
+      const bool ok = (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW;
+      rp[u] = *reinterpret_cast<const uint4*>(in + (ok ? (((long long)n * g.IH + iy) * g.IW + ix) * 16 : 0) + 8 * v);
+      if (!ok) rp[u] = uint4{0u, 0u, 0u, 0u};
+    }
+  };
+
+  if (t_begin < t_end) fetch(t_begin);
+  for (long long tile = t_begin; tile < t_end; ++tile) {
+    lds_sync();  // the previous tile's fragment reads are done
+#pragma unroll
+    for (int u = 0; u < NPV; ++u) {
+      const int e = lane + 64 * u;
+      if (e < PR * QC * 2) *reinterpret_cast<uint4*>(sP + (e >> 1) * PSTC + 8 * (e & 1)) = rp[u];
+    }
+    {
+      const int row = lane >> 2, c0 = 4 * (lane & 3);
+      const uint32_t w[2] = {rd.x, rd.y};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned short b = (unsigned short)(w[k >> 1] >> (16 * (k & 1)));
+        bsum += to_f(__builtin_bit_cast(T, b));
+        for (int s = 0; s < KW; ++s) sB[(s * 16 + row) * QC + c0 + k + s] = __builtin_bit_cast(T, b);
+      }
+    }
+    lds_sync();
+    if (tile + 1 < t_end) fetch(tile + 1);
+    // 12 chunks of 32 pixels: lane group g4 takes the 8-column run (row, cg) = pair 4 c + g4
+#pragma unroll 2
+    for (int c = 0; c < 12; ++c) {
+      const int idx = 4 * c + g4, row = idx / 3, cg = idx - (idx / 3) * 3;
+      const uint4 bq = *reinterpret_cast<const uint4*>(sB + (sft * 16 + row) * QC + 8 * cg);
+      const s16x8 bf = __builtin_bit_cast(s16x8, bq);
+#pragma unroll
+      for (int jy = 0; jy < 5; ++jy) {
+        if (jy >= KH) break;  // uniform
+        const T* pa = sP + ((row + jy) * QC + 8 * cg + q) * PSTC + 4 * pp;
+        const s16x4 lo = lds_tr16(pa), hi = lds_tr16(pa + 4 * PSTC);
+        const s16x8 af = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[jy] = mfma_s16<T>(af, bf, acc[jy]);
+      }
+    }
+  }
+  // D[m = ci][n = jx]: lane holds ci = 4 (lane >> 4) + r, jx = lane & 15
+  const long long z = blockIdx.x;
+  if (n16 < KW) {
+#pragma unroll
+    for (int jy = 0; jy < 5; ++jy) {
+      if (jy >= KH) break;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        a.part[z * g.Kf + (jy * KW + n16) * 16 + 4 * g4 + r] = acc[jy][r];
+    }
+  }
+  if (a.bpart) {
+    // fixed-order tree over the 64 lanes
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) bsum += __shfl_down(bsum, off);
+    if (lane == 0) a.bpart[z] = bsum;
+  }
+}
+
 // dst[e] += sum_{z < nz} part[z * n + e], always in the same order (bit-reproducible). One
 // launch carries two such sums (the weight and the bias gradient): blocks [0, nb0) do job 0.
 // A workgroup owns EW consecutive e (EW = 16, 4 or 1, fixed per job so that a small n still
@@ -1678,6 +1815,50 @@ __global__ void maxpool2_bwd_kernel(const T* __restrict__ dout, const unsigned c
       const long long o = (((long long)n * H + 2 * y + (q >> 1)) * W + 2 * x + (q & 1)) * C + c;
       din[o] = from_f<T>(q == arg ? gv : 0.f);
     }
+  }
+}
+
+// 16-bit, C % 8 == 0: one thread per (pooled pixel, 8 channels): 16-byte loads of dout and
+// the pooled values (ReLU mask), 8 argmax bytes, four 16-byte stores; 32-bit indexing
+// (check_sizes bounds every tensor below 2^31 elements)
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool2_bwd_vec_kernel(const T* __restrict__ dout,
+                                                               const unsigned char* __restrict__ am,
+                                                               const T* __restrict__ pooled, int N,
+                                                               int H, int W, int C,
+                                                               T* __restrict__ din) {
+  const int C8 = C >> 3, PW = W >> 1, PH = H >> 1;
+  const int i = blockIdx.x * 256 + threadIdx.x;  // (n, y, x, c8)
+  if (i >= N * PH * PW * C8) return;
+  const int c8 = i % C8, r = i / C8;
+  const int x = r % PW, r2 = r / PW;
+  const int y = r2 % PH, n = r2 / PH;
+  const int e = r * C + 8 * c8;  // pooled element index
+  const uint4 g = *reinterpret_cast<const uint4*>(dout + e);
+  const uint2 a2 = *reinterpret_cast<const uint2*>(am + e);
+  uint32_t gw[4] = {g.x, g.y, g.z, g.w};
+  if (pooled) {
+    const uint4 pv = *reinterpret_cast<const uint4*>(pooled + e);
+    const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float m = to_f(__builtin_bit_cast(T, (unsigned short)(pw[k >> 1] >> (16 * (k & 1)))));
+      if (!(m > 0.f)) gw[k >> 1] &= 0xffff0000u >> (16 * (k & 1));
+    }
+  }
+  const uint32_t aw[2] = {a2.x, a2.y};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      // channels 2k, 2k+1: keep the gradient half whose argmax is q
+      const uint32_t b0 = (aw[(2 * k) >> 2] >> (8 * ((2 * k) & 3))) & 0xffu;
+      const uint32_t b1 = (aw[(2 * k + 1) >> 2] >> (8 * ((2 * k + 1) & 3))) & 0xffu;
+      o[k] = gw[k] & ((b0 == (uint32_t)q ? 0x0000ffffu : 0u) | (b1 == (uint32_t)q ? 0xffff0000u : 0u));
+    }
+    const int oo = ((n * H + 2 * y + (q >> 1)) * W + 2 * x + (q & 1)) * C + 8 * c8;
+    *reinterpret_cast<uint4*>(din + oo) = uint4{o[0], o[1], o[2], o[3]};
   }
 }
 
@@ -2017,6 +2198,14 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
   long long z = 4096 / std::max(1LL, (long long)nchunk * a.ncog * nph);
   z = std::min<long long>(z, std::max(1LL, tiles / 4));
   a.Z = (int)std::max(1LL, std::min<long long>(z, wgrad_tr_zmax(g0.CO, g0.Kf)));
+  // one output channel over 16 input channels: jy-shifted input x jx-shifted dOut
+  if (nph == 1 && g0.CO == 1 && g0.C == 16 && g0.KH <= 5 && g0.KW <= 5 &&
+      !getenv_flag("SPECENH_WGRAD_NO_CO1")) {
+    a.Z = (int)std::max(1LL, std::min<long long>({tiles / 2, (long long)wgrad_tr_zmax(1, g0.Kf), 4096LL}));
+    hipLaunchKernelGGL(wgrad_co1_kernel<T>, dim3((unsigned)a.Z), dim3(64), 0, st, a);
+    launch_ordered_sums(a.part, a.Z, g0.Kf, dw, a.bpart, a.Z, 1, db, st);
+    return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
+  }
   // Conv2DTranspose stride 2: all four phases per workgroup over one union patch
   if (!c1 && nph == 4 && g0.CO % 16 == 0 && !getenv_flag("SPECENH_WGRAD_PERPHASE")) {
     bool ok = true;
@@ -2115,6 +2304,12 @@ int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, cons
   if (a.pool && (nph != 1 || (OH & 1) || (OW & 1) || mask || logits || out_f32))
     return set_error(SPECENH_EUNSUPPORTED, "fused max-pool: plain conv with even output only");
   hipStream_t st = (hipStream_t)stream;
+  // 1 input channel: window rows as MFMA K runs (conv_c1_mfma.hip)
+  if (stride == 1 && in_dil == 1 && C == 1 && !getenv_flag("SPECENH_CONV_NO_C1MFMA")) {
+    const int r = launch_conv_c1_mfma(dtype, in, N, IH, IW, C, w_gemm, KH, KW, CO, bias, pad_t,
+                                      pad_l, OH, OW, act, out, out_f32, logits, pool2, argmax, mask, st);
+    if (r != 0) return r < 0 ? r : SPECENH_OK;
+  }
   // 1 input or 1 output channel: direct VALU convolution (conv_narrow.hip)
   if (stride == 1 && in_dil == 1 && !getenv_flag("SPECENH_CONV_NO_NARROW")) {
     const int r = launch_conv_narrow(dtype, in, N, IH, IW, C, w_gemm, KH, KW, CO, bias, pad_t,
@@ -2197,7 +2392,16 @@ int specenh_maxpool2_bwd(int dtype, const void* dout, const unsigned char* argma
   if (dtype == 0)
     hipLaunchKernelGGL(maxpool2_bwd_kernel<float>, dim3(grid1d(n)), dim3(256), 0, st,
                        (const float*)dout, argmax, (const float*)pooled, N, H, W, C, (float*)din);
-  else if (dtype == 1)
+  else if ((dtype == 1 || dtype == 2) && (C & 7) == 0 && 4 * n < (1LL << 31)) {
+    const unsigned blocks = (unsigned)((n / 8 + 255) / 256);
+    if (dtype == 1)
+      hipLaunchKernelGGL(maxpool2_bwd_vec_kernel<__bf16>, dim3(blocks), dim3(256), 0, st,
+                         (const __bf16*)dout, argmax, (const __bf16*)pooled, N, H, W, C, (__bf16*)din);
+    else
+      hipLaunchKernelGGL(maxpool2_bwd_vec_kernel<_Float16>, dim3(blocks), dim3(256), 0, st,
+                         (const _Float16*)dout, argmax, (const _Float16*)pooled, N, H, W, C,
+                         (_Float16*)din);
+  } else if (dtype == 1)
     hipLaunchKernelGGL(maxpool2_bwd_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st,
                        (const __bf16*)dout, argmax, (const __bf16*)pooled, N, H, W, C,
                        (__bf16*)din);

@@ -1,0 +1,289 @@
+// conv_c1_mfma.hip — one-input-channel convolutions on MFMA (gfx950).
+//
+// The first Conv2D of the reference model (1 -> 16 channels, k 5, relu, then
+// MaxPooling2D((2,2)); VAE/manual_scan_3layers.py:187-188) and the input gradient of the
+// last one (16 -> 1: dIn = conv(dOut[1 channel], flipped weights) through the previous
+// ReLU's mask, :199). With C == 1 the GEMM-K of a pixel is its K x K window. The window
+// rows are contiguous runs of the input row, so the MFMA K index is laid out as (ky, kx)
+// with kx padded to 8: a lane's 8 K-elements are ONE 8-element run of an input row, and
+// one 16x16x32 MFMA covers 4 kernel rows of 16 pixels x 16 output channels (2 MFMAs for
+// K <= 8 rows). The runs are built once per tile in LDS as 16-byte records
+// rec[row][x] = in[row][x .. x+7] (funnel shifts of the staged rows), so every B fragment
+// is one conflict-free ds_read_b128 (16 lanes = 16 consecutive pixels = 256 contiguous
+// bytes). Weights (the A operand: rows = output channels, kx >= K zero) stay in registers
+// for the whole workgroup.
+//
+// Workgroup: a 32 x 32 output tile x 16 output channels (blockIdx.y), 4 waves of 8 output
+// rows x 2 blocks of 16 columns. Epilogues as in conv_patch_kernel (csrc/conv_ae.hip):
+// fused 2x2 max-pool (+ argmax; values compared as stored in T, first max wins; without
+// argmax the max accumulator is taken first, a monotone map, bitwise the same), or plain
+// stores with the optional ReLU mask of the backward pass (act(0) = 0 there).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <string>
+
+#include "specenh.h"
+
+namespace specenh {
+int set_error(int code, const std::string& msg);  // stft_psd.hip
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+struct C1mArgs {
+  const void* in;    // [N][IH][IW] (C == 1)
+  const void* w;     // w_gemm [CO][K][K]
+  const float* bias;
+  void* out;         // [N][OH][OW][CO] or pooled [N][OH/2][OW/2][CO]
+  const void* mask;  // plain epilogue only: out = 0 where mask <= 0
+  unsigned char* argmax;
+  int N, IH, IW, OH, OW, CO, K, pad_t, pad_l, act;
+};
+
+constexpr int TILE = 32;
+constexpr int PRW = TILE + 8;  // staged row: 40 elements (32 + K - 1 <= 39)
+constexpr int PRS = 40;        // patch rows (32 + K - 1 <= 39), + 1 for clamped reads
+
+template <typename T>
+__device__ __forceinline__ float tof(T x) { return (float)x; }
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma(uint4 a, uint4 b, f32x4 c) {
+  if constexpr (__is_same(T, __bf16))
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+template <typename T>
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  if constexpr (__is_same(T, __bf16)) {
+    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, b2{(__bf16)a, (__bf16)b});
+  } else {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, h2{(_Float16)a, (_Float16)b});
+  }
+}
+
+__device__ __forceinline__ float vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+__device__ __forceinline__ float act_f(float v, int act) {
+  if (act == SPECENH_ACT_RELU) return fmaxf(v, 0.f);
+  if (act == SPECENH_ACT_SIGMOID) return 1.f / (1.f + __expf(-v));
+  return v;
+}
+
+template <typename T, bool POOL>
+__global__ __launch_bounds__(256) void conv_c1_mfma_kernel(C1mArgs a) {
+  __shared__ __attribute__((aligned(16))) T sRow[PRS * PRW];
+  __shared__ __attribute__((aligned(16))) uint4 sRec[PRS * TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntx = (a.OW + TILE - 1) / TILE, nty = (a.OH + TILE - 1) / TILE;
+  const int n = blockIdx.x / (ntx * nty);
+  const int trem = blockIdx.x - n * (ntx * nty);
+  const int oy0 = (trem / ntx) * TILE, ox0 = (trem - (trem / ntx) * ntx) * TILE;
+  const int iy0 = oy0 - a.pad_t, ix0 = ox0 - a.pad_l;
+  const int co0 = blockIdx.y * 16;
+  const int K = a.K, PR = TILE + K - 1;
+  const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
+  const T* __restrict__ W = reinterpret_cast<const T*>(a.w);
+
+  // ---- stage the patch rows (all loads in flight, zero outside the image) ----
+  {
+    constexpr int NE = (PRS * PRW + 255) / 256;
+    T v[NE];
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      const int e = tid + 256 * k;
+      const int r = e / PRW, c = e - (e / PRW) * PRW;
+      const int iy = iy0 + r, ix = ix0 + c;
+      const bool ok = e < PRS * PRW && r < PR && (unsigned)iy < (unsigned)a.IH &&
+                      (unsigned)ix < (unsigned)a.IW;
+      v[k] = in[ok ? ((long long)n * a.IH + iy) * a.IW + ix : 0];
+      if (!ok) v[k] = (T)0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < NE; ++k)
+      if (tid + 256 * k < PRS * PRW) sRow[tid + 256 * k] = v[k];
+  }
+  // ---- weights (A operand): lane = (co = lane & 15, kernel row 4 s + (lane >> 4)) ----
+  const int g4 = lane >> 4, l16 = lane & 15;
+  uint4 wf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int ky = 4 * s + g4, co = co0 + l16;
+    uint32_t w4[4] = {0u, 0u, 0u, 0u};
+    if (ky < K && co < a.CO) {
+      const T* wr = W + ((long long)co * K + ky) * K;
+#pragma unroll
+      for (int kx = 0; kx < 8; ++kx)
+        if (kx < K) w4[kx >> 1] |= (uint32_t)__builtin_bit_cast(unsigned short, wr[kx]) << (16 * (kx & 1));
+    }
+    wf[s] = uint4{w4[0], w4[1], w4[2], w4[3]};
+  }
+  __syncthreads();
+  // ---- records rec[r][x] = row r, elements x .. x+7 ----
+  const uint32_t* rw = reinterpret_cast<const uint32_t*>(sRow);
+  for (int e = tid; e < PRS * TILE; e += 256) {
+    const int r = e / TILE, x = e - (e / TILE) * TILE;
+    const uint32_t* p = rw + (r * PRW + (x & ~1)) / 2;
+    uint32_t d[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) d[k] = p[k];
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = (x & 1) ? __builtin_amdgcn_alignbit(d[k + 1], d[k], 16) : d[k];
+    sRec[e] = uint4{o[0], o[1], o[2], o[3]};
+  }
+  __syncthreads();
+
+  // ---- MFMAs: wave rows 8 wave + i, column blocks cb (pixels 16 cb + l16) ----
+  const int nks = (K + 3) / 4;
+  f32x4 acc[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (s >= nks) break;  // uniform
+        const int r = min(8 * wave + i + 4 * s + g4, PRS - 1);  // rows past K meet zero weights
+        acc[i][cb] = mfma<T>(wf[s], sRec[r * TILE + 16 * cb + l16], acc[i][cb]);
+      }
+
+  // ---- epilogue: lane holds channels co0 + 4 g4 + r of pixel (8 wave + i, 16 cb + l16) ----
+  float bv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int ch = co0 + 4 * g4 + r;
+    bv[r] = (a.bias && ch < a.CO) ? a.bias[ch] : 0.f;
+  }
+  const int ch0 = co0 + 4 * g4;
+  const bool vec = (a.CO & 3) == 0;
+  if constexpr (POOL) {
+    const int PHo = a.OH / 2, PWo = a.OW / 2;
+#pragma unroll
+    for (int ip = 0; ip < 4; ++ip)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int ox = ox0 + 16 * cb + l16;
+        const int py = (oy0 + 8 * wave + 2 * ip) / 2, px = ox / 2;
+        const bool store = (l16 & 1) == 0 && py < PHo && px < PWo && ch0 < a.CO;
+        const long long o = (((long long)n * PHo + py) * PWo + px) * a.CO + ch0;
+        T* dst = reinterpret_cast<T*>(a.out) + o;
+        float m[4];
+        unsigned arg4 = 0;
+        if (!a.argmax && a.act <= 1) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float m1 = vmax(acc[2 * ip][cb][r], acc[2 * ip + 1][cb][r]);
+            const float v = vmax(m1, __shfl_xor(m1, 1)) + bv[r];
+            m[r] = a.act == 1 ? vmax(v, 0.f) : v;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v00 = tof((T)act_f(acc[2 * ip][cb][r] + bv[r], a.act));
+            const float v10 = tof((T)act_f(acc[2 * ip + 1][cb][r] + bv[r], a.act));
+            const float v01 = __shfl_xor(v00, 1), v11 = __shfl_xor(v10, 1);
+            float b = v00;
+            unsigned q = 0;
+            if (v01 > b) { b = v01; q = 1; }
+            if (v10 > b) { b = v10; q = 2; }
+            if (v11 > b) { b = v11; q = 3; }
+            m[r] = b;
+            arg4 |= q << (8 * r);
+          }
+        }
+        if (!store) continue;
+        if (vec) {
+          *reinterpret_cast<uint2*>(dst) = uint2{pack2<T>(m[0], m[1]), pack2<T>(m[2], m[3])};
+          if (a.argmax) *reinterpret_cast<unsigned*>(a.argmax + o) = arg4;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (ch0 + r < a.CO) {
+              dst[r] = (T)m[r];
+              if (a.argmax) a.argmax[o + r] = (unsigned char)(arg4 >> (8 * r));
+            }
+        }
+      }
+  } else {
+    const T* __restrict__ mk = reinterpret_cast<const T*>(a.mask);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int oy = oy0 + 8 * wave + i, ox = ox0 + 16 * cb + l16;
+        if (oy >= a.OH || ox >= a.OW || ch0 >= a.CO) continue;
+        const long long o = (((long long)n * a.OH + oy) * a.OW + ox) * a.CO + ch0;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = act_f(acc[i][cb][r] + bv[r], a.act);
+        if (vec) {
+          if (mk) {
+            const uint2 mm = *reinterpret_cast<const uint2*>(mk + o);
+            const uint32_t mw[2] = {mm.x, mm.y};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const T mv = __builtin_bit_cast(T, (unsigned short)(mw[r >> 1] >> (16 * (r & 1))));
+              v[r] = tof(mv) > 0.f ? v[r] : 0.f;
+            }
+          }
+          *reinterpret_cast<uint2*>(reinterpret_cast<T*>(a.out) + o) =
+              uint2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (ch0 + r >= a.CO) continue;
+            float x = v[r];
+            if (mk && !(tof(mk[o + r]) > 0.f)) x = 0.f;
+            reinterpret_cast<T*>(a.out)[o + r] = (T)x;
+          }
+        }
+      }
+  }
+}
+
+template <typename T>
+int launch(const C1mArgs& a, bool pool, hipStream_t st) {
+  const long long tiles = (long long)a.N * ((a.OH + TILE - 1) / TILE) * ((a.OW + TILE - 1) / TILE);
+  const dim3 grid((unsigned)tiles, (unsigned)((a.CO + 15) / 16));
+  if (pool) hipLaunchKernelGGL((conv_c1_mfma_kernel<T, true>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((conv_c1_mfma_kernel<T, false>), grid, dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? 1 : set_error(SPECENH_EHIP, "conv_c1_mfma launch");
+}
+
+}  // namespace
+
+// C == 1, 16-bit, stride 1, undilated, square kernel <= 8, T output (no fp32 logits /
+// output), a mask only with act(0) = 0. Returns 1 when launched, 0 when not covered.
+int launch_conv_c1_mfma(int dtype, const void* in, int N, int IH, int IW, int C, const void* w,
+                        int KH, int KW, int CO, const float* bias, int pad_t, int pad_l, int OH,
+                        int OW, int act, void* out, int out_f32, float* logits, int pool,
+                        unsigned char* argmax, const void* mask, hipStream_t st) {
+  if (C != 1 || (dtype != SPECENH_DTYPE_BF16 && dtype != SPECENH_DTYPE_F16)) return 0;
+  if (KH != KW || KH > 8 || out_f32 || logits) return 0;
+  if (mask && (pool || act == SPECENH_ACT_SIGMOID)) return 0;
+  if (pool && ((OH & 1) || (OW & 1))) return 0;
+  if ((long long)N * ((OH + TILE - 1) / TILE) * ((OW + TILE - 1) / TILE) >= (1LL << 31)) return 0;
+  C1mArgs a{in, w, bias, out, mask, argmax, N, IH, IW, OH, OW, CO, KH, pad_t, pad_l, act};
+  if (dtype == SPECENH_DTYPE_BF16) return launch<__bf16>(a, pool != 0, st);
+  return launch<_Float16>(a, pool != 0, st);
+}
+
+}  // namespace specenh

@@ -3,8 +3,8 @@
 // The first Conv2D of the reference model (1 -> 16 channels, VAE/manual_scan_3layers.py:187)
 // and the last one (16 -> 1, sigmoid, :199) have a GEMM dimension of 1: on the MFMA path
 // (conv_ae.hip) they fill 1/16 of a 16x16 tile and their fragments are gathered element by
-// element. Here they are direct convolutions with packed dot products (v_dot2_f32_f16: two
-// products + fp32 accumulate per lane and instruction; bf16 unpacks by a shift), the input
+// element. Here they are direct convolutions with packed dot products (v_dot2_f32_f16 /
+// v_dot2c_f32_bf16: two products + fp32 accumulate per lane and instruction), the input
 // patch staged once per workgroup in LDS and the weights read as LDS broadcasts:
 //
 //   conv_c1_kernel<T, K, POOL>   C == 1, any CO (16-channel blocks): each lane computes a
@@ -68,9 +68,10 @@ __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
   if constexpr (__is_same(T, _Float16)) {
     return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, a), __builtin_bit_cast(f16x2, b), c,
                                   false);
-  } else {  // bf16 -> fp32 is a shift: exact products, fp32 accumulate
-    c = fmaf(__uint_as_float(a << 16), __uint_as_float(b << 16), c);
-    return fmaf(__uint_as_float(a & 0xffff0000u), __uint_as_float(b & 0xffff0000u), c);
+  } else {  // v_dot2c_f32_bf16 (gfx950)
+    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b2, a), __builtin_bit_cast(b2, b), c,
+                                          false);
   }
 }
 

@@ -1,9 +1,11 @@
-"""Narrow-channel direct convolutions (csrc/conv_narrow.hip) on the GPU against a float64
-torch convolution of the same 16-bit operands.
+"""Narrow-channel convolutions on the GPU against a float64 torch convolution of the same
+16-bit operands.
 
-conv_c1_kernel (1 input channel) with the ReLU mask of the backward pass (the input gradient
-of the 16 -> 1 output conv, VAE/manual_scan_3layers.py:199), and conv_co1_kernel (1 output
-channel) split into row bands at batch sizes and heights that leave ragged last bands.
+One input channel: conv_c1_mfma_kernel (csrc/conv_c1_mfma.hip, window rows as MFMA K runs),
+conv_c1_kernel (csrc/conv_narrow.hip, VALU dot2) and the generic MFMA kernels, forward with
+and without the fused 2x2 max-pool, and with the ReLU mask of the backward pass (the input
+gradient of the 16 -> 1 output conv, VAE/manual_scan_3layers.py:199). One output channel:
+conv_co1_kernel split into row bands at batch sizes and heights that leave ragged bands.
 Products of two 16-bit values are exact in fp32, so the fp32 accumulation differs from
 float64 by rounding only: |err| <= 1e-5 * sum|products| (fp32 out), or one rounding to the
 16-bit type on top of that (16-bit out)."""
@@ -27,6 +29,15 @@ def _ref(x, w, bias, k):
     return out.permute(0, 2, 3, 1), mag.permute(0, 2, 3, 1)
 
 
+def _path(monkeypatch, path):
+    """c1mfma: conv_c1_mfma.hip (the default for C == 1); narrow: the VALU dot2 kernel;
+    generic: the MFMA patch/gather kernels."""
+    if path in ("narrow", "generic"):
+        monkeypatch.setenv("SPECENH_CONV_NO_C1MFMA", "1")
+    if path == "generic":
+        monkeypatch.setenv("SPECENH_CONV_NO_NARROW", "1")
+
+
 def _conv(x, w, bias, k, co, act, out_dtype, mask=None):
     N, H, W, _ = x.shape
     out = torch.empty((N, H, W, co), dtype=out_dtype, device=x.device)
@@ -37,10 +48,9 @@ def _conv(x, w, bias, k, co, act, out_dtype, mask=None):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("N,H,W", [(3, 64, 64), (2, 37, 70), (1, 128, 128)])
-@pytest.mark.parametrize("path", ["narrow", "mfma"])
+@pytest.mark.parametrize("path", ["c1mfma", "narrow", "generic"])
 def test_c1_masked_dgrad(gpu_device, monkeypatch, dtype, N, H, W, path):
-    if path == "mfma":
-        monkeypatch.setenv("SPECENH_CONV_NO_NARROW", "1")
+    _path(monkeypatch, path)
     rng = np.random.default_rng(N * 1000 + H + W)
     k, co = 5, 16
     x = torch.tensor(rng.standard_normal((N, H, W, 1)), dtype=dtype, device=gpu_device)
@@ -69,3 +79,74 @@ def test_co1_bands(gpu_device, dtype, C, N, H, W):
     got = _conv(x, w, bias, k, 1, 0, torch.float32).double().cpu()
     ref, mag = _ref(x, w, bias, k)
     assert torch.all((got - ref).abs() <= 1e-5 * (mag + 0.25) + 1e-30)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("C", [16, 8, 3])
+@pytest.mark.parametrize("masked", [False, True])
+def test_maxpool2_bwd_routes_to_argmax(gpu_device, dtype, C, masked):
+    """MaxPooling2D backward (the 16-byte vector kernel for C % 8 == 0, the scalar one
+    otherwise): the gradient goes to the argmax position, zero where the pooled value is not
+    positive (the ReLU mask), exactly."""
+    rng = np.random.default_rng(C + 2 * masked)
+    N, H, W = 3, 18, 22
+    x = torch.tensor(rng.standard_normal((N, H, W, C)), dtype=dtype, device=gpu_device)
+    pooled, am = torch.ops.specenh.maxpool2(x)
+    dy = torch.tensor(rng.standard_normal((N, H // 2, W // 2, C)), dtype=dtype, device=gpu_device)
+    dx = torch.ops.specenh.maxpool2_bwd(dy, am, pooled if masked else None).cpu()
+    g = dy.cpu().clone()
+    if masked:
+        g[pooled.cpu().float() <= 0] = 0
+    ref = torch.zeros((N, H, W, C), dtype=dtype)
+    a = am.cpu().long()
+    for q in range(4):
+        sel = (a == q)
+        ref[:, (q >> 1)::2, (q & 1)::2, :] = torch.where(sel, g, torch.zeros_like(g))
+    assert torch.equal(dx, ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("k,co,N,H,W", [(5, 16, 3, 64, 64), (5, 16, 2, 50, 70), (3, 32, 2, 36, 34),
+                                        (7, 16, 1, 40, 24), (4, 16, 2, 32, 32)])
+@pytest.mark.parametrize("path", ["c1mfma", "narrow", "generic"])
+@pytest.mark.parametrize("pool", [False, True])
+def test_c1_forward(gpu_device, monkeypatch, dtype, k, co, N, H, W, path, pool):
+    """Conv2D(1 -> co, relu) [+ MaxPooling2D]: values within one 16-bit rounding of the
+    float64 result; the pooled output is the max of the stored values with its argmax."""
+    if path == "narrow" and k % 2 == 0:
+        pytest.skip("the VALU kernel takes odd kernels")
+    if path == "generic" and pool and k > 5:
+        pytest.skip("the fused pool needs the LDS-patch kernel (k <= 5)")
+    _path(monkeypatch, path)
+    rng = np.random.default_rng(k * 100 + co + H)
+    x = torch.tensor(rng.uniform(0, 1, (N, H, W, 1)), dtype=dtype, device=gpu_device)
+    w = torch.tensor(rng.standard_normal((co, k, k, 1)) * 0.3, dtype=dtype, device=gpu_device)
+    bias = torch.tensor(rng.standard_normal(co) * 0.1, dtype=torch.float32, device=gpu_device)
+    pt, pl = (k - 1) // 2, (k - 1) // 2
+    xd = F.pad(x.double().cpu().permute(0, 3, 1, 2), (pl, k - 1 - pl, pt, k - 1 - pt))
+    wd = w.double().cpu().permute(0, 3, 1, 2)
+    ref = (F.conv2d(xd, wd) + bias.double().cpu().view(1, -1, 1, 1)).clamp_min(0)
+    mag = F.conv2d(xd.abs(), wd.abs()) + bias.double().cpu().abs().view(1, -1, 1, 1)
+    ref, mag = ref.permute(0, 2, 3, 1), mag.permute(0, 2, 3, 1)
+    eps = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
+    if not pool:
+        out = torch.empty((N, H, W, co), dtype=dtype, device=gpu_device)
+        torch.ops.specenh.conv2d_out(x, w, bias, k, k, co, 1, pt, pl, 1, H, W, 1, None, None,
+                                     out, False, None)
+        got = out.double().cpu()
+        assert torch.all((got - ref).abs() <= eps * ref.abs() + 1e-5 * mag + 1e-30)
+        return
+    out = torch.empty((N, H // 2, W // 2, co), dtype=dtype, device=gpu_device)
+    am = torch.empty((N, H // 2, W // 2, co), dtype=torch.uint8, device=gpu_device)
+    torch.ops.specenh.conv2d_out(x, w, bias, k, k, co, 1, pt, pl, 1, H, W, 1, None, None, out,
+                                 True, am)
+    got = out.double().cpu()
+    win = ref[:, :H // 2 * 2, :W // 2 * 2].reshape(N, H // 2, 2, W // 2, 2, co)
+    pref = win.amax(dim=(2, 4))
+    pmag = mag[:, :H // 2 * 2, :W // 2 * 2].reshape(N, H // 2, 2, W // 2, 2, co).amax(dim=(2, 4))
+    assert torch.all((got - pref).abs() <= eps * pref.abs() + 1e-5 * pmag + 1e-30)
+    # the argmax points at a window element whose value rounds to the pooled value
+    a = am.cpu().long()
+    sel = win.permute(0, 1, 3, 5, 2, 4).reshape(N, H // 2, W // 2, co, 4)
+    picked = torch.gather(sel, 4, a.unsqueeze(-1)).squeeze(-1)
+    assert torch.all((picked - got).abs() <= 2 * eps * got.abs() + 2e-5 * pmag + 1e-30)

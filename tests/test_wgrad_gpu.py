@@ -2,7 +2,8 @@
 
 The MFMA paths (csrc/conv_ae.hip wgrad_tr_kernel: C % 16 == 0 or C == 1 via an LDS im2col
 block, transposed LDS fragment reads; wgrad_trp_kernel: the four Conv2DTranspose phases per
-workgroup, SPECENH_WGRAD_PERPHASE=1 forces one phase per workgroup)
+workgroup, SPECENH_WGRAD_PERPHASE=1 forces one phase per workgroup; wgrad_co1_kernel: one
+output channel as shifted-input x shifted-dOut MFMAs, SPECENH_WGRAD_NO_CO1=1 turns it off)
 and the generic gather kernel (SPECENH_WGRAD_GENERIC=1) are both checked against the
 float64 im2col product dW = dZ^T A of the header's gather formula (test_ae_mapping.igemm)
 on the same bf16 / f16-rounded operands: products are exact in the fp32 accumulators, so
@@ -23,7 +24,8 @@ CASES = [("conv", 16, 32, 5, 20, 18, 3), ("conv", 32, 64, 5, 16, 16, 2),
          ("conv", 16, 1, 5, 24, 20, 2), ("conv", 32, 16, 3, 9, 13, 3),
          ("convT", 64, 64, 5, 8, 8, 2), ("convT", 64, 32, 5, 10, 6, 3),
          ("convT", 32, 16, 5, 12, 12, 2), ("conv", 64, 48, 5, 17, 17, 1),
-         ("conv", 1, 16, 5, 33, 18, 2), ("conv", 1, 32, 3, 16, 16, 1)]
+         ("conv", 1, 16, 5, 33, 18, 2), ("conv", 1, 32, 3, 16, 16, 1),
+         ("conv", 16, 1, 5, 37, 29, 3), ("conv", 16, 1, 3, 16, 40, 1)]
 
 
 def _reference(x, dz, op):
@@ -37,14 +39,15 @@ def _reference(x, dz, op):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("kind,cin,cout,k,H,W,N", CASES)
-@pytest.mark.parametrize("path", ["mfma", "mfma_perphase", "generic"])
+@pytest.mark.parametrize("path", ["mfma", "mfma_alt", "generic"])
 def test_wgrad_matches_im2col(gpu_device, monkeypatch, dtype, kind, cin, cout, k, H, W, N, path):
     if path == "generic":
         monkeypatch.setenv("SPECENH_WGRAD_GENERIC", "1")
-    elif path == "mfma_perphase":
-        if kind != "convT":
-            pytest.skip("phase-shared launches are Conv2DTranspose only")
+    elif path == "mfma_alt":  # the general MFMA kernel where a specialised one exists
+        if kind != "convT" and cout != 1:
+            pytest.skip("no specialised launch for this geometry")
         monkeypatch.setenv("SPECENH_WGRAD_PERPHASE", "1")
+        monkeypatch.setenv("SPECENH_WGRAD_NO_CO1", "1")
     op = ae.ConvOp(kind, cin, cout, k, "relu", stride=2 if kind == "convT" else 1)
     OH, OW = op.out_hw(H, W)
     rng = np.random.default_rng(cin * 131 + cout * 7 + k + H)
@@ -68,6 +71,18 @@ def test_wgrad_mfma_is_bitwise_deterministic(gpu_device, monkeypatch, dtype, per
     rng = np.random.default_rng(5)
     x = torch.tensor(rng.standard_normal((4, 32, 32, 32)), dtype=dtype, device=gpu_device)
     dz = torch.tensor(rng.standard_normal((4, 64, 64, 16)), dtype=dtype, device=gpu_device)
+    s, pt, pl, dil = op.fwd_geom()
+    a = torch.ops.specenh.conv2d_wgrad(x, dz, 5, 5, s, pt, pl, dil)
+    b = torch.ops.specenh.conv2d_wgrad(x, dz, 5, 5, s, pt, pl, dil)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_wgrad_co1_is_bitwise_deterministic(gpu_device, dtype):
+    op = ae.ConvOp("conv", 16, 1, 5, "sigmoid")
+    rng = np.random.default_rng(6)
+    x = torch.tensor(rng.standard_normal((8, 64, 64, 16)), dtype=dtype, device=gpu_device)
+    dz = torch.tensor(rng.standard_normal((8, 64, 64, 1)), dtype=dtype, device=gpu_device)
     s, pt, pl, dil = op.fwd_geom()
     a = torch.ops.specenh.conv2d_wgrad(x, dz, 5, 5, s, pt, pl, dil)
     b = torch.ops.specenh.conv2d_wgrad(x, dz, 5, 5, s, pt, pl, dil)

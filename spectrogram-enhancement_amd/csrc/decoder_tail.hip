@@ -58,6 +58,7 @@ constexpr int CI = 32, CO = 16, KT = 5, KO = 5;
 constexpr int XPST = 48;               // patch pixel stride (elements): 32 channels + pad
 constexpr int YW = 2 * NP;             // 36: map region side
 constexpr int PT = KT - 1 - (KT - 2) / 2;  // 3: pad of the dilated-input conv
+constexpr int PXW = 48;                // Conv2D(1) scratch: positions x' per row (3 blocks)
 
 struct TailArgs {
   const void* x;      // [N][H][W][CI]
@@ -214,6 +215,17 @@ __device__ __forceinline__ void tail_body(const TailArgs& a, T* sx, T* sy, int w
 #pragma unroll
   for (int r = 0; r < 4; ++r) bias[r] = a.bt[4 * kg + r];
   const float bo = a.bo[0];
+  // Conv2D(1) weights as MFMA B fragments: k = (kernel row 2 s + (kg >> 1), 8 channels
+  // 8 (kg & 1) ..), n = kx = m (zero for kx >= KO or row >= KO)
+  uint4 wo_frag[3];
+#pragma unroll
+  for (int s2 = 0; s2 < 3; ++s2) {
+    const int ky = 2 * s2 + (kg >> 1);
+    wo_frag[s2] = uint4{0u, 0u, 0u, 0u};
+    if (ky < KO && m < KO)
+      wo_frag[s2] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.wo) +
+                                                    (ky * KO + m) * CO + 8 * (kg & 1));
+  }
   const int b0 = half * MAXBLK, nb = (a.dev & 1) ? 0 : min(MAXBLK, NBLK - b0);
 
   uint4 pf[XPF];
@@ -253,41 +265,45 @@ __device__ __forceinline__ void tail_body(const TailArgs& a, T* sx, T* sy, int w
     const bool next = tile + G < total && !(a.dev & 4);
     if (next) load_patch<T>(a, tile + G, pf);
 
-    // ---- Conv2D(1, 5x5) + sigmoid: lane = column x, output rows (2rp, 2rp + 1) ----
-    const int x = lane & 31, rp = wave * 2 + (lane >> 5);
-    float s0 = 0.f, s1 = 0.f;
-    const uint32_t* __restrict__ Wo = reinterpret_cast<const uint32_t*>(a.wo);
+    // ---- Conv2D(1, 5x5) + sigmoid on MFMA: per output row y,
+    //   D[x'][kx] = sum_{ky, ci} map[y + ky][x'][ci] w[ky][kx][ci]   (A = map, B = weights)
+    //   out[y][x] = sum_kx D[x + kx][kx]
+    // 3 MFMAs (kernel-row pairs) per 16 positions x', 3 position blocks per row; the
+    // diagonal sums go through a per-wave scratch in the dead patch region ----
+    if (!(a.dev & 2)) {
+      float* sp = reinterpret_cast<float*>(sx) + wave * (2 * KO * PXW);
+      const int x = lane & 31, hh = lane >> 5;
+      float* __restrict__ O = a.out + (long long)g.n * H2 * W2;
+      const int gx = g.ox0 + x;
 #pragma unroll 1
-    for (int kx = 0; kx < ((a.dev & 2) ? 0 : KO); ++kx) {
-      int wb = kx * 8;  // opaque: the weights are re-read per tile, not hoisted
-      asm volatile("" : "+s"(wb));
+      for (int j = 0; j < 2; ++j) {  // rows 4 wave + 2 j + {0, 1}
 #pragma unroll
-      for (int yy = 0; yy <= KO; ++yy) {
-        const int pix = (2 * rp + yy) * YW + x + kx;
-        const uint4 h0 = *reinterpret_cast<const uint4*>(sy + ymap(pix, 0));
-        const uint4 h1 = *reinterpret_cast<const uint4*>(sy + ymap(pix, 1));
-        const uint32_t hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        for (int h = 0; h < 2; ++h) {
+          const int yrow = 4 * wave + 2 * j + h;
 #pragma unroll
-        for (int o = 0; o < 2; ++o) {  // output row 2rp + o uses kernel row ky = yy - o
-          const int ky = yy - o;
-          if (ky < 0 || ky >= KO) continue;
-          uint32_t wv[8];  // wave-uniform: scalar loads into SGPRs (no LDS traffic)
+          for (int xb = 0; xb < 3; ++xb) {
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int xc = min(16 * xb + m, YW - 1);  // columns >= 36 feed no output
 #pragma unroll
-          for (int c = 0; c < 8; ++c) wv[c] = Wo[ky * KO * 8 + wb + c];
-          float sacc = o ? s1 : s0;
-#pragma unroll
-          for (int c = 0; c < 8; ++c) sacc = dot2<T>(hv[c], wv[c], sacc);
-          if (o) s1 = sacc; else s0 = sacc;
+            for (int s2 = 0; s2 < 3; ++s2) {
+              const int row = min(yrow + 2 * s2 + (kg >> 1), YW - 1);  // row 5: zero weights
+              const uint4 av = *reinterpret_cast<const uint4*>(sy + ymap(row * YW + xc, kg & 1));
+              acc = mfma<T>(av, wo_frag[s2], acc);
+            }
+            if (m < KO)  // D[x' = 16 xb + 4 kg + r][kx = m]
+              *reinterpret_cast<f32x4*>(sp + (h * KO + m) * PXW + 16 * xb + 4 * kg) = acc;
+          }
         }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: D in the scratch
+        float sum = bo;
+#pragma unroll
+        for (int kx = 0; kx < KO; ++kx) sum += sp[(hh * KO + kx) * PXW + x + kx];
+        const int gy = g.oy0 + 4 * wave + 2 * j + hh;
+        if (gx < W2 && gy < H2) O[(long long)gy * W2 + gx] = 1.f / (1.f + __expf(-sum));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next D
       }
     }
-    const int gx = g.ox0 + x;
-    float* __restrict__ O = a.out + (long long)g.n * H2 * W2;
-    const int gy0 = g.oy0 + 2 * rp;
-    if (gx < W2) {
-      if (gy0 < H2) O[(long long)gy0 * W2 + gx] = 1.f / (1.f + __expf(-(s0 + bo)));
-      if (gy0 + 1 < H2) O[(long long)(gy0 + 1) * W2 + gx] = 1.f / (1.f + __expf(-(s1 + bo)));
-    }
+    lds_barrier();  // every wave's scratch use is over before the next patch lands there
     if (next) store_patch<T>(sx, pf);  // the patch is dead since the first barrier
     lds_barrier();                      // next patch in; this tile's map reads done
   }
@@ -301,6 +317,7 @@ __device__ __forceinline__ void tail_body(const TailArgs& a, T* sx, T* sy, int w
 template <typename T>
 __global__ __launch_bounds__(512, 4) void convt_conv_out_kernel(TailArgs a) {
   __shared__ __attribute__((aligned(16))) T sx[XW * XW * XPST];  // input patch
+  static_assert(8 * 2 * KO * PXW * sizeof(float) <= sizeof(sx), "Conv2D(1) scratch in the patch");
   __shared__ __attribute__((aligned(16))) T sy[YW * YW * CO];    // 16-channel map
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   switch (wave) {

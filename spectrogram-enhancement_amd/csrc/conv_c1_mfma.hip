@@ -1,9 +1,10 @@
 // conv_c1_mfma.hip — one-input-channel convolutions on MFMA (gfx950).
 //
 // The first Conv2D of the reference model (1 -> 16 channels, k 5, relu, then
-// MaxPooling2D((2,2)); VAE/manual_scan_3layers.py:187-188) and the input gradient of the
-// last one (16 -> 1: dIn = conv(dOut[1 channel], flipped weights) through the previous
-// ReLU's mask, :199). With C == 1 the GEMM-K of a pixel is its K x K window. The window
+// MaxPooling2D((2,2)); VAE/manual_scan_3layers.py:187-188). (The masked epilogue below also
+// serves the input gradient of the last conv, 16 -> 1 through the previous ReLU, :199, but
+// the dispatcher sends that one to the VALU kernel, which measured faster for it.) With
+// C == 1 the GEMM-K of a pixel is its K x K window. The window
 // rows are contiguous runs of the input row, so the MFMA K index is laid out as (ky, kx)
 // with kx padded to 8: a lane's 8 K-elements are ONE 8-element run of an input row, and
 // one 16x16x32 MFMA covers 4 kernel rows of 16 pixels x 16 output channels (2 MFMAs for
@@ -91,19 +92,19 @@ __global__ __launch_bounds__(256) void conv_c1_mfma_kernel(C1mArgs a) {
   __shared__ __attribute__((aligned(16))) uint4 sRec[PRS * TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntx = (a.OW + TILE - 1) / TILE, nty = (a.OH + TILE - 1) / TILE;
-  const int n = blockIdx.x / (ntx * nty);
-  const int trem = blockIdx.x - n * (ntx * nty);
-  const int oy0 = (trem / ntx) * TILE, ox0 = (trem - (trem / ntx) * ntx) * TILE;
-  const int iy0 = oy0 - a.pad_t, ix0 = ox0 - a.pad_l;
+  const int ntiles = a.N * ntx * nty;
   const int co0 = blockIdx.y * 16;
   const int K = a.K, PR = TILE + K - 1;
   const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
   const T* __restrict__ W = reinterpret_cast<const T*>(a.w);
 
-  // ---- stage the patch rows (all loads in flight, zero outside the image) ----
-  {
-    constexpr int NE = (PRS * PRW + 255) / 256;
-    T v[NE];
+  // a tile's patch rows -> registers (all loads in flight, zero outside the image)
+  constexpr int NE = (PRS * PRW + 255) / 256;
+  T v[NE];
+  auto fetch = [&](int tile) {
+    const int n = tile / (ntx * nty), trem = tile - n * (ntx * nty);
+    const int iy0 = (trem / ntx) * TILE - a.pad_t;
+    const int ix0 = (trem - (trem / ntx) * ntx) * TILE - a.pad_l;
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
       const int e = tid + 256 * k;
@@ -114,10 +115,7 @@ __global__ __launch_bounds__(256) void conv_c1_mfma_kernel(C1mArgs a) {
       v[k] = in[ok ? ((long long)n * a.IH + iy) * a.IW + ix : 0];
       if (!ok) v[k] = (T)0.f;
     }
-#pragma unroll
-    for (int k = 0; k < NE; ++k)
-      if (tid + 256 * k < PRS * PRW) sRow[tid + 256 * k] = v[k];
-  }
+  };
   // ---- weights (A operand): lane = (co = lane & 15, kernel row 4 s + (lane >> 4)) ----
   const int g4 = lane >> 4, l16 = lane & 15;
   uint4 wf[2];
@@ -133,6 +131,19 @@ __global__ __launch_bounds__(256) void conv_c1_mfma_kernel(C1mArgs a) {
     }
     wf[s] = uint4{w4[0], w4[1], w4[2], w4[3]};
   }
+
+  // persistent over tiles blockIdx.x, + gridDim.x, ...: the next tile's rows are loaded
+  // into registers while this tile's records, MFMAs and stores run
+  int tile = blockIdx.x;
+  if (tile < ntiles) fetch(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+  const int n = tile / (ntx * nty);
+  const int trem = tile - n * (ntx * nty);
+  const int oy0 = (trem / ntx) * TILE, ox0 = (trem - (trem / ntx) * ntx) * TILE;
+  __syncthreads();  // the previous tile's record reads are done
+#pragma unroll
+  for (int k = 0; k < NE; ++k)
+    if (tid + 256 * k < PRS * PRW) sRow[tid + 256 * k] = v[k];
   __syncthreads();
   // ---- records rec[r][x] = row r, elements x .. x+7 ----
   const uint32_t* rw = reinterpret_cast<const uint32_t*>(sRow);
@@ -148,6 +159,7 @@ __global__ __launch_bounds__(256) void conv_c1_mfma_kernel(C1mArgs a) {
     sRec[e] = uint4{o[0], o[1], o[2], o[3]};
   }
   __syncthreads();
+  if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
 
   // ---- MFMAs: wave rows 8 wave + i, column blocks cb (pixels 16 cb + l16) ----
   const int nks = (K + 3) / 4;
@@ -257,12 +269,27 @@ __global__ __launch_bounds__(256) void conv_c1_mfma_kernel(C1mArgs a) {
         }
       }
   }
+  }  // tile loop
 }
 
 template <typename T>
 int launch(const C1mArgs& a, bool pool, hipStream_t st) {
   const long long tiles = (long long)a.N * ((a.OH + TILE - 1) / TILE) * ((a.OW + TILE - 1) / TILE);
-  const dim3 grid((unsigned)tiles, (unsigned)((a.CO + 15) / 16));
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  // persistent workgroups, as many as are resident at once, each over a run of tiles
+  const void* fn = pool ? (const void*)conv_c1_mfma_kernel<T, true> : (const void*)conv_c1_mfma_kernel<T, false>;
+  static int per_cu[2] = {0, 0};
+  int& pc = per_cu[pool ? 1 : 0];
+  if (pc == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, fn, 256, 0) != hipSuccess || pc <= 0))
+    pc = 2;
+  const unsigned cob = (unsigned)((a.CO + 15) / 16);
+  const dim3 grid((unsigned)std::max<long long>(1, std::min<long long>(tiles, (long long)pc * cus / cob)), cob);
   if (pool) hipLaunchKernelGGL((conv_c1_mfma_kernel<T, true>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((conv_c1_mfma_kernel<T, false>), grid, dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? 1 : set_error(SPECENH_EHIP, "conv_c1_mfma launch");
@@ -271,14 +298,16 @@ int launch(const C1mArgs& a, bool pool, hipStream_t st) {
 }  // namespace
 
 // C == 1, 16-bit, stride 1, undilated, square kernel <= 8, T output (no fp32 logits /
-// output), a mask only with act(0) = 0. Returns 1 when launched, 0 when not covered.
+// output, no mask). Returns 1 when launched, 0 when not covered.
 int launch_conv_c1_mfma(int dtype, const void* in, int N, int IH, int IW, int C, const void* w,
                         int KH, int KW, int CO, const float* bias, int pad_t, int pad_l, int OH,
                         int OW, int act, void* out, int out_f32, float* logits, int pool,
                         unsigned char* argmax, const void* mask, hipStream_t st) {
   if (C != 1 || (dtype != SPECENH_DTYPE_BF16 && dtype != SPECENH_DTYPE_F16)) return 0;
   if (KH != KW || KH > 8 || out_f32 || logits) return 0;
-  if (mask && (pool || act == SPECENH_ACT_SIGMOID)) return 0;
+  // the masked full-resolution store (the C4 input gradient of the last conv) is faster on
+  // the VALU kernel (tools/c1_bench.py: 630 vs 834 us per 2048 shots, fp16)
+  if (mask) return 0;
   if (pool && ((OH & 1) || (OW & 1))) return 0;
   if ((long long)N * ((OH + TILE - 1) / TILE) * ((OW + TILE - 1) / TILE) >= (1LL << 31)) return 0;
   C1mArgs a{in, w, bias, out, mask, argmax, N, IH, IW, OH, OW, CO, KH, pad_t, pad_l, act};

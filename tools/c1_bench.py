@@ -1,0 +1,58 @@
+"""Time the one-input-channel conv launches (dev A/B tool).
+
+    python tools/c1_bench.py [--batch 2048] [--reps 20]
+
+Conv2D(1 -> 16, k 5, relu) + fused 2x2 max-pool (the model's first layer, inference) and
+the masked 16-channel input gradient of the last conv (C4 backward) on the MFMA kernel
+(conv_c1_mfma.hip) and on the VALU dot2 kernel (SPECENH_CONV_NO_C1MFMA=1), fp16 and bf16."""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "spectrogram-enhancement_amd"))
+import specenh  # noqa: E402,F401
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    dev, N, H = "cuda:0", a.batch, 128
+    for dt in (torch.float16, torch.bfloat16):
+        x = torch.rand(N, H, H, 1, device=dev, dtype=dt)
+        w = torch.randn(16, 5, 5, 1, device=dev, dtype=dt) * 0.2
+        b = torch.zeros(16, device=dev)
+        pooled = torch.empty(N, H // 2, H // 2, 16, device=dev, dtype=dt)
+        full = torch.empty(N, H, H, 16, device=dev, dtype=dt)
+        mask = torch.randn(N, H, H, 16, device=dev, dtype=dt)
+        for path in ("mfma", "valu"):
+            if path == "valu":
+                os.environ["SPECENH_CONV_NO_C1MFMA"] = "1"
+            else:
+                os.environ.pop("SPECENH_CONV_NO_C1MFMA", None)
+            t_pool = timeit(lambda: torch.ops.specenh.conv2d_out(
+                x, w, b, 5, 5, 16, 1, 2, 2, 1, H, H, 1, None, None, pooled, True, None), a.reps)
+            t_mask = timeit(lambda: torch.ops.specenh.conv2d_out(
+                x, w, None, 5, 5, 16, 1, 2, 2, 1, H, H, 0, mask, None, full, False, None), a.reps)
+            print(f"{str(dt):15s} {path}: conv+pool {t_pool:8.1f} us   masked dgrad {t_mask:8.1f} us")
+    os.environ.pop("SPECENH_CONV_NO_C1MFMA", None)
+
+
+if __name__ == "__main__":
+    main()

@@ -120,8 +120,10 @@ def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4, tail=False):
     """Per launch of the fused forward (conv+pool fused; with ``tail`` the last
     Conv2DTranspose + Conv2D(1) are one launch, csrc/decoder_tail.hip): useful FLOPs and
     algorithmic HBM bytes per sample (activations read once + written once), the weights
-    read once per launch, and the units that do the arithmetic (the narrow 1-in / 1-out
-    channel layers run on the VALU). ``mfma_flops`` is the part on the matrix cores."""
+    read once per launch, and the units that do the arithmetic: every layer is on the
+    matrix cores (the 1-input-channel conv in csrc/conv_c1_mfma.hip, the fused tail's
+    Conv2D(1) as per-row MFMAs + diagonal sums) except an unfused 1-output-channel conv
+    (VALU dot2, csrc/conv_narrow.hip). ``mfma_flops`` is the part on the matrix cores."""
     lays = ae_layers()
     res, hh, ww, i = [], h, w, 0
     while i < len(lays):
@@ -132,19 +134,19 @@ def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4, tail=False):
         sh, sw = (oh // 2, ow // 2) if pool else (oh, ow)
         last = i + (2 if pool else 1) >= len(lays)
         nbytes = hh * ww * cin * act_bytes + sh * sw * cout * (out_bytes if last else act_bytes)
-        unit = "valu" if (cin == 1 or cout == 1) else "mfma"
+        unit = "valu" if cout == 1 else "mfma"
         res.append({"flops": 2 * macs, "mfma_flops": 2 * macs if unit == "mfma" else 0,
                     "bytes": nbytes, "weight_bytes": k * k * cin * cout * act_bytes + 4 * cout,
                     "unit": unit})
         hh, ww = sh, sw
         i += 2 if pool else 1
-    if tail:  # convT3 (MFMA) + conv_out (VALU): the 16-channel map is not HBM traffic
+    if tail:  # convT3 + conv_out, both on MFMA: the 16-channel map is not HBM traffic
         a, b = res[-2], res[-1]
-        res = res[:-2] + [{"flops": a["flops"] + b["flops"], "mfma_flops": a["mfma_flops"],
+        res = res[:-2] + [{"flops": a["flops"] + b["flops"], "mfma_flops": a["flops"] + b["flops"],
                            "bytes": (h // 2) * (w // 2) * AE_FILTERS[1] * act_bytes +
                            h * w * out_bytes,
                            "weight_bytes": a["weight_bytes"] + b["weight_bytes"],
-                           "unit": "mfma+valu"}]
+                           "unit": "mfma"}]
     return res
 
 

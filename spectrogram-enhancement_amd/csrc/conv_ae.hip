@@ -454,13 +454,17 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 // (row, column) parity sub-patches of 18 x 18, so tap (jy, jx) of output pixel (y, x) is
 // pixel (y + jy/2, x + jx/2) of sub-patch (jy&1, jx&1): the lanes' fragment reads stay
 // unit-stride and the k-step loop is the stride-1 one.
-template <typename T, int NT, int CC, bool POOL, bool PAIR = false, bool S2 = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SPECENH_PATCH_WPE(PAIR, NT, CC))))
+template <typename T, int NT, int CC, bool POOL, bool PAIR = false, bool S2 = false, bool WS = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WS ? 1 : SPECENH_PATCH_WPE(PAIR, NT, CC))))
 void conv_patch_kernel(ConvArgs a) {
   static_assert(!S2 || (CC == 16 && !POOL && !PAIR), "stride-2 patches: CC 16, plain epilogue");
+  static_assert(!WS || !PAIR, "wave split: not with the row-phase pair epilogue");
   constexpr int TILE = 16;
   constexpr int PST = Patch<CC>::PST;
-  constexpr int MT = 4;  // output rows per wave
+  // output rows per wave: 4 (waves stacked over the 16 rows, each wave all 16 NT channels),
+  // or 8 with WS (2 x 2 waves: row halves x channel halves of a 32 NT-channel workgroup;
+  // each weight fragment feeds 8 MFMAs instead of 4 and the waves load different weights)
+  constexpr int MT = WS ? 8 : 4;
   // the patch (and PAIR's output stage) in dynamic LDS sized by the launch for the actual
   // patch (patch_lds_bytes): a Conv2DTranspose's 4 phases share an 18 x 18 patch, not 20 x 20
   // (CC = 64: 52 KB -> 3 workgroups per CU instead of 2)
@@ -492,8 +496,9 @@ void conv_patch_kernel(ConvArgs a) {
   const int PW = shared ? a.PW : (S2 ? 2 * TILE - 2 : TILE - 1) + g0.KW;
   const int SPH = S2 ? (PH + 1) / 2 : PH, SPW = S2 ? (PW + 1) / 2 : PW;  // S2 sub-patches
   const int iy0 = (S2 ? 2 : 1) * oy0 - upt, ix0 = (S2 ? 2 : 1) * ox0 - upl;
-  const int n0 = blockIdx.y * 16 * NT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wrow = WS ? (wave >> 1) : wave;
+  const int n0 = blockIdx.y * 16 * NT * (WS ? 2 : 1) + (WS ? (wave & 1) * 16 * NT : 0);
   const int kgrp = lane >> 4, px = lane & 15;
   const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
   const T* __restrict__ W = reinterpret_cast<const T*>(a.w);
@@ -509,7 +514,7 @@ void conv_patch_kernel(ConvArgs a) {
 
   int rbase[MT];  // this lane's pixel (row i of the wave, column px) in the patch
 #pragma unroll
-  for (int i = 0; i < MT; ++i) rbase[i] = ((wave * MT + i) * SPW + px) * PST;
+  for (int i = 0; i < MT; ++i) rbase[i] = ((wrow * MT + i) * SPW + px) * PST;
 
   auto stage = [&](int c) {
     if constexpr (CC == 1) {
@@ -793,7 +798,7 @@ void conv_patch_kernel(ConvArgs a) {
         const bool relu = a.act == 1;
 #pragma unroll
         for (int ip = 0; ip < 2; ++ip) {
-          const int oy = oy0 + wave * MT + 2 * ip;
+          const int oy = oy0 + wrow * MT + 2 * ip;
           const int py = oy / 2, pxo = ox / 2;
           const bool store = (px & 1) == 0 && py < PHo && pxo < PWo;
 #pragma unroll
@@ -816,7 +821,7 @@ void conv_patch_kernel(ConvArgs a) {
       } else
 #pragma unroll
       for (int ip = 0; ip < 2; ++ip) {
-        const int oy = oy0 + wave * MT + 2 * ip;
+        const int oy = oy0 + wrow * MT + 2 * ip;
         const int py = oy / 2, pxo = ox / 2;
         const bool store = (px & 1) == 0 && py < PHo && pxo < PWo;
 #pragma unroll
@@ -889,7 +894,7 @@ void conv_patch_kernel(ConvArgs a) {
         for (int i = 0; i < MT; ++i)
 #pragma unroll
           for (int j = 0; j < NT; ++j) {
-            const int o = ((wave * MT + i) * 16 + px) * PS + 16 * j + 4 * kgrp;
+            const int o = ((wrow * MT + i) * 16 + px) * PS + 16 * j + 4 * kgrp;
             *reinterpret_cast<uint2*>(sP + o) = uint2{hold[i][j][0], hold[i][j][1]};
             *reinterpret_cast<uint2*>(sP + o + CO) = uint2{pk[i][j][0], pk[i][j][1]};
           }
@@ -915,7 +920,7 @@ void conv_patch_kernel(ConvArgs a) {
       const T* __restrict__ mk = reinterpret_cast<const T*>(a.mask);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
-        const int oy = oy0 + wave * MT + i;
+        const int oy = oy0 + wrow * MT + i;
         if (oy >= g.OH || ox >= g.OW) continue;
         const int o = (pbase + oy * g.oys * OWs) * CO;
 #pragma unroll
@@ -943,7 +948,7 @@ void conv_patch_kernel(ConvArgs a) {
     } else {
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
-        const int oy = oy0 + wave * MT + i;
+        const int oy = oy0 + wrow * MT + i;
         if (oy >= g.OH || ox >= g.OW) continue;
         const long long pix =
             ((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0;
@@ -2052,6 +2057,24 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
     else if (nt == 3) SPECENH_PAIR(3);
     else SPECENH_PAIR(4);
 #undef SPECENH_PAIR
+    return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "conv launch");
+  }
+  // wave split (2 x 2 waves, 8 rows x 16 NTW channels each, 32 NTW channels per workgroup)
+  // where the channels fill whole 32-channel pairs and the grid stays >= 2 workgroups per CU
+  const int ntw = nt >= 4 ? 2 : 1;
+  if (CC != 1 && nt >= 2 && CO % (32 * ntw) == 0 && getenv_flag("SPECENH_PATCH_WSPLIT") &&
+      (unsigned long long)tiles * (CO / (32 * ntw)) * (a.ph_shared ? 1 : nph) >= 512) {
+    const dim3 gridw(tiles, (unsigned)(CO / (32 * ntw)), a.ph_shared ? 1 : nph);
+    const size_t ldsw = patch_lds_bytes<T, CC>(a, nph, ntw, false);
+#define SPECENH_PATCHW(NT, P) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC, P, false, false, true>), gridw, dim3(256), ldsw, st, a)
+    if (a.pool) {
+      if (ntw == 1) SPECENH_PATCHW(1, true);
+      else SPECENH_PATCHW(2, true);
+    } else {
+      if (ntw == 1) SPECENH_PATCHW(1, false);
+      else SPECENH_PATCHW(2, false);
+    }
+#undef SPECENH_PATCHW
     return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "conv launch");
   }
   const dim3 grid(tiles, (unsigned)((CO + 16 * nt - 1) / (16 * nt)), a.ph_shared ? 1 : nph);

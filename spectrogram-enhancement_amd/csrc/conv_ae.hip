@@ -2059,11 +2059,19 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
 #undef SPECENH_PAIR
     return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "conv launch");
   }
-  // wave split (2 x 2 waves, 8 rows x 16 NTW channels each, 32 NTW channels per workgroup)
-  // where the channels fill whole 32-channel pairs and the grid stays >= 2 workgroups per CU
+  // wave split (2 x 2 waves, 8 rows x 16 NTW channels each, 32 NTW channels per workgroup):
+  // each weight fragment feeds 8 MFMAs and the waves load different weights. It pays where
+  // it keeps the occupancy: the 32-channel-chunk pooled conv with 64 outputs (conv3 + pool:
+  // 0.32 -> 0.21 ms per 2048 shots, tools/conv_one.py l3); the other layers measured slower
+  // (registers: 4 -> 2 waves per SIMD). SPECENH_PATCH_WSPLIT=1 forces it wherever the
+  // channels allow, =0 turns it off. The accumulation order is unchanged: bitwise the same.
   const int ntw = nt >= 4 ? 2 : 1;
-  if (CC != 1 && nt >= 2 && CO % (32 * ntw) == 0 && getenv_flag("SPECENH_PATCH_WSPLIT") &&
-      (unsigned long long)tiles * (CO / (32 * ntw)) * (a.ph_shared ? 1 : nph) >= 512) {
+  const char* wse = std::getenv("SPECENH_PATCH_WSPLIT");
+  const int wsm = wse ? std::atoi(wse) : -1;
+  const bool ws_shape = CC != 1 && nt >= 2 && CO % (32 * ntw) == 0;
+  const bool ws_auto = CC == 32 && a.pool && nt == 4 &&
+                       (unsigned long long)tiles * (CO / (32 * ntw)) * (a.ph_shared ? 1 : nph) >= 512;
+  if (ws_shape && (wsm == 1 || (wsm < 0 && ws_auto))) {
     const dim3 gridw(tiles, (unsigned)(CO / (32 * ntw)), a.ph_shared ? 1 : nph);
     const size_t ldsw = patch_lds_bytes<T, CC>(a, nph, ntw, false);
 #define SPECENH_PATCHW(NT, P) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC, P, false, false, true>), gridw, dim3(256), ldsw, st, a)

@@ -548,3 +548,26 @@ def test_convt_row_phase_pairs_bitwise_identical(gpu_device, dtype, hw, monkeypa
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
     assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.parametrize("dtype", ["mixed_bfloat16", "float16"])
+def test_wave_split_patch_kernel_is_bitwise_identical(gpu_device, dtype, monkeypatch):
+    """conv_patch_kernel's 2 x 2 wave split (8 rows x half the channels per wave, the
+    default for the pooled 32-channel-chunk conv) runs the same k-step order per output as
+    the 4 x 1 split: forward outputs and gradients are bitwise equal, forced on and off."""
+    ops = ref_model_ops()
+    eng, _ = make(ops, (64, 64, 1), dtype=dtype, seed=47)
+    rng = np.random.default_rng(13)
+    x = rng.uniform(0, 1, (4, 64, 64, 1)).astype(np.float32)
+    y = rng.uniform(0, 1, (4, 64, 64, 1)).astype(np.float32)
+    outs, grads = [], []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SPECENH_PATCH_WSPLIT", flag)
+        outs.append(eng.forward(upload(eng, x), train=False).clone())
+        eng.forward(upload(eng, x), train=True)
+        eng.loss_and_grad(upload(eng, y))
+        eng.backward()
+        grads.append(eng.g.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(grads[0], grads[1])

@@ -455,7 +455,7 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 // pixel (y + jy/2, x + jx/2) of sub-patch (jy&1, jx&1): the lanes' fragment reads stay
 // unit-stride and the k-step loop is the stride-1 one.
 template <typename T, int NT, int CC, bool POOL, bool PAIR = false, bool S2 = false, bool WS = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WS ? 1 : SPECENH_PATCH_WPE(PAIR, NT, CC))))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WS ? 3 : SPECENH_PATCH_WPE(PAIR, NT, CC))))
 void conv_patch_kernel(ConvArgs a) {
   static_assert(!S2 || (CC == 16 && !POOL && !PAIR), "stride-2 patches: CC 16, plain epilogue");
   static_assert(!WS || !PAIR, "wave split: not with the row-phase pair epilogue");
@@ -603,7 +603,7 @@ void conv_patch_kernel(ConvArgs a) {
           return ((jy + dy) * PW + jx + dx) * PST + 32 * h;
         };
         // ring of PD weight fragments consumed in place (no copies) and refilled PD steps ahead
-        constexpr int PD = NT >= 3 ? (CC == 64 ? 1 : 2) : (NT == 2 ? 2 : 8);
+        constexpr int PD = WS ? (NT == 1 ? 4 : 2) : (NT >= 3 ? (CC == 64 ? 1 : 2) : (NT == 2 ? 2 : 8));
         V8<T> wring[PD][NT];
 #pragma unroll
         for (int u = 0; u < PD; ++u)
@@ -663,7 +663,7 @@ void conv_patch_kernel(ConvArgs a) {
           const int c0 = wcol_t(2 * st), c1 = wcol_t(min(2 * st + 1, ntap - 1));
           return second ? c1 : c0;
         };
-        constexpr int PD = NT >= 3 ? 2 : (NT == 2 ? 2 : 8);
+        constexpr int PD = WS ? (NT == 1 ? 4 : 2) : (NT >= 3 ? 2 : (NT == 2 ? 2 : 8));
         V8<T> wring[PD][NT];
 #pragma unroll
         for (int u = 0; u < PD; ++u)
@@ -2060,17 +2060,19 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "conv launch");
   }
   // wave split (2 x 2 waves, 8 rows x 16 NTW channels each, 32 NTW channels per workgroup):
-  // each weight fragment feeds 8 MFMAs and the waves load different weights. It pays where
-  // it keeps the occupancy: the 32-channel-chunk pooled conv with 64 outputs (conv3 + pool:
-  // 0.32 -> 0.21 ms per 2048 shots, tools/conv_one.py l3); the other layers measured slower
-  // (registers: 4 -> 2 waves per SIMD). SPECENH_PATCH_WSPLIT=1 forces it wherever the
-  // channels allow, =0 turns it off. The accumulation order is unchanged: bitwise the same.
-  const int ntw = nt >= 4 ? 2 : 1;
+  // each weight fragment feeds 8 MFMAs instead of 4 and the waves load different weights,
+  // so the weight loads' L2 latency has twice the MFMA work to hide behind. Register budget
+  // held at 3 waves per SIMD. Per 2048 shots (tools/conv_one.py, 4x1 -> 2x2): conv2+pool
+  // 0.50 -> 0.45, conv3+pool 0.32 -> 0.21, convT1 0.39 -> 0.36, convT2 0.89 -> 0.80 ms.
+  // Default wherever the channels allow and the grid keeps >= 2 workgroups per CU;
+  // SPECENH_PATCH_WSPLIT=1 forces it, =0 turns it off. The accumulation order per output
+  // is unchanged: bitwise the same results.
+  const int ntw = nt >= 4 && CC == 32 ? 2 : 1;  // (2 with 64-channel chunks spills)
   const char* wse = std::getenv("SPECENH_PATCH_WSPLIT");
   const int wsm = wse ? std::atoi(wse) : -1;
   const bool ws_shape = CC != 1 && nt >= 2 && CO % (32 * ntw) == 0;
-  const bool ws_auto = CC == 32 && a.pool && nt == 4 &&
-                       (unsigned long long)tiles * (CO / (32 * ntw)) * (a.ph_shared ? 1 : nph) >= 512;
+  const bool ws_auto =
+      (unsigned long long)tiles * (CO / (32 * ntw)) * (a.ph_shared ? 1 : nph) >= 512;
   if (ws_shape && (wsm == 1 || (wsm < 0 && ws_auto))) {
     const dim3 gridw(tiles, (unsigned)(CO / (32 * ntw)), a.ph_shared ? 1 : nph);
     const size_t ldsw = patch_lds_bytes<T, CC>(a, nph, ntw, false);

@@ -87,7 +87,7 @@ __device__ __forceinline__ float act_f(float v, int act) {
 }
 
 template <typename T, bool POOL>
-__global__ __launch_bounds__(256) void conv_c1_mfma_kernel(C1mArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv_c1_mfma_kernel(C1mArgs a) {
   __shared__ __attribute__((aligned(16))) T sRow[PRS * PRW];
   __shared__ __attribute__((aligned(16))) uint4 sRec[PRS * TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -161,19 +161,23 @@ __global__ __launch_bounds__(256) void conv_c1_mfma_kernel(C1mArgs a) {
   __syncthreads();
   if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
 
-  // ---- MFMAs: wave rows 8 wave + i, column blocks cb (pixels 16 cb + l16) ----
+  // ---- MFMAs: wave rows 8 wave + 4 hf + i (two halves of 4 rows: half the accumulator
+  // registers live at a time), column blocks cb (pixels 16 cb + l16) ----
   const int nks = (K + 3) / 4;
-  f32x4 acc[8][2];
+#pragma unroll 1
+  for (int hf = 0; hf < 2; ++hf) {
+  const int rw0 = 8 * wave + 4 * hf;  // first tile row of this half
+  f32x4 acc[4][2];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         if (s >= nks) break;  // uniform
-        const int r = min(8 * wave + i + 4 * s + g4, PRS - 1);  // rows past K meet zero weights
+        const int r = min(rw0 + i + 4 * s + g4, PRS - 1);  // rows past K meet zero weights
         acc[i][cb] = mfma<T>(wf[s], sRec[r * TILE + 16 * cb + l16], acc[i][cb]);
       }
 
@@ -189,11 +193,11 @@ __global__ __launch_bounds__(256) void conv_c1_mfma_kernel(C1mArgs a) {
   if constexpr (POOL) {
     const int PHo = a.OH / 2, PWo = a.OW / 2;
 #pragma unroll
-    for (int ip = 0; ip < 4; ++ip)
+    for (int ip = 0; ip < 2; ++ip)
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         const int ox = ox0 + 16 * cb + l16;
-        const int py = (oy0 + 8 * wave + 2 * ip) / 2, px = ox / 2;
+        const int py = (oy0 + rw0 + 2 * ip) / 2, px = ox / 2;
         const bool store = (l16 & 1) == 0 && py < PHo && px < PWo && ch0 < a.CO;
         const long long o = (((long long)n * PHo + py) * PWo + px) * a.CO + ch0;
         T* dst = reinterpret_cast<T*>(a.out) + o;
@@ -237,10 +241,10 @@ __global__ __launch_bounds__(256) void conv_c1_mfma_kernel(C1mArgs a) {
   } else {
     const T* __restrict__ mk = reinterpret_cast<const T*>(a.mask);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
-        const int oy = oy0 + 8 * wave + i, ox = ox0 + 16 * cb + l16;
+        const int oy = oy0 + rw0 + i, ox = ox0 + 16 * cb + l16;
         if (oy >= a.OH || ox >= a.OW || ch0 >= a.CO) continue;
         const long long o = (((long long)n * a.OH + oy) * a.OW + ox) * a.CO + ch0;
         float v[4];
@@ -269,6 +273,7 @@ __global__ __launch_bounds__(256) void conv_c1_mfma_kernel(C1mArgs a) {
         }
       }
   }
+  }  // row halves
   }  // tile loop
 }
 

@@ -132,6 +132,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     wf[s] = uint4{w4[0], w4[1], w4[2], w4[3]};
   }
 
+  float bv[4];  // biases of this lane's channels co0 + 4 g4 + r
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int ch = co0 + 4 * g4 + r;
+    bv[r] = (a.bias && ch < a.CO) ? a.bias[ch] : 0.f;
+  }
+  // weights and biases are in registers before the loop: a wait for them inside the loop
+  // would also wait for the prefetch and (CDNA4 vmcnt counts stores) the previous stores
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0)
+
   // persistent over tiles blockIdx.x, + gridDim.x, ...: the next tile's rows are loaded
   // into registers while this tile's records, MFMAs and stores run
   int tile = blockIdx.x;
@@ -182,12 +192,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       }
 
   // ---- epilogue: lane holds channels co0 + 4 g4 + r of pixel (8 wave + i, 16 cb + l16) ----
-  float bv[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int ch = co0 + 4 * g4 + r;
-    bv[r] = (a.bias && ch < a.CO) ? a.bias[ch] : 0.f;
-  }
   const int ch0 = co0 + 4 * g4;
   const bool vec = (a.CO & 3) == 0;
   if constexpr (POOL) {

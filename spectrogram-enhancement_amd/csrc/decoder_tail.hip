@@ -226,6 +226,10 @@ __device__ __forceinline__ void tail_body(const TailArgs& a, T* sx, T* sy, int w
       wo_frag[s2] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.wo) +
                                                     (ky * KO + m) * CO + 8 * (kg & 1));
   }
+  // the weights and biases are in registers before the tile loop starts: otherwise the
+  // compiler's wait for them sits inside the loop, and on CDNA4 vmcnt also counts the
+  // previous tile's output stores, so every tile would wait for its predecessor's writes
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0)
   const int b0 = half * MAXBLK, nb = (a.dev & 1) ? 0 : min(MAXBLK, NBLK - b0);
 
   uint4 pf[XPF];

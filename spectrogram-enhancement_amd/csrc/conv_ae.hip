@@ -797,7 +797,7 @@ void conv_patch_kernel(ConvArgs a) {
         // (in-lane rows, then the lane pair), one bias add / ReLU / rounding per output.
         const bool relu = a.act == 1;
 #pragma unroll
-        for (int ip = 0; ip < 2; ++ip) {
+        for (int ip = 0; ip < MT / 2; ++ip) {
           const int oy = oy0 + wrow * MT + 2 * ip;
           const int py = oy / 2, pxo = ox / 2;
           const bool store = (px & 1) == 0 && py < PHo && pxo < PWo;
@@ -820,7 +820,7 @@ void conv_patch_kernel(ConvArgs a) {
         }
       } else
 #pragma unroll
-      for (int ip = 0; ip < 2; ++ip) {
+      for (int ip = 0; ip < MT / 2; ++ip) {
         const int oy = oy0 + wrow * MT + 2 * ip;
         const int py = oy / 2, pxo = ox / 2;
         const bool store = (px & 1) == 0 && py < PHo && pxo < PWo;

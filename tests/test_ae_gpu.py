@@ -556,18 +556,84 @@ def test_wave_split_patch_kernel_is_bitwise_identical(gpu_device, dtype, monkeyp
     default for the pooled 32-channel-chunk conv) runs the same k-step order per output as
     the 4 x 1 split: forward outputs and gradients are bitwise equal, forced on and off."""
     ops = ref_model_ops()
-    eng, _ = make(ops, (64, 64, 1), dtype=dtype, seed=47)
     rng = np.random.default_rng(13)
     x = rng.uniform(0, 1, (4, 64, 64, 1)).astype(np.float32)
     y = rng.uniform(0, 1, (4, 64, 64, 1)).astype(np.float32)
     outs, grads = [], []
     for flag in ("1", "0"):
+        # a fresh engine whose every activation buffer starts as NaN: an output element a
+        # variant fails to write cannot inherit the other variant's value
+        eng, _ = make(ops, (64, 64, 1), dtype=dtype, seed=47)
         monkeypatch.setenv("SPECENH_PATCH_WSPLIT", flag)
+        poison(eng, 4, False)
         outs.append(eng.forward(upload(eng, x), train=False).clone())
+        poison(eng, 4, True)
         eng.forward(upload(eng, x), train=True)
         eng.loss_and_grad(upload(eng, y))
         eng.backward()
         grads.append(eng.g.clone())
     torch.cuda.synchronize()
+    assert bool(torch.isfinite(outs[0]).all())
     assert torch.equal(outs[0], outs[1])
     assert torch.equal(grads[0], grads[1])
+
+
+def poison(eng, N, train):
+    """Fill every cached activation / gradient buffer of the engine for batch N with NaN
+    (0xFF for argmax bytes), so unwritten output elements show up in comparisons."""
+    b = eng._buffers(N, train)
+    for key in ("h", "d"):
+        for i, t in enumerate(b[key]):
+            if t is not None and i > 0:
+                t.fill_(float("nan"))
+    for t in b["am"]:
+        if t is not None:
+            t.fill_(255)
+
+
+@pytest.mark.parametrize("dtype", ["mixed_bfloat16", "float16"])
+def test_c5_shape_layers_at_large_batch(gpu_device, dtype):
+    """Near the launch shapes of the C5 bench (256 shots, 128 x 128): at this batch every layer
+    takes its large-grid variant (wave split, persistent C = 1 and tail kernels), which small
+    parity cases never select. Every intermediate (poisoned with NaN beforehand) vs a torch
+    fp32 layer applied to the same low-precision input: relative error within the
+    compute dtype's rounding."""
+    ops = ref_model_ops()
+    N = 256
+    eng, params = make(ops, (128, 128, 1), dtype=dtype, seed=53)
+    rng = np.random.default_rng(14)
+    x = upload(eng, rng.uniform(0, 1, (N, 128, 128, 1)).astype(np.float32))
+    poison(eng, N, False)
+    out = eng.forward(x, train=False)
+    torch.cuda.synchronize()
+    b = eng._buffers(N, False)
+    ws = [p for p in params if p is not None]
+    tol = 4e-3 if eng.tdt == torch.bfloat16 else 1e-3
+    torch.backends.cudnn.allow_tf32 = False
+    h, j, i = x, 0, 0
+    while i < len(ops):
+        op = ops[i]
+        # the engine's low-precision weights, fp32 biases
+        w = torch.as_tensor(ws[j]["W"], device=gpu_device).to(eng.tdt).float()
+        bias = torch.as_tensor(ws[j]["b"], device=gpu_device).float()
+        with torch.no_grad():
+            r = (ora.conv2d_same if op.kind == "conv" else ora.conv2d_transpose_same)(
+                h.float(), w, bias)
+            r = torch.sigmoid(r) if op.act == "sigmoid" else torch.relu(r)
+            pool = i + 1 < len(ops) and isinstance(ops[i + 1], type(ops[1]))
+            if pool:
+                r = ora.maxpool2(r)
+        got = b["h"][i + (2 if pool else 1)]
+        if got is None:  # the fused tail's map never reaches memory: compare at the output
+            h = r.to(eng.tdt).contiguous()
+            i += 1
+            j += 1
+            continue
+        got = got.float()
+        assert bool(torch.isfinite(got).all()), f"layer {i}: unwritten / non-finite elements"
+        err = float((got - r).norm() / r.norm())
+        assert err <= tol, f"layer {i} ({op.kind} {op.cin}->{op.cout}): rel {err:.2e}"
+        h = got.to(eng.tdt) if got.dtype != eng.tdt else b["h"][i + (2 if pool else 1)]
+        i += 2 if pool else 1
+        j += 1
+    assert out is b["h"][len(ops)]

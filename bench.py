@@ -676,6 +676,9 @@ def main():
                     "ref_output_std": float(np.std(np.stack(ref_all))),
                     "shots": 8, "reference": "fp64 CPU chain: scipy-semantics specgr -> numpy "
                                              "SVD denoiseSignal -> fp64 autoencoder restatement"}
+        if not accuracy["pass"]:
+            print(f"[bench] ACCURACY CHECK FAILED: out_rel {max(rels):.3e} > {tol}",
+                  file=sys.stderr)
 
     if use_dist:
         dist.barrier()

@@ -2062,15 +2062,17 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   // wave split (2 x 2 waves, 8 rows x 16 NTW channels each, 32 NTW channels per workgroup):
   // each weight fragment feeds 8 MFMAs instead of 4 and the waves load different weights,
   // so the weight loads' L2 latency has twice the MFMA work to hide behind. Register budget
-  // held at 3 waves per SIMD. Per 2048 shots (tools/conv_one.py, 4x1 -> 2x2): conv2+pool
-  // 0.50 -> 0.45, conv3+pool 0.32 -> 0.21, convT1 0.39 -> 0.36, convT2 0.89 -> 0.80 ms.
+  // held at 3 waves per SIMD. Per 2048 shots (tools/layer_ab.py HIP events, 4x1 -> 2x2):
+  // conv3+pool 0.26 -> 0.21, convT1 0.27 -> 0.22, convT2 0.56 -> 0.46 ms.
   // Default wherever the channels allow and the grid keeps >= 2 workgroups per CU;
   // SPECENH_PATCH_WSPLIT=1 forces it, =0 turns it off. The accumulation order per output
   // is unchanged: bitwise the same results.
   const int ntw = nt >= 4 && CC == 32 ? 2 : 1;  // (2 with 64-channel chunks spills)
   const char* wse = std::getenv("SPECENH_PATCH_WSPLIT");
   const int wsm = wse ? std::atoi(wse) : -1;
-  const bool ws_shape = CC != 1 && nt >= 2 && CO % (32 * ntw) == 0;
+  // not with 16-channel chunks: conv2+pool (C 16 -> 32) runs 0.48 ms with the split vs
+  // 0.38 without per 2048 shots (tools/layer_ab.py); 32/64-channel chunks gain 20-25 %
+  const bool ws_shape = CC >= 32 && nt >= 2 && CO % (32 * ntw) == 0;
   const bool ws_auto =
       (unsigned long long)tiles * (CO / (32 * ntw)) * (a.ph_shared ? 1 : nph) >= 512;
   if (ws_shape && (wsm == 1 || (wsm < 0 && ws_auto))) {

@@ -1,0 +1,61 @@
+"""Per-layer A/B of the C5 autoencoder forward (GPU): HIP-event times of every launch at
+the bench's launch shape, for each environment variant given on the command line.
+
+    python tools/layer_ab.py [--batch 2048] [--reps 20] "" "SPECENH_PATCH_WSPLIT=0" ...
+
+Each variant is a space-separated list of NAME=VALUE settings applied to os.environ (the
+library reads its SPECENH_* switches at every launch). Variants are interleaved per
+repetition so clock drift hits them alike; medians are printed."""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "spectrogram-enhancement_amd")]
+import bench  # noqa: E402
+from specenh import ae  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("variants", nargs="*")
+    a = ap.parse_args()
+    variants = a.variants or [""]
+    dev = torch.device("cuda", 0)
+    ops = []
+    for lay in bench.ae_layers():
+        ops.append(ae.PoolOp() if lay[0] == "pool" else
+                   ae.ConvOp(lay[0], lay[1], lay[2], lay[3], lay[4],
+                             stride=2 if lay[0] == "convT" else 1))
+    eng = ae.AutoencoderEngine(ops, (128, 128, 1), compute_dtype="float16", device=dev)
+    eng.set_keras_weights(bench.ae_weights())
+    x = eng.to_compute(torch.rand(a.batch, 128, 128, 1, device=dev))
+    base = dict(os.environ)
+    res = {v: [] for v in variants}
+    for rep in range(a.reps + 2):
+        for v in variants:
+            os.environ.clear()
+            os.environ.update(base)
+            for kv in v.split():
+                k, val = kv.split("=", 1)
+                os.environ[k] = val
+            timing = []
+            eng.forward(x, timing=timing)
+            torch.cuda.synchronize()
+            if rep >= 2:
+                res[v].append([s.elapsed_time(e) for s, e in timing])
+    names = bench.LAYER_NAMES_TAIL if eng.tail else bench.LAYER_NAMES
+    print("variant".ljust(40) + "".join(n.rjust(17) for n in names) + "total".rjust(10))
+    for v in variants:
+        med = np.median(np.array(res[v]), axis=0)
+        print((v or "default").ljust(40) + "".join(f"{m:17.4f}" for m in med) +
+              f"{med.sum():10.4f}")
+
+
+if __name__ == "__main__":
+    main()

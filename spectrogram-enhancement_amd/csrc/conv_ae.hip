@@ -282,6 +282,9 @@ struct ConvArgs {
   unsigned char* argmax;  // pooled argmax (dy*2+dx), or null
   // LDS-patch kernel, all phases in one workgroup: union patch origin/extent
   int ph_shared, upt, upl, PH, PW;
+  // conv_patch_kernel<..., WL>: the workgroup's weight rows staged in LDS at byte offset
+  // wl_off, row stride wl_rs elements (wl_rs / 2 = 8 mod 64 dwords: conflict-free fragments)
+  int wl_off, wl_rs;
 };
 
 // ------------------------------------------------------------------ forward / dgrad
@@ -418,6 +421,25 @@ struct Patch<16> { static constexpr int PST = 16; };  // 32-byte pixels
 template <>
 struct Patch<1> { static constexpr int PST = 1; };
 
+// 8 consecutive 16-bit weights through a buffer descriptor: the lane's row offset stays in
+// one VGPR for the whole k-loop and the k-step's column offset is a wave-uniform soffset, so
+// a weight-ring refill costs no VALU address arithmetic (and no temporaries whose reuse
+// would make the compiler drain the ring's other in-flight loads).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t weight_rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
+                                           (int)(bytes < 0x7fffffffll ? bytes : 0x7fffffffll),
+                                           0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ V8<T> ldw(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  static_assert(sizeof(T) == 2, "16-bit weights");
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  V8<T> v;
+  v.w[0] = a.x; v.w[1] = a.y; v.w[2] = a.z; v.w[3] = a.w;
+  return v;
+}
+
 template <typename T>
 __device__ __forceinline__ f32x4 mfma32(const V8<T>& a, const V8<T>& b, f32x4 acc) {
   if constexpr (__is_same(T, __bf16)) {
@@ -454,10 +476,15 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 // (row, column) parity sub-patches of 18 x 18, so tap (jy, jx) of output pixel (y, x) is
 // pixel (y + jy/2, x + jx/2) of sub-patch (jy&1, jx&1): the lanes' fragment reads stay
 // unit-stride and the k-step loop is the stride-1 one.
-template <typename T, int NT, int CC, bool POOL, bool PAIR = false, bool S2 = false, bool WS = false>
+template <typename T, int NT, int CC, bool POOL, bool PAIR = false, bool S2 = false, bool WS = false,
+          bool WL = false, bool K5 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WS ? 3 : SPECENH_PATCH_WPE(PAIR, NT, CC))))
 void conv_patch_kernel(ConvArgs a) {
   static_assert(!S2 || (CC == 16 && !POOL && !PAIR), "stride-2 patches: CC 16, plain epilogue");
+  static_assert(!WL || (CC == 16 && !PAIR && !WS), "LDS weights: the 16-channel single-chunk kernel");
+  // K5: a plain stride-1 5 x 5 conv of one phase and one channel chunk (host-checked), so
+  // every tap offset is a compile-time immediate of the fully unrolled k-loop
+  static_assert(!K5 || (WL && !S2), "compile-time taps: with LDS weights");
   static_assert(!WS || !PAIR, "wave split: not with the row-phase pair epilogue");
   constexpr int TILE = 16;
   constexpr int PST = Patch<CC>::PST;
@@ -574,6 +601,26 @@ void conv_patch_kernel(ConvArgs a) {
       if (p == ph_lo || nchunk > 1) {
         if (c > 0 || p > ph_lo) lds_sync();  // previous chunk's fragment reads are done
         stage(c);
+        if constexpr (WL) {
+          if (p == ph_lo) {  // this workgroup's 16 NT weight rows (all phases), once
+            const int Kf = K5 ? 400 : g0.Kf, kv = Kf / 8, nv = 16 * NT * kv;
+            T* sWt = reinterpret_cast<T*>(sP_raw + a.wl_off);
+            for (int e0 = tid; e0 < nv; e0 += 4 * 256) {
+              uint4 v[4];
+              int dst[4];
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const int e = min(e0 + 256 * k, nv - 1);
+                const int rr = e / kv, q = e - rr * kv;
+                v[k] = *reinterpret_cast<const uint4*>(W + (long long)min(n0 + rr, g0.CO - 1) * Kf + 8 * q);
+                dst[k] = rr * a.wl_rs + 8 * q;
+              }
+#pragma unroll
+              for (int k = 0; k < 4; ++k)
+                if (e0 + 256 * k < nv) *reinterpret_cast<uint4*>(sWt + dst[k]) = v[k];
+            }
+          }
+        }
         lds_sync();
       }
       if constexpr (CC >= 32) {
@@ -588,11 +635,12 @@ void conv_patch_kernel(ConvArgs a) {
         const int dy = upt - g.pad_t, dx = upl - g.pad_l;  // this phase's shift in the patch
         const int kwinv = (65536 + KWl - 1) / KWl;         // t / KW == (t * kwinv) >> 16, t < 32
         const int nsteps = ntap * SUB;
-        const T* wl[NT];
+        const __amdgpu_buffer_rsrc_t wrs = weight_rsrc(W, (long long)g.CO * Kfl * sizeof(T));
+        int wv[NT];  // byte offset of this lane's weight row (+ chunk, k group)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          wl[j] = W + (long long)min(n0 + 16 * j + px, g.CO - 1) * Kfl + c * CC + 8 * kgrp;
-        auto wcol_of = [&](int st) {
+          wv[j] = (int)(((long long)min(n0 + 16 * j + px, g.CO - 1) * Kfl + c * CC + 8 * kgrp) * sizeof(T));
+        auto wcol_of = [&](int st) {  // wave-uniform: scalar
           const int t = st / SUB, h = st - (st / SUB) * SUB;
           const int jy = (t * kwinv) >> 16, jx = t - jy * KWl;
           return ((ky0 + ks * jy) * KWf + kx0 + ks * jx) * Cl + 32 * h;
@@ -610,7 +658,7 @@ void conv_patch_kernel(ConvArgs a) {
           if (u < nsteps) {
             const int col = wcol_of(u);
 #pragma unroll
-            for (int j = 0; j < NT; ++j) wring[u][j] = ld8(wl[j] + col);
+            for (int j = 0; j < NT; ++j) wring[u][j] = ldw<T>(wrs, wv[j], col * (int)sizeof(T));
           }
         for (int s0 = 0; s0 < nsteps; s0 += PD)
 #pragma unroll
@@ -631,7 +679,7 @@ void conv_patch_kernel(ConvArgs a) {
           if (st + PD < nsteps) {
             const int col = wcol_of(st + PD);
 #pragma unroll
-            for (int j = 0; j < NT; ++j) wring[u][j] = ld8(wl[j] + col);
+            for (int j = 0; j < NT; ++j) wring[u][j] = ldw<T>(wrs, wv[j], col * (int)sizeof(T));
           }
         }
       } else if constexpr (CC == 16) {
@@ -644,10 +692,11 @@ void conv_patch_kernel(ConvArgs a) {
         const int kwinv = (65536 + KWl - 1) / KWl;
         const int nsteps = (ntap + 1) / 2;
         const bool second = (kgrp >> 1) != 0;
-        const T* wl[NT];
+        const __amdgpu_buffer_rsrc_t wrs = weight_rsrc(W, (long long)g.CO * Kfl * sizeof(T));
+        int wv[NT];
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          wl[j] = W + (long long)min(n0 + 16 * j + px, g.CO - 1) * Kfl + c * CC + 8 * (kgrp & 1);
+          wv[j] = (int)(((long long)min(n0 + 16 * j + px, g.CO - 1) * Kfl + c * CC + 8 * (kgrp & 1)) * sizeof(T));
         auto wcol_t = [&](int t) {
           const int jy = (t * kwinv) >> 16, jx = t - jy * KWl;
           return ((ky0 + ks * jy) * KWf + kx0 + ks * jx) * Cl;
@@ -659,19 +708,94 @@ void conv_patch_kernel(ConvArgs a) {
           else
             return ((jy + dy) * PW + jx + dx) * PST;
         };
-        auto wcol_of = [&](int st) {
+        // the two taps' columns are wave-uniform: the first as the soffset, the second as a
+        // per-lane delta (lane groups 2-3 take tap 2st + 1)
+        auto wload = [&](int st, V8<T> (&dst)[NT]) {
           const int c0 = wcol_t(2 * st), c1 = wcol_t(min(2 * st + 1, ntap - 1));
-          return second ? c1 : c0;
+          const int dl = second ? (c1 - c0) * (int)sizeof(T) : 0;
+#pragma unroll
+          for (int j = 0; j < NT; ++j) dst[j] = ldw<T>(wrs, wv[j] + dl, c0 * (int)sizeof(T));
         };
+        if constexpr (K5) {
+          // 13 steps of two taps, all offsets immediates: tap t = (jy, jx) sits at patch
+          // offset (jy * 20 + jx) * 16 and weight column 16 t. Lane groups 2-3 read tap
+          // 2st + 1: +16 elements in the weight row, and in the patch +16 (same kernel row)
+          // or +(20 - 4) * 16 (tap 2st ends a row) -- two per-lane bases, chosen per step
+          // at compile time.
+          constexpr int PWc = TILE - 1 + 5;
+          const T* wb = reinterpret_cast<const T*>(sP_raw + a.wl_off) + px * a.wl_rs +
+                        8 * (kgrp & 1) + (second ? 16 : 0);
+          // the last step has no tap 25: lane groups 2-3 re-read tap 24's weights (their
+          // patch operand is zero); past the last weight row is unallocated LDS, whose
+          // stale bits could be Inf/NaN (and 0 x Inf is NaN)
+          const T* wbl = wb - (second ? 16 : 0);
+          int pb0[MT], pb1[MT];
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            pb0[i] = rbase[i] + 8 * (kgrp & 1) + (second ? PST : 0);
+            pb1[i] = rbase[i] + 8 * (kgrp & 1) + (second ? (PWc - 4) * PST : 0);
+          }
+#pragma unroll
+          for (int st = 0; st < 13; ++st) {
+            const int t0 = 2 * st, jy = t0 / 5, jx = t0 % 5;
+            const int ao = (jy * PWc + jx) * PST;
+            V8<T> wf[NT], pv[MT];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+              const uint4 q = *reinterpret_cast<const uint4*>((st == 12 ? wbl : wb) + 16 * j * a.wl_rs + 16 * t0);
+              wf[j].w[0] = q.x; wf[j].w[1] = q.y; wf[j].w[2] = q.z; wf[j].w[3] = q.w;
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+              const uint4 q = *reinterpret_cast<const uint4*>(sP + (jx == 4 ? pb1[i] : pb0[i]) + ao);
+              pv[i].w[0] = q.x; pv[i].w[1] = q.y; pv[i].w[2] = q.z; pv[i].w[3] = q.w;
+            }
+            if (st == 12 && second) {  // tap 25 does not exist
+#pragma unroll
+              for (int i = 0; i < MT; ++i) zero8(pv[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+              for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wf[j], pv[i], acc[i][j]);
+          }
+        } else if constexpr (WL) {
+          // weights from the LDS copy: no global loads (and no vmcnt waits) in the k-loop
+          const T* sWt = reinterpret_cast<const T*>(sP_raw + a.wl_off) + px * a.wl_rs + 8 * (kgrp & 1);
+          for (int st = 0; st < nsteps; ++st) {
+            const int a0 = aoff_t(2 * st), a1 = aoff_t(min(2 * st + 1, ntap - 1));
+            const int aoff = (second ? a1 : a0) + 8 * (kgrp & 1);
+            const int c0 = wcol_t(2 * st), c1 = wcol_t(min(2 * st + 1, ntap - 1));
+            const int wo = second ? c1 : c0;
+            V8<T> wf[NT], pv[MT];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+              const uint4 q = *reinterpret_cast<const uint4*>(sWt + 16 * j * a.wl_rs + wo);
+              wf[j].w[0] = q.x; wf[j].w[1] = q.y; wf[j].w[2] = q.z; wf[j].w[3] = q.w;
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+              const uint4 q = *reinterpret_cast<const uint4*>(sP + rbase[i] + aoff);
+              pv[i].w[0] = q.x; pv[i].w[1] = q.y; pv[i].w[2] = q.z; pv[i].w[3] = q.w;
+            }
+            if (__builtin_expect(2 * st + 1 >= ntap, 0)) {
+              if (second) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i) zero8(pv[i]);
+              }
+              __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+              for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wf[j], pv[i], acc[i][j]);
+          }
+        } else {
         constexpr int PD = WS ? (NT == 1 ? 4 : 2) : (NT >= 3 ? 2 : (NT == 2 ? 2 : 8));
         V8<T> wring[PD][NT];
 #pragma unroll
         for (int u = 0; u < PD; ++u)
-          if (u < nsteps) {
-            const int col = wcol_of(u);
-#pragma unroll
-            for (int j = 0; j < NT; ++j) wring[u][j] = ld8(wl[j] + col);
-          }
+          if (u < nsteps) wload(u, wring[u]);
         for (int s0 = 0; s0 < nsteps; s0 += PD)
 #pragma unroll
         for (int u = 0; u < PD; ++u) {
@@ -697,12 +821,9 @@ void conv_patch_kernel(ConvArgs a) {
           for (int i = 0; i < MT; ++i)
 #pragma unroll
             for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wring[u][j], pv[i], acc[i][j]);
-          if (st + PD < nsteps) {
-            const int col = wcol_of(st + PD);
-#pragma unroll
-            for (int j = 0; j < NT; ++j) wring[u][j] = ld8(wl[j] + col);
-          }
+          if (st + PD < nsteps) wload(st + PD, wring[u]);
         }
+        }  // !WL
       } else {
         // ---- k-steps: one MFMA K=32 slab each; weights are the A operand (rows = output
         // channels), the patch the B operand (columns = pixels): D[channel][pixel] ----
@@ -2058,6 +2179,44 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
     else SPECENH_PAIR(4);
 #undef SPECENH_PAIR
     return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "conv launch");
+  }
+  // 16-channel single-chunk convs (the model's conv2, 16 -> 32): the workgroup's weight rows
+  // are staged in LDS next to the patch, so the k-loop issues no global loads. With the
+  // weights streamed from L2 into a register ring the compiler drained every in-flight ring
+  // load at each k-step (s_waitcnt vmcnt(0)); SPECENH_PATCH_NO_WL=1 restores that path.
+  if constexpr (CC == 16) {
+    const int Kf = a.g[0].Kf;
+    if (nph == 1 && !a.ph_shared && a.g[0].C == 16 && Kf % 8 == 0 &&
+        !getenv_flag("SPECENH_PATCH_NO_WL")) {
+      const int rs_dw = (Kf / 2 - 8 + 63) / 64 * 64 + 8;  // >= Kf / 2 and = 8 mod 64
+      a.wl_rs = 2 * rs_dw;
+      const size_t pl = patch_lds_bytes<T, CC>(a, nph, nt, false);
+      a.wl_off = (int)pl;
+      const size_t lds = pl + (size_t)16 * nt * a.wl_rs * sizeof(T);
+      const Geo& g = a.g[0];
+      const bool k5 = g.KH == 5 && g.KW == 5 && g.ky0 == 0 && g.kx0 == 0 && g.kstep == 1 &&
+                      g.KWf == 5 && Kf == 400 && !getenv_flag("SPECENH_PATCH_NO_K5");
+      if (lds <= 48 * 1024) {
+        const dim3 grid(tiles, (unsigned)((CO + 16 * nt - 1) / (16 * nt)), 1);
+#define SPECENH_PATCHL(NT, P)                                                                       \
+  if (k5) hipLaunchKernelGGL((conv_patch_kernel<T, NT, 16, P, false, false, false, true, true>), grid, \
+                             dim3(256), lds, st, a);                                                 \
+  else hipLaunchKernelGGL((conv_patch_kernel<T, NT, 16, P, false, false, false, true>), grid, dim3(256), lds, st, a)
+        if (a.pool) {
+          if (nt == 1) SPECENH_PATCHL(1, true);
+          else if (nt == 2) SPECENH_PATCHL(2, true);
+          else if (nt == 3) SPECENH_PATCHL(3, true);
+          else SPECENH_PATCHL(4, true);
+        } else {
+          if (nt == 1) SPECENH_PATCHL(1, false);
+          else if (nt == 2) SPECENH_PATCHL(2, false);
+          else if (nt == 3) SPECENH_PATCHL(3, false);
+          else SPECENH_PATCHL(4, false);
+        }
+#undef SPECENH_PATCHL
+        return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "conv launch");
+      }
+    }
   }
   // wave split (2 x 2 waves, 8 rows x 16 NTW channels each, 32 NTW channels per workgroup):
   // each weight fragment feeds 8 MFMAs instead of 4 and the waves load different weights,

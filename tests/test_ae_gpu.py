@@ -550,21 +550,25 @@ def test_convt_row_phase_pairs_bitwise_identical(gpu_device, dtype, hw, monkeypa
     assert torch.equal(grads[0], grads[1])
 
 
+@pytest.mark.parametrize("switch", [("SPECENH_PATCH_WSPLIT", "1", "0"),
+                                    ("SPECENH_PATCH_NO_WL", "0", "1")])
 @pytest.mark.parametrize("dtype", ["mixed_bfloat16", "float16"])
-def test_wave_split_patch_kernel_is_bitwise_identical(gpu_device, dtype, monkeypatch):
-    """conv_patch_kernel's 2 x 2 wave split (8 rows x half the channels per wave, the
-    default for the pooled 32-channel-chunk conv) runs the same k-step order per output as
-    the 4 x 1 split: forward outputs and gradients are bitwise equal, forced on and off."""
+def test_wave_split_patch_kernel_is_bitwise_identical(gpu_device, dtype, switch, monkeypatch):
+    """conv_patch_kernel's variants run the same k-step order per output: the 2 x 2 wave
+    split (8 rows x half the channels per wave, the default for 32/64-channel chunks) vs the
+    4 x 1 split, and the 16-channel kernel's LDS-resident weights vs the register ring fed
+    from L2. Forward outputs and gradients are bitwise equal, each variant forced on and off."""
+    env, on, off = switch
     ops = ref_model_ops()
     rng = np.random.default_rng(13)
     x = rng.uniform(0, 1, (4, 64, 64, 1)).astype(np.float32)
     y = rng.uniform(0, 1, (4, 64, 64, 1)).astype(np.float32)
     outs, grads = [], []
-    for flag in ("1", "0"):
+    for flag in (on, off):
         # a fresh engine whose every activation buffer starts as NaN: an output element a
         # variant fails to write cannot inherit the other variant's value
         eng, _ = make(ops, (64, 64, 1), dtype=dtype, seed=47)
-        monkeypatch.setenv("SPECENH_PATCH_WSPLIT", flag)
+        monkeypatch.setenv(env, flag)
         poison(eng, 4, False)
         outs.append(eng.forward(upload(eng, x), train=False).clone())
         poison(eng, 4, True)

@@ -660,11 +660,16 @@ void conv_patch_kernel(ConvArgs a) {
 #pragma unroll
             for (int j = 0; j < NT; ++j) wring[u][j] = ldw<T>(wrs, wv[j], col * (int)sizeof(T));
           }
-        for (int s0 = 0; s0 < nsteps; s0 += PD)
+        // whole rounds of PD steps with unconditional refills (the last PD refills re-load
+        // the last step's column, unused), so every ring slot is refilled exactly once per
+        // round and the compiler keeps the slots in place: a step waits only for its own
+        // slot's load, PD - 1 rounds old. A conditional refill had the slots rotated through
+        // register copies and every step waiting for the youngest load (vmcnt(0)).
+        int s0 = 0;
+        for (; s0 + PD <= nsteps; s0 += PD)
 #pragma unroll
         for (int u = 0; u < PD; ++u) {
           const int st = s0 + u;
-          if (st >= nsteps) break;
           const int aoff = aoff_of(st) + 8 * kgrp;
           V8<T> pv[MT];
 #pragma unroll
@@ -676,11 +681,25 @@ void conv_patch_kernel(ConvArgs a) {
           for (int i = 0; i < MT; ++i)
 #pragma unroll
             for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wring[u][j], pv[i], acc[i][j]);
-          if (st + PD < nsteps) {
-            const int col = wcol_of(st + PD);
+          const int col = wcol_of(min(st + PD, nsteps - 1));
 #pragma unroll
-            for (int j = 0; j < NT; ++j) wring[u][j] = ldw<T>(wrs, wv[j], col * (int)sizeof(T));
+          for (int j = 0; j < NT; ++j) wring[u][j] = ldw<T>(wrs, wv[j], col * (int)sizeof(T));
+        }
+#pragma unroll
+        for (int u = 0; u < PD - 1; ++u) {  // the remaining nsteps % PD steps: slots 0, 1, ..
+          const int st = s0 + u;
+          if (st >= nsteps) break;
+          const int aoff = aoff_of(st) + 8 * kgrp;
+          V8<T> pv[MT];
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            const uint4 q = *reinterpret_cast<const uint4*>(sP + rbase[i] + aoff);
+            pv[i].w[0] = q.x; pv[i].w[1] = q.y; pv[i].w[2] = q.z; pv[i].w[3] = q.w;
           }
+#pragma unroll
+          for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = mfma32<T>(wring[u][j], pv[i], acc[i][j]);
         }
       } else if constexpr (CC == 16) {
         // ---- 16 channels: one MFMA K=32 slab = two taps (lane groups kgrp 0-1: tap 2st,

@@ -471,6 +471,14 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 #define SPECENH_PATCH_WPE(PAIR, NT, CC) \
   ((PAIR && NT == 1) || (CC == 16 && NT == 2) ? 4 : ((CC == 32 && NT == 4) || CC == 64 ? 3 : 1))
 #endif
+// weight-ring depth of the wave-split kernel (k-steps of loads in flight per wave); 8 for
+// NT = 1 measured 5 % slower on convT1/convT2, 4 for NT = 2 spills
+#ifndef SPECENH_WS_PD1
+#define SPECENH_WS_PD1 4
+#endif
+#ifndef SPECENH_WS_PD2
+#define SPECENH_WS_PD2 2
+#endif
 // S2 (stride-2 conv, CC == 16, one phase: the input gradient of a Conv2DTranspose): the
 // 35 x 35 input patch of a 16 x 16 output tile is staged de-interleaved into its four
 // (row, column) parity sub-patches of 18 x 18, so tap (jy, jx) of output pixel (y, x) is
@@ -651,7 +659,7 @@ void conv_patch_kernel(ConvArgs a) {
           return ((jy + dy) * PW + jx + dx) * PST + 32 * h;
         };
         // ring of PD weight fragments consumed in place (no copies) and refilled PD steps ahead
-        constexpr int PD = WS ? (NT == 1 ? 4 : 2) : (NT >= 3 ? (CC == 64 ? 1 : 2) : (NT == 2 ? 2 : 8));
+        constexpr int PD = WS ? (NT == 1 ? SPECENH_WS_PD1 : SPECENH_WS_PD2) : (NT >= 3 ? (CC == 64 ? 1 : 2) : (NT == 2 ? 2 : 8));
         V8<T> wring[PD][NT];
 #pragma unroll
         for (int u = 0; u < PD; ++u)

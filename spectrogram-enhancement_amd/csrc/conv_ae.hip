@@ -461,10 +461,11 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 // and computes its two column phases (py, 0) and (py, 1) over one staged patch. Phase
 // (py, 0) waits in registers, packed to T; after (py, 1) the patch is dead, so both are
 // interleaved into an LDS image of the 16 output rows x 32 pixels x CO channels that
-// aliases the patch, and leave as 16-byte stores of whole rows. Without it every 128-B
-// output line is completed by two phase stores microseconds apart, and the half-written
-// line is evicted in between (2-2.6x the algorithmic write traffic). The
-// two row phases of a tile run on one XCD back to back and share its input lines in L2.
+// aliases the patch, and leave as 16-byte stores of whole rows, so no 128-B output line is
+// completed by two phase stores microseconds apart. Opt-in (SPECENH_CONVT_PAIR=1): with
+// all four phases in one workgroup (ph_shared, the default) the measured convT write
+// traffic is 1.02-1.25x algorithmic (profiles/pmc_traffic.json). The two row phases of a
+// tile run on one XCD back to back and share its input lines in L2.
 
 // waves per SIMD the register budget is sized for (4 -> 128 VGPRs, 3 -> 168, 2 -> 256)
 #ifndef SPECENH_PATCH_WPE

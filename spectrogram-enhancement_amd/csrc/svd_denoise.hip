@@ -513,99 +513,111 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
   __syncthreads();
   GZ(sZ, sY);
   __syncthreads();
-  for (int it = 0; it < iters; ++it) {
-    if (it + 1 < iters && (SPECENH_SS_SINGLE_QR)) {
-      // Intermediate rounds only have to keep the block well conditioned (G Z re-amplifies
-      // the dominant directions anyway): one CholeskyQR pass. The basis that feeds the
-      // Rayleigh-Ritz step below gets the full CholeskyQR2.
-      cholqr<P>(sY, sZ, r, sS, sRi);  // Z = orth(Y) to ~cond(Y) * eps
-      GZ(sZ, sY);                     // Y = G Z
-      __syncthreads();
-      continue;
-    }
-    cholqr<P>(sY, sZ, r, sS, sRi);  // Z = orth(Y)
-    cholqr<P>(sZ, sY, r, sS, sRi);  // second pass into Y ...
-    GZ(sY, sZ);                     // ... Z = G * orth(Y)
-    __syncthreads();
-    // swap names: basis in sY, product in sZ -> keep (Y := product, Z := basis)
-    float* t = sY;
-    sY = sZ;
-    sZ = t;
-  }
-  // Rayleigh-Ritz: H = Z^T (G Z) = Z^T Y
-  if constexpr (P == 8) {
-    prod8(sZ, sY, r, sPart, sS);
-    if (tid < 64) sH[tid] = (float)sS[tid];
-  } else {
-    for (int q = tid; q < P * P; q += SS_THREADS) {
-      const int a = q / P, c = q % P;
-      double s = 0.0;
-      for (int i = 0; i < r; ++i) s += (double)sZ[i * P + a] * (double)sY[i * P + c];
-      sH[q] = (float)s;
-    }
-  }
-  __syncthreads();
-  for (int q = tid; q < P * P; q += SS_THREADS) {  // symmetrise
-    const int a = q / P, c = q % P;
-    if (a < c) {
-      const float m = 0.5f * (sH[a * P + c] + sH[c * P + a]);
-      sH[a * P + c] = m;
-      sH[c * P + a] = m;
-    }
-  }
-  __syncthreads();
-  if (tid < 64) {
-    jacobi<P>(sH, sQ, sCS, sPair);
-    if (tid == 0) {  // sort Ritz values descending (insertion sort, P <= 64)
-      for (int c = 0; c < P; ++c) sOrd[c] = c;
-      for (int c = 1; c < P; ++c) {
-        const int key = sOrd[c];
-        int d = c - 1;
-        while (d >= 0 && sH[sOrd[d] * P + sOrd[d]] < sH[key * P + key]) {
-          sOrd[d + 1] = sOrd[d];
-          --d;
-        }
-        sOrd[d + 1] = key;
-      }
-    }
-  }
-  __syncthreads();
-  if (flags) {
-    auto bsum = [&](double v) {
+  auto bsum = [&](double v) {
 #pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
-      __syncthreads();
-      if ((tid & 63) == 0) sRed[tid >> 6] = v;
-      __syncthreads();
-      return (sRed[0] + sRed[1]) + (sRed[2] + sRed[3]);
-    };
-    double tr = 0.0;
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+    __syncthreads();
+    if ((tid & 63) == 0) sRed[tid >> 6] = v;
+    __syncthreads();
+    return (sRed[0] + sRed[1]) + (sRed[2] + sRed[3]);
+  };
+  double tr = 0.0;  // tr(G) = ||X||_F^2, for the flag's tolerance
+  if (flags) {
     for (int i = tid; i < r; i += SS_THREADS) tr += Gb[(long long)i * r + i];
     tr = bsum(tr);
-    int bad = 0;
-    for (int which = 0; which < 2; ++which) {
-      const int c = which == 0 ? K - 1 : cut2;  // uniform
-      if (c < 0 || c >= K) continue;
-      const int col = sOrd[c];
-      const double th = sH[col * P + col];
-      double acc = 0.0;
-      for (int i = tid; i < r; i += SS_THREADS) {
-        double ri = 0.0;
-#pragma unroll
-        for (int d = 0; d < P; ++d)
-          ri = fma((double)sY[i * P + d] - th * (double)sZ[i * P + d], (double)sQ[d * P + col], ri);
-        acc = fma(ri, ri, acc);
-      }
-      const double res = sqrt(bsum(acc));
-      if (c + 1 >= P) {
-        if (P < r) bad = 1;  // no Ritz value past the cut to measure the gap against
+  }
+  // Staged first pass for the default K = 1 (P = 8): 2 rounds, Rayleigh-Ritz and the
+  // convergence check; only a matrix the check flags runs the remaining rounds (from the
+  // current basis) and a second Rayleigh-Ritz. Log-spectrograms (a dominant first
+  // component) converge in 2 rounds; a small gap (the gapped C3 set, s2/s1 = 0.8) takes 5.
+  const int stage1 = (P == 8 && flags && !only && iters > 2) ? 2 : iters;
+  int bad = 0;
+  for (int stage = 0; stage < 2; ++stage) {
+    const int nit = stage == 0 ? stage1 : iters - stage1;
+    for (int it = 0; it < nit; ++it) {
+      if (it + 1 < nit && (SPECENH_SS_SINGLE_QR)) {
+        // Intermediate rounds only have to keep the block well conditioned (G Z
+        // re-amplifies the dominant directions anyway): one CholeskyQR pass. The basis
+        // that feeds the Rayleigh-Ritz step below gets the full CholeskyQR2.
+        cholqr<P>(sY, sZ, r, sS, sRi);  // Z = orth(Y) to ~cond(Y) * eps
+        GZ(sZ, sY);                     // Y = G Z
+        __syncthreads();
         continue;
       }
-      const double gap = th - (double)sH[sOrd[c + 1] * P + sOrd[c + 1]];
-      if (!(sqrt(fmax(th, 0.0)) * res <= (double)tolv * gap * sqrt(fmax(tr, 0.0)))) bad = 1;
+      cholqr<P>(sY, sZ, r, sS, sRi);  // Z = orth(Y)
+      cholqr<P>(sZ, sY, r, sS, sRi);  // second pass into Y ...
+      GZ(sY, sZ);                     // ... Z = G * orth(Y)
+      __syncthreads();
+      // swap names: basis in sY, product in sZ -> keep (Y := product, Z := basis)
+      float* t = sY;
+      sY = sZ;
+      sZ = t;
     }
-    if (tid == 0) flags[b] = bad;
+    // Rayleigh-Ritz: H = Z^T (G Z) = Z^T Y
+    if constexpr (P == 8) {
+      prod8(sZ, sY, r, sPart, sS);
+      if (tid < 64) sH[tid] = (float)sS[tid];
+    } else {
+      for (int q = tid; q < P * P; q += SS_THREADS) {
+        const int a = q / P, c = q % P;
+        double s = 0.0;
+        for (int i = 0; i < r; ++i) s += (double)sZ[i * P + a] * (double)sY[i * P + c];
+        sH[q] = (float)s;
+      }
+    }
+    __syncthreads();
+    for (int q = tid; q < P * P; q += SS_THREADS) {  // symmetrise
+      const int a = q / P, c = q % P;
+      if (a < c) {
+        const float m = 0.5f * (sH[a * P + c] + sH[c * P + a]);
+        sH[a * P + c] = m;
+        sH[c * P + a] = m;
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      jacobi<P>(sH, sQ, sCS, sPair);
+      if (tid == 0) {  // sort Ritz values descending (insertion sort, P <= 64)
+        for (int c = 0; c < P; ++c) sOrd[c] = c;
+        for (int c = 1; c < P; ++c) {
+          const int key = sOrd[c];
+          int d = c - 1;
+          while (d >= 0 && sH[sOrd[d] * P + sOrd[d]] < sH[key * P + key]) {
+            sOrd[d + 1] = sOrd[d];
+            --d;
+          }
+          sOrd[d + 1] = key;
+        }
+      }
+    }
+    __syncthreads();
+    bad = 0;
+    if (flags) {
+      for (int which = 0; which < 2; ++which) {
+        const int c = which == 0 ? K - 1 : cut2;  // uniform
+        if (c < 0 || c >= K) continue;
+        const int col = sOrd[c];
+        const double th = sH[col * P + col];
+        double acc = 0.0;
+        for (int i = tid; i < r; i += SS_THREADS) {
+          double ri = 0.0;
+#pragma unroll
+          for (int d = 0; d < P; ++d)
+            ri = fma((double)sY[i * P + d] - th * (double)sZ[i * P + d], (double)sQ[d * P + col], ri);
+          acc = fma(ri, ri, acc);
+        }
+        const double res = sqrt(bsum(acc));
+        if (c + 1 >= P) {
+          if (P < r) bad = 1;  // no Ritz value past the cut to measure the gap against
+          continue;
+        }
+        const double gap = th - (double)sH[sOrd[c + 1] * P + sOrd[c + 1]];
+        if (!(sqrt(fmax(th, 0.0)) * res <= (double)tolv * gap * sqrt(fmax(tr, 0.0)))) bad = 1;
+      }
+    }
+    if (!bad || stage1 >= iters) break;  // uniform: converged, or no second stage
   }
+  if (flags && tid == 0) flags[b] = bad;
   float* Vb = V + b * (long long)r * K;  // V[:, c] = Z Q[:, ord[c]], c < K
   for (int idx = tid; idx < r * K; idx += SS_THREADS) {
     const int i = idx / K, c = idx % K;

@@ -509,9 +509,14 @@ void conv_patch_kernel(ConvArgs a) {
   __shared__ int sTap[MAXPH][32];  // patch offset of tap t (elements), -1 past the last tap
   __shared__ int sCol[MAXPH][32];  // weight column of tap t at ci = 0
 
+  // the per-tile program; K5 workgroups run it persistently over tiles blockIdx.x,
+  // + gridDim.x, ... with the weight rows staged once (first)
+  auto body = [&](const int bx_in, const bool first) {
+  if (!first) lds_sync();  // every wave is done with the previous tile's patch
+
   // ---- phases of this workgroup: all of them over one shared patch, a row-phase pair
   // (PAIR), or blockIdx.z ----
-  int bx = (int)blockIdx.x, pyp = 0;
+  int bx = bx_in, pyp = 0;
   if constexpr (PAIR) {  // blocks 16q + 8py + x: tile 8q + x, row phase py, XCD x
     const int j = bx >> 3;
     pyp = j & 1;
@@ -611,7 +616,7 @@ void conv_patch_kernel(ConvArgs a) {
         if (c > 0 || p > ph_lo) lds_sync();  // previous chunk's fragment reads are done
         stage(c);
         if constexpr (WL) {
-          if (p == ph_lo) {  // this workgroup's 16 NT weight rows (all phases), once
+          if (p == ph_lo && first) {  // this workgroup's 16 NT weight rows (all phases), once
             const int Kf = K5 ? 400 : g0.Kf, kv = Kf / 8, nv = 16 * NT * kv;
             T* sWt = reinterpret_cast<T*>(sP_raw + a.wl_off);
             for (int e0 = tid; e0 < nv; e0 += 4 * 256) {
@@ -1134,6 +1139,19 @@ void conv_patch_kernel(ConvArgs a) {
         }
       }
     }
+  }
+  };
+  if constexpr (K5) {
+    // persistent: the weight rows stay in LDS for all of the workgroup's tiles
+    const Geo& gk = a.g[0];
+    const int total = gk.N * ((gk.OH + 15) / 16) * ((gk.OW + 15) / 16);
+    bool first = true;
+    for (int t = (int)blockIdx.x; t < total; t += (int)gridDim.x) {
+      body(t, first);
+      first = false;
+    }
+  } else {
+    body((int)blockIdx.x, true);
   }
 }
 
@@ -2224,10 +2242,20 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
       const Geo& g = a.g[0];
       const bool k5 = g.KH == 5 && g.KW == 5 && g.ky0 == 0 && g.kx0 == 0 && g.kstep == 1 &&
                       g.KWf == 5 && Kf == 400 && !getenv_flag("SPECENH_PATCH_NO_K5");
-      if (lds <= 48 * 1024) {
+      // LDS weights only with the persistent K5 kernel: restaged per tile (any other
+      // 16-channel geometry) they measured slower than the L2 weight ring
+      if (k5 && lds <= 48 * 1024) {
         const dim3 grid(tiles, (unsigned)((CO + 16 * nt - 1) / (16 * nt)), 1);
+        static int cus = 0;  // persistent K5 grid: 4 workgroups per CU (LDS and registers)
+        if (cus == 0) {
+          int dev = 0;
+          if (hipGetDevice(&dev) != hipSuccess ||
+              hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        }
+        const dim3 gridk(std::min<unsigned>(tiles, 4u * (unsigned)cus), grid.y, 1);
 #define SPECENH_PATCHL(NT, P)                                                                       \
-  if (k5) hipLaunchKernelGGL((conv_patch_kernel<T, NT, 16, P, false, false, false, true, true>), grid, \
+  if (k5) hipLaunchKernelGGL((conv_patch_kernel<T, NT, 16, P, false, false, false, true, true>), gridk, \
                              dim3(256), lds, st, a);                                                 \
   else hipLaunchKernelGGL((conv_patch_kernel<T, NT, 16, P, false, false, false, true>), grid, dim3(256), lds, st, a)
         if (a.pool) {

@@ -28,8 +28,9 @@ Rank 0 prints ONE JSON line with, besides the contract fields:
                 measured time (HIP events around every launch, on its stream). Its bound is
                 whichever floor is higher: algorithmic HBM bytes (activations read once and
                 written once + weights, ae_layer_costs) / 8 TB/s, or useful FLOPs (SURVEY §8
-                A7 MACs x 2) / the unit's peak (MFMA 2.5 PFLOP/s dense fp16; the 1-in / 1-out
-                channel layers run on the VALU, v_dot2 314.6 TFLOP/s). traffic = measured HBM
+                A7 MACs x 2) / the unit's peak (MFMA 2.5 PFLOP/s dense fp16 for every layer of
+                the fused forward; an unfused 1-output-channel conv would run on the VALU,
+                v_dot2 314.6 TFLOP/s). traffic = measured HBM
                 bytes of that launch from profiles/pmc_traffic.json (rocprofv3 --pmc passes of
                 tools/pmc_traffic.sh at the same shapes); stages.ae_layers has every layer.
   stages        per-stage ms of one slice (stages.shots_per_launch shots: the launch shape

@@ -154,13 +154,36 @@ def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4, tail=False):
     return res
 
 
-def load_pmc_traffic():
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+PMC_FILE = os.path.join(REPO, "profiles", "pmc_r03.json")
+
+
+def load_pmc():
+    """Per-stage PMC records of tools/pmc_fold.py: {target: {stage: {"symbol", "batch",
+    "fetch_bytes", "write_bytes", "hbm_bytes", ...}}} (rocprofv3 --pmc passes of
+    tools/pmc_refresh.sh at the bench's launch shapes)."""
     try:
-        with open(path) as fh:
+        with open(PMC_FILE) as fh:
             return json.load(fh)
     except (OSError, ValueError):
         return {}
+
+
+def pmc_traffic(pmc, target, stage, symbols, launch_batch):
+    """HBM bytes of one run of ``stage`` (its launches, ``symbols`` in order) at
+    ``launch_batch`` shots from the PMC record, or (None, reason) when there is no record or
+    it was taken on different kernels than the ones just timed (symbol mismatch: the
+    counters would describe code that no longer runs)."""
+    if isinstance(symbols, str):
+        symbols = [symbols]
+    rec = pmc.get(target, {}).get(stage)
+    if rec is None:
+        return None, f"no PMC record for {target}/{stage}"
+    if list(rec.get("symbols", [])) != list(symbols):
+        msg = (f"PMC record for {target}/{stage} is of {rec.get('symbols')}, the timed launch "
+               f"ran {list(symbols)}: traffic withheld (rerun tools/pmc_refresh.sh)")
+        print(f"[bench] WARNING: {msg}", file=sys.stderr)
+        return None, msg
+    return rec["hbm_bytes"] * launch_batch / rec["batch"], None
 
 
 # ------------------------------------------------------------------ CPU baseline
@@ -187,14 +210,42 @@ def _cpu_worker(shots):
     return len(shots)
 
 
+def host_cpu_share():
+    """(worker count, where it came from): the CPU bandwidth this job may use — the cgroup
+    quota (v2 cpu.max or v1 cfs_quota_us / cfs_period_us), capped by the affinity mask and
+    by OMP_NUM_THREADS when the launcher sets it (the GPU box: 16 per GPU) — never the whole
+    machine that sched_getaffinity alone reports there."""
+    affinity = len(os.sched_getaffinity(0))
+    share, src = affinity, f"sched_getaffinity ({affinity})"
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+                q = float(fh.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+                per = float(fh.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None and int(quota) < share:
+        share, src = max(1, int(quota)), f"cgroup cpu quota ({quota:g} CPUs)"
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < share:
+        share, src = int(omp), f"OMP_NUM_THREADS={omp} (launcher's per-job CPU share)"
+    return share, src
+
+
 def cpu_baseline(n_shots: int) -> dict:
     """The C5 chain on the host: one shot per task, one thread per worker, all cores."""
     from specenh.synthetic import plasma_chirps
 
-    # The GPU box allots 16 host CPUs per GPU (its job limits; sched_getaffinity shows
-    # the whole machine there), so the baseline uses at most 16 worker processes.
-    affinity = len(os.sched_getaffinity(0))
-    cores = min(16, affinity)
+    cores, cores_src = host_cpu_share()
     x = plasma_chirps(n_shots, L5, seed0=0, dtype=np.float16).astype(np.float64)
     chunks = [x[i::cores] for i in range(cores)]
     # one BLAS/OpenMP thread per worker, set before the workers import numpy/torch
@@ -216,9 +267,7 @@ def cpu_baseline(n_shots: int) -> dict:
         done = sum(pool.map(_cpu_worker, chunks))
         dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "spectrograms/s", "cores": cores, "kind": "port",
-            "affinity_cores": affinity,
-            "cores_note": "16 = the per-GPU host CPU share of the GPU box (not the whole "
-                          "machine that sched_getaffinity reports there)",
+            "cores_source": cores_src,
             "sample": f"{done} shots x {L5} fp16 samples: scipy.signal.spectrogram (256 hann/"
                       f"hop 128, linear detrend) + log + min-max + drop row, numpy SVD "
                       f"denoiseSignal default, torch-CPU fp32 autoencoder forward; {cores} "
@@ -284,36 +333,108 @@ def svd_c3_stage(dev, B=4096, m=513, n=256, k=16, reps=5):
     return res
 
 
-def ae_train_c4_stage(dev, ops, batch=128, steps=20):
-    """BASELINE config 4's step on one GPU: Keras fit() of the 3-layer model on 128 x 128 x 1
-    inputs, mixed_bfloat16 (bf16 MFMA, fp32 master weights + Adam), batch 128: forward, BCE
-    from logits, backward (dgrad + deterministic wgrad), Adam. 1.494 GFLOP per sample
-    (SURVEY §8 d C4: forward x 3) at the dense bf16 MFMA peak."""
-    import torch
+def ae_ops():
     from specenh import ae
-    eng = ae.AutoencoderEngine(ops, (HW5, HW5, 1), compute_dtype="mixed_bfloat16", device=dev)
+    return [ae.PoolOp() if lay[0] == "pool" else
+            ae.ConvOp(lay[0], lay[1], lay[2], lay[3], lay[4], stride=2 if lay[0] == "convT" else 1)
+            for lay in ae_layers()]
+
+
+def make_c5_engine(dev, dtype="float16"):
+    """The C5 model (manual_scan_3layers.py:186-199) with the trained weights."""
+    from specenh import ae
+    eng = ae.AutoencoderEngine(ae_ops(), (HW5, HW5, 1), compute_dtype=dtype, device=dev)
     eng.set_keras_weights(ae_weights())
+    return eng
+
+
+def c4_engine_and_batch(dev, batch=128, n=None, seed=4):
+    """A mixed_bfloat16 engine of the reference model and one C4 batch (device pairs,
+    specenh.synthetic.c4_pairs_torch), plus the whole device set when ``n`` is given."""
+    import torch
+    from specenh.synthetic import c4_pairs_torch
+    eng = make_c5_engine(dev, "mixed_bfloat16")
+    X, Y = c4_pairs_torch(n or batch, seed=seed, device=dev, dtype=torch.bfloat16)
+    if n is None:
+        return eng, X, Y
+    return eng, X, Y, X[:batch], Y[:batch]
+
+
+def ae_train_c4_stage(dev, dist=None, batch=128, steps=20, n_local=4096, seed=4):
+    """BASELINE config 4: Keras fit() steps of the 3-layer model on the C4 workload (SURVEY
+    §8 d: C1 spectrograms of seeded noisy chirps -> the noise-free chirps' spectrograms,
+    generated on the device), mixed_bfloat16 (bf16 MFMA, fp32 master weights + Adam):
+    forward, BCE from logits, backward (dgrad + deterministic wgrad), Adam. Each step draws
+    the next ``batch`` samples of a per-epoch permutation of this rank's ``n_local`` pairs.
+
+    Under torch.distributed (``dist``: every rank runs this stage) the flat fp32 gradient is
+    SUM-all-reduced over RCCL in two buckets before Adam (specenh.ae.dp_backward, SURVEY §8
+    E2), in two modes: per-GPU batch ``batch`` (global batch = batch x world: the scaling
+    configuration) and global batch ``batch`` (batch / world per rank: Keras parity).
+    Reported: global samples/s (all ranks' samples / max-over-ranks time), ms per step, and
+    the standalone all-reduce time of the gradient buffer with its share of the step.
+    1.494 GFLOP per sample (SURVEY §8 d C4: forward x 3) at the dense bf16 MFMA peak."""
+    import torch
+    world = dist.get_world_size() if dist else 1
+    rank = dist.get_rank() if dist else 0
+    group = dist.group.WORLD if dist else None
+    eng, X, Y, _, _ = c4_engine_and_batch(dev, batch, n=n_local, seed=seed + 7919 * rank)
+    if dist:
+        eng.sync_state(group)
     g = torch.Generator(device=dev)
-    g.manual_seed(4)
-    x = eng.to_compute(torch.rand((batch, HW5, HW5, 1), generator=g, device=dev))
-    y = eng.to_compute(torch.rand((batch, HW5, HW5, 1), generator=g, device=dev))
-    for _ in range(3):
-        eng.train_step(x, y)
-    st = torch.cuda.current_stream(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for _ in range(steps):
-        eng.train_step(x, y)
-    e1.record(st)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / steps
-    fl = 3.0 * ae_flops_per_sample() * batch
-    ach = fl / (ms * 1e-3) / 1e12
-    return {"workload": f"fit step, batch {batch}, 128x128x1, mixed_bfloat16, Adam",
-            "ms_per_step": ms, "samples_per_s": batch / (ms * 1e-3),
-            "roofline": {"bound": "mfma", "achieved": ach, "peak": MFMA_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": ach / MFMA_PEAK_TFLOPS,
-                         "flops_per_step": fl}}
+    g.manual_seed(seed)  # the same permutation sequence on every rank (own data)
+
+    def run(per_rank, nsteps):
+        perm = torch.randperm(n_local, generator=g, device=dev)
+        pos = 0
+        for _ in range(nsteps):
+            if pos + per_rank > n_local:
+                perm = torch.randperm(n_local, generator=g, device=dev)
+                pos = 0
+            idx = perm[pos:pos + per_rank]
+            pos += per_rank
+            eng.train_step(X.index_select(0, idx), Y.index_select(0, idx), process_group=group)
+
+    def timed(per_rank):
+        run(per_rank, 3)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(per_rank, steps)
+        torch.cuda.synchronize()
+        el = max_over_ranks(time.perf_counter() - t0, dist, dev)
+        return el / steps
+
+    fl = 3.0 * ae_flops_per_sample()
+    modes = {"per_gpu_batch": batch}
+    if dist and world > 1 and batch % world == 0:
+        modes["global_batch"] = batch // world
+    res = {"workload": f"fit steps on {n_local} device C4 pairs per rank (128x128x1 noisy "
+                       f"chirp spectrogram -> clean), mixed_bfloat16, Adam, world {world}",
+           "world": world}
+    for mode, per in modes.items():
+        sec = timed(per)
+        ach = fl * per * world / sec / 1e12
+        res[mode] = {"samples_per_rank": per, "global_batch": per * world,
+                     "ms_per_step": sec * 1e3, "samples_per_s": per * world / sec,
+                     "roofline": {"bound": "mfma", "achieved": ach,
+                                  "peak": MFMA_PEAK_TFLOPS * world, "unit": "TFLOP/s",
+                                  "frac": ach / (MFMA_PEAK_TFLOPS * world),
+                                  "flops_per_step": fl * per * world}}
+    if dist:  # the gradient exchange alone (both buckets, the flat fp32 buffer)
+        for _ in range(3):
+            dist.all_reduce(eng.g)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            dist.all_reduce(eng.g)
+        torch.cuda.synchronize()
+        ar = max_over_ranks(time.perf_counter() - t0, dist, dev) / 20
+        res["allreduce"] = {"bytes": eng.g.numel() * 4, "ms": ar * 1e3,
+                            "share_of_step": ar * 1e3 / res["per_gpu_batch"]["ms_per_step"]}
+    del X, Y
+    return res
 
 
 def c5_host_stream_stage(dev, make_engine, shots=32768, chunk=2048, slots=3):
@@ -449,13 +570,7 @@ def main():
     x16 = plasma_chirps_torch(B, L5, seed=mine["seed"], device=dev).to(torch.float16)
     S = torch.empty((B, HW5, HW5), dtype=torch.float32, device=dev)
     A = torch.empty((B, HW5, HW5, 1), dtype=torch.float16, device=dev)
-    ops = []
-    for lay in ae_layers():
-        ops.append(ae.PoolOp() if lay[0] == "pool" else
-                   ae.ConvOp(lay[0], lay[1], lay[2], lay[3], lay[4],
-                             stride=2 if lay[0] == "convT" else 1))
-    eng = ae.AutoencoderEngine(ops, (HW5, HW5, 1), compute_dtype="float16", device=dev)
-    eng.set_keras_weights(ae_weights())
+    eng = make_c5_engine(dev)
     torch.cuda.synchronize()
 
     NS = max(1, args.streams) if B % max(1, args.streams) == 0 else 1
@@ -470,8 +585,8 @@ def main():
     def stage_svd():  # fp32 SVD, reconstruction stored as the autoencoder's fp16 input
         svd.denoise_batch(S[:Hs], out=A[:Hs].view(Hs, HW5, HW5))
 
-    def stage_ae(timing=None):
-        return eng.forward(A[:Hs], timing=timing)
+    def stage_ae(timing=None, kernels=None):
+        return eng.forward(A[:Hs], timing=timing, kernels=kernels)
 
     # The timed step: the batch splits into NS slices, each running the whole chain on its
     # own HIP stream with its own autoencoder buffers. Slice h > 0 starts once slice h-1's
@@ -480,11 +595,7 @@ def main():
     # step's tail). Every shot still goes through every stage inside the step.
     if NS > 1:
         sstreams = [torch.cuda.Stream(dev) for _ in range(NS)]
-        sengs = [eng]
-        for _ in range(NS - 1):
-            e2 = ae.AutoencoderEngine(ops, (HW5, HW5, 1), compute_dtype="float16", device=dev)
-            e2.set_keras_weights(ae_weights())
-            sengs.append(e2)
+        sengs = [eng] + [make_c5_engine(dev) for _ in range(NS - 1)]
         sdone = [torch.cuda.Event() for _ in range(NS)]
 
     def step():
@@ -529,16 +640,16 @@ def main():
     for _ in range(reps):
         stage_stft()
         stage_svd()
-        timing = []
-        stage_ae(timing)
+        timing, kernels = [], []
+        stage_ae(timing, kernels)
         torch.cuda.synchronize()
         conv_ms.append([a.elapsed_time(b) for a, b in timing])
     conv_ms = np.array(conv_ms)                       # [reps, launches]
     layer_ms = np.median(conv_ms, axis=0)
-    pmc = load_pmc_traffic()
+    pmc = load_pmc()
     layers = []
     names = LAYER_NAMES_TAIL if eng.tail else LAYER_NAMES
-    for name, c, ms in zip(names, ae_layer_costs(tail=eng.tail), layer_ms):
+    for name, c, ms, sym in zip(names, ae_layer_costs(tail=eng.tail), layer_ms, kernels):
         # compute floor: MFMA FLOPs at the dense fp16 MFMA peak + VALU FLOPs at the dot2 peak
         t_c = c["mfma_flops"] * Hs / (MFMA_PEAK_TFLOPS * 1e12) + \
             (c["flops"] - c["mfma_flops"]) * Hs / (VALU_DOT2_PEAK_TFLOPS * 1e12)
@@ -555,16 +666,23 @@ def main():
             ach = c["flops"] * Hs / (ms * 1e-3) / 1e12
             rl = {"bound": "mfma" if c["mfma_flops"] else "valu", "achieved": ach,
                   "peak": peak_c, "unit": "TFLOP/s", "frac": ach / peak_c}
-        tr = pmc.get(name)
-        rl.update({"layer": name, "kernel_ms": float(ms), "alg_bytes_per_launch": nb,
-                   "flops_per_launch": c["flops"] * Hs,
+        tr, why = pmc_traffic(pmc, "c5", name, sym, Hs)
+        rl.update({"layer": name, "kernel": sym, "kernel_ms": float(ms),
+                   "alg_bytes_per_launch": nb, "flops_per_launch": c["flops"] * Hs,
                    "mfma_flops_per_launch": c["mfma_flops"] * Hs,
-                   # PMC passes ran 4096-shot launches; these kernels' traffic is linear
-                   # in the shot count (per-image tiles), scaled to this launch
-                   "traffic": tr["hbm_bytes"] * Hs / tr.get("batch", 4096) if tr else None,
-                   "traffic_kernel": tr["kernel"] if tr else None})
+                   # PMC passes (tools/pmc_refresh.sh) ran the same kernel at the bench's
+                   # launch shape; traffic is per launch of Hs shots
+                   "traffic": tr, "traffic_ratio": tr / nb if tr else None})
+        if why:
+            rl["traffic_note"] = why
         layers.append(rl)
     dom = layers[int(np.argmax(layer_ms))]
+
+    # ---- BASELINE config 4 (training) on every rank: data-parallel over RCCL under
+    # torchrun, rank-local otherwise ----
+    c4 = None
+    if not args.no_stages:
+        c4 = ae_train_c4_stage(dev, dist if use_dist else None)
 
     # ---- per-stage breakdown of one step (events between stages) ----
     stages = None
@@ -590,7 +708,9 @@ def main():
         x2 = plasma_chirps_torch(B2, L2, seed=7, device=dev)
         o2 = torch.empty((B2, F2, T2), dtype=torch.float32, device=dev)
         for _ in range(2):
+            c0 = _lib.launch_count()
             pipeline_data.specgr_batch(x2, SPEC2, out=o2)
+            syms2 = _lib.kernel_names(c0, _lib.launch_count())
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
         for _ in range(5):
@@ -599,24 +719,26 @@ def main():
         e1.synchronize()
         k_ms = e0.elapsed_time(e1) / 5
         ach2 = ALG_BYTES_C2 * B2 / (k_ms * 1e-3) / 1e9
-        tr2 = pmc.get("stft_c2")
+        tr2, why2 = pmc_traffic(pmc, "c2", "stft_c2", syms2, B2)
         stages["stft_c2"] = {
             "workload": "4096 x 65536 fp32, nperseg 1024 hop 256 hamm, linear, density, "
                         "log + min-max + drop Nyquist -> 4096 x 512 x 253",
-            "spectrograms_per_s": B2 / (k_ms * 1e-3), "kernel": "stft_team_kernel<1024, 2>",
+            "spectrograms_per_s": B2 / (k_ms * 1e-3), "kernels": syms2,
             "kernel_ms": k_ms, "roofline": {"bound": "hbm", "achieved": ach2,
                                             "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                             "frac": ach2 / HBM_PEAK_GBPS,
                                             "alg_bytes_per_launch": ALG_BYTES_C2 * B2,
-                                            "traffic": tr2["hbm_bytes"] if tr2 else None}}
+                                            "traffic": tr2, "traffic_note": why2}}
         del o2
         # §8 A4 / f3: cross-power amplitude spectrogram of shot pairs at the C2 geometry
         from specenh import cross
         Bc = B2 // 2
         xa, xb_ = x2[:Bc], x2[Bc:]
         for _ in range(2):
+            c0 = _lib.launch_count()
             _, _, oc = cross.cross_spectrogram_batch(xa, xb_, 5e5, "hamm", 1024, 768, "linear",
                                                      "density", amplitude=True)
+            symsc = _lib.kernel_names(c0, _lib.launch_count())
         e0.record(st)
         for _ in range(5):
             _, _, oc = cross.cross_spectrogram_batch(xa, xb_, 5e5, "hamm", 1024, 768, "linear",
@@ -626,22 +748,18 @@ def main():
         c_ms = e0.elapsed_time(e1) / 5
         algc = (2 * 4 * L2 + 4 * (F2 + 1) * T2) * Bc
         achc = algc / (c_ms * 1e-3) / 1e9
+        trc, whyc = pmc_traffic(pmc, "csd", "csd_c2", symsc, Bc)
         stages["csd_c2"] = {
             "workload": f"{Bc} signal pairs x 65536 fp32, nperseg 1024 hop 256 hamm, linear, "
                         "density -> |Pxy| amplitude [pairs, 513, 253] (crosspowerspec.py:39)",
-            "pairs_per_s": Bc / (c_ms * 1e-3), "kernel": "csd_kernel", "kernel_ms": c_ms,
+            "pairs_per_s": Bc / (c_ms * 1e-3), "kernels": symsc, "kernel_ms": c_ms,
             "roofline": {"bound": "hbm", "achieved": achc, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achc / HBM_PEAK_GBPS, "alg_bytes_per_launch": algc,
-                         "traffic": None}}
+                         "traffic": trc, "traffic_note": whyc}}
         del x2, oc
         stages["svd_c3"] = svd_c3_stage(dev)
-        stages["ae_train_c4"] = ae_train_c4_stage(dev, ops)
-
-        def make_engine():
-            e = ae.AutoencoderEngine(ops, (HW5, HW5, 1), compute_dtype="float16", device=dev)
-            e.set_keras_weights(ae_weights())
-            return e
-        stages["c5_host_stream"] = c5_host_stream_stage(dev, make_engine)
+        stages["ae_train_c4"] = c4
+        stages["c5_host_stream"] = c5_host_stream_stage(dev, lambda: make_c5_engine(dev))
 
     # ---- accuracy vs the fp64 CPU chain on sample shots ----
     accuracy = None

@@ -45,6 +45,24 @@ extern "C" {
 const char* specenh_last_error(void);
 const char* specenh_version(void);
 
+/* Kernel-variant switches (no reference counterpart: A/B tests of kernels that compute
+ * the same result). name = "CONV_NO_S2", "PATCH_WSPLIT", ... (an optional "SPECENH_"
+ * prefix is accepted). Each is read from the environment variable SPECENH_<name> once per
+ * process; afterwards only these calls change it. Unknown names: SPECENH_EINVAL. */
+int specenh_set_variant(const char* name, int value);
+int specenh_get_variant(const char* name, int* value);
+
+/* Symbol (as the HIP runtime names it, mangled) of the last kernel this host thread
+ * launched through the library, "" before the first launch: measurements key their
+ * rocprofv3 PMC records by it (bench.py, tools/conv_one.py). */
+const char* specenh_last_kernel_name(void);
+/* Number of kernels this host thread has launched through the library: the i-th launch is
+ * the i-th specenh dispatch of the thread in a rocprofv3 trace (tools/pmc_workload.py). */
+long long specenh_launch_count(void);
+/* Symbol of this thread's launch number `index` (0-based, as counted by
+ * specenh_launch_count) while it is among the thread's last 256 launches, else "". */
+const char* specenh_kernel_name_at(long long index);
+
 /* Number of frames T = (length - nperseg) / (nperseg - noverlap) + 1 that
  * scipy.signal.spectrogram produces (no boundary padding), or a negative error. */
 long long specenh_stft_frames(long long length, int nperseg, int noverlap);

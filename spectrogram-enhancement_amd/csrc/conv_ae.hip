@@ -38,6 +38,7 @@
 #include <string>
 
 #include "specenh.h"
+#include "runtime.hpp"
 
 namespace specenh {
 int set_error(int code, const std::string& msg);  // stft_psd.hip
@@ -1937,7 +1938,7 @@ inline void launch_ordered_sums(const float* part, int nz, long long n, float* d
     j1 = sum_job(bpart, nzb, nb, db);
     blocks += sum_blocks(j1);
   }
-  hipLaunchKernelGGL(ordered_sum_kernel, dim3(blocks), dim3(256), 0, st, j0, j1, sum_blocks(j0));
+  SPECENH_LAUNCH(ordered_sum_kernel, dim3(blocks), dim3(256), 0, st, j0, j1, sum_blocks(j0));
 }
 
 // ------------------------------------------------------------------ elementwise
@@ -2097,12 +2098,6 @@ __global__ void cast_kernel(const TS* __restrict__ s, TD* __restrict__ d, long l
     d[i] = from_f<TD>(to_f(s[i]));
 }
 
-// Developer switch read once per process (A/B of kernel variants on the GPU box).
-inline bool getenv_flag(const char* name) {
-  const char* v = std::getenv(name);
-  return v && *v && *v != '0';
-}
-
 inline unsigned grid1d(long long n) {
   return (unsigned)std::max<long long>(1, std::min<long long>((n + 255) / 256, 65536));
 }
@@ -2209,7 +2204,7 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   const int nt = patch_nt(CO, tiles);
   // Conv2DTranspose stride 2: (tile, row phase) workgroups with whole-row stores
   bool pair = a.ph_shared && nph == 4 && !a.pool && !a.mask && !a.logits && !a.out_f32 &&
-              CO == 16 * nt && getenv_flag("SPECENH_CONVT_PAIR");
+              CO == 16 * nt && (variant(V_CONVT_PAIR) != 0);
   for (int i = 0; pair && i < nph; ++i) {
     const Geo& g = a.g[i];
     pair = g.oys == 2 && g.oxs == 2 && g.oy0 == i / 2 && g.ox0 == i % 2 && g.OHs == 2 * g.OH &&
@@ -2218,7 +2213,7 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   if (pair) {
     const dim3 grid2((tiles + 7) / 8 * 16, 1, 1);
     const size_t lds = patch_lds_bytes<T, CC>(a, nph, nt, true);
-#define SPECENH_PAIR(NT) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC, false, true>), grid2, dim3(256), lds, st, a)
+#define SPECENH_PAIR(NT) SPECENH_LAUNCH((conv_patch_kernel<T, NT, CC, false, true>), grid2, dim3(256), lds, st, a)
     if (nt == 1) SPECENH_PAIR(1);
     else if (nt == 2) SPECENH_PAIR(2);
     else if (nt == 3) SPECENH_PAIR(3);
@@ -2233,7 +2228,7 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   if constexpr (CC == 16) {
     const int Kf = a.g[0].Kf;
     if (nph == 1 && !a.ph_shared && a.g[0].C == 16 && Kf % 8 == 0 &&
-        !getenv_flag("SPECENH_PATCH_NO_WL")) {
+        !(variant(V_PATCH_NO_WL) != 0)) {
       const int rs_dw = (Kf / 2 - 8 + 63) / 64 * 64 + 8;  // >= Kf / 2 and = 8 mod 64
       a.wl_rs = 2 * rs_dw;
       const size_t pl = patch_lds_bytes<T, CC>(a, nph, nt, false);
@@ -2241,23 +2236,17 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
       const size_t lds = pl + (size_t)16 * nt * a.wl_rs * sizeof(T);
       const Geo& g = a.g[0];
       const bool k5 = g.KH == 5 && g.KW == 5 && g.ky0 == 0 && g.kx0 == 0 && g.kstep == 1 &&
-                      g.KWf == 5 && Kf == 400 && !getenv_flag("SPECENH_PATCH_NO_K5");
+                      g.KWf == 5 && Kf == 400 && !(variant(V_PATCH_NO_K5) != 0);
       // LDS weights only with the persistent K5 kernel: restaged per tile (any other
       // 16-channel geometry) they measured slower than the L2 weight ring
       if (k5 && lds <= 48 * 1024) {
         const dim3 grid(tiles, (unsigned)((CO + 16 * nt - 1) / (16 * nt)), 1);
-        static int cus = 0;  // persistent K5 grid: 4 workgroups per CU (LDS and registers)
-        if (cus == 0) {
-          int dev = 0;
-          if (hipGetDevice(&dev) != hipSuccess ||
-              hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
-        }
-        const dim3 gridk(std::min<unsigned>(tiles, 4u * (unsigned)cus), grid.y, 1);
+        // persistent K5 grid: 4 workgroups per CU (LDS and registers)
+        const dim3 gridk(std::min<unsigned>(tiles, 4u * (unsigned)device_cus()), grid.y, 1);
 #define SPECENH_PATCHL(NT, P)                                                                       \
-  if (k5) hipLaunchKernelGGL((conv_patch_kernel<T, NT, 16, P, false, false, false, true, true>), gridk, \
+  if (k5) SPECENH_LAUNCH((conv_patch_kernel<T, NT, 16, P, false, false, false, true, true>), gridk, \
                              dim3(256), lds, st, a);                                                 \
-  else hipLaunchKernelGGL((conv_patch_kernel<T, NT, 16, P, false, false, false, true>), grid, dim3(256), lds, st, a)
+  else SPECENH_LAUNCH((conv_patch_kernel<T, NT, 16, P, false, false, false, true>), grid, dim3(256), lds, st, a)
         if (a.pool) {
           if (nt == 1) SPECENH_PATCHL(1, true);
           else if (nt == 2) SPECENH_PATCHL(2, true);
@@ -2283,8 +2272,7 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   // SPECENH_PATCH_WSPLIT=1 forces it, =0 turns it off. The accumulation order per output
   // is unchanged: bitwise the same results.
   const int ntw = nt >= 4 && CC == 32 ? 2 : 1;  // (2 with 64-channel chunks spills)
-  const char* wse = std::getenv("SPECENH_PATCH_WSPLIT");
-  const int wsm = wse ? std::atoi(wse) : -1;
+  const int wsm = variant(V_PATCH_WSPLIT);
   // not with 16-channel chunks: conv2+pool (C 16 -> 32) runs 0.48 ms with the split vs
   // 0.38 without per 2048 shots (tools/layer_ab.py); 32/64-channel chunks gain 20-25 %
   const bool ws_shape = CC >= 32 && nt >= 2 && CO % (32 * ntw) == 0;
@@ -2293,7 +2281,7 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   if (ws_shape && (wsm == 1 || (wsm < 0 && ws_auto))) {
     const dim3 gridw(tiles, (unsigned)(CO / (32 * ntw)), a.ph_shared ? 1 : nph);
     const size_t ldsw = patch_lds_bytes<T, CC>(a, nph, ntw, false);
-#define SPECENH_PATCHW(NT, P) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC, P, false, false, true>), gridw, dim3(256), ldsw, st, a)
+#define SPECENH_PATCHW(NT, P) SPECENH_LAUNCH((conv_patch_kernel<T, NT, CC, P, false, false, true>), gridw, dim3(256), ldsw, st, a)
     if (a.pool) {
       if (ntw == 1) SPECENH_PATCHW(1, true);
       else SPECENH_PATCHW(2, true);
@@ -2306,7 +2294,7 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   }
   const dim3 grid(tiles, (unsigned)((CO + 16 * nt - 1) / (16 * nt)), a.ph_shared ? 1 : nph);
   const size_t lds = patch_lds_bytes<T, CC>(a, nph, nt, false);
-#define SPECENH_PATCH(NT, P) hipLaunchKernelGGL((conv_patch_kernel<T, NT, CC, P>), grid, dim3(256), lds, st, a)
+#define SPECENH_PATCH(NT, P) SPECENH_LAUNCH((conv_patch_kernel<T, NT, CC, P>), grid, dim3(256), lds, st, a)
   if (a.pool) {
     if (nt == 1) SPECENH_PATCH(1, true);
     else if (nt == 2) SPECENH_PATCH(2, true);
@@ -2331,7 +2319,7 @@ int launch_patch_s2(const ConvArgs& a, hipStream_t st) {
   const int sph = (30 + g.KH + 1) / 2, spw = (30 + g.KW + 1) / 2;
   const size_t lds = ((size_t)4 * sph * spw * Patch<16>::PST * sizeof(T) + 15) / 16 * 16;
   const dim3 grid(tiles, (unsigned)((g.CO + 16 * nt - 1) / (16 * nt)), 1);
-#define SPECENH_S2(NT) hipLaunchKernelGGL((conv_patch_kernel<T, NT, 16, false, false, true>), grid, dim3(256), lds, st, a)
+#define SPECENH_S2(NT) SPECENH_LAUNCH((conv_patch_kernel<T, NT, 16, false, false, true>), grid, dim3(256), lds, st, a)
   if (nt == 1) SPECENH_S2(1);
   else if (nt == 2) SPECENH_S2(2);
   else if (nt == 3) SPECENH_S2(3);
@@ -2344,7 +2332,7 @@ int launch_patch_s2(const ConvArgs& a, hipStream_t st) {
 // stride-2 16-channel patch kernel)
 int patch_cc(const ConvArgs& a, int nph) {
   if (nph == 1 && a.g[0].stride == 2 && a.g[0].C % 16 == 0 && a.g[0].KH <= 5 && a.g[0].KW <= 5 &&
-      !a.pool && !getenv_flag("SPECENH_CONV_NO_S2"))
+      !a.pool && !(variant(V_CONV_NO_S2) != 0))
     return -2;
   if (nph != 1 && nph != 4) return 0;
   for (int i = 0; i < nph; ++i) {
@@ -2362,7 +2350,7 @@ int patch_cc(const ConvArgs& a, int nph) {
 template <typename T>
 int launch_fwd(const ConvArgs& a, int nph, hipStream_t st) {
   if constexpr (!__is_same(T, float)) {
-    if (!getenv_flag("SPECENH_CONV_NO_PATCH")) {
+    if (!(variant(V_CONV_NO_PATCH) != 0)) {
       switch (patch_cc(a, nph)) {
         case -2: return launch_patch_s2<T>(a, st);
         case 64: return launch_patch<T, 64>(a, nph, st);
@@ -2382,7 +2370,7 @@ int launch_fwd(const ConvArgs& a, int nph, hipStream_t st) {
   const unsigned gx = (unsigned)((maxM + 64 * mt - 1) / (64 * mt));
   const unsigned gy = (unsigned)((CO + 16 * nt - 1) / (16 * nt));
   const dim3 grid(gx, gy, nph);
-#define SPECENH_FWD(MT, NT) hipLaunchKernelGGL((conv_fwd_kernel<T, MT, NT>), grid, dim3(256), 0, st, a)
+#define SPECENH_FWD(MT, NT) SPECENH_LAUNCH((conv_fwd_kernel<T, MT, NT>), grid, dim3(256), 0, st, a)
   if (nt == 1) SPECENH_FWD(4, 1);
   else if (nt == 2) SPECENH_FWD(4, 2);
   else if (nt == 3) SPECENH_FWD(2, 3);
@@ -2416,7 +2404,7 @@ WgradPlan wgrad_plan(int Kf, int CO) {
 template <typename T>
 bool wgrad_tr_applies(const WgradArgs& a, int nph) {
   if constexpr (__is_same(T, float)) return false;
-  if (getenv_flag("SPECENH_WGRAD_GENERIC")) return false;
+  if ((variant(V_WGRAD_GENERIC) != 0)) return false;
   for (int i = 0; i < nph; ++i) {
     const Geo& g = a.g[i];
     if ((g.C % 16 != 0 && g.C != 1) || g.stride != 1 || g.KH * g.KW > 28 || g.KH > 5 || g.KW > 5)
@@ -2450,14 +2438,14 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
   a.Z = (int)std::max(1LL, std::min<long long>(z, wgrad_tr_zmax(g0.CO, g0.Kf)));
   // one output channel over 16 input channels: jy-shifted input x jx-shifted dOut
   if (nph == 1 && g0.CO == 1 && g0.C == 16 && g0.KH <= 5 && g0.KW <= 5 &&
-      !getenv_flag("SPECENH_WGRAD_NO_CO1")) {
+      !(variant(V_WGRAD_NO_CO1) != 0)) {
     a.Z = (int)std::max(1LL, std::min<long long>({tiles / 2, (long long)wgrad_tr_zmax(1, g0.Kf), 4096LL}));
-    hipLaunchKernelGGL(wgrad_co1_kernel<T>, dim3((unsigned)a.Z), dim3(64), 0, st, a);
+    SPECENH_LAUNCH(wgrad_co1_kernel<T>, dim3((unsigned)a.Z), dim3(64), 0, st, a);
     launch_ordered_sums(a.part, a.Z, g0.Kf, dw, a.bpart, a.Z, 1, db, st);
     return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
   }
   // Conv2DTranspose stride 2: all four phases per workgroup over one union patch
-  if (!c1 && nph == 4 && g0.CO % 16 == 0 && !getenv_flag("SPECENH_WGRAD_PERPHASE")) {
+  if (!c1 && nph == 4 && g0.CO % 16 == 0 && !(variant(V_WGRAD_PERPHASE) != 0)) {
     bool ok = true;
     int upt = -1 << 20, upl = -1 << 20, lo_y = 1 << 20, hi_y = -(1 << 20), lo_x = 1 << 20,
         hi_x = -(1 << 20), U = 0;
@@ -2482,7 +2470,7 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
       long long zp = 4096 / std::max(1LL, (long long)nchunk * a.ncog);
       zp = std::min<long long>(zp, std::max(1LL, tiles / 4));
       a.Z = (int)std::max(1LL, std::min<long long>(zp, wgrad_tr_zmax(g0.CO, g0.Kf)));
-      hipLaunchKernelGGL(wgrad_trp_kernel<T>, dim3((unsigned)a.Z, (unsigned)(nchunk * a.ncog)), dim3(256), 0,
+      SPECENH_LAUNCH(wgrad_trp_kernel<T>, dim3((unsigned)a.Z, (unsigned)(nchunk * a.ncog)), dim3(256), 0,
                          st, a);
       launch_ordered_sums(a.part, a.Z, (long long)g0.CO * g0.Kf, dw, a.bpart, nph * a.Z, g0.CO, db, st);
       return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
@@ -2490,11 +2478,11 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
   }
   const dim3 grid((unsigned)a.Z, (unsigned)(nchunk * a.ncog), (unsigned)nph);
   if (c1) {
-    if (ntw == 1) hipLaunchKernelGGL((wgrad_tr_kernel<T, 1, true>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((wgrad_tr_kernel<T, 2, true>), grid, dim3(256), 0, st, a);
+    if (ntw == 1) SPECENH_LAUNCH((wgrad_tr_kernel<T, 1, true>), grid, dim3(256), 0, st, a);
+    else SPECENH_LAUNCH((wgrad_tr_kernel<T, 2, true>), grid, dim3(256), 0, st, a);
   } else {
-    if (ntw == 1) hipLaunchKernelGGL((wgrad_tr_kernel<T, 1, false>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((wgrad_tr_kernel<T, 2, false>), grid, dim3(256), 0, st, a);
+    if (ntw == 1) SPECENH_LAUNCH((wgrad_tr_kernel<T, 1, false>), grid, dim3(256), 0, st, a);
+    else SPECENH_LAUNCH((wgrad_tr_kernel<T, 2, false>), grid, dim3(256), 0, st, a);
   }
   launch_ordered_sums(a.part, a.Z, (long long)g0.CO * g0.Kf, dw, a.bpart, nph * a.Z, g0.CO, db, st);
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
@@ -2517,7 +2505,7 @@ int launch_wgrad(WgradArgs& a, int nph, float* dw, float* db, hipStream_t st) {
   for (int i = 0; i < nph; ++i)
     gx = std::max(gx, (unsigned)((a.g[i].KH * a.g[i].KW * a.g[i].C + 63) / 64));
   const dim3 grid(gx, p.gy, (unsigned)(nph * p.Z));
-#define SPECENH_WG(NT) hipLaunchKernelGGL((conv_wgrad_kernel<T, NT>), grid, dim3(256), 0, st, a)
+#define SPECENH_WG(NT) SPECENH_LAUNCH((conv_wgrad_kernel<T, NT>), grid, dim3(256), 0, st, a)
   if (p.nt == 1) SPECENH_WG(1);
   else if (p.nt == 2) SPECENH_WG(2);
   else if (p.nt == 3) SPECENH_WG(3);
@@ -2555,13 +2543,13 @@ int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, cons
     return set_error(SPECENH_EUNSUPPORTED, "fused max-pool: plain conv with even output only");
   hipStream_t st = (hipStream_t)stream;
   // 1 input channel: window rows as MFMA K runs (conv_c1_mfma.hip)
-  if (stride == 1 && in_dil == 1 && C == 1 && !getenv_flag("SPECENH_CONV_NO_C1MFMA")) {
+  if (stride == 1 && in_dil == 1 && C == 1 && !(variant(V_CONV_NO_C1MFMA) != 0)) {
     const int r = launch_conv_c1_mfma(dtype, in, N, IH, IW, C, w_gemm, KH, KW, CO, bias, pad_t,
                                       pad_l, OH, OW, act, out, out_f32, logits, pool2, argmax, mask, st);
     if (r != 0) return r < 0 ? r : SPECENH_OK;
   }
   // 1 input or 1 output channel: direct VALU convolution (conv_narrow.hip)
-  if (stride == 1 && in_dil == 1 && !getenv_flag("SPECENH_CONV_NO_NARROW")) {
+  if (stride == 1 && in_dil == 1 && !(variant(V_CONV_NO_NARROW) != 0)) {
     const int r = launch_conv_narrow(dtype, in, N, IH, IW, C, w_gemm, KH, KW, CO, bias, pad_t,
                                      pad_l, OH, OW, act, out, out_f32, logits, pool2, argmax, mask, st);
     if (r != 0) return r < 0 ? r : SPECENH_OK;
@@ -2618,13 +2606,13 @@ int specenh_maxpool2_fwd(int dtype, const void* in, int N, int H, int W, int C, 
   const long long n = (long long)N * (H / 2) * (W / 2) * C;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == 0)
-    hipLaunchKernelGGL(maxpool2_fwd_kernel<float>, dim3(grid1d(n)), dim3(256), 0, st,
+    SPECENH_LAUNCH(maxpool2_fwd_kernel<float>, dim3(grid1d(n)), dim3(256), 0, st,
                        (const float*)in, N, H, W, C, (float*)out, argmax);
   else if (dtype == 1)
-    hipLaunchKernelGGL(maxpool2_fwd_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st,
+    SPECENH_LAUNCH(maxpool2_fwd_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st,
                        (const __bf16*)in, N, H, W, C, (__bf16*)out, argmax);
   else if (dtype == 2)
-    hipLaunchKernelGGL(maxpool2_fwd_kernel<_Float16>, dim3(grid1d(n)), dim3(256), 0, st,
+    SPECENH_LAUNCH(maxpool2_fwd_kernel<_Float16>, dim3(grid1d(n)), dim3(256), 0, st,
                        (const _Float16*)in, N, H, W, C, (_Float16*)out, argmax);
   else
     return set_error(SPECENH_EINVAL, "dtype");
@@ -2640,23 +2628,23 @@ int specenh_maxpool2_bwd(int dtype, const void* dout, const unsigned char* argma
   const long long n = (long long)N * (H / 2) * (W / 2) * C;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == 0)
-    hipLaunchKernelGGL(maxpool2_bwd_kernel<float>, dim3(grid1d(n)), dim3(256), 0, st,
+    SPECENH_LAUNCH(maxpool2_bwd_kernel<float>, dim3(grid1d(n)), dim3(256), 0, st,
                        (const float*)dout, argmax, (const float*)pooled, N, H, W, C, (float*)din);
   else if ((dtype == 1 || dtype == 2) && (C & 7) == 0 && 4 * n < (1LL << 31)) {
     const unsigned blocks = (unsigned)((n / 8 + 255) / 256);
     if (dtype == 1)
-      hipLaunchKernelGGL(maxpool2_bwd_vec_kernel<__bf16>, dim3(blocks), dim3(256), 0, st,
+      SPECENH_LAUNCH(maxpool2_bwd_vec_kernel<__bf16>, dim3(blocks), dim3(256), 0, st,
                          (const __bf16*)dout, argmax, (const __bf16*)pooled, N, H, W, C, (__bf16*)din);
     else
-      hipLaunchKernelGGL(maxpool2_bwd_vec_kernel<_Float16>, dim3(blocks), dim3(256), 0, st,
+      SPECENH_LAUNCH(maxpool2_bwd_vec_kernel<_Float16>, dim3(blocks), dim3(256), 0, st,
                          (const _Float16*)dout, argmax, (const _Float16*)pooled, N, H, W, C,
                          (_Float16*)din);
   } else if (dtype == 1)
-    hipLaunchKernelGGL(maxpool2_bwd_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st,
+    SPECENH_LAUNCH(maxpool2_bwd_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st,
                        (const __bf16*)dout, argmax, (const __bf16*)pooled, N, H, W, C,
                        (__bf16*)din);
   else if (dtype == 2)
-    hipLaunchKernelGGL(maxpool2_bwd_kernel<_Float16>, dim3(grid1d(n)), dim3(256), 0, st,
+    SPECENH_LAUNCH(maxpool2_bwd_kernel<_Float16>, dim3(grid1d(n)), dim3(256), 0, st,
                        (const _Float16*)dout, argmax, (const _Float16*)pooled, N, H, W, C,
                        (_Float16*)din);
   else
@@ -2670,7 +2658,7 @@ int specenh_bce_logits(const float* z, const void* target, int target_dtype, lon
   hipStream_t st = (hipStream_t)stream;
   const unsigned gx = std::min<unsigned>(grid1d(n), 1024);
 #define SPECENH_BCE(TT, TG)                                                                   \
-  hipLaunchKernelGGL((bce_logits_kernel<TT, TG>), dim3(gx), dim3(256), 0, st, z,             \
+  SPECENH_LAUNCH((bce_logits_kernel<TT, TG>), dim3(gx), dim3(256), 0, st, z,             \
                      (const TT*)target, n, (TG*)grad, loss_sum)
   if (target_dtype == 0 && grad_dtype == 0) SPECENH_BCE(float, float);
   else if (target_dtype == 0 && grad_dtype == 1) SPECENH_BCE(float, __bf16);
@@ -2690,10 +2678,10 @@ int specenh_adam_step(float* w, const float* g, float* m, float* v, long long n,
   if (!w || !g || !m || !v || n <= 0) return set_error(SPECENH_EINVAL, "adam args");
   hipStream_t st = (hipStream_t)stream;
   if (lowp_dtype == SPECENH_DTYPE_F16)
-    hipLaunchKernelGGL(adam_kernel<_Float16>, dim3(grid1d(n)), dim3(256), 0, st, w, g, m, v, n,
+    SPECENH_LAUNCH(adam_kernel<_Float16>, dim3(grid1d(n)), dim3(256), 0, st, w, g, m, v, n,
                        lr_t, b1, b2, eps, grad_scale, (_Float16*)w_lowp);
   else if (lowp_dtype == SPECENH_DTYPE_BF16 || !w_lowp)
-    hipLaunchKernelGGL(adam_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st, w, g, m, v, n,
+    SPECENH_LAUNCH(adam_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st, w, g, m, v, n,
                        lr_t, b1, b2, eps, grad_scale, (__bf16*)w_lowp);
   else
     return set_error(SPECENH_EINVAL, "adam: low-precision copy must be bf16 or f16");
@@ -2706,13 +2694,13 @@ int specenh_weight_flip_transpose(int dtype, const void* bt, int k, int ci, int 
   if (!bt || !bd || n <= 0) return set_error(SPECENH_EINVAL, "flip args");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == 0)
-    hipLaunchKernelGGL(flip_transpose_kernel<float>, dim3(grid1d(n)), dim3(256), 0, st,
+    SPECENH_LAUNCH(flip_transpose_kernel<float>, dim3(grid1d(n)), dim3(256), 0, st,
                        (const float*)bt, k, ci, co, (float*)bd);
   else if (dtype == 1)
-    hipLaunchKernelGGL(flip_transpose_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st,
+    SPECENH_LAUNCH(flip_transpose_kernel<__bf16>, dim3(grid1d(n)), dim3(256), 0, st,
                        (const __bf16*)bt, k, ci, co, (__bf16*)bd);
   else if (dtype == 2)
-    hipLaunchKernelGGL(flip_transpose_kernel<_Float16>, dim3(grid1d(n)), dim3(256), 0, st,
+    SPECENH_LAUNCH(flip_transpose_kernel<_Float16>, dim3(grid1d(n)), dim3(256), 0, st,
                        (const _Float16*)bt, k, ci, co, (_Float16*)bd);
   else
     return set_error(SPECENH_EINVAL, "dtype");
@@ -2726,7 +2714,7 @@ int specenh_cast(int src_dtype, const void* src, int dst_dtype, void* dst, long 
   hipStream_t st = (hipStream_t)stream;
   const dim3 g(grid1d(n)), b(256);
 #define SPECENH_CAST(TS, TD) \
-  hipLaunchKernelGGL((cast_kernel<TS, TD>), g, b, 0, st, (const TS*)src, (TD*)dst, n)
+  SPECENH_LAUNCH((cast_kernel<TS, TD>), g, b, 0, st, (const TS*)src, (TD*)dst, n)
   const int key = src_dtype * 3 + dst_dtype;
   switch (src_dtype < 0 || src_dtype > 2 || dst_dtype < 0 || dst_dtype > 2 ? -1 : key) {
     case 0 * 3 + 1: SPECENH_CAST(float, __bf16); break;

@@ -26,6 +26,7 @@
 #include <string>
 
 #include "specenh.h"
+#include "runtime.hpp"
 
 namespace specenh {
 int set_error(int code, const std::string& msg);  // stft_psd.hip
@@ -284,13 +285,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 template <typename T>
 int launch(const C1mArgs& a, bool pool, hipStream_t st) {
   const long long tiles = (long long)a.N * ((a.OH + TILE - 1) / TILE) * ((a.OW + TILE - 1) / TILE);
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-  }
+  const int cus = device_cus();
   // persistent workgroups, as many as are resident at once, each over a run of tiles
   const void* fn = pool ? (const void*)conv_c1_mfma_kernel<T, true> : (const void*)conv_c1_mfma_kernel<T, false>;
   static int per_cu[2] = {0, 0};
@@ -299,8 +294,8 @@ int launch(const C1mArgs& a, bool pool, hipStream_t st) {
     pc = 2;
   const unsigned cob = (unsigned)((a.CO + 15) / 16);
   const dim3 grid((unsigned)std::max<long long>(1, std::min<long long>(tiles, (long long)pc * cus / cob)), cob);
-  if (pool) hipLaunchKernelGGL((conv_c1_mfma_kernel<T, true>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((conv_c1_mfma_kernel<T, false>), grid, dim3(256), 0, st, a);
+  if (pool) SPECENH_LAUNCH((conv_c1_mfma_kernel<T, true>), grid, dim3(256), 0, st, a);
+  else SPECENH_LAUNCH((conv_c1_mfma_kernel<T, false>), grid, dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? 1 : set_error(SPECENH_EHIP, "conv_c1_mfma launch");
 }
 

@@ -25,6 +25,7 @@
 #include <string>
 
 #include "specenh.h"
+#include "runtime.hpp"
 
 namespace specenh {
 int set_error(int code, const std::string& msg);  // stft_psd.hip
@@ -469,7 +470,7 @@ int launch_co1(const NarrowArgs& a, hipStream_t st) {
   NarrowArgs b = a;
   b.band_steps = std::max<int>(min_steps, (int)((steps + bands - 1) / bands));
   bands = (steps + b.band_steps - 1) / b.band_steps;
-  hipLaunchKernelGGL((conv_co1_kernel<T, C, K>), dim3((unsigned)strips, (unsigned)bands), dim3(256),
+  SPECENH_LAUNCH((conv_co1_kernel<T, C, K>), dim3((unsigned)strips, (unsigned)bands), dim3(256),
                      Rg::LDS, st, b);
   return hipGetLastError() == hipSuccess ? 1 : set_error(SPECENH_EHIP, "conv_co1 launch");
 }
@@ -479,8 +480,8 @@ int launch_c1(const NarrowArgs& a, bool pool, hipStream_t st) {
   const long long tiles = (long long)a.N * ((a.OH + C1_TILE - 1) / C1_TILE) *
                           ((a.OW + C1_TILE - 1) / C1_TILE);
   const dim3 grid((unsigned)tiles, (unsigned)((a.CO + 15) / 16));
-  if (pool) hipLaunchKernelGGL((conv_c1_kernel<T, K, true>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((conv_c1_kernel<T, K, false>), grid, dim3(256), 0, st, a);
+  if (pool) SPECENH_LAUNCH((conv_c1_kernel<T, K, true>), grid, dim3(256), 0, st, a);
+  else SPECENH_LAUNCH((conv_c1_kernel<T, K, false>), grid, dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? 1 : set_error(SPECENH_EHIP, "conv_c1 launch");
 }
 

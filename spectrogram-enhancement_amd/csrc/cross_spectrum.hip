@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "specenh.h"
+#include "runtime.hpp"
 
 namespace specenh {
 int set_error(int code, const std::string& msg);  // stft_psd.hip
@@ -237,7 +238,7 @@ int specenh_csd(const specenh_csd_plan* plan, const float* x, const float* y, lo
   a.T = (int)T; a.N = plan->N; a.step = plan->step; a.detrend = plan->detrend;
   a.log2n = plan->log2n; a.mode = mode; a.win = plan->d_window; a.tw = plan->d_tw;
   a.scale = plan->scale; a.out = out;
-  hipLaunchKernelGGL(specenh::csd_kernel, dim3((unsigned)T, (unsigned)batch), dim3(specenh::CT),
+  SPECENH_LAUNCH(specenh::csd_kernel, dim3((unsigned)T, (unsigned)batch), dim3(specenh::CT),
                      2 * plan->N * sizeof(float2), (hipStream_t)stream, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, std::string("csd launch: ") + hipGetErrorString(e));

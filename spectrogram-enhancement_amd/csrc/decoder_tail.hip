@@ -24,10 +24,10 @@
 //  2. Epilogue: + bias, ReLU, round to T (exactly what the unfused layer stores), into a
 //     36 x 36 x 16 LDS image of the map (48-byte pixels: conflict-free reads below) that
 //     aliases the dead input patch; pixels outside the image are the conv's zero padding.
-//  3. Conv2D 16 -> 1, 5 x 5, on the VALU (v_dot2_f32_{f16,bf16}, fp32 accumulation): a lane
-//     computes two vertically adjacent outputs and reuses each loaded pixel for both; the
-//     400 weights are wave-uniform (scalar loads into SGPRs). + bias, sigmoid, fp32 store (coalesced
-//     128-byte row segments).
+//  3. Conv2D 16 -> 1, 5 x 5, on MFMA: per output row y, D[x'][kx] = sum_{ky,ci}
+//     map[y + ky][x'][ci] w[ky][kx][ci] (A = map rows from LDS, B = the weights as fragments
+//     held in registers), then out[y][x] = sum_kx D[x + kx][kx] through a per-wave scratch;
+//     + bias, sigmoid, fp32 store (coalesced 128-byte row segments).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "specenh.h"
+#include "runtime.hpp"
 
 namespace specenh {
 int set_error(int code, const std::string& msg);  // stft_psd.hip
@@ -68,7 +69,6 @@ struct TailArgs {
   const float* bo;    // [1]
   float* out;         // [N][2H][2W]
   int N, H, W, tiles_y, tiles_x;
-  int dev;  // development: bit 0 skips the MFMA items, bit 1 the Conv2D(1), bit 2 staging
 };
 
 // tap row ky of neighbourhood offset dy for output row phase py (-1 <= dy <= 1; valid when
@@ -230,11 +230,11 @@ __device__ __forceinline__ void tail_body(const TailArgs& a, T* sx, T* sy, int w
   // compiler's wait for them sits inside the loop, and on CDNA4 vmcnt also counts the
   // previous tile's output stores, so every tile would wait for its predecessor's writes
   __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0)
-  const int b0 = half * MAXBLK, nb = (a.dev & 1) ? 0 : min(MAXBLK, NBLK - b0);
+  const int b0 = half * MAXBLK, nb = min(MAXBLK, NBLK - b0);
 
   uint4 pf[XPF];
   int tile = blockIdx.x;
-  if (tile < total && !(a.dev & 4)) {
+  if (tile < total) {
     load_patch<T>(a, tile, pf);
     store_patch<T>(sx, pf);
   }
@@ -266,7 +266,7 @@ __device__ __forceinline__ void tail_body(const TailArgs& a, T* sx, T* sy, int w
     }
     lds_barrier();  // the map is complete; every patch read is done
     // the next tile's patch: loads in flight during this tile's Conv2D(1)
-    const bool next = tile + G < total && !(a.dev & 4);
+    const bool next = tile + G < total;
     if (next) load_patch<T>(a, tile + G, pf);
 
     // ---- Conv2D(1, 5x5) + sigmoid on MFMA: per output row y,
@@ -274,7 +274,7 @@ __device__ __forceinline__ void tail_body(const TailArgs& a, T* sx, T* sy, int w
     //   out[y][x] = sum_kx D[x + kx][kx]
     // 3 MFMAs (kernel-row pairs) per 16 positions x', 3 position blocks per row; the
     // diagonal sums go through a per-wave scratch in the dead patch region ----
-    if (!(a.dev & 2)) {
+    {
       float* sp = reinterpret_cast<float*>(sx) + wave * (2 * KO * PXW);
       const int x = lane & 31, hh = lane >> 5;
       float* __restrict__ O = a.out + (long long)g.n * H2 * W2;
@@ -336,17 +336,7 @@ __global__ __launch_bounds__(512, 4) void convt_conv_out_kernel(TailArgs a) {
   }
 }
 
-int resident_grid(const void* fn) {  // 2 workgroups per CU (LDS and registers allow 2)
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-  }
-  (void)fn;
-  return 2 * cus;
-}
+int resident_grid() { return 2 * device_cus(); }  // 2 workgroups per CU (LDS and registers)
 
 }  // namespace
 }  // namespace specenh
@@ -379,17 +369,14 @@ extern "C" int specenh_convt_conv_out(int dtype, const void* x, int N, int H, in
   a.W = W;
   a.tiles_y = (2 * H + TO - 1) / TO;
   a.tiles_x = (2 * W + TO - 1) / TO;
-  if (const char* d = std::getenv("SPECENH_TAIL_DEV")) a.dev = std::atoi(d);
   const long long tiles = (long long)N * a.tiles_y * a.tiles_x;
   if (tiles >= (1ll << 31)) return set_error(SPECENH_EINVAL, "too many tiles");
   hipStream_t st = (hipStream_t)stream;
-  const void* fn = dtype == SPECENH_DTYPE_F16 ? (const void*)convt_conv_out_kernel<_Float16>
-                                              : (const void*)convt_conv_out_kernel<__bf16>;
-  const unsigned grid = (unsigned)std::min<long long>(tiles, resident_grid(fn));
+  const unsigned grid = (unsigned)std::min<long long>(tiles, resident_grid());
   if (dtype == SPECENH_DTYPE_F16)
-    hipLaunchKernelGGL(convt_conv_out_kernel<_Float16>, dim3(grid), dim3(512), 0, st, a);
+    SPECENH_LAUNCH(convt_conv_out_kernel<_Float16>, dim3(grid), dim3(512), 0, st, a);
   else
-    hipLaunchKernelGGL(convt_conv_out_kernel<__bf16>, dim3(grid), dim3(512), 0, st, a);
+    SPECENH_LAUNCH(convt_conv_out_kernel<__bf16>, dim3(grid), dim3(512), 0, st, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("convt_conv_out: ") +
                                                           hipGetErrorString(e));

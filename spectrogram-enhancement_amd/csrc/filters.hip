@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "specenh.h"
+#include "runtime.hpp"
 
 namespace specenh {
 int set_error(int code, const std::string& msg);  // stft_psd.hip
@@ -312,11 +313,11 @@ int run_filter(int op, const T* S, long long batch, int rows, int cols, long lon
   double* stats = ws;
   double* rm = ws + 2 * batch;
   if (op == SPECENH_FILTER_MEANSUB)
-    hipLaunchKernelGGL(rowmean_kernel<T>, dim3(grid_for(batch * rows * 64)), dim3(256), 0, st, S,
+    SPECENH_LAUNCH(rowmean_kernel<T>, dim3(grid_for(batch * rows * 64)), dim3(256), 0, st, S,
                        batch, rows, cols, stride, rm);
-  hipLaunchKernelGGL(stats_kernel<T>, dim3((unsigned)batch), dim3(256), 0, st, S, rows, cols,
+  SPECENH_LAUNCH(stats_kernel<T>, dim3((unsigned)batch), dim3(256), 0, st, S, rows, cols,
                      stride, op, rm, stats);
-  hipLaunchKernelGGL(apply_kernel<T>, dim3(grid_for(batch * rows * cols)), dim3(256), 0, st, S,
+  SPECENH_LAUNCH(apply_kernel<T>, dim3(grid_for(batch * rows * cols)), dim3(256), 0, st, S,
                      out, batch, rows, cols, stride, op, rm, stats);
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "filter launch");
 }
@@ -330,7 +331,7 @@ int run_quantfilt(const T* S, long long batch, int rows, int cols, long long str
     return set_error(SPECENH_EHIP, "quantfilt attribute");
   for (long long b0 = 0; b0 < batch; b0 += 65535) {
     const long long nb = std::min<long long>(65535, batch - b0);
-    hipLaunchKernelGGL(quantfilt_kernel<T>, dim3((cols + QF_COLS - 1) / QF_COLS, (unsigned)nb),
+    SPECENH_LAUNCH(quantfilt_kernel<T>, dim3((cols + QF_COLS - 1) / QF_COLS, (unsigned)nb),
                        dim3(256), lds, st, S + b0 * stride, out + b0 * stride, rows, cols, stride,
                        lo, hi, gamma);
   }
@@ -406,29 +407,29 @@ int run_u8_filter(bool gauss, const T* S, long long batch, int rows, int cols, l
   const long long n = batch * rows * cols;
   U8Work w = u8_work(ws, batch, n);
   const unsigned g = grid_for(n);
-  hipLaunchKernelGGL(stats_kernel<T>, dim3((unsigned)batch), dim3(256), 0, st, S, rows, cols,
+  SPECENH_LAUNCH(stats_kernel<T>, dim3((unsigned)batch), dim3(256), 0, st, S, rows, cols,
                      stride, (int)SPECENH_FILTER_RESCALE, (const double*)nullptr, w.stats);
-  hipLaunchKernelGGL(quant_u8_kernel<T>, dim3(g), dim3(256), 0, st, S, batch, rows, cols, stride,
+  SPECENH_LAUNCH(quant_u8_kernel<T>, dim3(g), dim3(256), 0, st, S, batch, rows, cols, stride,
                      w.stats, w.a);
   if (gauss) {
-    hipLaunchKernelGGL(gauss_rows_kernel, dim3(g), dim3(256), 0, st, w.a, batch, rows, cols, *tp,
+    SPECENH_LAUNCH(gauss_rows_kernel, dim3(g), dim3(256), 0, st, w.a, batch, rows, cols, *tp,
                        w.h);
-    hipLaunchKernelGGL(gauss_cols_kernel, dim3(g), dim3(256), 0, st, w.h, batch, rows, cols, *tp,
+    SPECENH_LAUNCH(gauss_cols_kernel, dim3(g), dim3(256), 0, st, w.h, batch, rows, cols, *tp,
                        w.b);
   } else {  // MORPH_CLOSE 4x4 (dilate, erode) then MORPH_OPEN 3x1 (erode, dilate)
-    hipLaunchKernelGGL(morph_u8_kernel<true>, dim3(g), dim3(256), 0, st, w.a, batch, rows, cols,
+    SPECENH_LAUNCH(morph_u8_kernel<true>, dim3(g), dim3(256), 0, st, w.a, batch, rows, cols,
                        4, 4, w.b);
-    hipLaunchKernelGGL(morph_u8_kernel<false>, dim3(g), dim3(256), 0, st, w.b, batch, rows, cols,
+    SPECENH_LAUNCH(morph_u8_kernel<false>, dim3(g), dim3(256), 0, st, w.b, batch, rows, cols,
                        4, 4, w.a);
-    hipLaunchKernelGGL(morph_u8_kernel<false>, dim3(g), dim3(256), 0, st, w.a, batch, rows, cols,
+    SPECENH_LAUNCH(morph_u8_kernel<false>, dim3(g), dim3(256), 0, st, w.a, batch, rows, cols,
                        1, 3, w.b);
-    hipLaunchKernelGGL(morph_u8_kernel<true>, dim3(g), dim3(256), 0, st, w.b, batch, rows, cols,
+    SPECENH_LAUNCH(morph_u8_kernel<true>, dim3(g), dim3(256), 0, st, w.b, batch, rows, cols,
                        1, 3, w.a);
     std::swap(w.a, w.b);
   }
-  hipLaunchKernelGGL(u8_stats_kernel, dim3((unsigned)batch), dim3(256), 0, st, w.b, rows, cols,
+  SPECENH_LAUNCH(u8_stats_kernel, dim3((unsigned)batch), dim3(256), 0, st, w.b, rows, cols,
                      w.stats);
-  hipLaunchKernelGGL(u8_rescale_kernel<T>, dim3(g), dim3(256), 0, st, w.b, batch, rows, cols,
+  SPECENH_LAUNCH(u8_rescale_kernel<T>, dim3(g), dim3(256), 0, st, w.b, batch, rows, cols,
                      stride, w.stats, out);
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "u8 filter launch");
 }

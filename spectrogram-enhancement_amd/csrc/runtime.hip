@@ -1,0 +1,108 @@
+// runtime.hip — variant switches, per-device CU counts, last-launch record (runtime.hpp).
+#include "runtime.hpp"
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "specenh.h"
+
+namespace specenh {
+int set_error(int code, const std::string& msg);  // stft_psd.hip
+
+namespace {
+
+struct VariantName {
+  const char* name;
+  int dflt;
+};
+constexpr VariantName kVariants[V_COUNT] = {
+    {"CONVT_PAIR", 0},      {"PATCH_NO_WL", 0},      {"PATCH_NO_K5", 0},
+    {"PATCH_WSPLIT", -1},   {"CONV_NO_S2", 0},       {"CONV_NO_PATCH", 0},
+    {"CONV_NO_C1MFMA", 0},  {"CONV_NO_NARROW", 0},   {"WGRAD_GENERIC", 0},
+    {"WGRAD_NO_CO1", 0},    {"WGRAD_PERPHASE", 0},   {"SVD_GRAM_TILES", 0},
+};
+
+std::atomic<int> g_variant[V_COUNT];
+std::once_flag g_variant_once;
+
+void init_variants() {
+  for (int i = 0; i < V_COUNT; ++i) {
+    int v = kVariants[i].dflt;
+    std::string env = std::string("SPECENH_") + kVariants[i].name;
+    if (const char* s = std::getenv(env.c_str()); s && *s) v = std::atoi(s);
+    g_variant[i].store(v, std::memory_order_relaxed);
+  }
+}
+
+int variant_index(const char* name) {
+  if (!name) return -1;
+  if (std::strncmp(name, "SPECENH_", 8) == 0) name += 8;
+  for (int i = 0; i < V_COUNT; ++i)
+    if (std::strcmp(name, kVariants[i].name) == 0) return i;
+  return -1;
+}
+
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_cus[kMaxDevices];
+
+constexpr int kRing = 256;  // the calling thread's last kRing launches
+thread_local const void* g_ring[kRing];
+thread_local long long g_launches = 0;
+
+}  // namespace
+
+int variant(Variant v) {
+  std::call_once(g_variant_once, init_variants);
+  return g_variant[v].load(std::memory_order_relaxed);
+}
+
+int device_cus() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 256;
+  int c = g_cus[dev].load(std::memory_order_relaxed);
+  if (c > 0) return c;
+  if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+    c = 256;
+  g_cus[dev].store(c, std::memory_order_relaxed);  // same value from any racing thread
+  return c;
+}
+
+void note_launch(const void* kernel) { g_ring[g_launches++ % kRing] = kernel; }
+
+}  // namespace specenh
+
+extern "C" {
+
+int specenh_set_variant(const char* name, int value) {
+  const int i = specenh::variant_index(name);
+  if (i < 0) return specenh::set_error(SPECENH_EINVAL, std::string("unknown variant ") + (name ? name : "(null)"));
+  std::call_once(specenh::g_variant_once, specenh::init_variants);
+  specenh::g_variant[i].store(value, std::memory_order_relaxed);
+  return SPECENH_OK;
+}
+
+int specenh_get_variant(const char* name, int* value) {
+  const int i = specenh::variant_index(name);
+  if (i < 0 || !value)
+    return specenh::set_error(SPECENH_EINVAL, std::string("unknown variant ") + (name ? name : "(null)"));
+  *value = specenh::variant((specenh::Variant)i);
+  return SPECENH_OK;
+}
+
+long long specenh_launch_count(void) { return specenh::g_launches; }
+
+const char* specenh_kernel_name_at(long long index) {
+  using namespace specenh;
+  if (index < 0 || index >= g_launches || index < g_launches - kRing) return "";
+  const char* n = hipKernelNameRefByPtr(g_ring[index % kRing], nullptr);
+  return n ? n : "";
+}
+
+const char* specenh_last_kernel_name(void) {
+  return specenh_kernel_name_at(specenh::g_launches - 1);
+}
+
+}  // extern "C"

@@ -1,0 +1,48 @@
+// runtime.hpp — host-side runtime shared by the kernel files: kernel-variant switches,
+// the per-device CU count for persistent grids, and the record of the last launched kernel.
+//
+// Variant switches select between kernels that compute the same result (A/B tests and the
+// per-layer tools). They are read from the environment ONCE per process (SPECENH_<NAME>,
+// first use) and can be changed afterwards only through specenh_set_variant() — a launch
+// reads one atomic, never the environment.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace specenh {
+
+enum Variant : int {
+  V_CONVT_PAIR = 0,   // Conv2DTranspose forward in (tile, row-phase) workgroups (opt-in)
+  V_PATCH_NO_WL,      // 16-channel conv: weights from the L2 ring instead of LDS
+  V_PATCH_NO_K5,      // 16-channel conv: no compile-time 5x5 taps / persistent grid
+  V_PATCH_WSPLIT,     // 2x2 wave split: -1 auto (default), 0 off, 1 forced
+  V_CONV_NO_S2,       // stride-2 conv: generic gather kernel instead of the S2 patch kernel
+  V_CONV_NO_PATCH,    // every conv through the generic gather kernel
+  V_CONV_NO_C1MFMA,   // C = 1 conv on the VALU kernel instead of MFMA
+  V_CONV_NO_NARROW,   // no VALU narrow kernels (1 in / 1 out channel)
+  V_WGRAD_GENERIC,    // weight gradients through the generic gather kernel
+  V_WGRAD_NO_CO1,     // CO = 1 weight gradient through the general MFMA kernel
+  V_WGRAD_PERPHASE,   // Conv2DTranspose weight gradient one phase per workgroup
+  V_SVD_GRAM_TILES,   // Gram matrix through the triangle-tile kernel instead of LDS rows
+  V_COUNT
+};
+
+// current value of a switch (0 = the shipped default path; V_PATCH_WSPLIT: -1)
+int variant(Variant v);
+
+// CU count of the calling thread's current HIP device, queried once per device
+int device_cus();
+
+// record `kernel` (the host stub a launch used) as the calling thread's last launch:
+// specenh_last_kernel_name() reports its symbol, so a measurement can key PMC counters by
+// the exact kernel it timed
+void note_launch(const void* kernel);
+
+}  // namespace specenh
+
+// hipLaunchKernelGGL + note_launch. K may be parenthesised (a template-id with commas).
+#define SPECENH_LAUNCH(K, ...)                                        \
+  do {                                                                \
+    ::specenh::note_launch(reinterpret_cast<const void*>(&K));        \
+    hipLaunchKernelGGL(K, __VA_ARGS__);                               \
+  } while (0)

@@ -45,6 +45,7 @@
 #define SPECENH_STFT_PF_EARLY 0
 #endif
 #include "specenh.h"
+#include "runtime.hpp"
 
 // Development-only flag bit (not part of the public header): skip the output store,
 // to separate compute from store cost when profiling.
@@ -749,7 +750,7 @@ hipError_t launch_stft(const StftArgs& a, long long batch, hipStream_t stream) {
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((stft_psd_kernel<N, XH>), dim3((unsigned)batch), dim3(Lo::THREADS),
+  SPECENH_LAUNCH((stft_psd_kernel<N, XH>), dim3((unsigned)batch), dim3(Lo::THREADS),
                      Lo::BYTES, stream, a);
   return hipGetLastError();
 }
@@ -1032,14 +1033,14 @@ hipError_t launch_team_mode(const StftArgs& a, long long batch, void* workspace,
     e = hipMemsetAsync(workspace, 0, zero, stream);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((stft_team_kernel<N, MODE>), dim3((unsigned)(Q * M)), dim3(Lo::THREADS), Lo::BYTES,
+  SPECENH_LAUNCH((stft_team_kernel<N, MODE>), dim3((unsigned)(Q * M)), dim3(Lo::THREADS), Lo::BYTES,
                      stream, a, gran, batch, M, (int)Q, tmo, tflag, xcd_teams);
   e = hipGetLastError();
   if (e != hipSuccess || !normalize) {
     *launched = e == hipSuccess;
     return e;
   }
-  hipLaunchKernelGGL(team_fixup_kernel, dim3(1024), dim3(256), 0, stream, a.out, a.F_out, a.T,
+  SPECENH_LAUNCH(team_fixup_kernel, dim3(1024), dim3(256), 0, stream, a.out, a.F_out, a.T,
                      Lo::TF, gran, tflag, batch, M, tmo);
   e = hipGetLastError();
   *launched = e == hipSuccess;

@@ -13,6 +13,7 @@
 #include <string>
 
 #include "specenh.h"
+#include "runtime.hpp"
 
 namespace specenh {
 int set_error(int code, const std::string& msg);  // stft_psd.hip
@@ -90,13 +91,13 @@ int specenh_strips_pack(int dst_dtype, const float* S, long long batch, int F, i
   const long long total = batch * n_strips * rows * (width / 4);
   hipStream_t st = (hipStream_t)stream;
   if (dst_dtype == SPECENH_DTYPE_F32)
-    hipLaunchKernelGGL(pack_kernel<float>, dim3(blocks_for(total)), dim3(256), 0, st, S, batch, T,
+    SPECENH_LAUNCH(pack_kernel<float>, dim3(blocks_for(total)), dim3(256), 0, st, S, batch, T,
                        s_stride, rows, width, n_strips, (float*)out);
   else if (dst_dtype == SPECENH_DTYPE_BF16)
-    hipLaunchKernelGGL(pack_kernel<__bf16>, dim3(blocks_for(total)), dim3(256), 0, st, S, batch,
+    SPECENH_LAUNCH(pack_kernel<__bf16>, dim3(blocks_for(total)), dim3(256), 0, st, S, batch,
                        T, s_stride, rows, width, n_strips, (__bf16*)out);
   else if (dst_dtype == SPECENH_DTYPE_F16)
-    hipLaunchKernelGGL(pack_kernel<_Float16>, dim3(blocks_for(total)), dim3(256), 0, st, S,
+    SPECENH_LAUNCH(pack_kernel<_Float16>, dim3(blocks_for(total)), dim3(256), 0, st, S,
                        batch, T, s_stride, rows, width, n_strips, (_Float16*)out);
   else
     return set_error(SPECENH_EINVAL, "strips_pack: dtype");
@@ -111,13 +112,13 @@ int specenh_strips_unpack(int src_dtype, const void* strips, long long batch, in
   const long long total = batch * n_strips * rows * (width / 4);
   hipStream_t st = (hipStream_t)stream;
   if (src_dtype == SPECENH_DTYPE_F32)
-    hipLaunchKernelGGL(unpack_kernel<float>, dim3(blocks_for(total)), dim3(256), 0, st,
+    SPECENH_LAUNCH(unpack_kernel<float>, dim3(blocks_for(total)), dim3(256), 0, st,
                        (const float*)strips, batch, rows, width, n_strips, out);
   else if (src_dtype == SPECENH_DTYPE_BF16)
-    hipLaunchKernelGGL(unpack_kernel<__bf16>, dim3(blocks_for(total)), dim3(256), 0, st,
+    SPECENH_LAUNCH(unpack_kernel<__bf16>, dim3(blocks_for(total)), dim3(256), 0, st,
                        (const __bf16*)strips, batch, rows, width, n_strips, out);
   else if (src_dtype == SPECENH_DTYPE_F16)
-    hipLaunchKernelGGL(unpack_kernel<_Float16>, dim3(blocks_for(total)), dim3(256), 0, st,
+    SPECENH_LAUNCH(unpack_kernel<_Float16>, dim3(blocks_for(total)), dim3(256), 0, st,
                        (const _Float16*)strips, batch, rows, width, n_strips, out);
   else
     return set_error(SPECENH_EINVAL, "strips_unpack: dtype");

@@ -29,6 +29,7 @@
 
 #include "fft_common.hpp"
 #include "specenh.h"
+#include "runtime.hpp"
 
 namespace specenh {
 int set_error(int code, const std::string& msg);  // stft_psd.hip
@@ -1257,15 +1258,11 @@ __global__ __launch_bounds__(256) void recon_eig_kernel(XView x, int Kr, int r, 
 using namespace specenh;
 
 namespace {
-bool getenv_set(const char* name) {
-  const char* v = std::getenv(name);
-  return v && *v && *v != '0';
-}
 
 // G = X^T X for every matrix: the LDS-chunked kernel for r <= 128 (r % 4 == 0), else
 // one wave per 32x32 tile.
 void launch_gram(const XView& xv, int Kr, int r, float* G, long long batch, hipStream_t st) {
-  const bool lds = r <= 128 && r % 4 == 0 && !getenv_set("SPECENH_SVD_GRAM_TILES");
+  const bool lds = r <= 128 && r % 4 == 0 && variant(V_SVD_GRAM_TILES) == 0;
   const int nts = (r + 31) / 32;
   const int ntri = nts * (nts + 1) / 2;
   for (long long b0 = 0; b0 < batch; b0 += 65535) {
@@ -1273,10 +1270,10 @@ void launch_gram(const XView& xv, int Kr, int r, float* G, long long batch, hipS
     XView xb = xv;
     xb.base = xv.base + b0 * xv.batch_stride;
     if (lds)
-      hipLaunchKernelGGL(gram_lds_kernel, dim3((unsigned)nb), dim3(256), 0, st, xb, Kr, r,
+      SPECENH_LAUNCH(gram_lds_kernel, dim3((unsigned)nb), dim3(256), 0, st, xb, Kr, r,
                          G + b0 * (long long)r * r);
     else
-      hipLaunchKernelGGL(gram_kernel, dim3((ntri + 3) / 4, (unsigned)nb), dim3(256), 0, st, xb,
+      SPECENH_LAUNCH(gram_kernel, dim3((ntri + 3) / 4, (unsigned)nb), dim3(256), 0, st, xb,
                          Kr, r, G + b0 * (long long)r * r, nts);
   }
 }
@@ -1293,7 +1290,7 @@ hipError_t launch_subspace_t(const float* G, int r, int K, float* V, float* thet
   // 3 rounds when the subspace oversamples the wanted K by >= 8 columns, else 5
   // (a second pass over flagged matrices starts elsewhere and iterates 4x longer)
   const int iters = (P >= K + 8 ? 3 : 5) * (seed ? 4 : 1);
-  hipLaunchKernelGGL(subspace_kernel<P>, dim3((unsigned)batch), dim3(SS_THREADS), lds, st, G, r,
+  SPECENH_LAUNCH(subspace_kernel<P>, dim3((unsigned)batch), dim3(SS_THREADS), lds, st, G, r,
                      K, iters, V, theta, cut2, 5e-6f, flags, seed, only);
   return hipGetLastError();
 }
@@ -1319,7 +1316,7 @@ hipError_t launch_recon_t(XView xb, int Kr, int r, const float* V, int K, int lo
   hipError_t e = hipFuncSetAttribute((const void*)recon_kernel<KP, TO>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((recon_kernel<KP, TO>), dim3((Kr + RB - 1) / RB, (unsigned)nb), dim3(256),
+  SPECENH_LAUNCH((recon_kernel<KP, TO>), dim3((Kr + RB - 1) / RB, (unsigned)nb), dim3(256),
                      lds, st, xb, Kr, r, V, K, lo, hi, comp, only, reinterpret_cast<TO*>(out),
                      ob, osk, osi);
   return hipGetLastError();
@@ -1375,7 +1372,7 @@ hipError_t launch_recon_eig_t(XView xb, int Kr, int r, const double* Z, long lon
   hipError_t e = hipFuncSetAttribute((const void*)recon_eig_kernel<TO>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(recon_eig_kernel<TO>, dim3((Kr + RB - 1) / RB, (unsigned)nb), dim3(256), lds,
+  SPECENH_LAUNCH(recon_eig_kernel<TO>, dim3((Kr + RB - 1) / RB, (unsigned)nb), dim3(256), lds,
                      st, xb, Kr, r, Z, ld, kinfo, reinterpret_cast<TO*>(out), ob, osk, osi, only);
   return hipGetLastError();
 }
@@ -1433,15 +1430,15 @@ int eig_denoise(const float* A, long long batch, int m, int n, long long a_strid
     const long long nb = std::min(ch, batch - b0);
     xv.base = A + b0 * a_stride;
     const int* on = only ? only + b0 : nullptr;
-    hipLaunchKernelGGL(gram64_kernel, dim3(ntri64, (unsigned)nb), dim3(256), 0, st, xv, Kr, r,
+    SPECENH_LAUNCH(gram64_kernel, dim3(ntri64, (unsigned)nb), dim3(256), 0, st, xv, Kr, r,
                        G64, nts64, on);
-    hipLaunchKernelGGL(tridiag_kernel, dim3((unsigned)nb), dim3(256), 0, st, G64, r, dd, ee, tau,
+    SPECENH_LAUNCH(tridiag_kernel, dim3((unsigned)nb), dim3(256), 0, st, G64, r, dd, ee, tau,
                        on);
     const int* rg = nullptr;
     if (opt_mode >= 0) {
-      hipLaunchKernelGGL(optimal_rank_kernel, dim3((unsigned)nb), dim3(64), 0, st, dd, ee, r,
+      SPECENH_LAUNCH(optimal_rank_kernel, dim3((unsigned)nb), dim3(64), 0, st, dd, ee, r,
                          omega, num, med);
-      hipLaunchKernelGGL(optimal_ranges_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0,
+      SPECENH_LAUNCH(optimal_ranges_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0,
                          st, num, nb, r, opt_mode, ranges, bad);
       if (num_out && hipMemcpyAsync(num_out + b0, num, (size_t)nb * 4, hipMemcpyDeviceToDevice,
                                     st) != hipSuccess)
@@ -1451,7 +1448,7 @@ int eig_denoise(const float* A, long long batch, int m, int n, long long a_strid
         return set_error(SPECENH_EHIP, "median copy");
       rg = ranges;
     }
-    hipLaunchKernelGGL(eigvec_kernel, dim3((unsigned)nb), dim3(256), 0, st, G64, dd, ee, tau, r,
+    SPECENH_LAUNCH(eigvec_kernel, dim3((unsigned)nb), dim3(256), 0, st, G64, dd, ee, tau, r,
                        lo, hi, rg, Z, fac, L.ld, kinfo, on);
     if (hipGetLastError() != hipSuccess) return set_error(SPECENH_EHIP, "eigen path launch");
     const hipError_t e = launch_recon_eig(odt, xv, Kr, r, Z, L.ld, kinfo,

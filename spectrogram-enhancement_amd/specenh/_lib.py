@@ -51,6 +51,11 @@ _c = ctypes
 SIGNATURES = {
     "specenh_last_error": (_c.c_char_p, []),
     "specenh_version": (_c.c_char_p, []),
+    "specenh_set_variant": (_c.c_int, [_c.c_char_p, _c.c_int]),
+    "specenh_get_variant": (_c.c_int, [_c.c_char_p, _c.POINTER(_c.c_int)]),
+    "specenh_last_kernel_name": (_c.c_char_p, []),
+    "specenh_launch_count": (_c.c_longlong, []),
+    "specenh_kernel_name_at": (_c.c_char_p, [_c.c_longlong]),
     "specenh_stft_frames": (_c.c_longlong, [_c.c_longlong, _c.c_int, _c.c_int]),
     "specenh_stft_plan_create": (_c.c_int, [_c.POINTER(_c.c_void_p), _c.c_int, _c.c_int,
                                             _c.POINTER(_c.c_double), _c.c_double, _c.c_int,
@@ -179,3 +184,47 @@ def check(rc: int, what: str = "") -> int:
 
 def current_stream_handle(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def get_variant(name: str) -> int:
+    v = ctypes.c_int(0)
+    check(lib().specenh_get_variant(name.encode(), ctypes.byref(v)), "get_variant")
+    return v.value
+
+
+def set_variant(name: str, value: int) -> None:
+    """Select a kernel variant (runtime.hpp: the A/B switches; SPECENH_<name> in the
+    environment sets the process default, read once)."""
+    check(lib().specenh_set_variant(name.encode(), int(value)), "set_variant")
+
+
+class variant:
+    """Context manager: ``with _lib.variant("CONV_NO_S2", 1): ...`` restores the old value."""
+
+    def __init__(self, name: str, value: int):
+        self.name, self.value = name, int(value)
+
+    def __enter__(self):
+        self.old = get_variant(self.name)
+        set_variant(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        set_variant(self.name, self.old)
+        return False
+
+
+def last_kernel_name() -> str:
+    """Mangled symbol of the last kernel the calling thread launched through the library."""
+    return lib().specenh_last_kernel_name().decode(errors="replace")
+
+
+def launch_count() -> int:
+    """Kernels the calling thread has launched through the library so far."""
+    return int(lib().specenh_launch_count())
+
+
+def kernel_names(first: int, end: int) -> list:
+    """Symbols of this thread's launches [first, end) (specenh_launch_count numbering)."""
+    L = lib()
+    return [L.specenh_kernel_name_at(i).decode(errors="replace") for i in range(first, end)]

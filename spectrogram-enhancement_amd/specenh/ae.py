@@ -287,11 +287,13 @@ class AutoencoderEngine:
         ops.conv2d_out(x, weights, self._bv[i] if bias else None, op.k, op.k, cout, s, pt, pl,
                        dil, OH, OW, ACT[act], mask, logits, out, pool, argmax)
 
-    def forward(self, x, train=False, timing=None):
+    def forward(self, x, train=False, timing=None, kernels=None):
         """x: device [N, H, W, C] in the compute dtype. Returns the output buffer
         (fp32 for inference, compute dtype for training; reused between calls).
         ``timing``: optional list; a (start, end) pair of torch.cuda.Event recorded on the
-        launch stream is appended around every convolution launch."""
+        launch stream is appended around every convolution launch. ``kernels``: optional
+        list; the symbol of each such launch's kernel is appended (the key of its PMC
+        record, tools/pmc_fold.py)."""
         N = x.shape[0]
         if x.dtype != self.tdt or not x.is_contiguous() or tuple(x.shape[1:]) != self.input_shape:
             raise ValueError(f"forward expects a contiguous {self.tdt} [N, *{self.input_shape}]")
@@ -318,6 +320,8 @@ class AutoencoderEngine:
                 if timing is not None:
                     ev[1].record(torch.cuda.current_stream(self.device))
                     timing.append(ev)
+                if kernels is not None:
+                    kernels.append(_lib.last_kernel_name())
                 skip = True
                 continue
             if isinstance(op, PoolOp):
@@ -342,6 +346,8 @@ class AutoencoderEngine:
                 if timing is not None:
                     ev[1].record(torch.cuda.current_stream(self.device))
                     timing.append(ev)
+                if kernels is not None:
+                    kernels.append(_lib.last_kernel_name())
                 break
             self._conv(i, hin, hout, weights=self._wv[i], geom=op.fwd_geom(), act=op.act,
                        logits=b["z"] if (train and last) else None,
@@ -349,6 +355,8 @@ class AutoencoderEngine:
             if timing is not None:
                 ev[1].record(torch.cuda.current_stream(self.device))
                 timing.append(ev)
+            if kernels is not None:
+                kernels.append(_lib.last_kernel_name())
         return b["h"][n_ops]
 
     def last_logits(self):
@@ -449,7 +457,8 @@ class AutoencoderEngine:
         the flat gradient buffer is SUM-all-reduced and Adam scales it by 1/world_size:
         every rank then applies the identical update. The decoder's
         bucket is all-reduced asynchronously while the encoder's backward runs
-        (dp_backward)."""
+        (dp_backward). Without it the step is rank-local even when a default process
+        group is initialised."""
         self.forward(x, train=True)
         loss = self.loss_and_grad(y)
         scale = dp_backward(self, process_group)
@@ -477,10 +486,15 @@ def dp_backward(eng, group=None, dist=None) -> float:
     bucket (eng.grad_bucket_split) goes out asynchronously as soon as its weight gradients
     are enqueued and overlaps the encoder's backward; the encoder bucket follows when
     backward ends; both are awaited before returning. Returns Adam's grad_scale
-    (1/world_size), or 1.0 (plain backward) without a process group."""
-    if dist is None:
-        import torch.distributed as tdist
-        dist = tdist if (tdist.is_available() and tdist.is_initialized()) else None
+    (1/world_size), or 1.0 (plain backward) without a process group.
+
+    The exchange is opt-in: it runs only when the caller names a group or passes the
+    ``torch.distributed`` module (Model.fit does, under an initialised default group). An
+    initialised default group alone never turns a single-model step into a collective, so
+    rank-local training (a per-rank sweep task, the bench's rank-0 stages) cannot
+    deadlock against ranks that are not stepping."""
+    if dist is None and group is not None:
+        import torch.distributed as dist
     if dist is None:
         eng.backward()
         return 1.0

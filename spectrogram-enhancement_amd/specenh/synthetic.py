@@ -91,3 +91,35 @@ def plasma_chirps_torch(n_shots: int, length: int, seed: int = 0, fs: float = FS
         x += d * n / length
         out[s0:s0 + b] = x.to(dtype)
     return out
+
+
+# BASELINE config 4 / SURVEY.md §8(d) C4: C1-style spectrograms (16,512 samples, hann 256 /
+# hop 128 -> 128 x 128, specgr's log + min-max) of seeded noisy chirps as inputs, the
+# spectrograms of the same chirps without noise (sigma = 0), normalised identically, as
+# targets: a synthetic stand-in for the cv2 label pipeline (pipeline_data.py:101-110).
+C4_LENGTH = 16512
+C4_SPEC = {"nperseg": 256, "noverlap": 128, "fs": 500000, "window": "hann",
+           "scaling": "density", "detrend": "linear", "eps": 1e-11}
+
+
+def c4_pairs_torch(n: int, seed: int = 0, device="cuda", dtype=None, chunk: int = 2048):
+    """Device C4 pairs ``(x, y)`` [n, 128, 128, 1] (``dtype``, default fp32) generated and
+    transformed on the GPU (plasma_chirps_torch -> specgr_batch): the bench's training set.
+    The noisy and clean shots of one seed share every chirp parameter (the noise draw is
+    made either way)."""
+    import torch
+
+    from .pipeline_data import specgr_batch
+
+    dtype = dtype or torch.float32
+    x = torch.empty((n, 128, 128, 1), dtype=dtype, device=device)
+    y = torch.empty_like(x)
+    S = torch.empty((min(n, chunk), 128, 128), dtype=torch.float32, device=device)
+    for s0 in range(0, n, chunk):
+        b = min(chunk, n - s0)
+        for dst, sigma in ((x, 0.5), (y, 0.0)):
+            sh = plasma_chirps_torch(b, C4_LENGTH, seed=seed + s0, sigma=sigma, device=device)
+            specgr_batch(sh, C4_SPEC, out=S[:b])
+            dst[s0:s0 + b, :, :, 0] = S[:b].to(dtype)
+            del sh
+    return x, y

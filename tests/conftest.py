@@ -52,3 +52,22 @@ def gpu_device():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def kernel_variant():
+    """kernel_variant("CONV_NO_S2", 1): select a kernel variant through the C-ABI switch
+    (specenh_set_variant; the library reads the environment once), restored afterwards."""
+    from specenh import _lib
+
+    saved = {}
+
+    def setv(name, value):
+        name = name[8:] if name.startswith("SPECENH_") else name
+        if name not in saved:
+            saved[name] = _lib.get_variant(name)
+        _lib.set_variant(name, int(value))
+
+    yield setv
+    for name, value in saved.items():
+        _lib.set_variant(name, value)

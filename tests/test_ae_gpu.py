@@ -525,7 +525,7 @@ def test_fused_conv_pool_is_bitwise_identical_to_unfused(gpu_device, dtype):
 
 @pytest.mark.parametrize("dtype", ["mixed_bfloat16", "float16"])
 @pytest.mark.parametrize("hw", [(128, 128), (40, 56), (24, 8)])
-def test_convt_row_phase_pairs_bitwise_identical(gpu_device, dtype, hw, monkeypatch):
+def test_convt_row_phase_pairs_bitwise_identical(gpu_device, dtype, hw, kernel_variant):
     """Conv2DTranspose forward in (tile, row-phase) workgroups with LDS-staged whole-row
     stores (opt-in: SPECENH_CONVT_PAIR=1, measured slower) gives the same
     bits as the four-phase workgroups with per-phase stores, at
@@ -539,7 +539,7 @@ def test_convt_row_phase_pairs_bitwise_identical(gpu_device, dtype, hw, monkeypa
     y = rng.uniform(0, 1, (5, H, W, 1)).astype(np.float32)
     outs, grads = [], []
     for flag in ("1", "0"):
-        monkeypatch.setenv("SPECENH_CONVT_PAIR", flag)
+        kernel_variant("CONVT_PAIR", int(flag))
         outs.append(eng.forward(upload(eng, x), train=False).clone())
         eng.forward(upload(eng, x), train=True)
         eng.loss_and_grad(upload(eng, y))
@@ -553,7 +553,7 @@ def test_convt_row_phase_pairs_bitwise_identical(gpu_device, dtype, hw, monkeypa
 @pytest.mark.parametrize("switch", [("SPECENH_PATCH_WSPLIT", "1", "0"),
                                     ("SPECENH_PATCH_NO_WL", "0", "1")])
 @pytest.mark.parametrize("dtype", ["mixed_bfloat16", "float16"])
-def test_wave_split_patch_kernel_is_bitwise_identical(gpu_device, dtype, switch, monkeypatch):
+def test_wave_split_patch_kernel_is_bitwise_identical(gpu_device, dtype, switch, kernel_variant):
     """conv_patch_kernel's variants run the same k-step order per output: the 2 x 2 wave
     split (8 rows x half the channels per wave, the default for 32/64-channel chunks) vs the
     4 x 1 split, and the 16-channel kernel's LDS-resident weights vs the register ring fed
@@ -568,7 +568,7 @@ def test_wave_split_patch_kernel_is_bitwise_identical(gpu_device, dtype, switch,
         # a fresh engine whose every activation buffer starts as NaN: an output element a
         # variant fails to write cannot inherit the other variant's value
         eng, _ = make(ops, (64, 64, 1), dtype=dtype, seed=47)
-        monkeypatch.setenv(env, flag)
+        kernel_variant(env, int(flag))
         poison(eng, 4, False)
         outs.append(eng.forward(upload(eng, x), train=False).clone())
         poison(eng, 4, True)

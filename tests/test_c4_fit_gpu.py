@@ -1,0 +1,128 @@
+"""BASELINE config 4 on the GPU: Model.fit of the reference model
+(VAE/manual_scan_3layers.py:186-212: 16/32/64 filters, 5x5, 128 x 128 x 1, Adam, BCE) on the
+C4 workload of SURVEY.md §8(d) — C1 spectrograms of seeded noisy chirps as inputs, the
+spectrograms of the same chirps without noise as targets — must track the oracle's
+(oracle/autoencoder.py, fp64 Keras-Adam) loss and val_loss trajectory epoch by epoch.
+
+Both sides train on the same float32 pairs (made on the host by the byte-exact generator
+and the scipy-semantics oracle spectrogram) from the same initial weights, without
+shuffling, with validation_data as manual_scan_3layers.py:203-212 passes it.
+
+Tolerances (relative, per epoch): float32 compute 1e-3 (fp32 accumulation vs fp64 over a
+few Adam steps), mixed_bfloat16 3e-2 (bf16 operands; the measured gap is recorded in
+DESIGN.md). The device generator of the bench (specenh.synthetic.c4_pairs_torch) is checked
+against the host pairs' statistics and against specgr of the same device shots.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import autoencoder as ora
+from oracle.spectrogram import specgr_arrays
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"float32": 1e-3, "mixed_bfloat16": 3e-2}
+
+
+def host_c4_pairs(n, seed0):
+    from specenh.synthetic import C4_LENGTH, C4_SPEC, plasma_chirps
+    noisy = plasma_chirps(n, C4_LENGTH, seed0=seed0, dtype=np.float64)
+    clean = plasma_chirps(n, C4_LENGTH, seed0=seed0, sigma=0.0, dtype=np.float64)
+    x = specgr_arrays(noisy, C4_SPEC)[0].astype(np.float32)[..., None]
+    y = specgr_arrays(clean, C4_SPEC)[0].astype(np.float32)[..., None]
+    return x, y
+
+
+def reference_model(policy):
+    from specenh.keras import layers, mixed_precision, utils
+    from specenh.keras.models import Model
+    utils.set_random_seed(3)
+    mixed_precision.set_global_policy(policy)
+    try:
+        inp = layers.Input(shape=(128, 128, 1))
+        x = layers.Conv2D(16, 5, activation="relu", padding="same")(inp)
+        x = layers.MaxPooling2D((2, 2), padding="same")(x)
+        x = layers.Conv2D(32, 5, activation="relu", padding="same")(x)
+        x = layers.MaxPooling2D((2, 2), padding="same")(x)
+        x = layers.Conv2D(64, 5, activation="relu", padding="same")(x)
+        x = layers.MaxPooling2D((2, 2), padding="same")(x)
+        x = layers.Conv2DTranspose(64, 5, strides=2, activation="relu", padding="same")(x)
+        x = layers.Conv2DTranspose(32, 5, strides=2, activation="relu", padding="same")(x)
+        x = layers.Conv2DTranspose(16, 5, strides=2, activation="relu", padding="same")(x)
+        x = layers.Conv2D(1, 5, activation="sigmoid", padding="same")(x)
+        m = Model(inp, x)
+    finally:
+        mixed_precision.set_global_policy("float32")
+    m.compile(optimizer="adam", loss="binary_crossentropy")
+    return m
+
+
+def oracle_fit(spec, ws, x, y, xv, yv, epochs, batch):
+    tp, j = [], 0
+    for s in spec:
+        if s[0] == "pool":
+            tp.append(None)
+        else:
+            tp.append({"W": torch.tensor(ws[j], dtype=torch.float64, requires_grad=True),
+                       "b": torch.tensor(ws[j + 1], dtype=torch.float64, requires_grad=True)})
+            j += 2
+    opt = ora.KerasAdam()
+    xt, yt = torch.tensor(x, dtype=torch.float64), torch.tensor(y, dtype=torch.float64)
+    xvt, yvt = torch.tensor(xv, dtype=torch.float64), torch.tensor(yv, dtype=torch.float64)
+    hist = {"loss": [], "val_loss": []}
+    n = x.shape[0]
+    for _ in range(epochs):
+        tot = 0.0
+        for s in range(0, n, batch):
+            tot += ora.train_step(spec, tp, xt[s:s + batch], yt[s:s + batch], opt) * \
+                min(batch, n - s)
+        hist["loss"].append(tot / n)
+        with torch.no_grad():
+            _, z = ora.forward(spec, tp, xvt, return_logits=True)
+            hist["val_loss"].append(float(ora.bce_from_logits(z, yvt)))
+    return hist
+
+
+@pytest.fixture(scope="module")
+def c4_data():
+    x, y = host_c4_pairs(24, seed0=40000)
+    xv, yv = host_c4_pairs(8, seed0=41000)
+    return x, y, xv, yv
+
+
+@pytest.mark.parametrize("policy", ["float32", "mixed_bfloat16"])
+def test_c4_fit_tracks_oracle_val_loss(gpu_device, c4_data, policy):
+    x, y, xv, yv = c4_data
+    m = reference_model(policy)
+    spec = [("pool",) if op.kind == "pool" else (op.kind, op.cin, op.cout, op.k, op.act)
+            for op in m._ops]
+    ref = oracle_fit(spec, m.get_weights(), x, y, xv, yv, epochs=3, batch=8)
+    hist = m.fit(x=x, y=y, epochs=3, batch_size=8, shuffle=False,
+                 validation_data=(xv, yv), verbose=0).history
+    for key in ("loss", "val_loss"):
+        got, want = np.array(hist[key]), np.array(ref[key])
+        rel = np.abs(got - want) / want
+        assert np.all(rel <= TOL[policy]), (key, got, want, rel)
+    assert ref["val_loss"][-1] < ref["val_loss"][0]  # the workload is learnable
+
+
+def test_device_c4_pairs_match_host_pipeline(gpu_device):
+    """The bench's device C4 set: inputs and targets are specgr of the device shots with and
+    without noise (same chirps), in [0, 1] with the per-spectrogram min 0 and max 1."""
+    from specenh import pipeline_data
+    from specenh.synthetic import C4_LENGTH, C4_SPEC, c4_pairs_torch, plasma_chirps_torch
+    x, y = c4_pairs_torch(64, seed=77, device=gpu_device, chunk=32)
+    assert x.shape == y.shape == (64, 128, 128, 1)
+    for t in (x, y):
+        flat = t.view(64, -1)
+        assert torch.all(flat.min(1).values == 0) and torch.all(flat.max(1).values == 1)
+    # chunk 0 reproduces from the same seed
+    sh = plasma_chirps_torch(32, C4_LENGTH, seed=77, sigma=0.0, device=gpu_device)
+    S = pipeline_data.specgr_batch(sh, C4_SPEC)
+    assert torch.equal(S, y[:32, :, :, 0])
+    # noisy and clean differ, but share the chirps: their spectrograms correlate
+    d = (x - y).abs().mean().item()
+    assert 0.01 < d < 0.5
+    c = torch.corrcoef(torch.stack([x.flatten(), y.flatten()]))[0, 1].item()
+    assert c > 0.3

@@ -94,3 +94,23 @@ def test_python_boundary_rejects_cpu_tensors():
 
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         stft.stft_psd(torch.zeros(2, 4096), 256, 128)
+
+
+def test_variant_switches_read_once_and_settable():
+    """Kernel-variant switches: known names round-trip through the C-ABI, unknown names are
+    refused, and the environment is not consulted per launch (runtime.hpp)."""
+    from specenh import _lib
+
+    old = _lib.get_variant("CONV_NO_S2")
+    with _lib.variant("SPECENH_CONV_NO_S2", 1):
+        assert _lib.get_variant("CONV_NO_S2") == 1
+        os.environ["SPECENH_CONV_NO_S2"] = "0"  # too late: read once per process
+        try:
+            assert _lib.get_variant("CONV_NO_S2") == 1
+        finally:
+            del os.environ["SPECENH_CONV_NO_S2"]
+    assert _lib.get_variant("CONV_NO_S2") == old
+    assert _lib.get_variant("PATCH_WSPLIT") in (-1, 0, 1)
+    with pytest.raises(ValueError, match="unknown variant"):
+        _lib.set_variant("NO_SUCH_SWITCH", 1)
+    assert _lib.last_kernel_name() == ""  # nothing launched on this thread

@@ -23,9 +23,9 @@ CASES = [(16, 32, 5, 40, 36, 2, 2), (32, 64, 5, 32, 32, 2, 2), (64, 64, 5, 18, 3
 @pytest.mark.parametrize("C,CO,K,H,W,N,pad", CASES)
 @pytest.mark.parametrize("path", ["patch", "generic"])
 @pytest.mark.parametrize("masked", [False, True])
-def test_stride2_conv(gpu_device, monkeypatch, dtype, C, CO, K, H, W, N, pad, path, masked):
+def test_stride2_conv(gpu_device, kernel_variant, dtype, C, CO, K, H, W, N, pad, path, masked):
     if path == "generic":
-        monkeypatch.setenv("SPECENH_CONV_NO_S2", "1")
+        kernel_variant("CONV_NO_S2", 1)
     rng = np.random.default_rng(C * 7 + CO + K + H)
     OH, OW = (H + 1) // 2, (W + 1) // 2
     x = torch.tensor(rng.standard_normal((N, H, W, C)), dtype=dtype, device=gpu_device)

@@ -200,3 +200,74 @@ def test_dp_fit_unseeded_ranks_stay_in_lockstep():
         np.testing.assert_array_equal(a, b)
     h = results[0][1]
     assert h["loss"][-1] < h["loss"][0]
+
+
+def _rank_local_steps(out_q, rank, world, port):
+    """Only rank 0 trains (as bench.py's rank-0 stages and a per-rank sweep task do) while
+    rank 1 waits in the final barrier: with no group named, the step must stay rank-local
+    even though a default group is initialised (no collective that rank 1 never joins)."""
+    from specenh import ae
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        scales = []
+        if rank == 0:
+            m = _build(0)
+            eng = OracleEngine(_oracle_ops(), (16, 16, 1))
+            eng.set_keras_weights(m.get_weights())
+            x, y = _data()
+            for s in range(3):
+                eng.forward(torch.as_tensor(x[:8], dtype=torch.float64), train=True)
+                eng.loss_and_grad(torch.as_tensor(y[:8], dtype=torch.float64),
+                                  accumulate=torch.zeros(1, dtype=torch.float64))
+                scales.append(ae.dp_backward(eng))
+                eng.adam(1e-3, 0.9, 0.999, 1e-7, grad_scale=scales[-1])
+        dist.barrier()
+        # both ranks: an explicit group does exchange (and averages over the world)
+        eng2 = _TwoLayerGrad(rank)
+        sc = ae.dp_backward(eng2, group=dist.group.WORLD)
+        out_q.put((rank, scales, sc, eng2.g.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+class _TwoLayerGrad:
+    """Minimal engine: backward() writes a rank-dependent flat gradient."""
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.g = torch.zeros(6, dtype=torch.float64)
+
+    def grad_bucket_split(self):
+        return 1, 3
+
+    def backward(self, on_layer_done=None):
+        self.g = torch.arange(6, dtype=torch.float64) + 10 * self.rank
+        if on_layer_done is not None:
+            on_layer_done(1)
+            on_layer_done(0)
+
+
+def _oracle_ops():
+    from specenh import ae
+    return [ae.ConvOp("conv", 1, 4, 3, "relu"), ae.PoolOp(),
+            ae.ConvOp("convT", 4, 4, 3, "relu", stride=2), ae.ConvOp("conv", 4, 1, 3, "sigmoid")]
+
+
+def test_rank_local_step_under_initialised_group_does_not_collect():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_local_steps, args=(q, r, 2, port)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert results[0][0] == [1.0, 1.0, 1.0] and results[1][0] == []
+    for r in (0, 1):
+        scale, g = results[r][1], results[r][2]
+        assert scale == 0.5
+        np.testing.assert_array_equal(g, 2 * np.arange(6) + 10)  # SUM over the two ranks

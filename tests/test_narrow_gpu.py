@@ -29,13 +29,13 @@ def _ref(x, w, bias, k):
     return out.permute(0, 2, 3, 1), mag.permute(0, 2, 3, 1)
 
 
-def _path(monkeypatch, path):
+def _path(kernel_variant, path):
     """c1mfma: conv_c1_mfma.hip (the default for C == 1); narrow: the VALU dot2 kernel;
     generic: the MFMA patch/gather kernels."""
     if path in ("narrow", "generic"):
-        monkeypatch.setenv("SPECENH_CONV_NO_C1MFMA", "1")
+        kernel_variant("CONV_NO_C1MFMA", 1)
     if path == "generic":
-        monkeypatch.setenv("SPECENH_CONV_NO_NARROW", "1")
+        kernel_variant("CONV_NO_NARROW", 1)
 
 
 def _conv(x, w, bias, k, co, act, out_dtype, mask=None):
@@ -49,8 +49,8 @@ def _conv(x, w, bias, k, co, act, out_dtype, mask=None):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("N,H,W", [(3, 64, 64), (2, 37, 70), (1, 128, 128)])
 @pytest.mark.parametrize("path", ["c1mfma", "narrow", "generic"])
-def test_c1_masked_dgrad(gpu_device, monkeypatch, dtype, N, H, W, path):
-    _path(monkeypatch, path)
+def test_c1_masked_dgrad(gpu_device, kernel_variant, dtype, N, H, W, path):
+    _path(kernel_variant, path)
     rng = np.random.default_rng(N * 1000 + H + W)
     k, co = 5, 16
     x = torch.tensor(rng.standard_normal((N, H, W, 1)), dtype=dtype, device=gpu_device)
@@ -110,14 +110,14 @@ def test_maxpool2_bwd_routes_to_argmax(gpu_device, dtype, C, masked):
                                         (7, 16, 1, 40, 24), (4, 16, 2, 32, 32)])
 @pytest.mark.parametrize("path", ["c1mfma", "narrow", "generic"])
 @pytest.mark.parametrize("pool", [False, True])
-def test_c1_forward(gpu_device, monkeypatch, dtype, k, co, N, H, W, path, pool):
+def test_c1_forward(gpu_device, kernel_variant, dtype, k, co, N, H, W, path, pool):
     """Conv2D(1 -> co, relu) [+ MaxPooling2D]: values within one 16-bit rounding of the
     float64 result; the pooled output is the max of the stored values with its argmax."""
     if path == "narrow" and k % 2 == 0:
         pytest.skip("the VALU kernel takes odd kernels")
     if path == "generic" and pool and k > 5:
         pytest.skip("the fused pool needs the LDS-patch kernel (k <= 5)")
-    _path(monkeypatch, path)
+    _path(kernel_variant, path)
     rng = np.random.default_rng(k * 100 + co + H)
     x = torch.tensor(rng.uniform(0, 1, (N, H, W, 1)), dtype=dtype, device=gpu_device)
     w = torch.tensor(rng.standard_normal((co, k, k, 1)) * 0.3, dtype=dtype, device=gpu_device)

@@ -41,7 +41,8 @@ def test_every_compute_entry_point_has_an_operator():
                  "specenh_csd_plan_destroy", "specenh_svd_workspace_bytes",
                  "specenh_svd_denoise_workspace_bytes", "specenh_svd_optimal_workspace_bytes",
                  "specenh_conv2d_wgrad_workspace_bytes", "specenh_filter_workspace_bytes",
-                 "specenh_u8filter_workspace_bytes",
+                 "specenh_u8filter_workspace_bytes", "specenh_set_variant",
+                 "specenh_get_variant", "specenh_last_kernel_name", "specenh_launch_count", "specenh_kernel_name_at",
                  "specenh_svd_denoise"}  # = specenh_svd_denoise_ex with an fp32 output
     compute = [n for n in declared_functions() if n not in host_only]
     assert sorted(compute) == sorted(CABI)

@@ -246,7 +246,7 @@ def test_rank_deficient_complement(gpu_device):
 
 
 @pytest.mark.parametrize("shape", [(128, 128), (96, 128), (128, 40), (52, 100)])
-def test_gram_paths_agree(gpu_device, shape, monkeypatch):
+def test_gram_paths_agree(gpu_device, shape, kernel_variant):
     """The LDS-chunked Gram (r <= 128: row-major and transposed X, ragged chunks and tiles)
     and the one-wave-per-tile Gram give the same reconstruction to fp32 rounding, and both
     match the oracle on a gapped matrix."""
@@ -263,7 +263,7 @@ def test_gram_paths_agree(gpu_device, shape, monkeypatch):
     A = np.stack([gapped_matrix(700 + i, m, n, dtype=np.float32) for i in range(3)])
     outs = []
     for flag in ("0", "1"):
-        monkeypatch.setenv("SPECENH_SVD_GRAM_TILES", flag)
+        kernel_variant("SVD_GRAM_TILES", int(flag))
         outs.append(svd.denoise_batch(torch.as_tensor(A, device=gpu_device), 0, 16).double().cpu().numpy())
     for b in range(3):
         truth = ref.denoiseSignal(A[b].astype(np.float64), 0, 16)

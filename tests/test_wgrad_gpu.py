@@ -40,14 +40,14 @@ def _reference(x, dz, op):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("kind,cin,cout,k,H,W,N", CASES)
 @pytest.mark.parametrize("path", ["mfma", "mfma_alt", "generic"])
-def test_wgrad_matches_im2col(gpu_device, monkeypatch, dtype, kind, cin, cout, k, H, W, N, path):
+def test_wgrad_matches_im2col(gpu_device, kernel_variant, dtype, kind, cin, cout, k, H, W, N, path):
     if path == "generic":
-        monkeypatch.setenv("SPECENH_WGRAD_GENERIC", "1")
+        kernel_variant("WGRAD_GENERIC", 1)
     elif path == "mfma_alt":  # the general MFMA kernel where a specialised one exists
         if kind != "convT" and cout != 1:
             pytest.skip("no specialised launch for this geometry")
-        monkeypatch.setenv("SPECENH_WGRAD_PERPHASE", "1")
-        monkeypatch.setenv("SPECENH_WGRAD_NO_CO1", "1")
+        kernel_variant("WGRAD_PERPHASE", 1)
+        kernel_variant("WGRAD_NO_CO1", 1)
     op = ae.ConvOp(kind, cin, cout, k, "relu", stride=2 if kind == "convT" else 1)
     OH, OW = op.out_hw(H, W)
     rng = np.random.default_rng(cin * 131 + cout * 7 + k + H)
@@ -64,9 +64,9 @@ def test_wgrad_matches_im2col(gpu_device, monkeypatch, dtype, kind, cin, cout, k
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("perphase", [False, True])
-def test_wgrad_mfma_is_bitwise_deterministic(gpu_device, monkeypatch, dtype, perphase):
+def test_wgrad_mfma_is_bitwise_deterministic(gpu_device, kernel_variant, dtype, perphase):
     if perphase:
-        monkeypatch.setenv("SPECENH_WGRAD_PERPHASE", "1")
+        kernel_variant("WGRAD_PERPHASE", 1)
     op = ae.ConvOp("convT", 32, 16, 5, "relu", stride=2)
     rng = np.random.default_rng(5)
     x = torch.tensor(rng.standard_normal((4, 32, 32, 32)), dtype=dtype, device=gpu_device)

@@ -19,8 +19,10 @@ save :257. Semantics kept from Keras:
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
+import threading
 import time
 
 import numpy as np
@@ -59,9 +61,26 @@ def _to_op(layer):
     raise NotImplementedError(f"layer type {type(layer).__name__}")
 
 
+_local = threading.local()
+
+
+@contextlib.contextmanager
+def rank_local():
+    """Within this context fit/evaluate ignore an initialised process group: each rank trains
+    its own model with no collective (the sweep's one-task-per-GPU mode, specenh.sweep)."""
+    prev = getattr(_local, "on", False)
+    _local.on = True
+    try:
+        yield
+    finally:
+        _local.on = prev
+
+
 def _dist():
     """torch.distributed when a process group is initialised (any world size: a 1-rank RCCL
-    group still runs the exchange), else None."""
+    group still runs the exchange) and not inside rank_local(), else None."""
+    if getattr(_local, "on", False):
+        return None
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():
         return dist

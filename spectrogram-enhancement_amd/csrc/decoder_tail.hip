@@ -338,6 +338,207 @@ __global__ __launch_bounds__(512, 4) void convt_conv_out_kernel(TailArgs a) {
 
 int resident_grid() { return 2 * device_cus(); }  // 2 workgroups per CU (LDS and registers)
 
+// ============================================================================ row sweep
+// tail_rows_kernel: the same two layers for 64-position-wide inputs (the model's 128-wide
+// spectrogram strips and C5 images), walked DOWN the image one input-position row at a
+// time instead of in 2-D tiles with halos. A workgroup owns a band of output rows of one
+// image; its 4 waves own 16 position columns each (64 = the input width: no column halo).
+//
+// Step q (input-position row q):
+//  a. Conv2DTranspose: for each of the 9 neighbourhood offsets (dy, dx) ONE B fragment
+//     (32 channels x 16 positions of input row q + dy, shifted by dx) feeds every phase
+//     that has the tap: 25 MFMAs from 9 LDS reads (the 2-D tile kernel: one read per
+//     MFMA). The A operands (16 output channels x 32 input channels per tap, 25 taps) stay
+//     in registers for the whole launch. Epilogue + bias, ReLU, round to T -> map rows
+//     2q, 2q+1 of a 6-row LDS ring. A wave writes exactly the 32 map columns its own
+//     Conv2D(1) blocks read, so the map needs no barrier.
+//  b. Conv2D(16 -> 1, 5x5) for output rows 2q-2, 2q-1 (map rows 2q-4 .. 2q+1), on MFMA:
+//     D[x'][(r, kx)] = sum_{p, dr, ci} map[2q-4+2p+dr][x'][ci] w[2p+dr-r][kx][ci], three
+//     MFMAs (map-row pairs p) per 16 columns x' give 2 output rows x 5 kx (10 of 16 N
+//     columns; the tile kernel's per-row form used 5), then out[y][x] = sum_kx D[x+kx-2]
+//     [(r, kx)] through an LDS scratch (double-buffered).
+//  c. input row q + 2 (loaded into registers two steps earlier) -> the 4-row LDS ring.
+//  d. one barrier (ring slot and scratch), then the diagonal sums, sigmoid, fp32 stores,
+//     and the load of input row q + 4.
+// Map rows outside the image are the Conv2D(1) zero padding: the ring starts zeroed and
+// steps past the last position row write zero rows.
+namespace rows {
+constexpr int QW = 64;               // input positions per row (the kernel's input width)
+constexpr int XST = 48;              // input pixel stride (elements): 96 B, conflict-free
+constexpr int XROW = (QW + 2) * XST;  // input ring row: pixels x = -1 .. 64
+constexpr int NXR = 4;               // input ring rows
+constexpr int MW = 2 * QW;           // 128 map / output columns
+constexpr int MROW = MW * CO;        // map ring row (elements): 32-B pixels, conflict-free
+constexpr int NMR = 6;               // map ring rows
+constexpr int SCW = MW + 8;          // scratch row (floats): 4 zero pads each side
+constexpr int SCR = 10;              // scratch rows (n = 5 r + kx)
+constexpr int LDS_X = NXR * XROW * 2;          // bytes
+constexpr int LDS_M = NMR * MROW * 2;
+constexpr int LDS_S = 2 * SCR * SCW * 4;
+constexpr int LDS_BYTES = LDS_X + LDS_M + LDS_S;  // 60,800 B: 2 workgroups per CU
+}  // namespace rows
+
+struct RowsArgs {
+  const void* x;    // [N][H][64][32]
+  const void* wt;   // convT forward GEMM weights [CO][KT][KT][CI]
+  const float* bt;  // [CO]
+  const void* wo;   // conv_out GEMM weights [KO][KO][CO]
+  const float* bo;  // [1]
+  float* out;       // [N][2H][128]
+  int N, H, R, nb;  // R: output rows per band (even), nb: bands per image
+};
+
+template <typename T>
+__global__ __launch_bounds__(256, 2) void tail_rows_kernel(RowsArgs a) {
+  using namespace rows;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  T* const xr = reinterpret_cast<T*>(lds_raw);                  // input ring
+  T* const mr = reinterpret_cast<T*>(lds_raw + LDS_X);          // map ring
+  float* const sc = reinterpret_cast<float*>(lds_raw + LDS_X + LDS_M);  // D scratch x2
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = lane & 15, kg = lane >> 4;
+  const int n = blockIdx.x / a.nb, band = blockIdx.x - n * a.nb;
+  const int H = a.H, H2 = 2 * H;
+  const int Y0 = band * a.R, Y1 = min(H2, Y0 + a.R);
+  const int qa = max(0, Y0 / 2 - 1), qe = Y1 / 2;  // steps qa .. qe inclusive
+  const T* __restrict__ X = reinterpret_cast<const T*>(a.x) + (long long)n * H * QW * CI;
+  float* __restrict__ O = a.out + (long long)n * H2 * MW;
+
+  // ---- resident operands: Conv2DTranspose taps (A: co = m, ci = 8 kg ..), bias; Conv2D(1)
+  // B fragments per map-row pair p: k = (dr = kg >> 1, ci = 8 (kg & 1) ..), n = 5 r + kx
+  uint4 wt[25];
+  {
+    const T* __restrict__ Wt = reinterpret_cast<const T*>(a.wt);
+    int u = 0;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          const int ky = ky_of(ph >> 1, dy), kx = ky_of(ph & 1, dx);
+          if (ky < 0 || ky >= KT || kx < 0 || kx >= KT) continue;
+          wt[u++] = *reinterpret_cast<const uint4*>(Wt + ((m * KT + ky) * KT + kx) * CI + 8 * kg);
+        }
+  }
+  float bias[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias[i] = a.bt[4 * kg + i];
+  const float bo = a.bo[0];
+  uint4 wo[3];
+  {
+    const T* __restrict__ Wo = reinterpret_cast<const T*>(a.wo);
+    const int r = m / 5, kx = m - 5 * (m / 5), dr = kg >> 1;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int ky = 2 * p + dr - r;
+      wo[p] = uint4{0u, 0u, 0u, 0u};
+      if (m < 10 && ky >= 0 && ky < KO)
+        wo[p] = *reinterpret_cast<const uint4*>(Wo + (ky * KO + kx) * CO + 8 * (kg & 1));
+    }
+  }
+
+  // ---- zero the rings and the scratch pads, then stage input rows qa-1 .. qa+1 ----
+  {
+    uint4* z = reinterpret_cast<uint4*>(lds_raw);
+    for (int e = tid; e < LDS_BYTES / 16; e += 256) z[e] = uint4{0u, 0u, 0u, 0u};
+  }
+  __syncthreads();
+  const int spix = tid >> 2, scg = tid & 3;  // this thread's 16 B of a staged row
+  auto gload = [&](int row) -> uint4 {
+    const int rr = min(max(row, 0), H - 1);
+    uint4 v = *reinterpret_cast<const uint4*>(X + ((long long)rr * QW + spix) * CI + 8 * scg);
+    if (row < 0 || row >= H) v = uint4{0u, 0u, 0u, 0u};
+    return v;
+  };
+  auto lstore = [&](int row, const uint4& v) {
+    *reinterpret_cast<uint4*>(xr + ((row + 8) % NXR) * XROW + (spix + 1) * XST + 8 * scg) = v;
+  };
+#pragma unroll
+  for (int d = -1; d <= 1; ++d) lstore(qa + d, gload(qa + d));
+  uint4 pa = gload(qa + 2), pb = gload(qa + 3);  // rows q+2 (even steps), q+3 (odd steps)
+  lds_barrier();
+
+  auto step = [&](const int q, uint4& pre) {
+    // ---- a. Conv2DTranspose of position row q -> map rows 2q, 2q + 1 ----
+    const int ms0 = ((2 * q) % NMR) * MROW, ms1 = ((2 * q + 1) % NMR) * MROW;
+    if (q < H) {
+      f32x4 acc[4];
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) acc[ph] = f32x4{0.f, 0.f, 0.f, 0.f};
+      int u0[4] = {0, 4, 10, 16};  // first tap register of each phase (4 / 6 / 6 / 9 taps)
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy) {
+        const T* src = xr + ((q + dy + 8) % NXR) * XROW + (16 * w + m + 1) * XST + 8 * kg;
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          const uint4 b = *reinterpret_cast<const uint4*>(src + dx * XST);
+#pragma unroll
+          for (int ph = 0; ph < 4; ++ph) {
+            const int ky = ky_of(ph >> 1, dy), kx = ky_of(ph & 1, dx);
+            if (ky < 0 || ky >= KT || kx < 0 || kx >= KT) continue;
+            acc[ph] = mfma<T>(wt[u0[ph]++], b, acc[ph]);
+          }
+        }
+      }
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) {
+        uint2 v;
+        v.x = pack2<T>(fmaxf(acc[ph][0] + bias[0], 0.f), fmaxf(acc[ph][1] + bias[1], 0.f));
+        v.y = pack2<T>(fmaxf(acc[ph][2] + bias[2], 0.f), fmaxf(acc[ph][3] + bias[3], 0.f));
+        *reinterpret_cast<uint2*>(mr + ((ph >> 1) ? ms1 : ms0) +
+                                  (2 * (16 * w + m) + (ph & 1)) * CO + 4 * kg) = v;
+      }
+    } else {  // below the image: the Conv2D(1) zero padding
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph)
+        *reinterpret_cast<uint2*>(mr + ((ph >> 1) ? ms1 : ms0) +
+                                  (2 * (16 * w + m) + (ph & 1)) * CO + 4 * kg) = uint2{0u, 0u};
+    }
+    // ---- b. Conv2D(1) MFMAs for output rows 2q - 2, 2q - 1 -> scratch (q & 1) ----
+    const bool emit = 2 * q - 2 >= Y0;
+    float* const scb = sc + (q & 1) * (SCR * SCW);
+    if (emit) {
+      const int dr = kg >> 1;
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk) {
+        const int xc = 32 * w + 16 * blk + m;  // this lane's map column (A row)
+        f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const int Y = 2 * q - 4 + 2 * p + dr;
+          const uint4 av = *reinterpret_cast<const uint4*>(
+              mr + ((Y + 2 * NMR) % NMR) * MROW + xc * CO + 8 * (kg & 1));
+          d = mfma<T>(av, wo[p], d);
+        }
+        if (m < SCR)  // D[x' = 32 w + 16 blk + 4 kg + i][n = m]
+          *reinterpret_cast<f32x4*>(scb + m * SCW + 4 + 32 * w + 16 * blk + 4 * kg) = d;
+      }
+    }
+    // ---- c. input row q + 2 into the ring ----
+    lstore(q + 2, pre);
+    lds_barrier();  // lgkmcnt only: the prefetch loads stay in flight across it
+    // ---- d. diagonal sums -> sigmoid -> out; next prefetch ----
+    if (emit) {
+      const int r = lane >> 5, x = 32 * w + (lane & 31);
+      float s = bo;
+#pragma unroll
+      for (int kx = 0; kx < KO; ++kx) s += scb[(5 * r + kx) * SCW + 4 + x + kx - 2];
+      O[(long long)(2 * q - 2 + r) * MW + x] = __builtin_amdgcn_rcpf(1.f + __expf(-s));
+    }
+    pre = gload(q + 4);
+  };
+
+  int q = qa;
+  for (; q + 1 <= qe; q += 2) {
+    step(q, pa);
+    step(q + 1, pb);
+  }
+  if (q <= qe) step(q, pa);
+}
+
 }  // namespace
 }  // namespace specenh
 
@@ -354,6 +555,30 @@ extern "C" int specenh_convt_conv_out(int dtype, const void* x, int N, int H, in
     return set_error(SPECENH_EUNSUPPORTED,
                      "fused decoder tail: Conv2DTranspose(16, 5) on 32 channels + Conv2D(1, 5)");
   if (N == 0) return SPECENH_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (W == rows::QW && variant(V_TAIL_TILES) == 0) {  // the row-sweep kernel
+    if (!x || !wt_gemm || !bt || !wo_gemm || !bo || !out) return set_error(SPECENH_EINVAL, "null pointer");
+    if ((long long)N * H * W * C >= (1ll << 31) || (long long)N * 4 * H * W >= (1ll << 31))
+      return set_error(SPECENH_EINVAL, "tensor too large (2^31 elements)");
+    RowsArgs r{};
+    r.x = x; r.wt = wt_gemm; r.bt = bt; r.wo = wo_gemm; r.bo = bo; r.out = out;
+    r.N = N; r.H = H;
+    // bands of output rows per image: one band (no recomputed halo rows) unless the batch
+    // leaves fewer than 2 workgroups per CU
+    int nb = 1;
+    while (nb < 8 && (long long)N * nb < 2ll * device_cus() && 2 * H / (2 * nb) >= 8) nb *= 2;
+    r.R = ((2 * H + nb - 1) / nb + 1) & ~1;
+    r.nb = (2 * H + r.R - 1) / r.R;
+    const long long grid = (long long)N * r.nb;
+    if (grid >= (1ll << 31)) return set_error(SPECENH_EINVAL, "too many workgroups");
+    if (dtype == SPECENH_DTYPE_F16)
+      SPECENH_LAUNCH(tail_rows_kernel<_Float16>, dim3((unsigned)grid), dim3(256), rows::LDS_BYTES, st, r);
+    else
+      SPECENH_LAUNCH(tail_rows_kernel<__bf16>, dim3((unsigned)grid), dim3(256), rows::LDS_BYTES, st, r);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("tail_rows: ") + hipGetErrorString(e));
+    return SPECENH_OK;
+  }
   if (!x || !wt_gemm || !bt || !wo_gemm || !bo || !out) return set_error(SPECENH_EINVAL, "null pointer");
   if ((long long)N * H * W * C >= (1ll << 31) || (long long)N * 4 * H * W >= (1ll << 31))
     return set_error(SPECENH_EINVAL, "tensor too large (2^31 elements)");
@@ -371,7 +596,6 @@ extern "C" int specenh_convt_conv_out(int dtype, const void* x, int N, int H, in
   a.tiles_x = (2 * W + TO - 1) / TO;
   const long long tiles = (long long)N * a.tiles_y * a.tiles_x;
   if (tiles >= (1ll << 31)) return set_error(SPECENH_EINVAL, "too many tiles");
-  hipStream_t st = (hipStream_t)stream;
   const unsigned grid = (unsigned)std::min<long long>(tiles, resident_grid());
   if (dtype == SPECENH_DTYPE_F16)
     SPECENH_LAUNCH(convt_conv_out_kernel<_Float16>, dim3(grid), dim3(512), 0, st, a);

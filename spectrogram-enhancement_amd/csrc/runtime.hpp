@@ -24,6 +24,7 @@ enum Variant : int {
   V_WGRAD_NO_CO1,     // CO = 1 weight gradient through the general MFMA kernel
   V_WGRAD_PERPHASE,   // Conv2DTranspose weight gradient one phase per workgroup
   V_SVD_GRAM_TILES,   // Gram matrix through the triangle-tile kernel instead of LDS rows
+  V_TAIL_TILES,       // fused decoder tail: 2-D tile kernel instead of the row sweep
   V_COUNT
 };
 

@@ -109,14 +109,16 @@ def test_c4_fit_tracks_oracle_val_loss(gpu_device, c4_data, policy):
 
 def test_device_c4_pairs_match_host_pipeline(gpu_device):
     """The bench's device C4 set: inputs and targets are specgr of the device shots with and
-    without noise (same chirps), in [0, 1] with the per-spectrogram min 0 and max 1."""
+    without noise (same chirps), in [0, 1] (specgr normalises before dropping the Nyquist
+    row, so a shot's extremes may sit in the dropped row)."""
     from specenh import pipeline_data
     from specenh.synthetic import C4_LENGTH, C4_SPEC, c4_pairs_torch, plasma_chirps_torch
     x, y = c4_pairs_torch(64, seed=77, device=gpu_device, chunk=32)
     assert x.shape == y.shape == (64, 128, 128, 1)
     for t in (x, y):
         flat = t.view(64, -1)
-        assert torch.all(flat.min(1).values == 0) and torch.all(flat.max(1).values == 1)
+        assert torch.all(flat.min(1).values >= 0) and torch.all(flat.max(1).values <= 1)
+        assert flat.max(1).values.median() > 0.9
     # chunk 0 reproduces from the same seed
     sh = plasma_chirps_torch(32, C4_LENGTH, seed=77, sigma=0.0, device=gpu_device)
     S = pipeline_data.specgr_batch(sh, C4_SPEC)

@@ -56,3 +56,39 @@ def test_fused_tail_matches_two_launches_and_oracle(gpu_device, dtype, hw, monke
         ref = ora.forward(spec, params, torch.tensor(x, dtype=torch.float64)).numpy()
     err = checks.out_rel(fused.cpu().numpy(), ref)
     assert err <= checks.TOL[dtype]["out_rel"], err
+
+
+@pytest.mark.parametrize("dtype", ["float16", "mixed_bfloat16"])
+@pytest.mark.parametrize("hw,n", [((64, 64), 5), ((64, 64), 600), ((8, 64), 3), ((13, 64), 4),
+                                  ((128, 64), 2)])
+def test_row_sweep_tail_matches_tile_kernel(gpu_device, dtype, hw, n, kernel_variant):
+    """tail_rows_kernel (64-position-wide inputs: the model's 128-wide outputs) vs the 2-D
+    tile kernel (TAIL_TILES=1) and the fp64 oracle, with the output buffer NaN-poisoned
+    before each launch (an unwritten pixel fails). Batches of 5 / 3 / 4 / 2 images run in
+    8 / 2 / ... bands per image (recomputed halo position rows at band edges), 600 images
+    in one band; 8 and 13 position rows exercise short and odd heights, 128 rows the
+    reference's 256 x 128 input."""
+    eng, ops_, ws = _tail_model(dtype, hw, seed=hw[0] * 11 + n)
+    x = np.random.default_rng(n).uniform(0, 1, (n,) + hw + (1,)).astype(np.float32)
+    xd = eng.to_compute(torch.from_numpy(x))
+    outs = []
+    for tiles in (0, 1):
+        kernel_variant("TAIL_TILES", tiles)
+        eng.forward(xd)  # allocate, then poison the output and run again
+        eng._buffers(n, False)["h"][len(ops_)].fill_(float("nan"))
+        outs.append(eng.forward(xd).clone())
+    torch.cuda.synchronize()
+    rows_out, tile_out = outs
+    assert not torch.isnan(rows_out).any()
+    d = (rows_out - tile_out).abs().max().item()
+    assert d <= 2e-3, d
+    if n <= 5:
+        spec = [("conv", 1, 32, 3, "relu"), ("convT", 32, 16, 5, "relu"),
+                ("conv", 16, 1, 5, "sigmoid")]
+        it = iter(ws)
+        params = [{"W": torch.tensor(next(it), dtype=torch.float64),
+                   "b": torch.tensor(next(it), dtype=torch.float64)} for _ in spec]
+        with torch.no_grad():
+            ref = ora.forward(spec, params, torch.tensor(x, dtype=torch.float64)).numpy()
+        err = checks.out_rel(rows_out.cpu().numpy(), ref)
+        assert err <= checks.TOL[dtype]["out_rel"], err

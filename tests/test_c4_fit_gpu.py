@@ -123,8 +123,9 @@ def test_device_c4_pairs_match_host_pipeline(gpu_device):
     sh = plasma_chirps_torch(32, C4_LENGTH, seed=77, sigma=0.0, device=gpu_device)
     S = pipeline_data.specgr_batch(sh, C4_SPEC)
     assert torch.equal(S, y[:32, :, :, 0])
-    # noisy and clean differ, but share the chirps: their spectrograms correlate
+    # noisy and clean differ, but share the chirps: their spectrograms correlate (the host
+    # pipeline's pairs: mean |x - y| 0.545, correlation 0.474 on 16 shots)
     d = (x - y).abs().mean().item()
-    assert 0.01 < d < 0.5
+    assert 0.3 < d < 0.8
     c = torch.corrcoef(torch.stack([x.flatten(), y.flatten()]))[0, 1].item()
-    assert c > 0.3
+    assert 0.3 < c < 0.7

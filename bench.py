@@ -31,8 +31,10 @@ Rank 0 prints ONE JSON line with, besides the contract fields:
                 A7 MACs x 2) / the unit's peak (MFMA 2.5 PFLOP/s dense fp16 for every layer of
                 the fused forward; an unfused 1-output-channel conv would run on the VALU,
                 v_dot2 314.6 TFLOP/s). traffic = measured HBM
-                bytes of that launch from profiles/pmc_traffic.json (rocprofv3 --pmc passes of
-                tools/pmc_traffic.sh at the same shapes); stages.ae_layers has every layer.
+                bytes of that launch from profiles/pmc_r03.json (rocprofv3 --pmc passes of
+                tools/pmc_refresh.sh at the same shapes, keyed by the exact kernel symbol: null
+                with a warning when the timed launch ran a different kernel); stages.ae_layers
+                has every layer.
   stages        per-stage ms of one slice (stages.shots_per_launch shots: the launch shape
                 of the timed step, which splits the batch over --streams HIP streams;
                 default 2), and the C2 STFT-only configuration (4096 x
@@ -830,12 +832,15 @@ def main():
                    "parallelism": f"shot-sharded x{world}", "streams_per_gpu": NS},
         "roofline": {k: dom[k] for k in ("bound", "achieved", "peak", "unit", "frac",
                                            "traffic")} |
-                    {"kernel": f"{dom['layer']} launch of the autoencoder forward "
-                               f"({dom['traffic_kernel'] or 'see profiles/'})",
+                    {"layer": f"{dom['layer']} launch of the autoencoder forward",
+                     "kernel": dom["kernel"],
                      "kernel_ms": dom["kernel_ms"], "alg_bytes_per_launch":
                      dom["alg_bytes_per_launch"], "flops_per_launch": dom["flops_per_launch"],
-                     "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 "
-                                       "+ WRITE_SIZE, separate passes, same shapes)"},
+                     "traffic_ratio": dom["traffic_ratio"],
+                     "traffic_source": os.path.relpath(PMC_FILE, REPO) + " (tools/pmc_refresh.sh: "
+                                       "rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, separate "
+                                       "passes, the same kernel symbol at the same launch shape)"}
+                    | ({"traffic_note": dom["traffic_note"]} if "traffic_note" in dom else {}),
         "cpu_baseline": cpu,
         "psnr_db": accuracy["psnr_db"] if accuracy else None,
         "accuracy": accuracy,

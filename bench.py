@@ -120,9 +120,15 @@ VALU_DOT2_PEAK_TFLOPS = 314.6         # v_dot2_f32_f16: 4 FLOP/lane/instr, 128 l
 LAYER_NAMES = ["conv1+pool", "conv2+pool", "conv3+pool", "convT1", "convT2", "convT3",
                "conv_out"]
 LAYER_NAMES_TAIL = LAYER_NAMES[:5] + ["convT3+conv_out"]
+LAYER_NAMES_DEC3 = LAYER_NAMES[:4] + ["convT2+convT3+conv_out"]
 
 
-def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4, tail=False):
+def layer_names(eng):
+    """Names of the forward's launches (the engine's fusions: decoder3 / tail)."""
+    return LAYER_NAMES_DEC3 if eng.dec3 else (LAYER_NAMES_TAIL if eng.tail else LAYER_NAMES)
+
+
+def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4, tail=False, dec3=False):
     """Per launch of the fused forward (conv+pool fused; with ``tail`` the last
     Conv2DTranspose + Conv2D(1) are one launch, csrc/decoder_tail.hip): useful FLOPs and
     algorithmic HBM bytes per sample (activations read once + written once), the weights
@@ -146,10 +152,17 @@ def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4, tail=False):
                     "unit": unit})
         hh, ww = sh, sw
         i += 2 if pool else 1
-    if tail:  # convT3 + conv_out, both on MFMA: the 16-channel map is not HBM traffic
+    if tail or dec3:  # convT3 + conv_out, both on MFMA: the 16-channel map is not HBM traffic
         a, b = res[-2], res[-1]
         res = res[:-2] + [{"flops": a["flops"] + b["flops"], "mfma_flops": a["flops"] + b["flops"],
                            "bytes": (h // 2) * (w // 2) * AE_FILTERS[1] * act_bytes +
+                           h * w * out_bytes,
+                           "weight_bytes": a["weight_bytes"] + b["weight_bytes"],
+                           "unit": "mfma"}]
+    if dec3:  # + convT2 in front: its 32-channel map is not HBM traffic either
+        a, b = res[-2], res[-1]
+        res = res[:-2] + [{"flops": a["flops"] + b["flops"], "mfma_flops": a["flops"] + b["flops"],
+                           "bytes": (h // 4) * (w // 4) * AE_FILTERS[2] * act_bytes +
                            h * w * out_bytes,
                            "weight_bytes": a["weight_bytes"] + b["weight_bytes"],
                            "unit": "mfma"}]
@@ -650,8 +663,9 @@ def main():
     layer_ms = np.median(conv_ms, axis=0)
     pmc = load_pmc()
     layers = []
-    names = LAYER_NAMES_TAIL if eng.tail else LAYER_NAMES
-    for name, c, ms, sym in zip(names, ae_layer_costs(tail=eng.tail), layer_ms, kernels):
+    names = layer_names(eng)
+    for name, c, ms, sym in zip(names, ae_layer_costs(tail=eng.tail, dec3=eng.dec3), layer_ms,
+                                kernels):
         # compute floor: MFMA FLOPs at the dense fp16 MFMA peak + VALU FLOPs at the dot2 peak
         t_c = c["mfma_flops"] * Hs / (MFMA_PEAK_TFLOPS * 1e12) + \
             (c["flops"] - c["mfma_flops"]) * Hs / (VALU_DOT2_PEAK_TFLOPS * 1e12)

@@ -263,6 +263,21 @@ int specenh_convt_conv_out(int dtype, const void* x, int N, int H, int W, int C,
                            const void* wo_gemm, const float* bo, int ko, float* out,
                            void* stream);
 
+/* The decoder's last THREE layers in one launch (VAE/manual_scan_3layers.py:196-199, the
+ * inference path of predict :239):
+ *   x [N][H][W][C] -> Conv2DTranspose(CO1, k, strides=2, relu, "same")
+ *                  -> Conv2DTranspose(CO2, k, strides=2, relu, "same")
+ *                  -> Conv2D(1, k, sigmoid, "same") -> out fp32 [N][4H][4W]
+ * w1_gemm / b1, wt_gemm / bt, wo_gemm / bo: the three layers' specenh_conv2d weights (GEMM
+ * layout, dtype) and fp32 biases. Both intermediate maps stay in LDS, each rounded to dtype
+ * after its ReLU exactly as the unfused path stores it. dtype BF16 / F16; W = 32, C = 64,
+ * CO1 = 32, CO2 = 16, k = 5 (the reference model on 128 x 128 inputs), otherwise
+ * SPECENH_EUNSUPPORTED. */
+int specenh_decoder3(int dtype, const void* x, int N, int H, int W, int C,
+                     const void* w1_gemm, const float* b1, int CO1, const void* wt_gemm,
+                     const float* bt, int CO2, const void* wo_gemm, const float* bo, int k,
+                     float* out, void* stream);
+
 /* ---------------------------------------------------------------- label filters
  * The image-filter helpers of spec_denoising/pipeline_data.py:38-61 (the training-label
  * chain) on a batch of spectrograms, each a rows x cols row-major block at

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 #include <cstdlib>
 #include <cstdint>
 #include <string>
@@ -378,6 +379,12 @@ constexpr int LDS_S = 2 * SCR * SCW * 4;
 constexpr int LDS_BYTES = LDS_X + LDS_M + LDS_S;  // 60,800 B: 2 workgroups per CU
 }  // namespace rows
 
+// map pixel p, 4-channel group g (8 B): the two 16-B halves of a pixel swap when bit 2 of p
+// is set. The Conv2DTranspose epilogue writes 8 B per lane at 64-B pixel steps (plain
+// layout: 8-way bank conflicts on ds_write_b64, 4-way with the swap) and the Conv2D(1) A
+// reads (16 B = groups 2h, 2h + 1 of consecutive pixels) stay conflict-free.
+__device__ __forceinline__ int map_off(int p, int g) { return p * CO + 4 * (g ^ (2 * ((p >> 2) & 1))); }
+
 struct RowsArgs {
   const void* x;    // [N][H][64][32]
   const void* wt;   // convT forward GEMM weights [CO][KT][KT][CI]
@@ -386,6 +393,117 @@ struct RowsArgs {
   const float* bo;  // [1]
   float* out;       // [N][2H][128]
   int N, H, R, nb;  // R: output rows per band (even), nb: bands per image
+};
+
+// The last two layers' per-wave state and steps, shared by tail_rows_kernel and
+// decoder3_kernel: lane (m = lane & 15, kg = lane >> 4) of wave w (0..3) owns input
+// positions 16 w + m of a position row, i.e. map columns 32 w .. 32 w + 31.
+template <typename T>
+struct TailWave {
+  uint4 wt[25];  // Conv2DTranspose taps (A: co = m, ci = 8 kg ..), phase-major, (dy, dx) order
+  float bias[4];
+  float bo;
+  uint4 wo[3];   // Conv2D(1) B fragments per map-row pair p: k = (dr, ci), n = 5 r + kx
+
+  __device__ __forceinline__ void load(const void* wt_gemm, const float* bt, const void* wo_gemm,
+                                       const float* b_o, int m, int kg) {
+    const T* __restrict__ Wt = reinterpret_cast<const T*>(wt_gemm);
+    int u = 0;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          const int ky = ky_of(ph >> 1, dy), kx = ky_of(ph & 1, dx);
+          if (ky < 0 || ky >= KT || kx < 0 || kx >= KT) continue;
+          wt[u++] = *reinterpret_cast<const uint4*>(Wt + ((m * KT + ky) * KT + kx) * CI + 8 * kg);
+        }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[i] = bt[4 * kg + i];
+    bo = b_o[0];
+    const T* __restrict__ Wo = reinterpret_cast<const T*>(wo_gemm);
+    const int r = m / 5, kx = m - 5 * (m / 5), dr = kg >> 1;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int ky = 2 * p + dr - r;
+      wo[p] = uint4{0u, 0u, 0u, 0u};
+      if (m < 10 && ky >= 0 && ky < KO)
+        wo[p] = *reinterpret_cast<const uint4*>(Wo + (ky * KO + kx) * CO + 8 * (kg & 1));
+    }
+  }
+
+  // Conv2DTranspose of one position row: src[dy + 1] points at this lane's input pixel
+  // (column 16 w + m, channel group kg) of input rows q - 1, q, q + 1; pixel stride PS;
+  // soff(dx) gives the element offset of the dx-shifted pixel. -> map rows 2q, 2q + 1.
+  template <typename Off>
+  __device__ __forceinline__ void convt(const T* const (&src)[3], Off soff, T* mrow0, T* mrow1,
+                                        int w, int m, int kg) const {
+    f32x4 acc[4];
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) acc[ph] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int u0[4] = {0, 4, 10, 16};  // first tap register of each phase (4 / 6 / 6 / 9 taps)
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        const uint4 b = *reinterpret_cast<const uint4*>(src[dy + 1] + soff(dx));
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) {
+          const int ky = ky_of(ph >> 1, dy), kx = ky_of(ph & 1, dx);
+          if (ky < 0 || ky >= KT || kx < 0 || kx >= KT) continue;
+          acc[ph] = mfma<T>(wt[u0[ph]++], b, acc[ph]);
+        }
+      }
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      uint2 v;
+      v.x = pack2<T>(fmaxf(acc[ph][0] + bias[0], 0.f), fmaxf(acc[ph][1] + bias[1], 0.f));
+      v.y = pack2<T>(fmaxf(acc[ph][2] + bias[2], 0.f), fmaxf(acc[ph][3] + bias[3], 0.f));
+      const int pix = 2 * (16 * w + m) + (ph & 1);
+      *reinterpret_cast<uint2*>(((ph >> 1) ? mrow1 : mrow0) + map_off(pix, kg)) = v;
+    }
+  }
+
+  __device__ __forceinline__ static void zero_rows(T* mrow0, T* mrow1, int w, int m, int kg) {
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph)
+      *reinterpret_cast<uint2*>(((ph >> 1) ? mrow1 : mrow0) +
+                                map_off(2 * (16 * w + m) + (ph & 1), kg)) = uint2{0u, 0u};
+  }
+
+  // Conv2D(1) MFMAs for output rows 2q - 2, 2q - 1 (map rows 2q - 4 .. 2q + 1 of the ring
+  // mr, NMR rows) -> D into the scratch scb
+  __device__ __forceinline__ void conv_out_d(const T* mr, int q, int w, int m, int kg,
+                                             float* scb) const {
+    using namespace rows;
+    const int dr = kg >> 1;
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+      const int xc = 32 * w + 16 * blk + m;  // this lane's map column (A row)
+      f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int Y = 2 * q - 4 + 2 * p + dr;
+        const uint4 av = *reinterpret_cast<const uint4*>(
+            mr + ((Y + 2 * NMR) % NMR) * MROW + map_off(xc, 2 * (kg & 1)));
+        d = mfma<T>(av, wo[p], d);
+      }
+      if (m < SCR)  // D[x' = 32 w + 16 blk + 4 kg + i][n = m]
+        *reinterpret_cast<f32x4*>(scb + m * SCW + 4 + 32 * w + 16 * blk + 4 * kg) = d;
+    }
+  }
+
+  // diagonal sums of the scratch -> sigmoid -> output rows y0, y0 + 1 (O: the image's rows)
+  __device__ __forceinline__ void conv_out_sums(const float* scb, float* __restrict__ O, int y0,
+                                                int w, int lane) const {
+    using namespace rows;
+    const int r = lane >> 5, x = 32 * w + (lane & 31);
+    float s = bo;
+#pragma unroll
+    for (int kx = 0; kx < KO; ++kx) s += scb[(5 * r + kx) * SCW + 4 + x + kx - 2];
+    O[(long long)(y0 + r) * MW + x] = __builtin_amdgcn_rcpf(1.f + __expf(-s));
+  }
 };
 
 template <typename T>
@@ -406,39 +524,8 @@ __global__ __launch_bounds__(256, 2) void tail_rows_kernel(RowsArgs a) {
   const T* __restrict__ X = reinterpret_cast<const T*>(a.x) + (long long)n * H * QW * CI;
   float* __restrict__ O = a.out + (long long)n * H2 * MW;
 
-  // ---- resident operands: Conv2DTranspose taps (A: co = m, ci = 8 kg ..), bias; Conv2D(1)
-  // B fragments per map-row pair p: k = (dr = kg >> 1, ci = 8 (kg & 1) ..), n = 5 r + kx
-  uint4 wt[25];
-  {
-    const T* __restrict__ Wt = reinterpret_cast<const T*>(a.wt);
-    int u = 0;
-#pragma unroll
-    for (int ph = 0; ph < 4; ++ph)
-#pragma unroll
-      for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-        for (int dx = -1; dx <= 1; ++dx) {
-          const int ky = ky_of(ph >> 1, dy), kx = ky_of(ph & 1, dx);
-          if (ky < 0 || ky >= KT || kx < 0 || kx >= KT) continue;
-          wt[u++] = *reinterpret_cast<const uint4*>(Wt + ((m * KT + ky) * KT + kx) * CI + 8 * kg);
-        }
-  }
-  float bias[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) bias[i] = a.bt[4 * kg + i];
-  const float bo = a.bo[0];
-  uint4 wo[3];
-  {
-    const T* __restrict__ Wo = reinterpret_cast<const T*>(a.wo);
-    const int r = m / 5, kx = m - 5 * (m / 5), dr = kg >> 1;
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      const int ky = 2 * p + dr - r;
-      wo[p] = uint4{0u, 0u, 0u, 0u};
-      if (m < 10 && ky >= 0 && ky < KO)
-        wo[p] = *reinterpret_cast<const uint4*>(Wo + (ky * KO + kx) * CO + 8 * (kg & 1));
-    }
-  }
+  TailWave<T> tw;
+  tw.load(a.wt, a.bt, a.wo, a.bo, m, kg);
 
   // ---- zero the rings and the scratch pads, then stage input rows qa-1 .. qa+1 ----
   {
@@ -460,74 +547,30 @@ __global__ __launch_bounds__(256, 2) void tail_rows_kernel(RowsArgs a) {
   for (int d = -1; d <= 1; ++d) lstore(qa + d, gload(qa + d));
   uint4 pa = gload(qa + 2), pb = gload(qa + 3);  // rows q+2 (even steps), q+3 (odd steps)
   lds_barrier();
+  auto soff = [](int dx) { return dx * XST; };
 
   auto step = [&](const int q, uint4& pre) {
     // ---- a. Conv2DTranspose of position row q -> map rows 2q, 2q + 1 ----
-    const int ms0 = ((2 * q) % NMR) * MROW, ms1 = ((2 * q + 1) % NMR) * MROW;
+    T* const m0 = mr + ((2 * q) % NMR) * MROW;
+    T* const m1 = mr + ((2 * q + 1) % NMR) * MROW;
     if (q < H) {
-      f32x4 acc[4];
+      const T* src[3];
 #pragma unroll
-      for (int ph = 0; ph < 4; ++ph) acc[ph] = f32x4{0.f, 0.f, 0.f, 0.f};
-      int u0[4] = {0, 4, 10, 16};  // first tap register of each phase (4 / 6 / 6 / 9 taps)
-#pragma unroll
-      for (int dy = -1; dy <= 1; ++dy) {
-        const T* src = xr + ((q + dy + 8) % NXR) * XROW + (16 * w + m + 1) * XST + 8 * kg;
-#pragma unroll
-        for (int dx = -1; dx <= 1; ++dx) {
-          const uint4 b = *reinterpret_cast<const uint4*>(src + dx * XST);
-#pragma unroll
-          for (int ph = 0; ph < 4; ++ph) {
-            const int ky = ky_of(ph >> 1, dy), kx = ky_of(ph & 1, dx);
-            if (ky < 0 || ky >= KT || kx < 0 || kx >= KT) continue;
-            acc[ph] = mfma<T>(wt[u0[ph]++], b, acc[ph]);
-          }
-        }
-      }
-#pragma unroll
-      for (int ph = 0; ph < 4; ++ph) {
-        uint2 v;
-        v.x = pack2<T>(fmaxf(acc[ph][0] + bias[0], 0.f), fmaxf(acc[ph][1] + bias[1], 0.f));
-        v.y = pack2<T>(fmaxf(acc[ph][2] + bias[2], 0.f), fmaxf(acc[ph][3] + bias[3], 0.f));
-        *reinterpret_cast<uint2*>(mr + ((ph >> 1) ? ms1 : ms0) +
-                                  (2 * (16 * w + m) + (ph & 1)) * CO + 4 * kg) = v;
-      }
+      for (int dy = -1; dy <= 1; ++dy)
+        src[dy + 1] = xr + ((q + dy + 8) % NXR) * XROW + (16 * w + m + 1) * XST + 8 * kg;
+      tw.convt(src, soff, m0, m1, w, m, kg);
     } else {  // below the image: the Conv2D(1) zero padding
-#pragma unroll
-      for (int ph = 0; ph < 4; ++ph)
-        *reinterpret_cast<uint2*>(mr + ((ph >> 1) ? ms1 : ms0) +
-                                  (2 * (16 * w + m) + (ph & 1)) * CO + 4 * kg) = uint2{0u, 0u};
+      TailWave<T>::zero_rows(m0, m1, w, m, kg);
     }
     // ---- b. Conv2D(1) MFMAs for output rows 2q - 2, 2q - 1 -> scratch (q & 1) ----
     const bool emit = 2 * q - 2 >= Y0;
     float* const scb = sc + (q & 1) * (SCR * SCW);
-    if (emit) {
-      const int dr = kg >> 1;
-#pragma unroll
-      for (int blk = 0; blk < 2; ++blk) {
-        const int xc = 32 * w + 16 * blk + m;  // this lane's map column (A row)
-        f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          const int Y = 2 * q - 4 + 2 * p + dr;
-          const uint4 av = *reinterpret_cast<const uint4*>(
-              mr + ((Y + 2 * NMR) % NMR) * MROW + xc * CO + 8 * (kg & 1));
-          d = mfma<T>(av, wo[p], d);
-        }
-        if (m < SCR)  // D[x' = 32 w + 16 blk + 4 kg + i][n = m]
-          *reinterpret_cast<f32x4*>(scb + m * SCW + 4 + 32 * w + 16 * blk + 4 * kg) = d;
-      }
-    }
+    if (emit) tw.conv_out_d(mr, q, w, m, kg, scb);
     // ---- c. input row q + 2 into the ring ----
     lstore(q + 2, pre);
     lds_barrier();  // lgkmcnt only: the prefetch loads stay in flight across it
     // ---- d. diagonal sums -> sigmoid -> out; next prefetch ----
-    if (emit) {
-      const int r = lane >> 5, x = 32 * w + (lane & 31);
-      float s = bo;
-#pragma unroll
-      for (int kx = 0; kx < KO; ++kx) s += scb[(5 * r + kx) * SCW + 4 + x + kx - 2];
-      O[(long long)(2 * q - 2 + r) * MW + x] = __builtin_amdgcn_rcpf(1.f + __expf(-s));
-    }
+    if (emit) tw.conv_out_sums(scb, O, 2 * q - 2, w, lane);
     pre = gload(q + 4);
   };
 
@@ -537,6 +580,220 @@ __global__ __launch_bounds__(256, 2) void tail_rows_kernel(RowsArgs a) {
     step(q + 1, pb);
   }
   if (q <= qe) step(q, pa);
+}
+
+// ============================================================================ decoder3
+// decoder3_kernel: the model's last THREE layers in one launch, for 32-position-wide inputs
+// (the C5 images: 32 x 32 x 64 -> 128 x 128):
+//   Conv2DTranspose(32, 5, s2, relu) -> Conv2DTranspose(16, 5, s2, relu) -> Conv2D(1, 5,
+//   sigmoid)  (VAE/manual_scan_3layers.py:196-199)
+// The 64 x 64 x 32 map between the two Conv2DTransposes — 256 KB per image, the largest
+// tensor of the unfused decoder after the tail's own map — is produced and consumed in LDS
+// rows and never reaches HBM. One workgroup per image, 8 waves in two roles that share
+// nothing but LDS rings and one barrier per macro step:
+//  * producer waves 0-3 (one per (16-position window, 16-channel block) of the 32 x 32
+//    channel output): Conv2DTranspose(64 -> 32) one input row s per macro step, every
+//    neighbourhood offset's B fragment (2 K-steps) feeding all phases, 50 tap fragments
+//    resident in registers -> rows 2s, 2s + 1 of the tail's input ring (64 positions x 32
+//    channels, 64-byte pixels with a 16-byte group swizzle: conflict-free tail reads);
+//  * consumer waves 4-7: two steps of the row-sweep tail (TailWave) per macro step, two
+//    rows behind the producer.
+// Waves w and w + 4 share a SIMD (MI355X_MICROARCH.md, two waves per SIMD): each SIMD pairs
+// one producer and one consumer.
+namespace d3 {
+constexpr int CI1 = 64, CO1 = 32;     // the first Conv2DTranspose
+constexpr int W1 = 32;                // its input positions per row
+constexpr int X1ST = CI1;             // its input pixels: dense 128 B, 16-B groups swizzled
+constexpr int X1ROW = (W1 + 2) * X1ST;
+constexpr int NX1 = 4;
+constexpr int X2ST = 32;              // tail input pixel stride (elements): dense 64 B, swizzled
+constexpr int X2ROW = (2 * W1 + 2) * X2ST;
+constexpr int NX2 = 6;
+constexpr int LDS_X1 = NX1 * X1ROW * 2;
+constexpr int LDS_X2 = NX2 * X2ROW * 2;
+constexpr int LDS_M = rows::NMR * rows::MROW * 2;
+constexpr int LDS_S = 4 * rows::SCR * rows::SCW * 4;
+constexpr int LDS_BYTES = LDS_X1 + LDS_X2 + LDS_M + LDS_S;  // 89,088 B: one workgroup per CU
+}  // namespace d3
+
+// first Conv2DTranspose input pixel ps (x = ps - 1), 16-byte group g of its 8: group g sits
+// at g ^ (ps & 7), so the producers' fragment reads (16 consecutive pixels, one group) are
+// conflict-free; the rows arrive by LDS-DMA (lane-linear), the swizzle applied on the source
+__device__ __forceinline__ int x1_off(int ps, int g) { return ps * d3::X1ST + 8 * (g ^ (ps & 7)); }
+
+// tail input pixel p (-1 .. 64 stored at p + 1), 16-byte group g: groups swizzled by bits 1-2
+// of the stored pixel (producer 8-byte writes at 2-pixel steps 4-way instead of 8-way;
+// consumer 16-byte reads of consecutive pixels conflict-free)
+__device__ __forceinline__ int x2_off(int ps, int g) { return ps * d3::X2ST + 8 * (g ^ ((ps >> 1) & 3)); }
+
+// one 16-byte LDS-DMA per lane: LDS destination = wave-uniform dst + 16 x lane
+__device__ __forceinline__ void lds_dma16(const void* src, void* dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
+struct D3Args {
+  const void* x;     // [N][H][32][64]
+  const void* w1;    // first Conv2DTranspose forward GEMM weights [32][5][5][64]
+  const float* b1;   // [32]
+  const void* wt;    // second [16][5][5][32]
+  const float* bt;   // [16]
+  const void* wo;    // Conv2D(1) [5][5][16]
+  const float* bo;   // [1]
+  float* out;        // [N][4H][128]
+  int N, H;
+};
+
+template <typename T>
+__global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
+  using namespace d3;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  T* const x1r = reinterpret_cast<T*>(lds_raw);
+  T* const x2r = reinterpret_cast<T*>(lds_raw + LDS_X1);
+  T* const mr = reinterpret_cast<T*>(lds_raw + LDS_X1 + LDS_X2);
+  float* const sc = reinterpret_cast<float*>(lds_raw + LDS_X1 + LDS_X2 + LDS_M);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = lane & 15, kg = lane >> 4;
+  const int n = blockIdx.x;
+  const int H1 = a.H, H2 = 2 * H1, H3 = 4 * H1;
+  {
+    uint4* z = reinterpret_cast<uint4*>(lds_raw);
+    for (int e = tid; e < LDS_BYTES / 16; e += 512) z[e] = uint4{0u, 0u, 0u, 0u};
+  }
+  __syncthreads();
+
+  if (wv < 4) {
+    // ======================= producer: Conv2DTranspose(64 -> 32), input rows s - 1 .. s + 1
+    const int wx = wv & 1, nb = wv >> 1;
+    uint4 w1[50];  // [phase taps][k-step]
+    {
+      const T* __restrict__ Wg = reinterpret_cast<const T*>(a.w1);
+      int u = 0;
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+          for (int dx = -1; dx <= 1; ++dx) {
+            const int ky = ky_of(ph >> 1, dy), kx = ky_of(ph & 1, dx);
+            if (ky < 0 || ky >= KT || kx < 0 || kx >= KT) continue;
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh)
+              w1[u++] = *reinterpret_cast<const uint4*>(
+                  Wg + (((16 * nb + m) * KT + ky) * KT + kx) * CI1 + 32 * kh + 8 * kg);
+          }
+    }
+    float bias[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[i] = a.b1[16 * nb + 4 * kg + i];
+    const T* __restrict__ X = reinterpret_cast<const T*>(a.x) + (long long)n * H1 * W1 * CI1;
+    // input row r -> ring slot by LDS-DMA: wave wv moves stored pixels 1 + 8 wv .. 8 + 8 wv
+    // (1 KB, lane-linear); lane i takes stored group i & 7, i.e. source group (i & 7) ^ (ps & 7)
+    const int dps = 1 + 8 * wv + (lane >> 3);
+    const int dsrc = (dps - 1) * CI1 + 8 * ((lane & 7) ^ (dps & 7));
+    auto stage = [&](int row) {
+      unsigned char* dst = lds_raw + (((row + 8) % NX1) * X1ROW + (1 + 8 * wv) * X1ST) * 2;
+      if (row >= 0 && row < H1) {
+        lds_dma16(X + (long long)row * W1 * CI1 + dsrc, dst);
+      } else {  // outside the image: the zero padding rows
+        *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
+      }
+    };
+    int soffv[3];  // this lane's B-fragment offset in a ring row: pixel 16 wx + m + dx, group kg
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) soffv[dx + 1] = x1_off(16 * wx + m + dx + 1, kg);
+#pragma unroll
+    for (int d = -1; d <= 1; ++d) stage(d);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();  // (macro step -1: the consumers' matching barrier is below)
+    auto pstep = [&](const int s) {
+      stage(s + 2);  // lands while this row's MFMAs run; waited for before the barrier
+      T* const r0 = x2r + ((2 * s) % NX2) * X2ROW;
+      T* const r1 = x2r + ((2 * s + 1) % NX2) * X2ROW;
+      if (s < H1) {
+        f32x4 acc[4];
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) acc[ph] = f32x4{0.f, 0.f, 0.f, 0.f};
+        int u0[4] = {0, 8, 20, 32};
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy) {
+          const T* src = x1r + ((s + dy + 8) % NX1) * X1ROW;
+#pragma unroll
+          for (int dx = -1; dx <= 1; ++dx) {
+            // K-step kh reads group kg + 4 kh: the swizzle XOR only touches the low bits
+            // identically, so the second group is the first ^ 4 (= + or - 32 elements)
+            const int o0 = soffv[dx + 1];
+            const int o1 = o0 ^ 32;  // group bit 2 flips (the 8-group index is 8 elements wide)
+            const uint4 b0 = *reinterpret_cast<const uint4*>(src + o0);
+            const uint4 b1 = *reinterpret_cast<const uint4*>(src + o1);
+#pragma unroll
+            for (int ph = 0; ph < 4; ++ph) {
+              const int ky = ky_of(ph >> 1, dy), kx = ky_of(ph & 1, dx);
+              if (ky < 0 || ky >= KT || kx < 0 || kx >= KT) continue;
+              acc[ph] = mfma<T>(w1[u0[ph]], b0, acc[ph]);
+              acc[ph] = mfma<T>(w1[u0[ph] + 1], b1, acc[ph]);
+              u0[ph] += 2;
+            }
+          }
+        }
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) {
+          uint2 v;
+          v.x = pack2<T>(fmaxf(acc[ph][0] + bias[0], 0.f), fmaxf(acc[ph][1] + bias[1], 0.f));
+          v.y = pack2<T>(fmaxf(acc[ph][2] + bias[2], 0.f), fmaxf(acc[ph][3] + bias[3], 0.f));
+          const int ps = 2 * (16 * wx + m) + (ph & 1) + 1;  // stored tail-input pixel
+          const int ch = 16 * nb + 4 * kg;                 // first channel (8-B granule)
+          *reinterpret_cast<uint2*>(((ph >> 1) ? r1 : r0) + x2_off(ps, ch >> 3) + (ch & 7)) = v;
+        }
+      } else if (s == H1) {  // tail-input rows 2 H1, 2 H1 + 1: zero padding
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) {
+          const int ps = 2 * (16 * wx + m) + (ph & 1) + 1;
+          const int ch = 16 * nb + 4 * kg;
+          *reinterpret_cast<uint2*>(((ph >> 1) ? r1 : r0) + x2_off(ps, ch >> 3) + (ch & 7)) =
+              uint2{0u, 0u};
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // input row s + 2 has landed
+      lds_barrier();
+    };
+    for (int s = 0; s < H1 + 2; ++s) pstep(s);
+  } else {
+    // ======================= consumer: the row-sweep tail, tail steps t = 2s - 3, 2s - 2
+    const int w = wv - 4;
+    TailWave<T> tw;
+    tw.load(a.wt, a.bt, a.wo, a.bo, m, kg);
+    float* __restrict__ O = a.out + (long long)n * H3 * rows::MW;
+    lds_barrier();  // macro step -1
+    int soffv[3];   // element offset of pixel (16 w + m + dx) in a tail-input row, dx = -1..1
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) soffv[dx + 1] = x2_off(16 * w + m + dx + 1, kg);
+    auto soff = [&](int dx) { return soffv[dx + 1]; };
+    auto tstep = [&](const int t, float* scb) {
+      if (t < 0 || t > H2) return;
+      T* const m0 = mr + ((2 * t) % rows::NMR) * rows::MROW;
+      T* const m1 = mr + ((2 * t + 1) % rows::NMR) * rows::MROW;
+      if (t < H2) {
+        const T* src[3];
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy) src[dy + 1] = x2r + ((t + dy + 12) % NX2) * X2ROW;
+        tw.convt(src, soff, m0, m1, w, m, kg);
+      } else {
+        TailWave<T>::zero_rows(m0, m1, w, m, kg);
+      }
+      if (t >= 1) tw.conv_out_d(mr, t, w, m, kg, scb);
+    };
+    for (int s = 0; s < H1 + 2; ++s) {
+      float* const sc0 = sc + ((s & 1) * 2) * (rows::SCR * rows::SCW);
+      float* const sc1 = sc0 + rows::SCR * rows::SCW;
+      tstep(2 * s - 3, sc0);
+      tstep(2 * s - 2, sc1);
+      lds_barrier();
+      if (2 * s - 3 >= 1) tw.conv_out_sums(sc0, O, 2 * (2 * s - 3) - 2, w, lane);
+      if (2 * s - 2 >= 1) tw.conv_out_sums(sc1, O, 2 * (2 * s - 2) - 2, w, lane);
+    }
+  }
 }
 
 }  // namespace
@@ -604,5 +861,43 @@ extern "C" int specenh_convt_conv_out(int dtype, const void* x, int N, int H, in
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("convt_conv_out: ") +
                                                           hipGetErrorString(e));
+  return SPECENH_OK;
+}
+
+extern "C" int specenh_decoder3(int dtype, const void* x, int N, int H, int W, int C,
+                                const void* w1_gemm, const float* b1, int CO1, const void* wt_gemm,
+                                const float* bt, int CO2, const void* wo_gemm, const float* bo,
+                                int k, float* out, void* stream) {
+  if (N < 0 || H <= 0 || W <= 0) return set_error(SPECENH_EINVAL, "bad input shape");
+  if (dtype != SPECENH_DTYPE_F16 && dtype != SPECENH_DTYPE_BF16)
+    return set_error(SPECENH_EUNSUPPORTED, "fused decoder: fp16 / bf16 only");
+  if (W != d3::W1 || C != d3::CI1 || CO1 != d3::CO1 || CO2 != CO || k != KT)
+    return set_error(SPECENH_EUNSUPPORTED,
+                     "fused decoder: Conv2DTranspose(32, 5) on 32-wide 64-channel inputs + "
+                     "Conv2DTranspose(16, 5) + Conv2D(1, 5)");
+  if (N == 0) return SPECENH_OK;
+  if (!x || !w1_gemm || !b1 || !wt_gemm || !bt || !wo_gemm || !bo || !out)
+    return set_error(SPECENH_EINVAL, "null pointer");
+  if ((long long)N * H * W * C >= (1ll << 31) || (long long)N * 16 * H * W >= (1ll << 31))
+    return set_error(SPECENH_EINVAL, "tensor too large (2^31 elements)");
+  D3Args a{};
+  a.x = x; a.w1 = w1_gemm; a.b1 = b1; a.wt = wt_gemm; a.bt = bt; a.wo = wo_gemm; a.bo = bo;
+  a.out = out; a.N = N; a.H = H;
+  hipStream_t st = (hipStream_t)stream;
+  // (the kernels are named here, outside the lambda, so the device compilation instantiates
+  // them)
+  const void* const k16 = reinterpret_cast<const void*>(&decoder3_kernel<_Float16>);
+  const void* const kb16 = reinterpret_cast<const void*>(&decoder3_kernel<__bf16>);
+  static std::once_flag attr_once;
+  std::call_once(attr_once, [k16, kb16] {
+    (void)hipFuncSetAttribute(k16, hipFuncAttributeMaxDynamicSharedMemorySize, d3::LDS_BYTES);
+    (void)hipFuncSetAttribute(kb16, hipFuncAttributeMaxDynamicSharedMemorySize, d3::LDS_BYTES);
+  });
+  if (dtype == SPECENH_DTYPE_F16)
+    SPECENH_LAUNCH(decoder3_kernel<_Float16>, dim3((unsigned)N), dim3(512), d3::LDS_BYTES, st, a);
+  else
+    SPECENH_LAUNCH(decoder3_kernel<__bf16>, dim3((unsigned)N), dim3(512), d3::LDS_BYTES, st, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("decoder3: ") + hipGetErrorString(e));
   return SPECENH_OK;
 }

@@ -31,7 +31,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .ops import ops, tail_supported
+from .ops import decoder3_supported, ops, tail_supported
 
 F32, BF16, F16 = 0, 1, 2
 _DTYPES = {"float32": F32, "bfloat16": BF16, "bf16": BF16, "mixed_bfloat16": BF16,
@@ -159,6 +159,18 @@ class AutoencoderEngine:
                      and tail_supported(self.tdt, last2[0].cin, last2[0].cout, last2[0].k,
                                         last2[1].k)
                      and os.environ.get("SPECENH_NO_TAIL_FUSION", "0") in ("", "0"))
+        # inference: the last THREE layers (Conv2DTranspose x2 + Conv2D(1)) as one launch
+        # (csrc/decoder_tail.hip decoder3_kernel) when the shapes are the reference model's
+        # at 128-wide inputs; both intermediate maps stay in LDS
+        self.dec3 = False
+        if self.tail and len(self.ops) >= 3 and isinstance(self.ops[-3], ConvOp):
+            o3 = self.ops[-3]
+            w_in = self.shapes()[len(self.ops) - 3][1]
+            self.dec3 = (o3.kind == "convT" and o3.act == "relu" and o3.stride == 2
+                         and decoder3_supported(self.tdt, o3.cin, o3.cout, self.ops[-2].cout,
+                                                o3.k, w_in)
+                         and o3.k == self.ops[-2].k == self.ops[-1].k
+                         and _lib.get_variant("DECODER_UNFUSED") == 0)
         self.t = 0  # Adam iterations
         self._bufs = {}
         self._loss = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -222,7 +234,8 @@ class AutoencoderEngine:
             H, W, C = shp[i]
             last = i == len(self.ops)
             dtype = torch.float32 if (last and not train) else self.tdt
-            tail_map = self.tail and not train and i == len(self.ops) - 1
+            tail_map = not train and ((self.tail and i == len(self.ops) - 1) or
+                                      (self.dec3 and i == len(self.ops) - 2))
             if (i - 1) not in self.fused and not tail_map:  # never-stored fused outputs
                 b["h"][i] = torch.empty((N, H, W, C), dtype=dtype, device=dev)
             if train:
@@ -339,6 +352,17 @@ class AutoencoderEngine:
             if timing is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record(torch.cuda.current_stream(self.device))
+            if self.dec3 and not train and i == n_ops - 3:  # three-layer decoder, then done
+                o2, o3 = self.ops[i + 1], self.ops[i + 2]
+                ops.decoder3_out(hin, self._wv[i], self._bv[i], op.cout, self._wv[i + 1],
+                                 self._bv[i + 1], o2.cout, self._wv[i + 2], self._bv[i + 2],
+                                 op.k, b["h"][n_ops])
+                if timing is not None:
+                    ev[1].record(torch.cuda.current_stream(self.device))
+                    timing.append(ev)
+                if kernels is not None:
+                    kernels.append(_lib.last_kernel_name())
+                break
             if self.tail and not train and i == n_ops - 2:  # fused decoder tail, then done
                 o2 = self.ops[i + 1]
                 ops.convt_conv_out_out(hin, self._wv[i], self._bv[i], op.cout, op.k,

@@ -337,6 +337,45 @@ _op("convt_conv_out_out(Tensor x, Tensor wt, Tensor bt, int cout, int kt, Tensor
     "int ko, Tensor(a!) out) -> ()", _tail_out, lambda *a: None)
 
 
+def _dec3_out(x, w1, b1, cout1, wt, bt, cout2, wo, bo, k, out):
+    _need(x, "x")
+    _need(out, "out")
+    N, H, W, C = x.shape
+    if any(t.dtype != x.dtype for t in (w1, wt, wo)) or w1.numel() != cout1 * k * k * C or \
+            wt.numel() != cout2 * k * k * cout1 or wo.numel() != k * k * cout2:
+        raise ValueError("w1 / wt / wo must be the three layers' GEMM weights in x's dtype")
+    if any(t.dtype != torch.float32 for t in (b1, bt, bo)) or b1.numel() != cout1 or \
+            bt.numel() != cout2 or bo.numel() != 1:
+        raise ValueError("biases must be float32 [CO1], [CO2] and [1]")
+    if out.dtype != torch.float32 or out.numel() != N * 16 * H * W:
+        raise ValueError("out must be float32 [N, 4H, 4W(, 1)]")
+    _lib.check(_lib.lib().specenh_decoder3(
+        _code(x), _vp(x), N, H, W, C, _vp(w1), _vp(b1), cout1, _vp(wt), _vp(bt), cout2, _vp(wo),
+        _vp(bo), k, _vp(out), _st(x)), "decoder3")
+
+
+def _dec3(x, w1, b1, cout1, wt, bt, cout2, wo, bo, k):
+    N, H, W, _ = x.shape
+    out = torch.empty((N, 4 * H, 4 * W, 1), dtype=torch.float32, device=x.device)
+    _dec3_out(x, w1, b1, cout1, wt, bt, cout2, wo, bo, k, out)
+    return out
+
+
+_D3 = ("Tensor x, Tensor w1, Tensor b1, int cout1, Tensor wt, Tensor bt, int cout2, Tensor wo, "
+       "Tensor bo, int k")
+_op(f"decoder3({_D3}) -> Tensor", _dec3,
+    lambda x, w1, b1, cout1, wt, bt, cout2, wo, bo, k:
+    x.new_empty((x.shape[0], 4 * x.shape[1], 4 * x.shape[2], 1), dtype=torch.float32))
+_op(f"decoder3_out({_D3}, Tensor(a!) out) -> ()", _dec3_out, lambda *a: None)
+
+
+def decoder3_supported(dtype: torch.dtype, cin: int, cout1: int, cout2: int, k: int,
+                       width: int) -> bool:
+    """specenh_decoder3's configuration: the reference model's decoder on 128-wide images."""
+    return dtype in (torch.float16, torch.bfloat16) and (cin, cout1, cout2, k, width) == \
+        (64, 32, 16, 5, 32)
+
+
 def tail_supported(dtype: torch.dtype, cin: int, cout: int, kt: int, ko: int) -> bool:
     """specenh_convt_conv_out's configurations (the reference model's last two layers)."""
     return dtype in (torch.float16, torch.bfloat16) and (cin, cout, kt, ko) == (32, 16, 5, 5)

@@ -92,3 +92,59 @@ def test_row_sweep_tail_matches_tile_kernel(gpu_device, dtype, hw, n, kernel_var
             ref = ora.forward(spec, params, torch.tensor(x, dtype=torch.float64)).numpy()
         err = checks.out_rel(rows_out.cpu().numpy(), ref)
         assert err <= checks.TOL[dtype]["out_rel"], err
+
+
+def _dec3_model(dtype, hw, seed):
+    from specenh import ae
+    C = ae.ConvOp
+    ops_ = [C("conv", 1, 64, 3, "relu"), C("convT", 64, 32, 5, "relu", stride=2),
+            C("convT", 32, 16, 5, "relu", stride=2), C("conv", 16, 1, 5, "sigmoid")]
+    rng = np.random.default_rng(seed)
+    ws = [(0.5 * rng.standard_normal((3, 3, 1, 64))).astype(np.float32),
+          (0.1 * rng.standard_normal(64)).astype(np.float32),
+          (0.05 * rng.standard_normal((5, 5, 32, 64))).astype(np.float32),
+          (0.1 * rng.standard_normal(32)).astype(np.float32),
+          (0.08 * rng.standard_normal((5, 5, 16, 32))).astype(np.float32),
+          (0.1 * rng.standard_normal(16)).astype(np.float32),
+          (0.25 * rng.standard_normal((5, 5, 16, 1))).astype(np.float32),
+          (0.1 * rng.standard_normal(1)).astype(np.float32)]
+    eng = ae.AutoencoderEngine(ops_, hw + (1,), compute_dtype=dtype, device="cuda")
+    eng.set_keras_weights(ws)
+    return eng, ops_, ws
+
+
+@pytest.mark.parametrize("dtype", ["float16", "mixed_bfloat16"])
+@pytest.mark.parametrize("hw,n", [((32, 32), 3), ((8, 32), 2), ((5, 32), 1), ((64, 32), 2),
+                                  ((1, 32), 2)])
+def test_decoder3_matches_unfused_and_oracle(gpu_device, dtype, hw, n, kernel_variant):
+    """decoder3_kernel (Conv2DTranspose(32) + Conv2DTranspose(16) + Conv2D(1), both maps in
+    LDS) vs the same engine with the decoder unfused (DECODER_UNFUSED=1: convT2 through
+    conv_patch + the row-sweep tail) and the fp64 oracle; output NaN-poisoned first. The
+    32-channel map is rounded to T in both paths after its ReLU, so they differ only by
+    accumulation order (and the fp16 roundings that follow from it)."""
+    eng, ops_, ws = _dec3_model(dtype, hw, seed=hw[0] * 13 + n)
+    assert eng.dec3
+    x = np.random.default_rng(n + 5).uniform(0, 1, (n,) + hw + (1,)).astype(np.float32)
+    xd = eng.to_compute(torch.from_numpy(x))
+    eng.forward(xd)
+    eng._buffers(n, False)["h"][len(ops_)].fill_(float("nan"))
+    fused = eng.forward(xd).clone()
+    kernel_variant("DECODER_UNFUSED", 1)
+    from specenh import ae
+    plain_eng = ae.AutoencoderEngine(ops_, hw + (1,), compute_dtype=dtype, device="cuda")
+    assert not plain_eng.dec3 and plain_eng.tail
+    plain_eng.set_keras_weights(ws)
+    plain = plain_eng.forward(xd).clone()
+    torch.cuda.synchronize()
+    assert fused.shape == plain.shape == (n, 4 * hw[0], 4 * hw[1], 1)
+    assert not torch.isnan(fused).any()
+    d = (fused - plain).abs().max().item()
+    assert d <= 4e-3, d
+    spec = [(o.kind, o.cin, o.cout, o.k, o.act) for o in ops_]
+    it = iter(ws)
+    params = [{"W": torch.tensor(next(it), dtype=torch.float64),
+               "b": torch.tensor(next(it), dtype=torch.float64)} for _ in spec]
+    with torch.no_grad():
+        ref = ora.forward(spec, params, torch.tensor(x, dtype=torch.float64)).numpy()
+    err = checks.out_rel(fused.cpu().numpy(), ref)
+    assert err <= checks.TOL[dtype]["out_rel"], err

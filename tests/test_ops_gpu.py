@@ -33,6 +33,8 @@ def _cases(dev):
     wt, bc16 = r(16 * 25 * 32, dtype=torch.float16, lo=-0.1, hi=0.1), r(16, lo=-0.1, hi=0.1)
     wo, bo = r(25 * 16, dtype=torch.float16, lo=-0.2, hi=0.2), r(1)
     Sp = r(1, 256, 3845)
+    x3 = r(2, 3, 32, 64, dtype=torch.float16)
+    w3a, b3a = r(32 * 25 * 64, dtype=torch.float16, lo=-0.05, hi=0.05), r(32, lo=-0.1, hi=0.1)
     ops = torch.ops.specenh
     return [
         (ops.stft_psd, (x, 256, 128, "hann", 5e5, 0, 2, 1e-11, 7)),
@@ -58,6 +60,9 @@ def _cases(dev):
         (ops.convt_conv_out, (xt, wt, bc16, 16, 5, wo, bo, 5)),
         (ops.convt_conv_out_out, (xt, wt, bc16, 16, 5, wo, bo, 5,
                                   torch.empty(2, 40, 24, 1, device=dev))),
+        (ops.decoder3, (x3, w3a, b3a, 32, wt, bc16, 16, wo, bo, 5)),
+        (ops.decoder3_out, (x3, w3a, b3a, 32, wt, bc16, 16, wo, bo, 5,
+                            torch.empty(2, 12, 128, 1, device=dev))),
         (ops.maxpool2, (pin,)),
         (ops.maxpool2_out, (pin, torch.empty_like(pooled), torch.empty_like(am))),
         (ops.maxpool2_bwd, (pooled.clone(), am, pooled)),

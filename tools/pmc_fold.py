@@ -38,7 +38,7 @@ def demangled_match(symbol, csv_name):
     if not m:
         return False
     parts, s = [], m.group(1)
-    while s:
+    while s and s[0].isdigit():
         n = int(re.match(r"\d+", s).group())
         k = len(str(n))
         parts.append(s[k:k + n])

@@ -38,7 +38,7 @@ def stages_c5(dev):
     S = torch.empty((Hs, bench.HW5, bench.HW5), dtype=torch.float32, device=dev)
     A = torch.empty((Hs, bench.HW5, bench.HW5, 1), dtype=torch.float16, device=dev)
     eng = bench.make_c5_engine(dev)
-    names = bench.LAYER_NAMES_TAIL if eng.tail else bench.LAYER_NAMES
+    names = bench.layer_names(eng)
 
     def stft():
         pipeline_data.specgr_batch(x16, bench.SPEC5, out=S)

@@ -35,6 +35,7 @@
 #include <cstdlib>
 #include <cstdint>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "specenh.h"
@@ -369,14 +370,14 @@ constexpr int XST = 48;              // input pixel stride (elements): 96 B, con
 constexpr int XROW = (QW + 2) * XST;  // input ring row: pixels x = -1 .. 64
 constexpr int NXR = 4;               // input ring rows
 constexpr int MW = 2 * QW;           // 128 map / output columns
-constexpr int MROW = MW * CO;        // map ring row (elements): 32-B pixels, conflict-free
-constexpr int NMR = 6;               // map ring rows
+constexpr int MROW = MW * CO;        // map ring row (elements): 32-B pixels
+constexpr int NMR = 8;               // map ring rows (a step writes 2, the Conv2D(1) reads 6)
 constexpr int SCW = MW + 8;          // scratch row (floats): 4 zero pads each side
 constexpr int SCR = 10;              // scratch rows (n = 5 r + kx)
 constexpr int LDS_X = NXR * XROW * 2;          // bytes
 constexpr int LDS_M = NMR * MROW * 2;
 constexpr int LDS_S = 2 * SCR * SCW * 4;
-constexpr int LDS_BYTES = LDS_X + LDS_M + LDS_S;  // 60,800 B: 2 workgroups per CU
+constexpr int LDS_BYTES = LDS_X + LDS_M + LDS_S;  // 69,056 B: 2 workgroups per CU
 }  // namespace rows
 
 // map pixel p, 4-channel group g (8 B): the two 16-B halves of a pixel swap when bit 2 of p
@@ -395,18 +396,44 @@ struct RowsArgs {
   int N, H, R, nb;  // R: output rows per band (even), nb: bands per image
 };
 
+// bias + ReLU of four fp32 accumulators -> four T packed in 8 bytes. The accumulators start
+// at the bias (folded into the MFMA chain); ReLU commutes with the monotone rounding, so for
+// fp16 it runs on the packed halves (v_pk_max_f16: 2 instead of 4 VALU).
+template <typename T>
+__device__ __forceinline__ uint2 relu_pack(const f32x4& v) {
+  if constexpr (__is_same(T, _Float16)) {
+    const f16x2 lo = f16x2{(_Float16)v[0], (_Float16)v[1]};
+    const f16x2 hi = f16x2{(_Float16)v[2], (_Float16)v[3]};
+    const f16x2 z = f16x2{(_Float16)0.f, (_Float16)0.f};
+    return uint2{__builtin_bit_cast(uint32_t, __builtin_elementwise_max(lo, z)),
+                 __builtin_bit_cast(uint32_t, __builtin_elementwise_max(hi, z))};
+  } else {
+    return uint2{pack2<T>(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f)),
+                 pack2<T>(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f))};
+  }
+}
+
 // The last two layers' per-wave state and steps, shared by tail_rows_kernel and
 // decoder3_kernel: lane (m = lane & 15, kg = lane >> 4) of wave w (0..3) owns input
-// positions 16 w + m of a position row, i.e. map columns 32 w .. 32 w + 31.
+// positions 16 w + m of a position row, i.e. map columns 32 w .. 32 w + 31. Ring slots are
+// passed as values that are compile-time constants at every call site (the step loops are
+// unrolled by the ring period), so every LDS access is a per-lane base + an immediate.
 template <typename T>
 struct TailWave {
   uint4 wt[25];  // Conv2DTranspose taps (A: co = m, ci = 8 kg ..), phase-major, (dy, dx) order
-  float bias[4];
+  f32x4 bias;    // the accumulators' start
   float bo;
   uint4 wo[3];   // Conv2D(1) B fragments per map-row pair p: k = (dr, ci), n = 5 r + kx
+  int mw[2];     // map write offset (elements, in a row) of this lane's pixel, px = 0, 1
+  int mrd[2];    // map read offset of this lane's A row (pair row dr = kg >> 1), block 0, 1
+  int scw[2];    // scratch write offset, block 0, 1
+  int scr;       // scratch read offset of this lane's output (r, x), kx = 0
+  int ox;        // this lane's output column x = 32 w + (lane & 31) (row r = lane >> 5)
 
   __device__ __forceinline__ void load(const void* wt_gemm, const float* bt, const void* wo_gemm,
-                                       const float* b_o, int m, int kg) {
+                                       const float* b_o, int w, int lane) {
+    using namespace rows;
+    const int m = lane & 15, kg = lane >> 4;
     const T* __restrict__ Wt = reinterpret_cast<const T*>(wt_gemm);
     int u = 0;
 #pragma unroll
@@ -419,8 +446,7 @@ struct TailWave {
           if (ky < 0 || ky >= KT || kx < 0 || kx >= KT) continue;
           wt[u++] = *reinterpret_cast<const uint4*>(Wt + ((m * KT + ky) * KT + kx) * CI + 8 * kg);
         }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bias[i] = bt[4 * kg + i];
+    bias = f32x4{bt[4 * kg], bt[4 * kg + 1], bt[4 * kg + 2], bt[4 * kg + 3]};
     bo = b_o[0];
     const T* __restrict__ Wo = reinterpret_cast<const T*>(wo_gemm);
     const int r = m / 5, kx = m - 5 * (m / 5), dr = kg >> 1;
@@ -431,23 +457,29 @@ struct TailWave {
       if (m < 10 && ky >= 0 && ky < KO)
         wo[p] = *reinterpret_cast<const uint4*>(Wo + (ky * KO + kx) * CO + 8 * (kg & 1));
     }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      mw[i] = map_off(2 * (16 * w + m) + i, kg);
+      mrd[i] = (kg >> 1) * MROW + map_off(32 * w + 16 * i + m, 2 * (kg & 1));
+      scw[i] = min(m, SCR - 1) * SCW + 4 + 32 * w + 16 * i + 4 * kg;
+    }
+    scr = 5 * (lane >> 5) * SCW + 4 + 32 * w + (lane & 31) - 2;
+    ox = 32 * w + (lane & 31);
   }
 
-  // Conv2DTranspose of one position row: src[dy + 1] points at this lane's input pixel
-  // (column 16 w + m, channel group kg) of input rows q - 1, q, q + 1; pixel stride PS;
-  // soff(dx) gives the element offset of the dx-shifted pixel. -> map rows 2q, 2q + 1.
-  template <typename Off>
-  __device__ __forceinline__ void convt(const T* const (&src)[3], Off soff, T* mrow0, T* mrow1,
-                                        int w, int m, int kg) const {
-    f32x4 acc[4];
-#pragma unroll
-    for (int ph = 0; ph < 4; ++ph) acc[ph] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // Conv2DTranspose of one position row. xin: this lane's B-fragment address of input
+  // row q - 1 (pixel 16 w + m - 1, group kg); xrow: elements between ring rows q+dy; xo(dx):
+  // offset of the dx-shifted pixel; -> map rows at mrow0 / mrow1 (rows 2q, 2q + 1).
+  template <typename RowOff, typename Xo>
+  __device__ __forceinline__ void convt(const T* xin, RowOff xrow, Xo xo, T* mrow0,
+                                        T* mrow1) const {
+    f32x4 acc[4] = {bias, bias, bias, bias};
     int u0[4] = {0, 4, 10, 16};  // first tap register of each phase (4 / 6 / 6 / 9 taps)
 #pragma unroll
     for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
       for (int dx = -1; dx <= 1; ++dx) {
-        const uint4 b = *reinterpret_cast<const uint4*>(src[dy + 1] + soff(dx));
+        const uint4 b = *reinterpret_cast<const uint4*>(xin + xrow(dy) + xo(dx));
 #pragma unroll
         for (int ph = 0; ph < 4; ++ph) {
           const int ky = ky_of(ph >> 1, dy), kx = ky_of(ph & 1, dx);
@@ -456,55 +488,47 @@ struct TailWave {
         }
       }
 #pragma unroll
-    for (int ph = 0; ph < 4; ++ph) {
-      uint2 v;
-      v.x = pack2<T>(fmaxf(acc[ph][0] + bias[0], 0.f), fmaxf(acc[ph][1] + bias[1], 0.f));
-      v.y = pack2<T>(fmaxf(acc[ph][2] + bias[2], 0.f), fmaxf(acc[ph][3] + bias[3], 0.f));
-      const int pix = 2 * (16 * w + m) + (ph & 1);
-      *reinterpret_cast<uint2*>(((ph >> 1) ? mrow1 : mrow0) + map_off(pix, kg)) = v;
-    }
+    for (int ph = 0; ph < 4; ++ph)
+      *reinterpret_cast<uint2*>(((ph >> 1) ? mrow1 : mrow0) + mw[ph & 1]) = relu_pack<T>(acc[ph]);
   }
 
-  __device__ __forceinline__ static void zero_rows(T* mrow0, T* mrow1, int w, int m, int kg) {
+  __device__ __forceinline__ void zero_rows(T* mrow0, T* mrow1) const {
 #pragma unroll
     for (int ph = 0; ph < 4; ++ph)
-      *reinterpret_cast<uint2*>(((ph >> 1) ? mrow1 : mrow0) +
-                                map_off(2 * (16 * w + m) + (ph & 1), kg)) = uint2{0u, 0u};
+      *reinterpret_cast<uint2*>(((ph >> 1) ? mrow1 : mrow0) + mw[ph & 1]) = uint2{0u, 0u};
   }
 
-  // Conv2D(1) MFMAs for output rows 2q - 2, 2q - 1 (map rows 2q - 4 .. 2q + 1 of the ring
-  // mr, NMR rows) -> D into the scratch scb
-  __device__ __forceinline__ void conv_out_d(const T* mr, int q, int w, int m, int kg,
-                                             float* scb) const {
-    using namespace rows;
-    const int dr = kg >> 1;
+  // Conv2D(1) MFMAs for output rows 2q - 2, 2q - 1: mrow(j) = map row 2q - 4 + j (j even;
+  // row j + 1 is the next ring slot: the ring has an even row count and j is even) -> D into
+  // the scratch scb
+  template <typename MapRow>
+  __device__ __forceinline__ void conv_out_d(MapRow mrow, float* scb, int m) const {
 #pragma unroll
     for (int blk = 0; blk < 2; ++blk) {
-      const int xc = 32 * w + 16 * blk + m;  // this lane's map column (A row)
       f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
-        const int Y = 2 * q - 4 + 2 * p + dr;
-        const uint4 av = *reinterpret_cast<const uint4*>(
-            mr + ((Y + 2 * NMR) % NMR) * MROW + map_off(xc, 2 * (kg & 1)));
+        // map row 2q - 4 + 2p + dr: lane groups kg >> 1 = 0 / 1 read the pair's two rows
+        const uint4 av = *reinterpret_cast<const uint4*>(mrow(2 * p) + mrd[blk]);
         d = mfma<T>(av, wo[p], d);
       }
-      if (m < SCR)  // D[x' = 32 w + 16 blk + 4 kg + i][n = m]
-        *reinterpret_cast<f32x4*>(scb + m * SCW + 4 + 32 * w + 16 * blk + 4 * kg) = d;
+      if (m < rows::SCR)  // D[x' = 32 w + 16 blk + 4 kg + i][n = m]
+        *reinterpret_cast<f32x4*>(scb + scw[blk]) = d;
     }
   }
 
   // diagonal sums of the scratch -> sigmoid -> output rows y0, y0 + 1 (O: the image's rows)
   __device__ __forceinline__ void conv_out_sums(const float* scb, float* __restrict__ O, int y0,
-                                                int w, int lane) const {
-    using namespace rows;
-    const int r = lane >> 5, x = 32 * w + (lane & 31);
+                                                int lane) const {
     float s = bo;
 #pragma unroll
-    for (int kx = 0; kx < KO; ++kx) s += scb[(5 * r + kx) * SCW + 4 + x + kx - 2];
-    O[(long long)(y0 + r) * MW + x] = __builtin_amdgcn_rcpf(1.f + __expf(-s));
+    for (int kx = 0; kx < KO; ++kx) s += scb[scr + kx * rows::SCW + kx];
+    O[(long long)(y0 + (lane >> 5)) * rows::MW + ox] = __builtin_amdgcn_rcpf(1.f + __expf(-s));
   }
 };
+
+template <int I>
+using IC = std::integral_constant<int, I>;
 
 template <typename T>
 __global__ __launch_bounds__(256, 2) void tail_rows_kernel(RowsArgs a) {
@@ -525,7 +549,7 @@ __global__ __launch_bounds__(256, 2) void tail_rows_kernel(RowsArgs a) {
   float* __restrict__ O = a.out + (long long)n * H2 * MW;
 
   TailWave<T> tw;
-  tw.load(a.wt, a.bt, a.wo, a.bo, m, kg);
+  tw.load(a.wt, a.bt, a.wo, a.bo, w, lane);
 
   // ---- zero the rings and the scratch pads, then stage input rows qa-1 .. qa+1 ----
   {
@@ -533,53 +557,54 @@ __global__ __launch_bounds__(256, 2) void tail_rows_kernel(RowsArgs a) {
     for (int e = tid; e < LDS_BYTES / 16; e += 256) z[e] = uint4{0u, 0u, 0u, 0u};
   }
   __syncthreads();
+  // ring slots relative to the band: input row qa - 1 + j in slot j & 3, map row 2 qa + j in
+  // slot j & 7 (rows 2 qa - 4 .. 2 qa - 1 are the zeroed slots 4 .. 7 for the first band)
   const int spix = tid >> 2, scg = tid & 3;  // this thread's 16 B of a staged row
+  T* const xst = xr + (spix + 1) * XST + 8 * scg;
   auto gload = [&](int row) -> uint4 {
     const int rr = min(max(row, 0), H - 1);
     uint4 v = *reinterpret_cast<const uint4*>(X + ((long long)rr * QW + spix) * CI + 8 * scg);
     if (row < 0 || row >= H) v = uint4{0u, 0u, 0u, 0u};
     return v;
   };
-  auto lstore = [&](int row, const uint4& v) {
-    *reinterpret_cast<uint4*>(xr + ((row + 8) % NXR) * XROW + (spix + 1) * XST + 8 * scg) = v;
-  };
 #pragma unroll
-  for (int d = -1; d <= 1; ++d) lstore(qa + d, gload(qa + d));
+  for (int j = 0; j < 3; ++j) *reinterpret_cast<uint4*>(xst + j * XROW) = gload(qa - 1 + j);
   uint4 pa = gload(qa + 2), pb = gload(qa + 3);  // rows q+2 (even steps), q+3 (odd steps)
   lds_barrier();
-  auto soff = [](int dx) { return dx * XST; };
+  const T* const xin = xr + (16 * w + m) * XST + 8 * kg;  // pixel 16 w + m - 1 (stored + 1)
 
-  auto step = [&](const int q, uint4& pre) {
-    // ---- a. Conv2DTranspose of position row q -> map rows 2q, 2q + 1 ----
-    T* const m0 = mr + ((2 * q) % NMR) * MROW;
-    T* const m1 = mr + ((2 * q + 1) % NMR) * MROW;
-    if (q < H) {
-      const T* src[3];
-#pragma unroll
-      for (int dy = -1; dy <= 1; ++dy)
-        src[dy + 1] = xr + ((q + dy + 8) % NXR) * XROW + (16 * w + m + 1) * XST + 8 * kg;
-      tw.convt(src, soff, m0, m1, w, m, kg);
-    } else {  // below the image: the Conv2D(1) zero padding
-      TailWave<T>::zero_rows(m0, m1, w, m, kg);
-    }
-    // ---- b. Conv2D(1) MFMAs for output rows 2q - 2, 2q - 1 -> scratch (q & 1) ----
+  // step i (q = qa + i) with I = i & 3 compile-time
+  auto step = [&](auto ic, const int i, uint4& pre) {
+    constexpr int I = decltype(ic)::value;
+    const int q = qa + i;
+    T* const m0 = mr + ((2 * I) & 7) * MROW;
+    T* const m1 = mr + ((2 * I + 1) & 7) * MROW;
+    if (q < H)
+      tw.convt(xin, [](int dy) { return ((I + 1 + dy) & 3) * XROW; },
+               [](int dx) { return (dx + 1) * XST; }, m0, m1);
+    else  // below the image: the Conv2D(1) zero padding
+      tw.zero_rows(m0, m1);
     const bool emit = 2 * q - 2 >= Y0;
-    float* const scb = sc + (q & 1) * (SCR * SCW);
-    if (emit) tw.conv_out_d(mr, q, w, m, kg, scb);
-    // ---- c. input row q + 2 into the ring ----
-    lstore(q + 2, pre);
+    float* const scb = sc + (I & 1) * (SCR * SCW);
+    if (emit)
+      tw.conv_out_d([&](int j) { return mr + ((2 * I - 4 + j + 8) & 7) * MROW; }, scb, m);
+    *reinterpret_cast<uint4*>(xst + ((I + 3) & 3) * XROW) = pre;  // input row q + 2
     lds_barrier();  // lgkmcnt only: the prefetch loads stay in flight across it
-    // ---- d. diagonal sums -> sigmoid -> out; next prefetch ----
-    if (emit) tw.conv_out_sums(scb, O, 2 * q - 2, w, lane);
+    if (emit) tw.conv_out_sums(scb, O, 2 * q - 2, lane);
     pre = gload(q + 4);
   };
 
-  int q = qa;
-  for (; q + 1 <= qe; q += 2) {
-    step(q, pa);
-    step(q + 1, pb);
+  const int ns = qe - qa + 1;
+  int i = 0;
+  for (; i + 4 <= ns; i += 4) {
+    step(IC<0>{}, i, pa);
+    step(IC<1>{}, i + 1, pb);
+    step(IC<2>{}, i + 2, pa);
+    step(IC<3>{}, i + 3, pb);
   }
-  if (q <= qe) step(q, pa);
+  if (i < ns) step(IC<0>{}, i, pa);
+  if (i + 1 < ns) step(IC<1>{}, i + 1, pb);
+  if (i + 2 < ns) step(IC<2>{}, i + 2, pa);
 }
 
 // ============================================================================ decoder3
@@ -599,7 +624,7 @@ __global__ __launch_bounds__(256, 2) void tail_rows_kernel(RowsArgs a) {
 //  * consumer waves 4-7: two steps of the row-sweep tail (TailWave) per macro step, two
 //    rows behind the producer.
 // Waves w and w + 4 share a SIMD (MI355X_MICROARCH.md, two waves per SIMD): each SIMD pairs
-// one producer and one consumer.
+// one producer and one consumer. Macro steps are unrolled by 4, the rings' period.
 namespace d3 {
 constexpr int CI1 = 64, CO1 = 32;     // the first Conv2DTranspose
 constexpr int W1 = 32;                // its input positions per row
@@ -608,12 +633,12 @@ constexpr int X1ROW = (W1 + 2) * X1ST;
 constexpr int NX1 = 4;
 constexpr int X2ST = 32;              // tail input pixel stride (elements): dense 64 B, swizzled
 constexpr int X2ROW = (2 * W1 + 2) * X2ST;
-constexpr int NX2 = 6;
+constexpr int NX2 = 8;
 constexpr int LDS_X1 = NX1 * X1ROW * 2;
 constexpr int LDS_X2 = NX2 * X2ROW * 2;
 constexpr int LDS_M = rows::NMR * rows::MROW * 2;
 constexpr int LDS_S = 4 * rows::SCR * rows::SCW * 4;
-constexpr int LDS_BYTES = LDS_X1 + LDS_X2 + LDS_M + LDS_S;  // 89,088 B: one workgroup per CU
+constexpr int LDS_BYTES = LDS_X1 + LDS_X2 + LDS_M + LDS_S;  // 105,728 B: one workgroup per CU
 }  // namespace d3
 
 // first Conv2DTranspose input pixel ps (x = ps - 1), 16-byte group g of its 8: group g sits
@@ -657,6 +682,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
   const int m = lane & 15, kg = lane >> 4;
   const int n = blockIdx.x;
   const int H1 = a.H, H2 = 2 * H1, H3 = 4 * H1;
+  const int S = H1 + 2;  // macro steps
   {
     uint4* z = reinterpret_cast<uint4*>(lds_raw);
     for (int e = tid; e < LDS_BYTES / 16; e += 512) z[e] = uint4{0u, 0u, 0u, 0u};
@@ -684,49 +710,55 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
                   Wg + (((16 * nb + m) * KT + ky) * KT + kx) * CI1 + 32 * kh + 8 * kg);
           }
     }
-    float bias[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bias[i] = a.b1[16 * nb + 4 * kg + i];
+    const f32x4 bias = f32x4{a.b1[16 * nb + 4 * kg], a.b1[16 * nb + 4 * kg + 1],
+                             a.b1[16 * nb + 4 * kg + 2], a.b1[16 * nb + 4 * kg + 3]};
     const T* __restrict__ X = reinterpret_cast<const T*>(a.x) + (long long)n * H1 * W1 * CI1;
-    // input row r -> ring slot by LDS-DMA: wave wv moves stored pixels 1 + 8 wv .. 8 + 8 wv
-    // (1 KB, lane-linear); lane i takes stored group i & 7, i.e. source group (i & 7) ^ (ps & 7)
+    // input row r -> ring slot r & 3 by LDS-DMA: wave wv moves stored pixels 1 + 8 wv ..
+    // 8 + 8 wv (1 KB, lane-linear); lane i takes stored group i & 7, i.e. source group
+    // (i & 7) ^ (ps & 7)
     const int dps = 1 + 8 * wv + (lane >> 3);
     const int dsrc = (dps - 1) * CI1 + 8 * ((lane & 7) ^ (dps & 7));
-    auto stage = [&](int row) {
-      unsigned char* dst = lds_raw + (((row + 8) % NX1) * X1ROW + (1 + 8 * wv) * X1ST) * 2;
+    unsigned char* const ddst = lds_raw + (1 + 8 * wv) * X1ST * 2;
+    auto stage = [&](int row, int slot) {
+      unsigned char* dst = ddst + slot * X1ROW * 2;
       if (row >= 0 && row < H1) {
         lds_dma16(X + (long long)row * W1 * CI1 + dsrc, dst);
       } else {  // outside the image: the zero padding rows
         *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
       }
     };
-    int soffv[3];  // this lane's B-fragment offset in a ring row: pixel 16 wx + m + dx, group kg
+    // this lane's B-fragment offsets (pixel 16 wx + m + dx, group kg) in an input ring row,
+    // and its tail-input write offsets (pixel 2 (16 wx + m) + px, channels 16 nb + 4 kg ..)
+    int xo[3], x2w[2];
 #pragma unroll
-    for (int dx = -1; dx <= 1; ++dx) soffv[dx + 1] = x1_off(16 * wx + m + dx + 1, kg);
+    for (int dx = -1; dx <= 1; ++dx) xo[dx + 1] = x1_off(16 * wx + m + dx + 1, kg);
 #pragma unroll
-    for (int d = -1; d <= 1; ++d) stage(d);
+    for (int px = 0; px < 2; ++px) {
+      const int ps = 2 * (16 * wx + m) + px + 1, ch = 16 * nb + 4 * kg;
+      x2w[px] = x2_off(ps, ch >> 3) + (ch & 7);
+    }
+#pragma unroll
+    for (int d = -1; d <= 1; ++d) stage(d, d & 3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();  // (macro step -1: the consumers' matching barrier is below)
-    auto pstep = [&](const int s) {
-      stage(s + 2);  // lands while this row's MFMAs run; waited for before the barrier
-      T* const r0 = x2r + ((2 * s) % NX2) * X2ROW;
-      T* const r1 = x2r + ((2 * s + 1) % NX2) * X2ROW;
+
+    auto pstep = [&](auto ic, const int s) {
+      constexpr int I = decltype(ic)::value;  // s & 3
+      stage(s + 2, (I + 2) & 3);  // lands while this row's MFMAs run
+      T* const r0 = x2r + ((2 * I) & 7) * X2ROW;
+      T* const r1 = x2r + ((2 * I + 1) & 7) * X2ROW;
       if (s < H1) {
-        f32x4 acc[4];
-#pragma unroll
-        for (int ph = 0; ph < 4; ++ph) acc[ph] = f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 acc[4] = {bias, bias, bias, bias};
         int u0[4] = {0, 8, 20, 32};
 #pragma unroll
         for (int dy = -1; dy <= 1; ++dy) {
-          const T* src = x1r + ((s + dy + 8) % NX1) * X1ROW;
+          const T* src = x1r + ((I + dy + 4) & 3) * X1ROW;
 #pragma unroll
           for (int dx = -1; dx <= 1; ++dx) {
-            // K-step kh reads group kg + 4 kh: the swizzle XOR only touches the low bits
-            // identically, so the second group is the first ^ 4 (= + or - 32 elements)
-            const int o0 = soffv[dx + 1];
-            const int o1 = o0 ^ 32;  // group bit 2 flips (the 8-group index is 8 elements wide)
-            const uint4 b0 = *reinterpret_cast<const uint4*>(src + o0);
-            const uint4 b1 = *reinterpret_cast<const uint4*>(src + o1);
+            // group kg + 4 (the second K-step) sits at the first's offset ^ 32 elements:
+            // the swizzle XORs the group index, whose bit 2 is element-offset bit 5
+            const uint4 b0 = *reinterpret_cast<const uint4*>(src + xo[dx + 1]);
+            const uint4 b1 = *reinterpret_cast<const uint4*>(src + (xo[dx + 1] ^ 32));
 #pragma unroll
             for (int ph = 0; ph < 4; ++ph) {
               const int ky = ky_of(ph >> 1, dy), kx = ky_of(ph & 1, dx);
@@ -738,61 +770,72 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
           }
         }
 #pragma unroll
-        for (int ph = 0; ph < 4; ++ph) {
-          uint2 v;
-          v.x = pack2<T>(fmaxf(acc[ph][0] + bias[0], 0.f), fmaxf(acc[ph][1] + bias[1], 0.f));
-          v.y = pack2<T>(fmaxf(acc[ph][2] + bias[2], 0.f), fmaxf(acc[ph][3] + bias[3], 0.f));
-          const int ps = 2 * (16 * wx + m) + (ph & 1) + 1;  // stored tail-input pixel
-          const int ch = 16 * nb + 4 * kg;                 // first channel (8-B granule)
-          *reinterpret_cast<uint2*>(((ph >> 1) ? r1 : r0) + x2_off(ps, ch >> 3) + (ch & 7)) = v;
-        }
+        for (int ph = 0; ph < 4; ++ph)
+          *reinterpret_cast<uint2*>(((ph >> 1) ? r1 : r0) + x2w[ph & 1]) = relu_pack<T>(acc[ph]);
       } else if (s == H1) {  // tail-input rows 2 H1, 2 H1 + 1: zero padding
 #pragma unroll
-        for (int ph = 0; ph < 4; ++ph) {
-          const int ps = 2 * (16 * wx + m) + (ph & 1) + 1;
-          const int ch = 16 * nb + 4 * kg;
-          *reinterpret_cast<uint2*>(((ph >> 1) ? r1 : r0) + x2_off(ps, ch >> 3) + (ch & 7)) =
-              uint2{0u, 0u};
-        }
+        for (int ph = 0; ph < 4; ++ph)
+          *reinterpret_cast<uint2*>(((ph >> 1) ? r1 : r0) + x2w[ph & 1]) = uint2{0u, 0u};
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // input row s + 2 has landed
       lds_barrier();
     };
-    for (int s = 0; s < H1 + 2; ++s) pstep(s);
+    int s = 0;
+    for (; s + 4 <= S; s += 4) {
+      pstep(IC<0>{}, s);
+      pstep(IC<1>{}, s + 1);
+      pstep(IC<2>{}, s + 2);
+      pstep(IC<3>{}, s + 3);
+    }
+    if (s < S) pstep(IC<0>{}, s);
+    if (s + 1 < S) pstep(IC<1>{}, s + 1);
+    if (s + 2 < S) pstep(IC<2>{}, s + 2);
   } else {
     // ======================= consumer: the row-sweep tail, tail steps t = 2s - 3, 2s - 2
     const int w = wv - 4;
     TailWave<T> tw;
-    tw.load(a.wt, a.bt, a.wo, a.bo, m, kg);
+    tw.load(a.wt, a.bt, a.wo, a.bo, w, lane);
     float* __restrict__ O = a.out + (long long)n * H3 * rows::MW;
+    int xo[3];  // element offset of pixel 16 w + m + dx (stored + 1), group kg, in a ring row
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) xo[dx + 1] = x2_off(16 * w + m + dx + 1, kg);
     lds_barrier();  // macro step -1
-    int soffv[3];   // element offset of pixel (16 w + m + dx) in a tail-input row, dx = -1..1
-#pragma unroll
-    for (int dx = -1; dx <= 1; ++dx) soffv[dx + 1] = x2_off(16 * w + m + dx + 1, kg);
-    auto soff = [&](int dx) { return soffv[dx + 1]; };
-    auto tstep = [&](const int t, float* scb) {
+    // tail step t (= 2s - 3 or 2s - 2) with T8 = t & 7 compile-time from s & 3
+    auto tstep = [&](auto ic, const int t, float* scb) {
+      constexpr int T8 = decltype(ic)::value;  // t & 7: the tail-input ring slot of row t
+      constexpr int T4 = T8 & 3;                // the map ring: rows 2t, 2t + 1 in slots 2 T4 ..
       if (t < 0 || t > H2) return;
-      T* const m0 = mr + ((2 * t) % rows::NMR) * rows::MROW;
-      T* const m1 = mr + ((2 * t + 1) % rows::NMR) * rows::MROW;
-      if (t < H2) {
-        const T* src[3];
-#pragma unroll
-        for (int dy = -1; dy <= 1; ++dy) src[dy + 1] = x2r + ((t + dy + 12) % NX2) * X2ROW;
-        tw.convt(src, soff, m0, m1, w, m, kg);
-      } else {
-        TailWave<T>::zero_rows(m0, m1, w, m, kg);
-      }
-      if (t >= 1) tw.conv_out_d(mr, t, w, m, kg, scb);
+      T* const m0 = mr + ((2 * T4) & 7) * rows::MROW;
+      T* const m1 = mr + ((2 * T4 + 1) & 7) * rows::MROW;
+      if (t < H2)
+        tw.convt(x2r, [](int dy) { return ((T8 + dy + 8) & 7) * X2ROW; },
+                 [&](int dx) { return xo[dx + 1]; }, m0, m1);
+      else
+        tw.zero_rows(m0, m1);
+      if (t >= 1)
+        tw.conv_out_d([&](int j) { return mr + ((2 * T4 - 4 + j + 8) & 7) * rows::MROW; }, scb,
+                      m);
     };
-    for (int s = 0; s < H1 + 2; ++s) {
-      float* const sc0 = sc + ((s & 1) * 2) * (rows::SCR * rows::SCW);
+    auto cstep = [&](auto ic, const int s) {
+      constexpr int I = decltype(ic)::value;  // s & 3
+      float* const sc0 = sc + ((I & 1) * 2) * (rows::SCR * rows::SCW);
       float* const sc1 = sc0 + rows::SCR * rows::SCW;
-      tstep(2 * s - 3, sc0);
-      tstep(2 * s - 2, sc1);
+      tstep(IC<(2 * I + 5) & 7>{}, 2 * s - 3, sc0);  // (2s - 3) & 7 = (2 I - 3) & 7
+      tstep(IC<(2 * I + 6) & 7>{}, 2 * s - 2, sc1);
       lds_barrier();
-      if (2 * s - 3 >= 1) tw.conv_out_sums(sc0, O, 2 * (2 * s - 3) - 2, w, lane);
-      if (2 * s - 2 >= 1) tw.conv_out_sums(sc1, O, 2 * (2 * s - 2) - 2, w, lane);
+      if (2 * s - 3 >= 1) tw.conv_out_sums(sc0, O, 2 * (2 * s - 3) - 2, lane);
+      if (2 * s - 2 >= 1) tw.conv_out_sums(sc1, O, 2 * (2 * s - 2) - 2, lane);
+    };
+    int s = 0;
+    for (; s + 4 <= S; s += 4) {
+      cstep(IC<0>{}, s);
+      cstep(IC<1>{}, s + 1);
+      cstep(IC<2>{}, s + 2);
+      cstep(IC<3>{}, s + 3);
     }
+    if (s < S) cstep(IC<0>{}, s);
+    if (s + 1 < S) cstep(IC<1>{}, s + 1);
+    if (s + 2 < S) cstep(IC<2>{}, s + 2);
   }
 }
 

@@ -700,6 +700,542 @@ __global__ __launch_bounds__(256) void recon_kernel(XView x, int Kr, int r, cons
   }
 }
 
+// ---------------------------------------------------------------- 2'. top-1 complement
+// The default kept range of denoiseSignal (denoising_by_svd.ipynb:188-229 with start = 1,
+// stop = None: every component but the first) is out = X - (X v1) v1^T. For Kr, r <= 128
+// one workgroup per matrix does it in one pass over HBM: X (zero-padded to 128 x 128) is
+// resident in LDS and block power iteration with 4 vectors runs on it directly,
+//   U = X Z,  Y = X^T U (= G Z),  Z <- Y R^-1 (CholeskyQR, fp64 Gram of Y),
+// so the Gram matrix G is never formed. From the second round on, Rayleigh-Ritz in span(Z)
+// (generalised, with the basis Gram M = Z^T Z: H q = theta M q, H = U^T U = Z^T G Z) gives
+// theta_1 >= theta_2 and v = Z q_1, u = U q_1 = X v, and the same residual test as the
+// subspace kernel: sqrt(theta_1) ||G v - theta_1 v|| <= tolv (theta_1 - theta_2) ||X||_F
+// with G v = Y q_1. A matrix that fails it after TOP1_MAX_ROUNDS is flagged for the fp64
+// eigen path (its output is overwritten there).
+namespace top1 {
+constexpr int N = 128;              // X tile (rows k, columns i), zero-padded
+constexpr int LD = N + 4;           // LDS row pitch in words: conflict-free row walks
+constexpr int MAX_ROUNDS = 24;
+// X | Zt (4 x N, basis transposed) | U (N x 4) | part (4 waves x N x 4) | reduction scratch
+constexpr size_t LDS_BYTES = (size_t)N * LD * 4 + 4 * N * 4 + N * 4 * 4 + 4 * N * 4 * 4 + 64 * 8;
+
+// 1/sqrt(d) for d > 0: v_rsq_f64 plus one Newton step (the factors below only need to be
+// consistent with each other, not correctly rounded)
+__device__ __forceinline__ double rsq64(double d) {
+  const double r = __builtin_amdgcn_rsq(d);
+  return r * fma(-0.5 * d * r, r, 1.5);
+}
+
+// 4 x 4 Cholesky M = L L^T (lower) in fp64, returned as the strictly lower part of L and
+// rinv = 1 / diag(L). A pivot below 1e-20 of its diagonal entry marks the column dead (its
+// vector lies in the span of the earlier ones, or is zero): rinv = 0, column of L zero.
+__device__ __forceinline__ void chol4(const double (&M)[4][4], double (&L)[4][4], double (&rinv)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double d = M[j][j];
+#pragma unroll
+    for (int l = 0; l < j; ++l) d = fma(-L[j][l], L[j][l], d);
+    const bool live = d > 1e-20 * M[j][j] && d > 0.0;
+    rinv[j] = live ? rsq64(d) : 0.0;
+    L[j][j] = 0.0;
+#pragma unroll
+    for (int k = j + 1; k < 4; ++k) {
+      double s = M[k][j];
+#pragma unroll
+      for (int l = 0; l < j; ++l) s = fma(-L[k][l], L[j][l], s);
+      L[k][j] = s * rinv[j];
+      L[j][k] = 0.0;
+    }
+  }
+}
+
+// solve z L^T = y for the row vector z (z = y R^-1 with R = L^T); dead columns -> 0
+__device__ __forceinline__ void solve_row(const double (&L)[4][4], const double (&rinv)[4],
+                                          const double (&y)[4], double (&z)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double s = y[j];
+#pragma unroll
+    for (int l = 0; l < j; ++l) s = fma(-z[l], L[j][l], s);
+    z[j] = s * rinv[j];
+  }
+}
+
+// cyclic Jacobi on a symmetric 4 x 4 in registers, fp32 (only the top eigenvector's
+// direction and the second Ritz value are taken from it: the Rayleigh quotient and the
+// residual test are redone in fp64). A -> diag, Q accumulates.
+__device__ __forceinline__ void jacobi4(float (&A)[4][4], float (&Q)[4][4]) {
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) Q[a][b] = a == b ? 1.f : 0.f;
+  for (int sweep = 0; sweep < 6; ++sweep) {
+    float off = 0.f, dg = 0.f;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      dg = fmaf(A[a][a], A[a][a], dg);
+#pragma unroll
+      for (int b = a + 1; b < 4; ++b) off = fmaf(A[a][b], A[a][b], off);
+    }
+    if (!(off > 1e-14f * dg)) break;  // uniform (every thread holds the same matrix)
+#pragma unroll
+    for (int pr = 0; pr < 6; ++pr) {
+      const int p = pr < 3 ? 0 : (pr < 5 ? 1 : 2);
+      const int q = pr < 3 ? pr + 1 : (pr < 5 ? pr - 1 : 3);
+      const float apq = A[p][q];
+      if (apq == 0.f) continue;
+      const float tau = 0.5f * (A[q][q] - A[p][p]) * __builtin_amdgcn_rcpf(apq);
+      const float t = copysignf(__builtin_amdgcn_rcpf(fabsf(tau) + __builtin_amdgcn_sqrtf(fmaf(tau, tau, 1.f))), tau);
+      const float c = __builtin_amdgcn_rsqf(fmaf(t, t, 1.f)), s = t * c;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // columns p, q
+        const float akp = A[k][p], akq = A[k][q];
+        A[k][p] = c * akp - s * akq;
+        A[k][q] = s * akp + c * akq;
+        const float qkp = Q[k][p], qkq = Q[k][q];
+        Q[k][p] = c * qkp - s * qkq;
+        Q[k][q] = s * qkp + c * qkq;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // rows p, q
+        const float apk = A[p][k], aqk = A[q][k];
+        A[p][k] = c * apk - s * aqk;
+        A[q][k] = s * apk + c * aqk;
+      }
+    }
+  }
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double readlane64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// sum over the 64 lanes of a wave (every lane active): DPP inside rows of 16 (quad
+// swaps, half-row and row mirrors), then the four row sums; no LDS traffic
+__device__ __forceinline__ double wave_sum64(double v) {
+  v += dpp64<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp64<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp64<0x141>(v);  // row_half_mirror
+  v += dpp64<0x140>(v);  // row_mirror
+  return (readlane64(v, 0) + readlane64(v, 16)) + (readlane64(v, 32) + readlane64(v, 48));
+}
+
+// Sum NV doubles over the 128 threads of waves 0 and 1 (waves 2, 3 skip the wave sums);
+// every thread returns the totals. One barrier; the caller separates reuse of sR.
+template <int NV>
+__device__ __forceinline__ void bsum128(double (&v)[NV], double* sR) {
+  const int tid = threadIdx.x, w = tid >> 6;
+  if (w < 2) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = wave_sum64(v[j]);
+    if ((tid & 63) == 0)
+#pragma unroll
+      for (int j = 0; j < NV; ++j) sR[w * NV + j] = v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = sR[j] + sR[NV + j];
+}
+}  // namespace top1
+
+template <typename TO>
+__global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, float tolv,
+                                                       int* flags, TO* out, long long ob,
+                                                       long long osk, long long osi,
+                                                       long long* phase_clk) {
+  using namespace top1;
+#ifdef SPECENH_TOP1_STATS  // development build: shader clocks per phase (thread 0)
+  long long tacc[8] = {}, tlast = __builtin_amdgcn_s_memtime();
+#define T1_MARK(slot)                                      \
+  do {                                                     \
+    const long long now_ = __builtin_amdgcn_s_memtime();   \
+    tacc[slot] += now_ - tlast;                            \
+    tlast = now_;                                          \
+  } while (0)
+#else
+#define T1_MARK(slot) \
+  do {                \
+  } while (0)
+#endif
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* sX = reinterpret_cast<float*>(smem);  // N x LD
+  float* sZt = sX + N * LD;                     // 4 x N
+  float* sU = sZt + 4 * N;                      // N x 4
+  float* sP = sU + 4 * N;                       // 4 x N x 4
+  double* sR = reinterpret_cast<double*>(sP + 16 * N);  // 64
+  double* vd = reinterpret_cast<double*>(sP);  // N: final v (fp64), after the iteration
+  double* ud = vd + N;                            // N: u = X v
+  double* hd = ud + N;                            // N: half sums
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long b = blockIdx.x;
+  const float* X = x.base + b * x.batch_stride;
+
+  // ---- stage X into LDS (zero-padded), ||X||_F^2 in fp64
+  double fro = 0.0;
+  if (x.si == 1) {  // rows of X contiguous: 16-byte loads along i
+    float4 v[N * N / 4 / 256];
+#pragma unroll
+    for (int u = 0; u < N * N / 4 / 256; ++u) {
+      const int e = tid + 256 * u, k = e >> 5, i = 4 * (e & 31);
+      v[u] = (k < Kr && i < r) ? *reinterpret_cast<const float4*>(X + (long long)k * x.sk + i)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < N * N / 4 / 256; ++u) {
+      const int e = tid + 256 * u, k = e >> 5, i = 4 * (e & 31);
+      *reinterpret_cast<float4*>(sX + k * LD + i) = v[u];
+      fro += (double)v[u].x * v[u].x + (double)v[u].y * v[u].y + (double)v[u].z * v[u].z +
+             (double)v[u].w * v[u].w;
+    }
+  } else {  // X = A^T: contiguous along k
+    for (int e = tid; e < N * N / 4; e += 256) {
+      const int i = e >> 5, k = 4 * (e & 31);
+      const float4 v = (k < Kr && i < r)
+                           ? *reinterpret_cast<const float4*>(X + (long long)i * x.si + k)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      sX[k * LD + i] = v.x;
+      sX[(k + 1) * LD + i] = v.y;
+      sX[(k + 2) * LD + i] = v.z;
+      sX[(k + 3) * LD + i] = v.w;
+      fro += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) fro += __shfl_xor(fro, m);
+  if (lane == 0) sR[32 + w] = fro;
+  if (tid < N)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) sZt[p * N + tid] = tid < r ? hash_unit(tid, p) : 0.f;
+  __syncthreads();
+  const double tr = (sR[32] + sR[33]) + (sR[34] + sR[35]);
+  T1_MARK(0);
+
+  // XZ: lane (row group kb, column group g): rows kb + 32 m (m < 4), 4 float4 column chunks
+  // c(g, j) chosen so that the two groups of a 16-lane LDS window sit 32 banks apart
+  const int kb = 8 * w + (lane & 7), g = lane >> 3;
+  // XtU: lane (chunk cc = 4 columns, half h of the wave's 32 rows)
+  const int cc = lane & 31, h = lane >> 5;
+  float y[4], z[4], uk[4];  // thread i < N: row i of Y = G Z, of Z, and row k = i of U
+  int bad = 1, t_used = 0;
+  for (int t = 1;; ++t) {
+    {  // U = X Z
+      float a[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) a[q] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = 8 * (g & 1) + (g >> 1) + 16 * (j & 1) + 4 * (j >> 1);
+        float4 zv[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) zv[p] = *reinterpret_cast<const float4*>(sZt + p * N + 4 * c);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const float4 xv = *reinterpret_cast<const float4*>(sX + (kb + 32 * m) * LD + 4 * c);
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            float s = a[4 * m + p];
+            s = fmaf(xv.x, zv[p].x, s);
+            s = fmaf(xv.y, zv[p].y, s);
+            s = fmaf(xv.z, zv[p].z, s);
+            s = fmaf(xv.w, zv[p].w, s);
+            a[4 * m + p] = s;
+          }
+        }
+      }
+      // reduce-scatter over the 8 column groups (lane bits 5, 4, 3): the lane keeps
+      // rows m = g >> 1, columns p = 2 (g & 1) + {0, 1}
+      const int b5 = (g >> 2) & 1, b4 = (g >> 1) & 1, b3 = g & 1;
+      float a8[8], a4[4], a2[2];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float keep = b5 ? a[8 + q] : a[q], send = b5 ? a[q] : a[8 + q];
+        a8[q] = keep + __shfl_xor(send, 32);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float keep = b4 ? a8[4 + q] : a8[q], send = b4 ? a8[q] : a8[4 + q];
+        a4[q] = keep + __shfl_xor(send, 16);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const float keep = b3 ? a4[2 + q] : a4[q], send = b3 ? a4[q] : a4[2 + q];
+        a2[q] = keep + __shfl_xor(send, 8);
+      }
+      *reinterpret_cast<float2*>(sU + 4 * (kb + 32 * (g >> 1)) + 2 * b3) = make_float2(a2[0], a2[1]);
+    }
+    __syncthreads();
+    T1_MARK(1);
+    {  // Y = X^T U: wave w sums its 32 rows, lane halves 16 each
+      float a[16];  // [column q][p]
+#pragma unroll
+      for (int q = 0; q < 16; ++q) a[q] = 0.f;
+      const int k0 = 32 * w + 16 * h;
+#pragma unroll 4
+      for (int kk = 0; kk < 16; ++kk) {
+        const float4 xv = *reinterpret_cast<const float4*>(sX + (k0 + kk) * LD + 4 * cc);
+        const float4 uv = *reinterpret_cast<const float4*>(sU + 4 * (k0 + kk));
+        const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          a[4 * q + 0] = fmaf(xs[q], uv.x, a[4 * q + 0]);
+          a[4 * q + 1] = fmaf(xs[q], uv.y, a[4 * q + 1]);
+          a[4 * q + 2] = fmaf(xs[q], uv.z, a[4 * q + 2]);
+          a[4 * q + 3] = fmaf(xs[q], uv.w, a[4 * q + 3]);
+        }
+      }
+      float a8[8];  // halves meet: h keeps columns 2h, 2h + 1
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float keep = h ? a[8 + q] : a[q], send = h ? a[q] : a[8 + q];
+        a8[q] = keep + __shfl_xor(send, 32);
+      }
+      float* dst = sP + w * 4 * N + 4 * (4 * cc + 2 * h);
+      *reinterpret_cast<float4*>(dst) = make_float4(a8[0], a8[1], a8[2], a8[3]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(a8[4], a8[5], a8[6], a8[7]);
+    }
+    __syncthreads();
+    if (tid < N) {
+      float4 s = *reinterpret_cast<const float4*>(sP + 4 * tid);
+#pragma unroll
+      for (int ww = 1; ww < 4; ++ww) {
+        const float4 o = *reinterpret_cast<const float4*>(sP + ww * 4 * N + 4 * tid);
+        s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+      }
+      y[0] = s.x; y[1] = s.y; y[2] = s.z; y[3] = s.w;
+      const float4 u4 = *reinterpret_cast<const float4*>(sU + 4 * tid);
+      uk[0] = u4.x; uk[1] = u4.y; uk[2] = u4.z; uk[3] = u4.w;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) z[p] = sZt[p * N + tid];
+    } else {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) y[p] = z[p] = uk[p] = 0.f;
+    }
+    // Rayleigh-Ritz + residual test at rounds 2, 3, 4, then every second round
+    T1_MARK(2);
+    const bool check = t >= 2 && (t <= 4 || t % 2 == 0 || t == MAX_ROUNDS);  // uniform
+    double S[4][4];  // Y^T Y
+    if (check) {
+      double acc[30];  // Y^T Y | Z^T Z | U^T U, upper triangles
+      int n = 0;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = a; c < 4; ++c) {
+          acc[n] = (double)y[a] * y[c];
+          acc[10 + n] = (double)z[a] * z[c];
+          acc[20 + n] = (double)uk[a] * uk[c];
+          ++n;
+        }
+      bsum128<30>(acc, sR);
+      double M[4][4], H[4][4], L[4][4], ri[4];
+      n = 0;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = a; c < 4; ++c) {
+          S[a][c] = S[c][a] = acc[n];
+          M[a][c] = M[c][a] = acc[10 + n];
+          H[a][c] = H[c][a] = acc[20 + n];
+          ++n;
+        }
+      // C = L^-1 H L^-T with M = L L^T (dead basis columns: rows / columns of C zero)
+      chol4(M, L, ri);
+      double W[4][4];
+      float C[4][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {  // W = L^-1 H, column by column
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          double s = H[a][c];
+#pragma unroll
+          for (int l = 0; l < a; ++l) s = fma(-L[a][l], W[l][c], s);
+          W[a][c] = s * ri[a];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {  // C = L^-1 W^T (lower triangle, mirrored)
+        double col[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          double s = W[c][a];
+#pragma unroll
+          for (int l = 0; l < a; ++l) s = fma(-L[a][l], col[l], s);
+          col[a] = s * ri[a];
+        }
+#pragma unroll
+        for (int a = c; a < 4; ++a) C[a][c] = C[c][a] = (float)col[a];
+      }
+      float Q[4][4];
+      jacobi4(C, Q);
+      // top Ritz pair and the second Ritz value, without indexing registers dynamically
+      float th1f = C[0][0], th2f = -3.0e38f, qt[4] = {Q[0][0], Q[1][0], Q[2][0], Q[3][0]};
+#pragma unroll
+      for (int a = 1; a < 4; ++a) {
+        const bool gt = C[a][a] > th1f;
+        th2f = fmaxf(th2f, gt ? th1f : C[a][a]);
+        th1f = gt ? C[a][a] : th1f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) qt[c] = gt ? Q[c][a] : qt[c];
+      }
+      double q1[4];  // L^T q1 = qt (back substitution): v = Z q1 (unit norm up to fp32)
+#pragma unroll
+      for (int a = 3; a >= 0; --a) {
+        double s = qt[a];
+#pragma unroll
+        for (int l = a + 1; l < 4; ++l) s = fma(-L[l][a], q1[l], s);
+        q1[a] = s * ri[a];
+      }
+      double vi = 0.0, gv = 0.0;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        vi = fma((double)z[p], q1[p], vi);
+        gv = fma((double)y[p], q1[p], gv);  // (G v)_i
+      }
+      double rs[3] = {gv * vi, vi * vi, gv * gv};
+      __syncthreads();  // sR reuse
+      bsum128<3>(rs, sR);
+      // fp64 Rayleigh quotient theta = v^T G v / v^T v and the residual of the normalised
+      // v: ||G v - theta v||^2 / ||v||^2 = (g.g - theta g.v) / v.v
+      const double vv = fmax(rs[1], 1e-300);
+      const double th1 = rs[0] / vv;
+      const double res2 = fmax(rs[2] - th1 * rs[0], 0.0) / vv;
+      const double th2 = fmin((double)th2f, th1);
+      // Accuracy target on the OUTPUT: after the fp64 power step below, the error of v is
+      // at most f * res / gap with f = theta_2 / theta_1 <= (tr - theta_1) / theta_1, and
+      // the output error ~ sqrt(theta_1) * that, against tolv * ||out||_F where
+      // ||out||_F^2 = tr - theta_1 (floored at 1e-4 tr: 1% of ||X||_F, rank-1 inputs)
+      const double rest = fmax(tr - th1, 1e-4 * fmax(tr, 0.0));
+      const double f = fmin(1.0, rest / fmax(th1, 1e-300));
+      const bool conv = sqrt(fmax(th1, 0.0) * res2) * f <= (double)tolv * (th1 - th2) * sqrt(rest);
+      if (conv || t >= MAX_ROUNDS) {  // uniform
+        bad = conv ? 0 : 1;
+        t_used = t;
+        if (tid < N) vd[tid] = vi * rsq64(vv);  // v / ||v|| (partials were read above)
+        T1_MARK(4);
+        break;
+      }
+      T1_MARK(4);
+    } else {
+      double acc[10];
+      int n = 0;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = a; c < 4; ++c) acc[n++] = (double)y[a] * y[c];
+      bsum128<10>(acc, sR);
+      n = 0;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = a; c < 4; ++c) {
+          S[a][c] = S[c][a] = acc[n];
+          ++n;
+        }
+    }
+    // Z = Y R^-1 (CholeskyQR, S = R^T R): each thread rewrites its own column of Zt
+    double L[4][4], ri[4], yd[4], zd[4];
+    chol4(S, L, ri);
+    if (tid < N) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) yd[p] = y[p];
+      solve_row(L, ri, yd, zd);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) sZt[p * N + tid] = (float)zd[p];
+    }
+    __syncthreads();
+    T1_MARK(3);
+  }
+  // ---- one power step in fp64 from the converged v: v <- X^T X v / ||X^T X v||, then
+  // u = X v, so that fp32 rounding in the iteration (relative ~1e-6, amplified by
+  // sigma_1 / ||out||_F in the output) is damped by theta_2 / theta_1
+  auto Xv = [&]() {  // ud = X vd: thread (row k, column half h)
+    const int k = tid & (N - 1), h = tid >> 7;
+    const float* xr = sX + k * LD + 64 * h;
+    const double* vv = vd + 64 * h;
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll 4
+    for (int j = 0; j < 16; ++j) {
+      const float4 x4 = *reinterpret_cast<const float4*>(xr + 4 * j);
+      const double2 v01 = *reinterpret_cast<const double2*>(vv + 4 * j);
+      const double2 v23 = *reinterpret_cast<const double2*>(vv + 4 * j + 2);
+      s0 = fma((double)x4.x, v01.x, s0);
+      s1 = fma((double)x4.y, v01.y, s1);
+      s0 = fma((double)x4.z, v23.x, s0);
+      s1 = fma((double)x4.w, v23.y, s1);
+    }
+    if (h) hd[k] = s0 + s1;
+    __syncthreads();
+    if (!h) ud[k] = (s0 + s1) + hd[k];
+    __syncthreads();
+  };
+  __syncthreads();
+  Xv();
+  {  // w = X^T u: thread (column i, row half h); v = w / ||w||
+    const int i = tid & (N - 1), h = tid >> 7;
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll 8
+    for (int kk = 0; kk < 64; kk += 2) {
+      const int k = 64 * h + kk;
+      s0 = fma((double)sX[k * LD + i], ud[k], s0);
+      s1 = fma((double)sX[(k + 1) * LD + i], ud[k + 1], s1);
+    }
+    if (h) hd[i] = s0 + s1;
+    __syncthreads();
+    const double w = h ? 0.0 : (s0 + s1) + hd[i];
+    double nn[1] = {w * w};
+    bsum128<1>(nn, sR);
+    if (!h) vd[i] = nn[0] > 0.0 ? w * rsq64(nn[0]) : 0.0;
+    __syncthreads();
+  }
+  Xv();
+  T1_MARK(5);
+#ifdef SPECENH_TOP1_STATS  // development build (tools/top1_stats.py): rounds in the flag word
+  if (flags && tid == 0) flags[b] = bad + 2 * t_used;
+#else
+  if (flags && tid == 0) flags[b] = bad;
+#endif
+  // ---- out = X - u v^T (fp64, rounded once to fp32) in A's orientation
+  TO* Ob = out + b * ob;
+  if (osi == 1) {
+    for (int e = tid; e < Kr * (r / 4); e += 256) {
+      const int k = e / (r / 4), i = 4 * (e % (r / 4));
+      const float4 xv = *reinterpret_cast<const float4*>(sX + k * LD + i);
+      const double2 v01 = *reinterpret_cast<const double2*>(vd + i);
+      const double2 v23 = *reinterpret_cast<const double2*>(vd + i + 2);
+      const double u = ud[k];
+      TO* o = Ob + (long long)k * osk + i;
+      o[0] = to_out<TO>((float)fma(-u, v01.x, (double)xv.x));
+      o[1] = to_out<TO>((float)fma(-u, v01.y, (double)xv.y));
+      o[2] = to_out<TO>((float)fma(-u, v23.x, (double)xv.z));
+      o[3] = to_out<TO>((float)fma(-u, v23.y, (double)xv.w));
+    }
+  } else {  // contiguous along k
+    for (int e = tid; e < r * (Kr / 4); e += 256) {
+      const int i = e / (Kr / 4), k = 4 * (e % (Kr / 4));
+      const double vi = vd[i];
+      TO* o = Ob + (long long)i * osi + k;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        o[c] = to_out<TO>((float)fma(-ud[k + c], vi, (double)sX[(k + c) * LD + i]));
+    }
+  }
+  T1_MARK(6);
+#ifdef SPECENH_TOP1_STATS
+  if (phase_clk && tid == 0)
+    for (int q = 0; q < 8; ++q) phase_clk[b * 8 + q] = tacc[q];
+#endif
+#undef T1_MARK
+}
+
 
 // ---------------------------------------------------------------- optimal hard threshold
 // use_optimal / computeSignal (denoising_by_svd.ipynb:174-181, 210-217) need the median of
@@ -1459,6 +1995,50 @@ int eig_denoise(const float* A, long long batch, int m, int n, long long a_strid
   return SPECENH_OK;
 }
 
+// top1_kernel's shapes: both dimensions <= 128 and multiples of 4 (16-byte rows / columns),
+// 16-byte aligned matrices
+bool top1_fits(const float* A, int m, int n, long long a_stride) {
+  return m <= top1::N && n <= top1::N && m % 4 == 0 && n % 4 == 0 && a_stride % 4 == 0 &&
+         ((uintptr_t)A & 15) == 0;
+}
+
+template <typename TO>
+hipError_t launch_top1_t(const float* A, long long batch, int m, int n, long long a_stride,
+                         int* flags, void* out, hipStream_t st, long long* phase_clk) {
+  const hipError_t attr = hipFuncSetAttribute(
+      (const void*)top1_kernel<TO>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)top1::LDS_BYTES);
+  if (attr != hipSuccess) return attr;
+  XView xv;
+  xv.base = A;
+  xv.batch_stride = a_stride;
+  int Kr, r = std::min(m, n);
+  long long osk, osi;
+  if (m >= n) {
+    xv.sk = n; xv.si = 1; Kr = m; osk = n; osi = 1;
+  } else {
+    xv.sk = 1; xv.si = n; Kr = n; osk = 1; osi = n;
+  }
+  for (long long b0 = 0; b0 < batch; b0 += 1LL << 30) {
+    const long long nb = std::min<long long>(1LL << 30, batch - b0);
+    XView xb = xv;
+    xb.base = A + b0 * a_stride;
+    SPECENH_LAUNCH(top1_kernel<TO>, dim3((unsigned)nb), dim3(256), top1::LDS_BYTES, st, xb, Kr,
+                   r, 5e-6f, flags + b0, reinterpret_cast<TO*>(out) + b0 * (long long)m * n,
+                   (long long)m * n, osk, osi, phase_clk ? phase_clk + 8 * b0 : nullptr);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_top1(const float* A, long long batch, int m, int n, long long a_stride,
+                       int* flags, void* out, int odt, hipStream_t st, long long* phase_clk) {
+  if (odt == SPECENH_DTYPE_F16)
+    return launch_top1_t<_Float16>(A, batch, m, n, a_stride, flags, out, st, phase_clk);
+  if (odt == SPECENH_DTYPE_BF16)
+    return launch_top1_t<__bf16>(A, batch, m, n, a_stride, flags, out, st, phase_clk);
+  return launch_top1_t<float>(A, batch, m, n, a_stride, flags, out, st, phase_clk);
+}
+
 // denoising_by_svd.ipynb:224-228: clamp start < 0 and stop > r, then Python slicing
 // u[:, start:stop] (a negative stop counts from the end) -> kept [lo, hi), hi <= lo empty.
 void resolve_slice(int r, int start, int stop, int& lo, int& hi) {
@@ -1504,7 +2084,9 @@ size_t specenh_svd_denoise_workspace_bytes(long long batch, int m, int n, int st
   resolve_slice(r, start, stop, lo, hi);
   switch (range_path(r, lo, hi, K)) {
     case 1: return specenh_svd_workspace_bytes(batch, m, n, K);
-    case 2: return r <= EIG_MAXN ? eig_layout(r).bytes(batch) : 16;
+    case 2:  // (+ top1_kernel's flags for the default range)
+      return r <= EIG_MAXN ? eig_layout(r).bytes(batch) + (lo == 1 && hi == r ? batch * 4 + 256 : 0)
+                           : 16;
     default: return 16;
   }
 }
@@ -1552,6 +2134,31 @@ int specenh_svd_denoise_ex(const float* A, long long batch, int m, int n, long l
       b += nb - 1;
     }
     return SPECENH_OK;
+  }
+  if (lo == 1 && hi == r && top1_fits(A, m, n, a_stride) && variant(V_SVD_NO_TOP1) == 0) {
+    // one pass: top1_kernel writes every output and flags the matrices without a converged
+    // gap at the cut; the fp64 eigen path redoes those (its kernels return at once for the
+    // others). Workspace: the flags and eigen-path regions of the subspace layout, or for
+    // r too small for a subspace the eigen-path layout followed by the flags.
+    size_t off, eoff;
+    if (path == 1) {
+      off = (size_t)(batch * r * r + batch * (long long)r * K + batch * K) * sizeof(float);
+      off = (off + 255) / 256 * 256;
+      eoff = (off + 2 * (size_t)batch * 4 + 255) / 256 * 256;
+    } else {
+      eoff = 0;
+      off = eig_layout(r).bytes(batch);
+    }
+    int* flags = (int*)((char*)workspace + off);
+#ifdef SPECENH_TOP1_STATS  // development build: phase clocks into the (unused) Gram region
+    long long* phase_clk = path == 1 ? (long long*)workspace : nullptr;
+#else
+    long long* phase_clk = nullptr;
+#endif
+    const hipError_t e = launch_top1(A, batch, m, n, a_stride, flags, out, out_dtype, st, phase_clk);
+    if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("top1: ") + hipGetErrorString(e));
+    return eig_denoise(A, batch, m, n, a_stride, 1, r, -1, out, out_dtype, nullptr, nullptr,
+                       nullptr, (char*)workspace + eoff, st, flags);
   }
   if (path == 2)  // wide or bottom-of-spectrum range: fp64 eigenvectors (r <= 256)
     return eig_denoise(A, batch, m, n, a_stride, lo, hi, -1, out, out_dtype, nullptr, nullptr,

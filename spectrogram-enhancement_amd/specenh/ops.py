@@ -166,6 +166,12 @@ _op("csd(Tensor x, Tensor y, int nperseg, int noverlap, str window, float fs, in
 
 
 # ---------------------------------------------------------------- SVD denoiser
+def _bstride(A):
+    """Batch stride for the C-ABI: a batch of one may carry any stride (e.g. 0 from a numpy
+    [None] view); the kernels only need it to reach matrix b for b >= 1."""
+    return A.stride(0) if A.shape[0] > 1 else A.shape[1] * A.shape[2]
+
+
 def _svd_check(A):
     if A.dim() != 3 or A.dtype != torch.float32 or A.stride(2) != 1 or A.stride(1) != A.shape[2]:
         raise ValueError("A must be float32 [batch, m, n] with row-major matrices")
@@ -179,7 +185,7 @@ def _svd_out(A, start, stop, out):
     L = _lib.lib()
     ws = torch.empty(max(16, int(L.specenh_svd_denoise_workspace_bytes(B, m, n, start, stop))),
                      dtype=torch.uint8, device=A.device)
-    _lib.check(L.specenh_svd_denoise_ex(_vp(A), B, m, n, A.stride(0), start, stop, _vp(out),
+    _lib.check(L.specenh_svd_denoise_ex(_vp(A), B, m, n, _bstride(A), start, stop, _vp(out),
                                         _code(out), _vp(ws), _st(A)), "svd_denoise")
 
 
@@ -189,18 +195,29 @@ def _svd(A, start, stop, out_dtype):
     return out
 
 
-def _svd_opt(A, mode):
+def _svd_opt_out(A, kind, out, num_sing, median):
     _svd_check(A)
     B, m, n = A.shape
+    if (out.shape != A.shape or out.dtype != torch.float32 or not out.is_contiguous()
+            or out.device != A.device):
+        raise ValueError("out must be a contiguous float32 [B, m, n] tensor on A's device")
+    if (num_sing.numel() != B or num_sing.dtype != torch.int32 or median.numel() != B
+            or median.dtype != torch.float64 or num_sing.device != A.device
+            or median.device != A.device):
+        raise ValueError("num_sing / median must be int32 / float64 [B] tensors on A's device")
     L = _lib.lib()
-    out = torch.empty(A.shape, dtype=torch.float32, device=A.device)
     ws = torch.empty(max(16, int(L.specenh_svd_optimal_workspace_bytes(B, m, n))),
                      dtype=torch.uint8, device=A.device)
-    ns = torch.empty(B, dtype=torch.int32, device=A.device)
-    med = torch.empty(B, dtype=torch.float64, device=A.device)
-    _lib.check(L.specenh_svd_denoise_optimal(_vp(A), B, m, n, A.stride(0), int(mode), _vp(out),
-                                             _vp(ns), _vp(med), _vp(ws), _st(A)),
+    _lib.check(L.specenh_svd_denoise_optimal(_vp(A), B, m, n, _bstride(A), int(kind), _vp(out),
+                                             _vp(num_sing), _vp(median), _vp(ws), _st(A)),
                "svd_denoise_optimal")
+
+
+def _svd_opt(A, mode):
+    out = torch.empty(A.shape, dtype=torch.float32, device=A.device)
+    ns = torch.empty(A.shape[0], dtype=torch.int32, device=A.device)
+    med = torch.empty(A.shape[0], dtype=torch.float64, device=A.device)
+    _svd_opt_out(A, mode, out, ns, med)
     return out, ns, med
 
 
@@ -211,6 +228,9 @@ _op("svd_denoise_out(Tensor A, int start, int stop, Tensor(a!) out) -> ()", _svd
 _op("svd_denoise_optimal(Tensor A, int mode) -> (Tensor, Tensor, Tensor)", _svd_opt,
     lambda A, mode: (A.new_empty(A.shape), A.new_empty((A.shape[0],), dtype=torch.int32),
                      A.new_empty((A.shape[0],), dtype=torch.float64)))
+# (the mode argument is "kind" here: auto_functionalized reserves the name "mode")
+_op("svd_denoise_optimal_out(Tensor A, int kind, Tensor(a!) out, Tensor(b!) num_sing, "
+    "Tensor(c!) median) -> ()", _svd_opt_out, lambda *a: None)
 
 
 # ---------------------------------------------------------------- convolutions
@@ -573,25 +593,43 @@ _op("morph(Tensor S) -> Tensor", _morph, lambda S: torch.empty_like(S))
 
 
 # ---------------------------------------------------------------- strip glue
-def _pack(S, rows, width, n_strips, dtype):
+def _pack_out(S, rows, width, n_strips, out):
     if S.dim() != 3 or S.dtype != torch.float32 or S.stride(2) != 1 or S.stride(1) != S.shape[2]:
         raise ValueError("S must be float32 [batch, F, T] with row-major spectrograms")
     B, F, T = S.shape
-    out = torch.empty((B * n_strips, rows, width, 1), dtype=dtype, device=S.device)
+    if (out.numel() != B * n_strips * rows * width or not out.is_contiguous()
+            or out.device != S.device or out.dtype not in (torch.float32, torch.bfloat16,
+                                                          torch.float16)):
+        raise ValueError(f"out must be a contiguous float32/bfloat16/float16 tensor of "
+                         f"{B * n_strips} x {rows} x {width} elements on S's device")
     _lib.check(_lib.lib().specenh_strips_pack(
         _code(out), _vp(S), B, F, T, S.stride(0), rows, width, n_strips, _vp(out), _st(S)),
         "strips_pack")
+
+
+def _pack(S, rows, width, n_strips, dtype):
+    out = torch.empty((S.shape[0] * n_strips, rows, width, 1), dtype=dtype, device=S.device)
+    _pack_out(S, rows, width, n_strips, out)
     return out
 
 
-def _unpack(strips, rows, width, n_strips):
+def _unpack_out(strips, rows, width, n_strips, out):
     _need(strips, "strips")
     if strips.shape[0] % n_strips or tuple(strips.shape[1:3]) != (rows, width):
         raise ValueError(f"strips must be [k*{n_strips}, {rows}, {width}(, 1)]")
     B = strips.shape[0] // n_strips
-    out = torch.empty((B, rows, n_strips * width), dtype=torch.float32, device=strips.device)
+    if (out.numel() != B * rows * n_strips * width or not out.is_contiguous()
+            or out.device != strips.device or out.dtype != torch.float32):
+        raise ValueError(f"out must be a contiguous float32 tensor of {B} x {rows} x "
+                         f"{n_strips * width} elements on the strips' device")
     _lib.check(_lib.lib().specenh_strips_unpack(_code(strips), _vp(strips), B, rows, width,
                                                 n_strips, _vp(out), _st(strips)), "strips_unpack")
+
+
+def _unpack(strips, rows, width, n_strips):
+    out = torch.empty((strips.shape[0] // n_strips, rows, n_strips * width), dtype=torch.float32,
+                      device=strips.device)
+    _unpack_out(strips, rows, width, n_strips, out)
     return out
 
 
@@ -601,5 +639,9 @@ _op("strips_pack(Tensor S, int rows, int width, int n_strips, ScalarType dtype) 
 _op("strips_unpack(Tensor strips, int rows, int width, int n_strips) -> Tensor", _unpack,
     lambda strips, rows, width, n_strips:
     strips.new_empty((strips.shape[0] // n_strips, rows, n_strips * width), dtype=torch.float32))
+_op("strips_pack_out(Tensor S, int rows, int width, int n_strips, Tensor(a!) out) -> ()",
+    _pack_out, lambda *a: None)
+_op("strips_unpack_out(Tensor strips, int rows, int width, int n_strips, Tensor(a!) out) -> ()",
+    _unpack_out, lambda *a: None)
 
 ops = torch.ops.specenh

@@ -33,10 +33,9 @@ def patch_batch(S: torch.Tensor, dtype=torch.float32, rows=ROWS, width=WIDTH,
     if not (S.stride(2) == 1 and S.stride(1) == S.shape[2]):
         S = S.contiguous()
     from .ops import ops
-    res = ops.strips_pack(S, rows, width, n_strips, dtype)
     if out is None:
-        return res
-    out.copy_(res)
+        return ops.strips_pack(S, rows, width, n_strips, dtype)
+    ops.strips_pack_out(S, rows, width, n_strips, out)  # straight into the caller's buffer
     return out
 
 
@@ -49,10 +48,9 @@ def unpatch_batch(strips: torch.Tensor, rows=ROWS, width=WIDTH, n_strips=N_STRIP
     if strips.shape[0] % n_strips or tuple(strips.shape[1:3]) != (rows, width):
         raise ValueError(f"strips must be [k*{n_strips}, {rows}, {width}(, 1)]")
     from .ops import ops
-    res = ops.strips_unpack(strips, rows, width, n_strips)
     if out is None:
-        return res
-    out.copy_(res)
+        return ops.strips_unpack(strips, rows, width, n_strips)
+    ops.strips_unpack_out(strips, rows, width, n_strips, out)
     return out
 
 

@@ -104,11 +104,12 @@ def optimal_batch(A: torch.Tensor, mode: int = _lib.SVD_OPTIMAL, out: torch.Tens
         A = A.contiguous()
     B, m, n = A.shape
     from .ops import ops
-    res_, ns, med = ops.svd_denoise_optimal(A, int(mode))
     if out is None:
-        out = res_
-    else:
-        out.copy_(res_)
+        out, ns, med = ops.svd_denoise_optimal(A, int(mode))
+    else:  # straight into the caller's buffer
+        ns = torch.empty(B, dtype=torch.int32, device=A.device)
+        med = torch.empty(B, dtype=torch.float64, device=A.device)
+        ops.svd_denoise_optimal_out(A, int(mode), out.view(B, m, n), ns, med)
     res = out[0] if squeeze else out
     return (res, ns, med) if return_rank else res
 

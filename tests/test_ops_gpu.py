@@ -45,6 +45,9 @@ def _cases(dev):
         (ops.svd_denoise, (A, 1, -1, torch.float16)),
         (ops.svd_denoise_out, (A, 2, 9, torch.empty_like(A))),
         (ops.svd_denoise_optimal, (A, 0)),
+        (ops.svd_denoise_optimal_out, (A, 1, torch.empty_like(A),
+                                       torch.empty(A.shape[0], dtype=torch.int32, device=dev),
+                                       torch.empty(A.shape[0], dtype=torch.float64, device=dev))),
         (ops.conv2d, (xc, wc, bc, 3, 3, 8, 1, 1, 1, 1, 8, 8, 1)),
         (ops.conv2d, (xc, wc, None, 3, 3, 8, 1, 1, 1, 2, 16, 16, 0)),
         (ops.conv2d_out, (xc, wc, bc, 3, 3, 8, 1, 1, 1, 1, 8, 8, 2, None,
@@ -83,6 +86,10 @@ def _cases(dev):
         (ops.morph, (F64,)),
         (ops.strips_pack, (Sp, 256, 128, 30, torch.float32)),
         (ops.strips_unpack, (r(60, 256, 128, 1), 256, 128, 30)),
+        (ops.strips_pack_out, (Sp, 256, 128, 30,
+                               torch.empty(30, 256, 128, 1, device=dev, dtype=torch.bfloat16))),
+        (ops.strips_unpack_out, (r(60, 256, 128, 1, dtype=torch.bfloat16), 256, 128, 30,
+                                 torch.empty(2, 256, 3840, device=dev))),
     ]
 
 

@@ -11,12 +11,13 @@ OPS = ["stft_psd", "stft_psd_out", "csd", "svd_denoise", "svd_denoise_out", "svd
        "convt_conv_out_out", "decoder3", "decoder3_out", "maxpool2", "maxpool2_out",
        "maxpool2_bwd", "maxpool2_bwd_out", "bce_logits", "bce_logits_out", "adam_step_",
        "weight_flip_transpose", "weight_flip_transpose_out", "cast", "cast_out", "label_filter",
-       "quantfilt", "gaussblr", "morph", "strips_pack", "strips_unpack"]
+       "quantfilt", "gaussblr", "morph", "strips_pack", "strips_unpack", "strips_pack_out",
+       "strips_unpack_out", "svd_denoise_optimal_out"]
 
 # C-ABI compute entry point -> operator(s) that reach it
 CABI = {"specenh_stft_psd": "stft_psd_out", "specenh_stft_psd_f16": "stft_psd_out",
         "specenh_csd": "csd", "specenh_svd_denoise_ex": "svd_denoise_out",
-        "specenh_svd_denoise_optimal": "svd_denoise_optimal", "specenh_conv2d": "conv2d_out",
+        "specenh_svd_denoise_optimal": "svd_denoise_optimal_out", "specenh_conv2d": "conv2d_out",
         "specenh_conv2d_wgrad": "conv2d_wgrad_out",
         "specenh_convt_conv_out": "convt_conv_out_out", "specenh_decoder3": "decoder3_out",
         "specenh_maxpool2_fwd": "maxpool2_out",
@@ -24,8 +25,8 @@ CABI = {"specenh_stft_psd": "stft_psd_out", "specenh_stft_psd_f16": "stft_psd_ou
         "specenh_adam_step": "adam_step_", "specenh_weight_flip_transpose":
         "weight_flip_transpose_out", "specenh_cast": "cast_out", "specenh_filter": "label_filter",
         "specenh_quantfilt": "quantfilt", "specenh_gaussblr": "gaussblr",
-        "specenh_morph": "morph", "specenh_strips_pack": "strips_pack",
-        "specenh_strips_unpack": "strips_unpack"}
+        "specenh_morph": "morph", "specenh_strips_pack": "strips_pack_out",
+        "specenh_strips_unpack": "strips_unpack_out"}
 
 
 def test_every_operator_is_registered():

@@ -1,12 +1,12 @@
 #!/bin/bash
 # Development A/B builds: tools/build_variant.sh NAME SOURCE "-DFLAG=V ..." ->
-# build/variants/libspecenh_NAME.so (every other object from the in-tree build); load it
-# with SPECENH_LIB=$PWD/build/variants/libspecenh_NAME.so.
+# tools/variants/libspecenh_NAME.so (every other object from the in-tree build); load it
+# with SPECENH_LIB=$PWD/tools/variants/libspecenh_NAME.so.
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; SRC=$2; DEFS=$3
 OBJ=$R/spectrogram-enhancement_amd/build/obj
-OUT=$R/build/variants
+OUT=$R/tools/variants
 mkdir -p $OUT
 python3 $R/spectrogram-enhancement_amd/build.py > /dev/null
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$R/include -I$R/spectrogram-enhancement_amd/csrc \

@@ -32,13 +32,21 @@ torch.cuda.synchronize()
 off = (B * r * r + B * r * K + B * K) * 4
 off = (off + 255) // 256 * 256
 flags = ws[off:off + 8 * B].view(torch.int32)
-print("flagged", int(flags[:B].sum()), "then", int(flags[B:].sum()), "of", B)
+print("flagged (top1_kernel, or the first subspace pass)", int(flags[:B].sum()), "of", B)
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-for _ in range(3):
-    svd.denoise_batch(S, out=A)
-e0.record()
-for _ in range(20):
-    svd.denoise_batch(S, out=A)
-e1.record()
-e1.synchronize()
-print(f"denoise_batch {B} x 128 x 128 -> fp16: {e0.elapsed_time(e1) / 20:.4f} ms")
+res = {}
+for rnd in range(4):
+    for v in (0, 1):  # SVD_NO_TOP1: one-pass top1_kernel vs Gram + subspace + recon
+        _lib.set_variant("SVD_NO_TOP1", v)
+        svd.denoise_batch(S, out=A)
+        e0.record()
+        for _ in range(10):
+            svd.denoise_batch(S, out=A)
+        e1.record()
+        e1.synchronize()
+        if rnd:
+            res.setdefault(v, []).append(e0.elapsed_time(e1) / 10)
+for v, name in ((0, "top1"), (1, "pipeline")):
+    print(f"denoise_batch {B} x 128 x 128 -> fp16 [{name}]: {min(res[v]):.4f} ms "
+          f"(rounds {', '.join(f'{t:.4f}' for t in res[v])})")
+_lib.set_variant("SVD_NO_TOP1", 0)

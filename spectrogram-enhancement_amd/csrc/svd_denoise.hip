@@ -845,6 +845,35 @@ __device__ __forceinline__ void bsum128(double (&v)[NV], double* sR) {
 #pragma unroll
   for (int j = 0; j < NV; ++j) v[j] = sR[j] + sR[NV + j];
 }
+
+// Gram entries of the 128-row blocks, fp64: value j < NV is sum_i A[i][a] A[i][b] for the
+// pair n = j % 10 of the upper triangle of block j / 10 (0: Y, 1: Z, 2: U). Thread
+// (j, chunk c) sums 16 rows, the 8 chunks meet through DPP inside each 8-lane group; every
+// thread returns all NV sums. Y and U are row-major N x 4, Z transposed (4 x N).
+template <int NV>
+__device__ __forceinline__ void gram_sums(const float* sY, const float* sZt, const float* sU,
+                                          double* sRed, double (&out)[NV]) {
+  const int t = threadIdx.x, j = t >> 3, c = t & 7;
+  double s = 0.0;
+  if (j < NV) {
+    const int n = j % 10, src = j / 10;
+    const int a = (int)((0x3221110000ULL >> (4 * n)) & 15);
+    const int b = (int)((0x3323213210ULL >> (4 * n)) & 15);
+    const float* base = src == 0 ? sY : (src == 1 ? sZt : sU);
+    const int rs = src == 1 ? 1 : 4;
+    const float* pa = base + (src == 1 ? a * N : a) + 16 * c * rs;
+    const float* pb = base + (src == 1 ? b * N : b) + 16 * c * rs;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s = fma((double)pa[i * rs], (double)pb[i * rs], s);
+  }
+  s += dpp64<0xB1>(s);   // quad_perm [1, 0, 3, 2]
+  s += dpp64<0x4E>(s);   // quad_perm [2, 3, 0, 1]
+  s += dpp64<0x141>(s);  // row_half_mirror: the two quads of each 8-lane group
+  if (c == 0 && j < NV) sRed[j] = s;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NV; ++q) out[q] = sRed[q];
+}
 }  // namespace top1
 
 template <typename TO>
@@ -914,7 +943,9 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
   if (lane == 0) sR[32 + w] = fro;
   if (tid < N)
 #pragma unroll
-    for (int p = 0; p < 4; ++p) sZt[p * N + tid] = tid < r ? hash_unit(tid, p) : 0.f;
+    for (int p = 0; p < 4; ++p)  // column 0 all ones (close to v1 for the non-negative
+                                   // log spectrograms), the others pseudo-random
+      sZt[p * N + tid] = tid < r ? (p == 0 ? 1.f : hash_unit(tid, p)) : 0.f;
   __syncthreads();
   const double tr = (sR[32] + sR[33]) + (sR[34] + sR[35]);
   T1_MARK(0);
@@ -1011,6 +1042,7 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
         s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
       }
       y[0] = s.x; y[1] = s.y; y[2] = s.z; y[3] = s.w;
+      *reinterpret_cast<float4*>(sP + 4 * tid) = s;  // Y in place of wave 0's partials
       const float4 u4 = *reinterpret_cast<const float4*>(sU + 4 * tid);
       uk[0] = u4.x; uk[1] = u4.y; uk[2] = u4.z; uk[3] = u4.w;
 #pragma unroll
@@ -1019,25 +1051,16 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
 #pragma unroll
       for (int p = 0; p < 4; ++p) y[p] = z[p] = uk[p] = 0.f;
     }
+    __syncthreads();
     // Rayleigh-Ritz + residual test at rounds 2, 3, 4, then every second round
     T1_MARK(2);
     const bool check = t >= 2 && (t <= 4 || t % 2 == 0 || t == MAX_ROUNDS);  // uniform
     double S[4][4];  // Y^T Y
     if (check) {
       double acc[30];  // Y^T Y | Z^T Z | U^T U, upper triangles
-      int n = 0;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = a; c < 4; ++c) {
-          acc[n] = (double)y[a] * y[c];
-          acc[10 + n] = (double)z[a] * z[c];
-          acc[20 + n] = (double)uk[a] * uk[c];
-          ++n;
-        }
-      bsum128<30>(acc, sR);
+      gram_sums<30>(sP, sZt, sU, sR, acc);
       double M[4][4], H[4][4], L[4][4], ri[4];
-      n = 0;
+      int n = 0;
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -1126,13 +1149,8 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
       T1_MARK(4);
     } else {
       double acc[10];
+      gram_sums<10>(sP, sZt, sU, sR, acc);
       int n = 0;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = a; c < 4; ++c) acc[n++] = (double)y[a] * y[c];
-      bsum128<10>(acc, sR);
-      n = 0;
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll

@@ -719,6 +719,15 @@ constexpr int MAX_ROUNDS = 24;
 // X | Zt (4 x N, basis transposed) | U (N x 4) | part (4 waves x N x 4) | reduction scratch
 constexpr size_t LDS_BYTES = (size_t)N * LD * 4 + 4 * N * 4 + N * 4 * 4 + 4 * N * 4 * 4 + 64 * 8;
 
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations, not for
+// its global loads (__syncthreads' release fence would also drain vmcnt, i.e. wait for the
+// next matrix's prefetch at the first barrier after it is issued).
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // 1/sqrt(d) for d > 0: v_rsq_f64 plus one Newton step (the factors below only need to be
 // consistent with each other, not correctly rounded)
 __device__ __forceinline__ double rsq64(double d) {
@@ -841,7 +850,7 @@ __device__ __forceinline__ void bsum128(double (&v)[NV], double* sR) {
 #pragma unroll
       for (int j = 0; j < NV; ++j) sR[w * NV + j] = v[j];
   }
-  __syncthreads();
+  lds_sync();
 #pragma unroll
   for (int j = 0; j < NV; ++j) v[j] = sR[j] + sR[NV + j];
 }
@@ -852,7 +861,7 @@ __device__ __forceinline__ void bsum128(double (&v)[NV], double* sR) {
 // thread returns all NV sums. Y and U are row-major N x 4, Z transposed (4 x N).
 template <int NV>
 __device__ __forceinline__ void gram_sums(const float* sY, const float* sZt, const float* sU,
-                                          double* sRed, double (&out)[NV]) {
+                                          double* sRed) {
   const int t = threadIdx.x, j = t >> 3, c = t & 7;
   double s = 0.0;
   if (j < NV) {
@@ -870,9 +879,19 @@ __device__ __forceinline__ void gram_sums(const float* sY, const float* sZt, con
   s += dpp64<0x4E>(s);   // quad_perm [2, 3, 0, 1]
   s += dpp64<0x141>(s);  // row_half_mirror: the two quads of each 8-lane group
   if (c == 0 && j < NV) sRed[j] = s;
-  __syncthreads();
+  lds_sync();
+}
+
+// symmetric 4 x 4 from the 10 upper-triangle sums at p (gram_sums order)
+__device__ __forceinline__ void sym4(const double* p, double (&M)[4][4]) {
+  int n = 0;
 #pragma unroll
-  for (int q = 0; q < NV; ++q) out[q] = sRed[q];
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = a; c < 4; ++c) {
+      M[a][c] = M[c][a] = p[n];
+      ++n;
+    }
 }
 }  // namespace top1
 
@@ -880,10 +899,10 @@ template <typename TO>
 __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, float tolv,
                                                        int* flags, TO* out, long long ob,
                                                        long long osk, long long osi,
-                                                       long long* phase_clk) {
+                                                       long long batch, long long* phase_clk) {
   using namespace top1;
 #ifdef SPECENH_TOP1_STATS  // development build: shader clocks per phase (thread 0)
-  long long tacc[8] = {}, tlast = __builtin_amdgcn_s_memtime();
+  long long tacc[8], tlast;
 #define T1_MARK(slot)                                      \
   do {                                                     \
     const long long now_ = __builtin_amdgcn_s_memtime();   \
@@ -905,21 +924,27 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
   double* ud = vd + N;                            // N: u = X v
   double* hd = ud + N;                            // N: half sums
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+#ifdef SPECENH_TOP1_STATS
+  for (int q = 0; q < 8; ++q) tacc[q] = 0;
+  tlast = __builtin_amdgcn_s_memtime();
+#endif
   const long long b = blockIdx.x;
+  if (b >= batch) return;
   const float* X = x.base + b * x.batch_stride;
 
   // ---- stage X into LDS (zero-padded), ||X||_F^2 in fp64
   double fro = 0.0;
-  if (x.si == 1) {  // rows of X contiguous: 16-byte loads along i
-    float4 v[N * N / 4 / 256];
+  if (x.si == 1) {  // rows of X contiguous: 16-byte loads along i, all in flight
+    constexpr int NLD = N * N / 4 / 256;
+    float4 v[NLD];
 #pragma unroll
-    for (int u = 0; u < N * N / 4 / 256; ++u) {
+    for (int u = 0; u < NLD; ++u) {
       const int e = tid + 256 * u, k = e >> 5, i = 4 * (e & 31);
       v[u] = (k < Kr && i < r) ? *reinterpret_cast<const float4*>(X + (long long)k * x.sk + i)
                                : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int u = 0; u < N * N / 4 / 256; ++u) {
+    for (int u = 0; u < NLD; ++u) {
       const int e = tid + 256 * u, k = e >> 5, i = 4 * (e & 31);
       *reinterpret_cast<float4*>(sX + k * LD + i) = v[u];
       fro += (double)v[u].x * v[u].x + (double)v[u].y * v[u].y + (double)v[u].z * v[u].z +
@@ -946,7 +971,7 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
     for (int p = 0; p < 4; ++p)  // column 0 all ones (close to v1 for the non-negative
                                    // log spectrograms), the others pseudo-random
       sZt[p * N + tid] = tid < r ? (p == 0 ? 1.f : hash_unit(tid, p)) : 0.f;
-  __syncthreads();
+  lds_sync();
   const double tr = (sR[32] + sR[33]) + (sR[34] + sR[35]);
   T1_MARK(0);
 
@@ -1003,7 +1028,7 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
       }
       *reinterpret_cast<float2*>(sU + 4 * (kb + 32 * (g >> 1)) + 2 * b3) = make_float2(a2[0], a2[1]);
     }
-    __syncthreads();
+    lds_sync();
     T1_MARK(1);
     {  // Y = X^T U: wave w sums its 32 rows, lane halves 16 each
       float a[16];  // [column q][p]
@@ -1033,7 +1058,7 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
       *reinterpret_cast<float4*>(dst) = make_float4(a8[0], a8[1], a8[2], a8[3]);
       *reinterpret_cast<float4*>(dst + 4) = make_float4(a8[4], a8[5], a8[6], a8[7]);
     }
-    __syncthreads();
+    lds_sync();
     if (tid < N) {
       float4 s = *reinterpret_cast<const float4*>(sP + 4 * tid);
 #pragma unroll
@@ -1051,27 +1076,22 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
 #pragma unroll
       for (int p = 0; p < 4; ++p) y[p] = z[p] = uk[p] = 0.f;
     }
-    __syncthreads();
+    lds_sync();
     // Rayleigh-Ritz + residual test at rounds 2, 3, 4, then every second round
     T1_MARK(2);
     const bool check = t >= 2 && (t <= 4 || t % 2 == 0 || t == MAX_ROUNDS);  // uniform
-    double S[4][4];  // Y^T Y
+    // Gram sums in sR: [0, 10) Y^T Y (every round), [10, 20) Z^T Z, [20, 30) U^T U (checks)
     if (check) {
-      double acc[30];  // Y^T Y | Z^T Z | U^T U, upper triangles
-      gram_sums<30>(sP, sZt, sU, sR, acc);
-      double M[4][4], H[4][4], L[4][4], ri[4];
-      int n = 0;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = a; c < 4; ++c) {
-          S[a][c] = S[c][a] = acc[n];
-          M[a][c] = M[c][a] = acc[10 + n];
-          H[a][c] = H[c][a] = acc[20 + n];
-          ++n;
-        }
+      gram_sums<30>(sP, sZt, sU, sR);
+      double L[4][4], ri[4];
+      {
+        double M[4][4];
+        sym4(sR + 10, M);
+        chol4(M, L, ri);
+      }
+      double H[4][4];
+      sym4(sR + 20, H);
       // C = L^-1 H L^-T with M = L L^T (dead basis columns: rows / columns of C zero)
-      chol4(M, L, ri);
       double W[4][4];
       float C[4][4];
 #pragma unroll
@@ -1124,8 +1144,8 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
         gv = fma((double)y[p], q1[p], gv);  // (G v)_i
       }
       double rs[3] = {gv * vi, vi * vi, gv * gv};
-      __syncthreads();  // sR reuse
-      bsum128<3>(rs, sR);
+      lds_sync();  // sR reuse
+      bsum128<3>(rs, sR + 40);
       // fp64 Rayleigh quotient theta = v^T G v / v^T v and the residual of the normalised
       // v: ||G v - theta v||^2 / ||v||^2 = (g.g - theta g.v) / v.v
       const double vv = fmax(rs[1], 1e-300);
@@ -1148,20 +1168,15 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
       }
       T1_MARK(4);
     } else {
-      double acc[10];
-      gram_sums<10>(sP, sZt, sU, sR, acc);
-      int n = 0;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = a; c < 4; ++c) {
-          S[a][c] = S[c][a] = acc[n];
-          ++n;
-        }
+      gram_sums<10>(sP, sZt, sU, sR);
     }
     // Z = Y R^-1 (CholeskyQR, S = R^T R): each thread rewrites its own column of Zt
     double L[4][4], ri[4], yd[4], zd[4];
-    chol4(S, L, ri);
+    {
+      double S[4][4];
+      sym4(sR, S);
+      chol4(S, L, ri);
+    }
     if (tid < N) {
 #pragma unroll
       for (int p = 0; p < 4; ++p) yd[p] = y[p];
@@ -1169,7 +1184,7 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
 #pragma unroll
       for (int p = 0; p < 4; ++p) sZt[p * N + tid] = (float)zd[p];
     }
-    __syncthreads();
+    lds_sync();
     T1_MARK(3);
   }
   // ---- one power step in fp64 from the converged v: v <- X^T X v / ||X^T X v||, then
@@ -1191,11 +1206,11 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
       s1 = fma((double)x4.w, v23.y, s1);
     }
     if (h) hd[k] = s0 + s1;
-    __syncthreads();
+    lds_sync();
     if (!h) ud[k] = (s0 + s1) + hd[k];
-    __syncthreads();
+    lds_sync();
   };
-  __syncthreads();
+  lds_sync();
   Xv();
   {  // w = X^T u: thread (column i, row half h); v = w / ||w||
     const int i = tid & (N - 1), h = tid >> 7;
@@ -1207,12 +1222,12 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
       s1 = fma((double)sX[(k + 1) * LD + i], ud[k + 1], s1);
     }
     if (h) hd[i] = s0 + s1;
-    __syncthreads();
+    lds_sync();
     const double w = h ? 0.0 : (s0 + s1) + hd[i];
     double nn[1] = {w * w};
-    bsum128<1>(nn, sR);
+    bsum128<1>(nn, sR + 40);
     if (!h) vd[i] = nn[0] > 0.0 ? w * rsq64(nn[0]) : 0.0;
-    __syncthreads();
+    lds_sync();
   }
   Xv();
   T1_MARK(5);
@@ -2037,13 +2052,13 @@ hipError_t launch_top1_t(const float* A, long long batch, int m, int n, long lon
   } else {
     xv.sk = 1; xv.si = n; Kr = n; osk = 1; osi = n;
   }
-  for (long long b0 = 0; b0 < batch; b0 += 1LL << 30) {
+  for (long long b0 = 0; b0 < batch; b0 += 1LL << 30) {  // one workgroup per matrix
     const long long nb = std::min<long long>(1LL << 30, batch - b0);
     XView xb = xv;
     xb.base = A + b0 * a_stride;
     SPECENH_LAUNCH(top1_kernel<TO>, dim3((unsigned)nb), dim3(256), top1::LDS_BYTES, st, xb, Kr,
                    r, 5e-6f, flags + b0, reinterpret_cast<TO*>(out) + b0 * (long long)m * n,
-                   (long long)m * n, osk, osi, phase_clk ? phase_clk + 8 * b0 : nullptr);
+                   (long long)m * n, osk, osi, nb, phase_clk ? phase_clk + 8 * b0 : nullptr);
   }
   return hipGetLastError();
 }

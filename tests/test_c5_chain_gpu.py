@@ -83,3 +83,49 @@ def test_c5_chain_matches_cpu_chain(gpu_device, streams):
         assert np.std(ref) > 0.1  # the trained model's output carries a signal
     print("C5 chain out_rel per shot:", ["%.1e" % e for e in errs])
     assert max(errs) <= checks.TOL["float16"]["out_rel"], errs
+
+
+def test_c5_chain_at_bench_launch_shape(gpu_device):
+    """The bench's own 2048-shot launch (bench.make_c5_engine: fused decoder, persistent and
+    wave-split variants, the one-pass SVD), every buffer poisoned with NaN first, checked
+    against the fp64 CPU chain on shots spread over the launch: both ends, the middle, and
+    positions that fall in different workgroups of each persistent grid."""
+    import bench
+    from specenh import pipeline_data, svd
+    from specenh.synthetic import plasma_chirps_torch
+
+    B = 2048
+    x = plasma_chirps_torch(B, L5, seed=777, device=gpu_device, dtype=torch.float16)
+    S = torch.full((B, 128, 128), float("nan"), dtype=torch.float32, device=gpu_device)
+    A = torch.full((B, 128, 128, 1), float("nan"), dtype=torch.float16, device=gpu_device)
+    eng = bench.make_c5_engine(gpu_device)
+    for lst in eng._buffers(B, False).values():  # every activation buffer of this launch
+        for t in (lst if isinstance(lst, list) else [lst]):
+            if torch.is_tensor(t) and t.is_floating_point():
+                t.fill_(float("nan"))
+    pipeline_data.specgr_batch(x, SPEC5, out=S)
+    svd.denoise_batch(S, out=A.view(B, 128, 128))
+    Y = eng.forward(A).float()
+    torch.cuda.synchronize()
+    assert torch.isfinite(Y).all()
+    shots = [0, 1, 511, 512, 1023, 1024, 1337, 2046, 2047]
+    xs = x[shots].double().cpu().numpy()
+    Yg = Y[shots].double().cpu().numpy()
+    Sg = S[shots].double().cpu().numpy()
+    ws = bench.ae_weights()
+    spec = ora.ae_spec()
+    it, params = iter(ws), []
+    for lay in spec:
+        params.append(None if lay[0] == "pool" else
+                      {"W": torch.tensor(next(it), dtype=torch.float64),
+                       "b": torch.tensor(next(it), dtype=torch.float64)})
+    errs = []
+    for j in range(len(shots)):
+        Sx, _, _ = specgr_arrays(xs[j], SPEC5)
+        assert np.abs(Sg[j] - Sx).max() <= 1e-5
+        D = osvd.denoiseSignal(Sx)
+        with torch.no_grad():
+            ref = ora.forward(spec, params, torch.from_numpy(D)[None, :, :, None]).numpy()[0]
+        errs.append(checks.out_rel(Yg[j], ref))
+    print("C5 launch-shape out_rel:", ["%.1e" % e for e in errs])
+    assert max(errs) <= checks.TOL["float16"]["out_rel"], errs

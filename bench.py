@@ -295,16 +295,19 @@ FP32_MFMA_PEAK_TFLOPS = 157.3        # v_mfma_f32_16x16x4_f32 / 32x32x2 (= the F
 
 def c3_matrices(dev, B=4096, m=513, n=256, k=16, seed=3):
     """B gapped m x n fp32 matrices: 16 components 10 * 0.8^i along random orthonormal
-    directions (QR of Gaussian matrices) + Gaussian noise (singular values ~0.003-0.017)."""
+    directions (QR of Gaussian matrices, on the host: the device QR library does not run
+    under rocprofv3 --pmc) + Gaussian noise (singular values ~0.003-0.017)."""
     import torch
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
+    gh = torch.Generator()
+    gh.manual_seed(seed)
     A = torch.empty((B, m, n), dtype=torch.float32, device=dev)
     s_sig = 10.0 * 0.8 ** torch.arange(k, device=dev, dtype=torch.float32)
     for b0 in range(0, B, 512):
         b1 = min(B, b0 + 512)
-        U = torch.linalg.qr(torch.randn((b1 - b0, m, k), generator=g, device=dev)).Q
-        V = torch.linalg.qr(torch.randn((b1 - b0, n, k), generator=g, device=dev)).Q
+        U = torch.linalg.qr(torch.randn((b1 - b0, m, k), generator=gh)).Q.to(dev)
+        V = torch.linalg.qr(torch.randn((b1 - b0, n, k), generator=gh)).Q.to(dev)
         A[b0:b1] = (U * s_sig) @ V.transpose(1, 2) + \
             (0.01 / m ** 0.5) * torch.randn((b1 - b0, m, n), generator=g, device=dev)
         del U, V

@@ -8,14 +8,15 @@
 // rows are contiguous runs of the input row, so the MFMA K index is laid out as (ky, kx)
 // with kx padded to 8: a lane's 8 K-elements are ONE 8-element run of an input row, and
 // one 16x16x32 MFMA covers 4 kernel rows of 16 pixels x 16 output channels (2 MFMAs for
-// K <= 8 rows). The runs are built once per tile in LDS as 16-byte records
-// rec[row][x] = in[row][x .. x+7] (funnel shifts of the staged rows), so every B fragment
-// is one conflict-free ds_read_b128 (16 lanes = 16 consecutive pixels = 256 contiguous
-// bytes). Weights (the A operand: rows = output channels, kx >= K zero) stay in registers
-// for the whole workgroup.
+// K <= 8 rows). The staged rows are kept twice in LDS as 32-bit words, as loaded and
+// shifted by one element, so every run starts on a word of one copy and a B fragment is
+// four word reads (no per-pixel record building). Weights (the A operand: rows = output
+// channels, kx >= K zero) stay in registers for the whole workgroup.
 //
 // Workgroup: a 32 x 32 output tile x 16 output channels (blockIdx.y), 4 waves of 8 output
-// rows x 2 blocks of 16 columns. Epilogues as in conv_patch_kernel (csrc/conv_ae.hip):
+// rows x 2 column blocks: block cb holds the pixels x = 2 l16 + cb, so the 2x2 max-pool
+// window of a lane's pooled pixel is in its own accumulators (no cross-lane exchange, every
+// lane stores). Epilogues as in conv_patch_kernel (csrc/conv_ae.hip):
 // fused 2x2 max-pool (+ argmax; values compared as stored in T, first max wins; without
 // argmax the max accumulator is taken first, a monotone map, bitwise the same), or plain
 // stores with the optional ReLU mask of the backward pass (act(0) = 0 there).
@@ -48,8 +49,10 @@ struct C1mArgs {
 };
 
 constexpr int TILE = 32;
-constexpr int PRW = TILE + 8;  // staged row: 40 elements (32 + K - 1 <= 39)
-constexpr int PRS = 40;        // patch rows (32 + K - 1 <= 39), + 1 for clamped reads
+constexpr int PRS = 40;  // patch rows (32 + K - 1 <= 39), + 1 for clamped reads
+constexpr int RW = 20;   // staged row: 20 words = 40 elements (runs start at <= 32, 8 long)
+constexpr int RDW = 48;  // LDS row pitch in words: the 4 kernel-row lane groups of a
+                         // fragment read sit 48 = -16 (mod 64) banks apart: conflict-free
 
 template <typename T>
 __device__ __forceinline__ float tof(T x) { return (float)x; }
@@ -87,34 +90,49 @@ __device__ __forceinline__ float act_f(float v, int act) {
   return v;
 }
 
-template <typename T, bool POOL>
+template <typename T, bool POOL, int PAR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv_c1_mfma_kernel(C1mArgs a) {
-  __shared__ __attribute__((aligned(16))) T sRow[PRS * PRW];
-  __shared__ __attribute__((aligned(16))) uint4 sRec[PRS * TILE];
+  // Staged rows as 32-bit words: P0[r][j] = elements (2j, 2j+1) of staged row r, and the
+  // copy shifted by one element P1[r][j] = (2j+1, 2j+2). Every 8-element run a fragment
+  // needs then starts on a word of one of them (even start: P0, odd start: P1).
+  __shared__ uint32_t sP0[PRS * RDW], sP1[PRS * RDW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntx = (a.OW + TILE - 1) / TILE, nty = (a.OH + TILE - 1) / TILE;
-  const int ntiles = a.N * ntx * nty;
+  const int tpi = ntx * nty;  // tiles per image; gridDim.x is a multiple of it
   const int co0 = blockIdx.y * 16;
   const int K = a.K, PR = TILE + K - 1;
+  // PAR = pad_l & 1: staged rows start at the even element ix0 - PAR
+  // this workgroup's tile position (fixed) and images n0, n0 + nstep, ...
+  const int trem = blockIdx.x % tpi, n0 = blockIdx.x / tpi, nstep = gridDim.x / tpi;
+  const int oy0 = (trem / ntx) * TILE, ox0 = (trem % ntx) * TILE;
+  const int iy0 = oy0 - a.pad_t, ix0 = ox0 - a.pad_l - PAR;
   const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
   const T* __restrict__ W = reinterpret_cast<const T*>(a.w);
 
-  // a tile's patch rows -> registers (all loads in flight, zero outside the image)
-  constexpr int NE = (PRS * PRW + 255) / 256;
-  T v[NE];
-  auto fetch = [&](int tile) {
-    const int n = tile / (ntx * nty), trem = tile - n * (ntx * nty);
-    const int iy0 = (trem / ntx) * TILE - a.pad_t;
-    const int ix0 = (trem - (trem / ntx) * ntx) * TILE - a.pad_l;
+  // a tile's patch rows -> registers as words (all loads in flight, zero outside the image;
+  // IW even and the word start even, so a word is entirely inside or outside). The
+  // per-thread (row, word) slots and their in-image test are the same for every image.
+  constexpr int NW = (PRS * RW + 255) / 256;
+  uint32_t v[NW];
+  int woff[NW];  // element offset of the word in an image, -1: zero
+  int soff[NW];  // LDS word index, -1: none
 #pragma unroll
-    for (int k = 0; k < NE; ++k) {
-      const int e = tid + 256 * k;
-      const int r = e / PRW, c = e - (e / PRW) * PRW;
-      const int iy = iy0 + r, ix = ix0 + c;
-      const bool ok = e < PRS * PRW && r < PR && (unsigned)iy < (unsigned)a.IH &&
-                      (unsigned)ix < (unsigned)a.IW;
-      v[k] = in[ok ? ((long long)n * a.IH + iy) * a.IW + ix : 0];
-      if (!ok) v[k] = (T)0.f;
+  for (int k = 0; k < NW; ++k) {
+    const int e = tid + 256 * k;
+    const int r = e / RW, j = e - (e / RW) * RW;
+    const int iy = iy0 + r, ix = ix0 + 2 * j;
+    const bool ok = e < PRS * RW && r < PR && (unsigned)iy < (unsigned)a.IH &&
+                    (unsigned)ix < (unsigned)a.IW;
+    woff[k] = ok ? iy * a.IW + ix : -1;
+    soff[k] = e < PRS * RW ? r * RDW + j : -1;
+  }
+  const long long img = (long long)a.IH * a.IW;
+  auto fetch = [&](int n) {
+    const T* src = in + n * img;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      v[k] = *reinterpret_cast<const uint32_t*>(src + (woff[k] >= 0 ? woff[k] : 0));
+      if (woff[k] < 0) v[k] = 0u;
     }
   };
   // ---- weights (A operand): lane = (co = lane & 15, kernel row 4 s + (lane >> 4)) ----
@@ -143,37 +161,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   // would also wait for the prefetch and (CDNA4 vmcnt counts stores) the previous stores
   __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0)
 
-  // persistent over tiles blockIdx.x, + gridDim.x, ...: the next tile's rows are loaded
-  // into registers while this tile's records, MFMAs and stores run
-  int tile = blockIdx.x;
-  if (tile < ntiles) fetch(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
-  const int n = tile / (ntx * nty);
-  const int trem = tile - n * (ntx * nty);
-  const int oy0 = (trem / ntx) * TILE, ox0 = (trem - (trem / ntx) * ntx) * TILE;
-  __syncthreads();  // the previous tile's record reads are done
+  // persistent over images n0, n0 + nstep, ... at a fixed tile position: the next image's
+  // rows are loaded into registers while this one's MFMAs and stores run
+  if (n0 < a.N) fetch(n0);
+  for (int n = n0; n < a.N; n += nstep) {
+  __syncthreads();  // the previous tile's fragment reads are done
 #pragma unroll
-  for (int k = 0; k < NE; ++k)
-    if (tid + 256 * k < PRS * PRW) sRow[tid + 256 * k] = v[k];
+  for (int k = 0; k < NW; ++k)
+    if (soff[k] >= 0) sP0[soff[k]] = v[k];
   __syncthreads();
-  // ---- records rec[r][x] = row r, elements x .. x+7 ----
-  const uint32_t* rw = reinterpret_cast<const uint32_t*>(sRow);
-  for (int e = tid; e < PRS * TILE; e += 256) {
-    const int r = e / TILE, x = e - (e / TILE) * TILE;
-    const uint32_t* p = rw + (r * PRW + (x & ~1)) / 2;
-    uint32_t d[5];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) d[k] = p[k];
-    uint32_t o[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) o[k] = (x & 1) ? __builtin_amdgcn_alignbit(d[k + 1], d[k], 16) : d[k];
-    sRec[e] = uint4{o[0], o[1], o[2], o[3]};
-  }
+  for (int k = 0; k < NW; ++k)  // the shifted copy (word RW of a row, element 40, unused)
+    if (soff[k] >= 0) sP1[soff[k]] = __builtin_amdgcn_alignbit(sP0[soff[k] + 1], sP0[soff[k]], 16);
   __syncthreads();
-  if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
+  if (n + nstep < a.N) fetch(n + nstep);
 
   // ---- MFMAs: wave rows 8 wave + 4 hf + i (two halves of 4 rows: half the accumulator
-  // registers live at a time), column blocks cb (pixels 16 cb + l16) ----
+  // registers live at a time). Column block cb holds the pixels x = 2 l16 + cb, so a 2x2
+  // pooling window is (acc[2ip][0..1], acc[2ip+1][0..1]) of ONE lane. Pixel x's run starts
+  // at staged element x + PAR: P0 word l16 + PAR when cb == PAR, else P1 word l16.
   const int nks = (K + 3) / 4;
 #pragma unroll 1
   for (int hf = 0; hf < 2; ++hf) {
@@ -188,68 +194,67 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         if (s >= nks) break;  // uniform
-        const int r = min(rw0 + i + 4 * s + g4, PRS - 1);  // rows past K meet zero weights
-        acc[i][cb] = mfma<T>(wf[s], sRec[r * TILE + 16 * cb + l16], acc[i][cb]);
+        const int r = rw0 + i + 4 * s + g4;  // <= 38 < PRS; rows past K meet zero weights
+        const uint32_t* q = (cb == PAR ? sP0 + PAR : sP1) + r * RDW + l16;
+        acc[i][cb] = mfma<T>(wf[s], uint4{q[0], q[1], q[2], q[3]}, acc[i][cb]);
       }
 
-  // ---- epilogue: lane holds channels co0 + 4 g4 + r of pixel (8 wave + i, 16 cb + l16) ----
+  // ---- epilogue: lane holds channels co0 + 4 g4 + r of pixels (rw0 + i, 2 l16 + cb) ----
   const int ch0 = co0 + 4 * g4;
   const bool vec = (a.CO & 3) == 0;
   if constexpr (POOL) {
     const int PHo = a.OH / 2, PWo = a.OW / 2;
 #pragma unroll
-    for (int ip = 0; ip < 2; ++ip)
+    for (int ip = 0; ip < 2; ++ip) {
+      const int py = (oy0 + rw0 + 2 * ip) / 2, px = ox0 / 2 + l16;
+      const bool store = py < PHo && px < PWo && ch0 < a.CO;
+      const long long o = (((long long)n * PHo + py) * PWo + px) * a.CO + ch0;
+      T* dst = reinterpret_cast<T*>(a.out) + o;
+      float m[4];
+      unsigned arg4 = 0;
+      if (!a.argmax && a.act <= 1) {
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const int ox = ox0 + 16 * cb + l16;
-        const int py = (oy0 + rw0 + 2 * ip) / 2, px = ox / 2;
-        const bool store = (l16 & 1) == 0 && py < PHo && px < PWo && ch0 < a.CO;
-        const long long o = (((long long)n * PHo + py) * PWo + px) * a.CO + ch0;
-        T* dst = reinterpret_cast<T*>(a.out) + o;
-        float m[4];
-        unsigned arg4 = 0;
-        if (!a.argmax && a.act <= 1) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float m1 = vmax(acc[2 * ip][cb][r], acc[2 * ip + 1][cb][r]);
-            const float v = vmax(m1, __shfl_xor(m1, 1)) + bv[r];
-            m[r] = a.act == 1 ? vmax(v, 0.f) : v;
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float v00 = tof((T)act_f(acc[2 * ip][cb][r] + bv[r], a.act));
-            const float v10 = tof((T)act_f(acc[2 * ip + 1][cb][r] + bv[r], a.act));
-            const float v01 = __shfl_xor(v00, 1), v11 = __shfl_xor(v10, 1);
-            float b = v00;
-            unsigned q = 0;
-            if (v01 > b) { b = v01; q = 1; }
-            if (v10 > b) { b = v10; q = 2; }
-            if (v11 > b) { b = v11; q = 3; }
-            m[r] = b;
-            arg4 |= q << (8 * r);
-          }
+        for (int r = 0; r < 4; ++r) {
+          const float v = vmax(vmax(acc[2 * ip][0][r], acc[2 * ip][1][r]),
+                               vmax(acc[2 * ip + 1][0][r], acc[2 * ip + 1][1][r])) + bv[r];
+          m[r] = a.act == 1 ? vmax(v, 0.f) : v;
         }
-        if (!store) continue;
-        if (vec) {
-          *reinterpret_cast<uint2*>(dst) = uint2{pack2<T>(m[0], m[1]), pack2<T>(m[2], m[3])};
-          if (a.argmax) *reinterpret_cast<unsigned*>(a.argmax + o) = arg4;
-        } else {
+      } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (ch0 + r < a.CO) {
-              dst[r] = (T)m[r];
-              if (a.argmax) a.argmax[o + r] = (unsigned char)(arg4 >> (8 * r));
-            }
+        for (int r = 0; r < 4; ++r) {
+          const float v00 = tof((T)act_f(acc[2 * ip][0][r] + bv[r], a.act));
+          const float v01 = tof((T)act_f(acc[2 * ip][1][r] + bv[r], a.act));
+          const float v10 = tof((T)act_f(acc[2 * ip + 1][0][r] + bv[r], a.act));
+          const float v11 = tof((T)act_f(acc[2 * ip + 1][1][r] + bv[r], a.act));
+          float b = v00;
+          unsigned q = 0;
+          if (v01 > b) { b = v01; q = 1; }
+          if (v10 > b) { b = v10; q = 2; }
+          if (v11 > b) { b = v11; q = 3; }
+          m[r] = b;
+          arg4 |= q << (8 * r);
         }
       }
+      if (!store) continue;
+      if (vec) {
+        *reinterpret_cast<uint2*>(dst) = uint2{pack2<T>(m[0], m[1]), pack2<T>(m[2], m[3])};
+        if (a.argmax) *reinterpret_cast<unsigned*>(a.argmax + o) = arg4;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (ch0 + r < a.CO) {
+            dst[r] = (T)m[r];
+            if (a.argmax) a.argmax[o + r] = (unsigned char)(arg4 >> (8 * r));
+          }
+      }
+    }
   } else {
     const T* __restrict__ mk = reinterpret_cast<const T*>(a.mask);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
-        const int oy = oy0 + rw0 + i, ox = ox0 + 16 * cb + l16;
+        const int oy = oy0 + rw0 + i, ox = ox0 + 2 * l16 + cb;
         if (oy >= a.OH || ox >= a.OW || ch0 >= a.CO) continue;
         const long long o = (((long long)n * a.OH + oy) * a.OW + ox) * a.CO + ch0;
         float v[4];
@@ -279,24 +284,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       }
   }
   }  // row halves
-  }  // tile loop
+  }  // images
+}
+
+template <typename T, bool POOL>
+int launch_t(const C1mArgs& a, hipStream_t st) {
+  const long long tpi = (long long)((a.OH + TILE - 1) / TILE) * ((a.OW + TILE - 1) / TILE);
+  const int cus = device_cus();
+  const bool par = a.pad_l & 1;
+  const void* fn = par ? (const void*)conv_c1_mfma_kernel<T, POOL, 1>
+                       : (const void*)conv_c1_mfma_kernel<T, POOL, 0>;
+  static int per_cu[2] = {0, 0};
+  int& pc = per_cu[POOL ? 1 : 0];
+  if (pc == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, fn, 256, 0) != hipSuccess || pc <= 0))
+    pc = 2;
+  const unsigned cob = (unsigned)((a.CO + 15) / 16);
+  // persistent: each workgroup keeps one tile position and walks the images; as many
+  // image groups as fill the resident slots (at least one)
+  const long long groups = std::max<long long>(1, std::min<long long>(a.N, (long long)pc * cus / cob / tpi));
+  const dim3 grid((unsigned)(groups * tpi), cob);
+  if (par) SPECENH_LAUNCH((conv_c1_mfma_kernel<T, POOL, 1>), grid, dim3(256), 0, st, a);
+  else SPECENH_LAUNCH((conv_c1_mfma_kernel<T, POOL, 0>), grid, dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? 1 : set_error(SPECENH_EHIP, "conv_c1_mfma launch");
 }
 
 template <typename T>
 int launch(const C1mArgs& a, bool pool, hipStream_t st) {
-  const long long tiles = (long long)a.N * ((a.OH + TILE - 1) / TILE) * ((a.OW + TILE - 1) / TILE);
-  const int cus = device_cus();
-  // persistent workgroups, as many as are resident at once, each over a run of tiles
-  const void* fn = pool ? (const void*)conv_c1_mfma_kernel<T, true> : (const void*)conv_c1_mfma_kernel<T, false>;
-  static int per_cu[2] = {0, 0};
-  int& pc = per_cu[pool ? 1 : 0];
-  if (pc == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, fn, 256, 0) != hipSuccess || pc <= 0))
-    pc = 2;
-  const unsigned cob = (unsigned)((a.CO + 15) / 16);
-  const dim3 grid((unsigned)std::max<long long>(1, std::min<long long>(tiles, (long long)pc * cus / cob)), cob);
-  if (pool) SPECENH_LAUNCH((conv_c1_mfma_kernel<T, true>), grid, dim3(256), 0, st, a);
-  else SPECENH_LAUNCH((conv_c1_mfma_kernel<T, false>), grid, dim3(256), 0, st, a);
-  return hipGetLastError() == hipSuccess ? 1 : set_error(SPECENH_EHIP, "conv_c1_mfma launch");
+  return pool ? launch_t<T, true>(a, st) : launch_t<T, false>(a, st);
 }
 
 }  // namespace
@@ -313,7 +327,10 @@ int launch_conv_c1_mfma(int dtype, const void* in, int N, int IH, int IW, int C,
   // the VALU kernel (tools/c1_bench.py: 630 vs 834 us per 2048 shots, fp16)
   if (mask) return 0;
   if (pool && ((OH & 1) || (OW & 1))) return 0;
-  if ((long long)N * ((OH + TILE - 1) / TILE) * ((OW + TILE - 1) / TILE) >= (1LL << 31)) return 0;
+  if ((IW & 1) || ((uintptr_t)in & 3)) return 0;  // staged as 32-bit words
+  if ((long long)((OH + TILE - 1) / TILE) * ((OW + TILE - 1) / TILE) >= (1LL << 24) ||
+      (long long)IH * IW >= (1LL << 31))
+    return 0;
   C1mArgs a{in, w, bias, out, mask, argmax, N, IH, IW, OH, OW, CO, KH, pad_t, pad_l, act};
   if (dtype == SPECENH_DTYPE_BF16) return launch<__bf16>(a, pool != 0, st);
   return launch<_Float16>(a, pool != 0, st);

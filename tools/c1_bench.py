@@ -42,10 +42,8 @@ def main():
         full = torch.empty(N, H, H, 16, device=dev, dtype=dt)
         mask = torch.randn(N, H, H, 16, device=dev, dtype=dt)
         for path in ("mfma", "valu"):
-            if path == "valu":
-                os.environ["SPECENH_CONV_NO_C1MFMA"] = "1"
-            else:
-                os.environ.pop("SPECENH_CONV_NO_C1MFMA", None)
+            from specenh import _lib  # the variant switch (the environment is read once)
+            _lib.set_variant("CONV_NO_C1MFMA", 1 if path == "valu" else 0)
             t_pool = timeit(lambda: torch.ops.specenh.conv2d_out(
                 x, w, b, 5, 5, 16, 1, 2, 2, 1, H, H, 1, None, None, pooled, True, None), a.reps)
             t_mask = timeit(lambda: torch.ops.specenh.conv2d_out(

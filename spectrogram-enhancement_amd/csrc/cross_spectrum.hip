@@ -9,6 +9,10 @@
 //   output (F, T) frequency-major, F = N/2 + 1.
 // scipy.signal.csd is the mean of Pxy over T. Parity is pinned against scipy (not ae_co2).
 //
+// AMPLITUDE mode (|Pxy|, what crosspowerspec.py plots) runs on the STFT team schedule
+// (stft_psd.hip, stft_team_kernel MODE 3): |Pxy| = sqrt(PSD_x PSD_y) from the same
+// two-for-one FFT pairs, frames staged as (bins x frames) tiles so the stores are whole
+// frequency-row segments. csd_kernel below is the COMPLEX mode and the fallback:
 // One workgroup per (frame, signal pair). Both real frames ride in one complex FFT,
 // z = x_w + i*y_w, and separate afterwards: X_k = (Z_k + conj Z_{N-k}) / 2,
 // Y_k = (Z_k - conj Z_{N-k}) / 2i. Detrend sums in fp64 (wave butterflies + LDS);
@@ -23,8 +27,13 @@
 #include "specenh.h"
 #include "runtime.hpp"
 
+struct specenh_stft_plan;
+
 namespace specenh {
 int set_error(int code, const std::string& msg);  // stft_psd.hip
+int stft_csd_amplitude(const specenh_stft_plan* plan, const float* x, const float* y,
+                       long long batch, long long length, long long x_stride, long long y_stride,
+                       float* out, hipStream_t stream, bool* launched);  // stft_psd.hip
 }
 
 struct specenh_csd_plan {
@@ -33,6 +42,9 @@ struct specenh_csd_plan {
   float* d_window;
   float2* d_tw;
   int device;
+  // amplitude mode: the STFT team schedule (stft_team_kernel MODE 3) with this plan's
+  // window / detrend / scaling; null when the STFT plan does not support nperseg
+  specenh_stft_plan* stft;
 };
 
 namespace specenh {
@@ -206,12 +218,17 @@ int specenh_csd_plan_create(specenh_csd_plan** plan, int nperseg, int noverlap,
     delete p;
     return set_error(SPECENH_EHIP, std::string("csd plan: ") + hipGetErrorString(e));
   }
+  if (N <= 1024 &&
+      specenh_stft_plan_create(&p->stft, N, noverlap, window_host, fs, scaling, detrend, 0.0) !=
+          SPECENH_OK)
+    p->stft = nullptr;  // amplitude mode then runs csd_kernel
   *plan = p;
   return SPECENH_OK;
 }
 
 int specenh_csd_plan_destroy(specenh_csd_plan* plan) {
   if (!plan) return SPECENH_OK;
+  if (plan->stft) specenh_stft_plan_destroy(plan->stft);
   (void)hipFree(plan->d_window);
   (void)hipFree(plan->d_tw);
   delete plan;
@@ -233,6 +250,13 @@ int specenh_csd(const specenh_csd_plan* plan, const float* x, const float* y, lo
   if (batch > 65535 || T > 2147483647LL)
     return set_error(SPECENH_EUNSUPPORTED, "cross spectrum: batch <= 65535 signal pairs per call");
   if (x_stride < length || y_stride < length) return set_error(SPECENH_EINVAL, "stride < length");
+  if (mode == SPECENH_CSD_AMPLITUDE && plan->stft) {
+    bool launched = false;
+    const int rc = specenh::stft_csd_amplitude(plan->stft, x, y, batch, length, x_stride, y_stride,
+                                               reinterpret_cast<float*>(out), (hipStream_t)stream,
+                                               &launched);
+    if (rc != SPECENH_OK || launched) return rc;
+  }
   specenh::CsdArgs a;
   a.x = x; a.y = y; a.xs = x_stride; a.ys = y_stride;
   a.T = (int)T; a.N = plan->N; a.step = plan->step; a.detrend = plan->detrend;

@@ -88,6 +88,9 @@ struct StftArgs {
   double dc_alpha;
   double dc_beta;
   const double* dc_coef;  // the same c_n as a table (fp64), staged in LDS when it fits
+  // cross spectrum (stft_team_kernel MODE 3): the second signal of each pair
+  const float* y;
+  long long y_stride;
 };
 
 // Per-N decomposition: G lanes per FFT, WAVES per workgroup, Stockham radices.
@@ -305,16 +308,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
 }
 
 // XH: the samples are fp16 (the C5 stream's shots), widened to fp32 on load (exact).
-template <int N, bool XH = false>
-__device__ __forceinline__ void load_pair(PairSamples<N>& s, __amdgpu_buffer_rsrc_t xr, int hop,
-                                          int fa, int T, int gl) {
+// XY: the pair is frame fa of two signals (x from xr, y from yr: the cross spectrum);
+// otherwise frames fa and fa + 1 of one signal (yr is unused).
+template <int N, bool XH = false, bool XY = false>
+__device__ __forceinline__ void load_pair(PairSamples<N>& s, __amdgpu_buffer_rsrc_t xr,
+                                          __amdgpu_buffer_rsrc_t yr, int hop, int fa, int T,
+                                          int gl) {
   constexpr int G = Cfg<N>::G;
   constexpr int NB1 = N / Cfg<N>::R1;
   constexpr int ES = XH ? 2 : 4;  // bytes per sample
   // Frames past the end duplicate the last frame: their spectra equal a valid one, so
   // they cannot move the min/max and need no masking; they are never stored.
   const int oa = ((fa < T ? fa : T - 1) * hop + gl) * ES;
-  const int ob = ((fa + 1 < T ? fa + 1 : T - 1) * hop + gl) * ES;
+  const int ob = XY ? oa : ((fa + 1 < T ? fa + 1 : T - 1) * hop + gl) * ES;
+  const __amdgpu_buffer_rsrc_t br = XY ? yr : xr;
   // The per-register offset o goes in the scalar soffset operand (an SGPR constant): as a
   // VGPR add it would cost one VALU op per load (the compiler does not fold it into the
   // instruction's immediate offset).
@@ -329,12 +336,12 @@ __device__ __forceinline__ void load_pair(PairSamples<N>& s, __amdgpu_buffer_rsr
       const int o = sbase + (i * G + r * NB1) * ES;
       if constexpr (XH) {
         const unsigned short ha = __builtin_amdgcn_raw_buffer_load_b16(xr, oa, o, 0);
-        const unsigned short hb = __builtin_amdgcn_raw_buffer_load_b16(xr, ob, o, 0);
+        const unsigned short hb = __builtin_amdgcn_raw_buffer_load_b16(br, ob, o, 0);
         s.x[i][r] = f2v{(float)__builtin_bit_cast(_Float16, ha),
                         (float)__builtin_bit_cast(_Float16, hb)};
       } else {
         s.x[i][r] = f2v{__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, oa, o, 0)),
-                        __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ob, o, 0))};
+                        __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(br, ob, o, 0))};
       }
     }
 }
@@ -344,13 +351,13 @@ __device__ __forceinline__ void load_pair(PairSamples<N>& s, __amdgpu_buffer_rsr
 // bins gl + i*G into pv[i] = (frame a, frame b) and the running min/max. DC bins come
 // from the fp64 path. With `prefetch`, the next tile's samples are loaded into `nxt` while
 // this pair computes (`in` and `nxt` may be the same set: `in` is consumed first).
-template <int N, bool XH = false>
+template <int N, bool XH = false, bool XY = false>
 __device__ __forceinline__ void pair_spectrum(const StftArgs& a, const PairSamples<N>& in,
                                               PairSamples<N>& nxt, const f2v* s_tw,
                                               const float* s_win, const double* s_dc,
                                               float* buf, int gl,
                                               double dc_base, __amdgpu_buffer_rsrc_t xr,
-                                              int fa_next, bool prefetch, bool want_log,
+                                              __amdgpu_buffer_rsrc_t yr, int fa_next, bool prefetch, bool want_log,
                                               bool log2_out, f2v (&pv)[Layout<N>::IB],
                                               float& lmin, float& lmax) {
   using C = Cfg<N>;
@@ -442,7 +449,8 @@ __device__ __forceinline__ void pair_spectrum(const StftArgs& a, const PairSampl
   auto issue_prefetch = [&]() {  // fences keep the loads after the FFT's reads of `in`
     __builtin_amdgcn_sched_barrier(0);
     if (prefetch)
-      load_pair<N, XH>(nxt, xr, a.hop, (a.flags & SPECENH_STFT_DEV_NOLOAD) ? 0 : fa_next, a.T, gl);
+      load_pair<N, XH, XY>(nxt, xr, yr, a.hop, (a.flags & SPECENH_STFT_DEV_NOLOAD) ? 0 : fa_next,
+                           a.T, gl);
     __builtin_amdgcn_sched_barrier(0);
   };
   // ---- Stockham passes 2 (and 3) ----
@@ -637,6 +645,57 @@ __device__ __forceinline__ void tile_store(const StftArgs& a, float* s_tile,
   lds_barrier();
 }
 
+// Cross-spectrum tiles (stft_team_kernel MODE 3): one frame per lane group, so the tile is
+// FFTS = TF / 2 frames wide, NBINS rows at an odd stride TS1 (the 4-B writes of a lane
+// group's bins k = gl + i G land in distinct banks). Same barrier discipline as tile_store.
+template <int N>
+struct Tile1 {
+  using Lo = Layout<N>;
+  static constexpr int TF1 = Lo::FFTS;
+  static constexpr int LOG_TF1 = ilog2(TF1);
+  static constexpr int TS1 = TF1 + 1;
+  static_assert(Lo::NBINS * TS1 * 4 <= Lo::REGION - 16, "one-frame tile fits the FFT buffers");
+  static_assert(Lo::THREADS % TF1 == 0, "row groups");
+};
+
+template <int N>
+__device__ __forceinline__ void tile_store1(const StftArgs& a, float* s_tile,
+                                            const float (&pv)[Layout<N>::IB], int gl, int fi,
+                                            int tid, __amdgpu_buffer_rsrc_t orr, int t0) {
+  using Lo = Layout<N>;
+  using T1 = Tile1<N>;
+  constexpr int G = Cfg<N>::G;
+  lds_barrier();  // every group is done with its FFT buffer
+#pragma unroll
+  for (int i = 0; i < Lo::IB; ++i) {
+    const int k = gl + i * G;
+    if (k < Lo::NBINS) s_tile[k * T1::TS1 + fi] = pv[i];
+  }
+  lds_barrier();
+  // rows out as segments out[k][t0 : t0 + TF1]; rows past F_out and frames past T fall
+  // outside the descriptor (dropped), as in tile_emit
+  const int tfv = min(T1::TF1, a.T - t0);
+  constexpr int ROWS_PER_IT = Lo::THREADS >> T1::LOG_TF1;
+  constexpr int ST = (Lo::NBINS + ROWS_PER_IT - 1) / ROWS_PER_IT;
+  constexpr int GRP = 9;
+  const int k0 = tid >> T1::LOG_TF1;
+  const int f = tid & (T1::TF1 - 1);
+  const int voff = f < tfv ? (k0 * a.T + t0 + f) * 4 : (1 << 30);
+  const int sstep = ROWS_PER_IT * a.T * 4;
+#pragma unroll
+  for (int g0 = 0; g0 < ST; g0 += GRP) {
+    float v[GRP];
+#pragma unroll
+    for (int u = 0; u < GRP; ++u)
+      if (g0 + u < ST) v[u] = s_tile[min(k0 + (g0 + u) * ROWS_PER_IT, Lo::NBINS - 1) * T1::TS1 + f];
+#pragma unroll
+    for (int u = 0; u < GRP; ++u)
+      if (g0 + u < ST)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[u]), orr, voff, (g0 + u) * sstep, 0);
+  }
+  lds_barrier();  // tile (= FFT buffers) free for the next tile's FFTs
+}
+
 // Per-lane base of the DC coefficients: alpha + beta * (gl - (N-1)/2).
 template <int N>
 __device__ __forceinline__ double dc_lane_base(const StftArgs& a, int gl) {
@@ -689,15 +748,15 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
 
   const __amdgpu_buffer_rsrc_t orr = make_rsrc(o_shot, (long long)a.F_out * a.T * 4);
   PairSamples<N> s0;
-  if constexpr (C::PF) load_pair<N, XH>(s0, xr, a.hop, 2 * fi, a.T, gl);
+  if constexpr (C::PF) load_pair<N, XH>(s0, xr, xr, a.hop, 2 * fi, a.T, gl);
   __syncthreads();
 
   for (int tile = 0; tile < ntiles; ++tile) {
     const int t0 = tile * Lo::TF;
     const int fa = t0 + 2 * fi;  // tail frames are clamped duplicates (load_pair)
-    if constexpr (!C::PF) load_pair<N, XH>(s0, xr, a.hop, fa, a.T, gl);
+    if constexpr (!C::PF) load_pair<N, XH>(s0, xr, xr, a.hop, fa, a.T, gl);
     f2v pv[IB];
-    pair_spectrum<N, XH>(a, s0, s0, s_tw, s_win, s_dc, buf, gl, dcb, xr, fa + Lo::TF, C::PF != 0,
+    pair_spectrum<N, XH>(a, s0, s0, s_tw, s_win, s_dc, buf, gl, dcb, xr, xr, fa + Lo::TF, C::PF != 0,
                          want_log, log2_out, pv, lmin, lmax);
     tile_store<N>(a, s_tile, pv, gl, fi, tid, orr, t0, 0.f, 1.f, false);
   }
@@ -819,7 +878,15 @@ __device__ __forceinline__ bool team_minmax(const unsigned long long* g, int M, 
 }
 
 // MODE (compile time, so each schedule keeps its own register allocation): 0 = plain
-// PSD, 1 = log PSD (independent tiles: no granules, no waits), 2 = NORMALIZE (teams).
+// PSD, 1 = log PSD (independent tiles: no granules, no waits), 2 = NORMALIZE (teams),
+// 3 = cross-spectrum amplitude |Pxy| of the signal pairs (x[b], y[b]) (independent tiles).
+// MODE 3 runs the same FFT pairs with the two frames of a pair taken from x and y at one
+// time t: the separated spectra are X_t and Y_t, and |Pxy| = |conj(X) Y| * scale * (2 off
+// DC/Nyquist) = sqrt(PSD_x * PSD_y), from the two PSD values pair_spectrum forms anyway
+// (DC from the fp64 path as for the PSD). A lane group runs one pair per tile, so a
+// member's tile is TF / 2 frames (tile_store1). (Two pairs per group for a TF-wide tile
+// held one frame's amplitudes across the second FFT: 88 VGPRs spilled at 3 waves per SIMD,
+// and at 2 waves per SIMD it ran 1.61 ms at C2.)
 template <int N, int MODE>
 __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_kernel(
     StftArgs a, unsigned long long* gran, long long batch, int M, int Q, unsigned* tmo,
@@ -863,10 +930,35 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
   // Without NORMALIZE the tiles are independent: the same persistent tile-parallel
   // schedule, no granules and no waits (log or plain PSD values stored as computed).
   constexpr bool normalize = MODE == 2;
-  constexpr bool want_log = MODE >= 1;
+  constexpr bool want_log = MODE == 1 || MODE == 2;
+  constexpr bool xy = MODE == 3;
 
   PairSamples<N> s0;
-  load_pair<N>(s0, make_rsrc(a.x + q * a.x_stride, xbytes), a.hop, fa, a.T, gl);
+  if constexpr (xy) {
+    // one frame per lane group: tile frames [mem * TF1, + TF1), frame t1 + fi per group
+    const int t1 = mem * Tile1<N>::TF1;
+    const int f1 = t1 + fi;
+    const long long ybytes = a.y_stride * 4;
+    load_pair<N, false, true>(s0, make_rsrc(a.x + q * a.x_stride, xbytes),
+                              make_rsrc(a.y + q * a.y_stride, ybytes), a.hop, f1, a.T, gl);
+    __syncthreads();
+    for (long long it = 0; it < ntask; ++it) {
+      const long long shot = q + it * Q;
+      const long long nshot = it + 1 < ntask ? shot + Q : shot;
+      float dmin = INFINITY, dmax = -INFINITY;  // (pair_spectrum's running extremes: unused)
+      f2v pv[IB];
+      pair_spectrum<N, false, true>(a, s0, s0, s_tw, s_win, s_dc, buf, gl, dcb,
+                                    make_rsrc(a.x + nshot * a.x_stride, xbytes),
+                                    make_rsrc(a.y + nshot * a.y_stride, ybytes), f1, true, false,
+                                    false, pv, dmin, dmax);
+      float amp[IB];
+#pragma unroll
+      for (int i = 0; i < IB; ++i) amp[i] = __builtin_sqrtf(pv[i].x) * __builtin_sqrtf(pv[i].y);
+      tile_store1<N>(a, s_tile, amp, gl, fi, tid, make_rsrc(a.out + shot * plane, plane * 4), t1);
+    }
+    return;
+  }
+  load_pair<N>(s0, make_rsrc(a.x + q * a.x_stride, xbytes), make_rsrc(a.x, 0), a.hop, fa, a.T, gl);
   __syncthreads();
 
   // Per task: the tile's spectrum (next task's samples prefetched meanwhile), publish the
@@ -883,7 +975,7 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
     // pair_spectrum: vmcnt is in order, so the wave polling the granules would otherwise
     // first wait for its whole prefetch to land while the workgroup idles at the barrier
     constexpr bool pf_inside = !normalize || !SPECENH_STFT_PF_AFTER_WAIT;
-    pair_spectrum<N>(a, s0, s0, s_tw, s_win, s_dc, buf, gl, dcb, xn, fa, pf_inside, want_log, normalize,
+    pair_spectrum<N>(a, s0, s0, s_tw, s_win, s_dc, buf, gl, dcb, xn, xn, fa, pf_inside, want_log, normalize,
                      pv, dmin, dmax);
     const __amdgpu_buffer_rsrc_t orr = make_rsrc(a.out + shot * plane, plane * 4);
     if constexpr (!normalize) {
@@ -936,7 +1028,7 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
     lds_barrier();
     if constexpr (!pf_inside) {
       __builtin_amdgcn_sched_barrier(0);
-      load_pair<N>(s0, xn, a.hop, (a.flags & SPECENH_STFT_DEV_NOLOAD) ? 0 : fa, a.T, gl);
+      load_pair<N>(s0, xn, xn, a.hop, (a.flags & SPECENH_STFT_DEV_NOLOAD) ? 0 : fa, a.T, gl);
       __builtin_amdgcn_sched_barrier(0);
     }
     const float mn = s_red[2 * C::WAVES];
@@ -984,7 +1076,8 @@ hipError_t launch_team_mode(const StftArgs& a, long long batch, void* workspace,
                             bool* launched) {
   using Lo = Layout<N>;
   *launched = false;
-  const int M = (a.T + Lo::TF - 1) / Lo::TF;
+  const int TFM = MODE == 3 ? Tile1<N>::TF1 : Lo::TF;  // frames per member tile
+  const int M = (a.T + TFM - 1) / TFM;
   if (M > TEAM_MAX) return hipSuccess;
   static int cap[64] = {};  // resident workgroups per device (0 = not queried)
   int dev = 0;
@@ -1059,6 +1152,19 @@ hipError_t launch_team(const StftArgs& a, long long batch, void* workspace, hipS
 }  // namespace specenh
 
 using namespace specenh;
+
+struct specenh_stft_plan;
+
+namespace specenh {
+// Cross-spectrum amplitude |Pxy| [batch][N/2 + 1][T] of the signal pairs (x[b], y[b]) on the
+// team schedule (stft_team_kernel MODE 3), with the tables of an STFT plan of the same
+// window / detrend / scaling (eps unused). *launched = false when it does not apply
+// (nperseg > 1024, a plane of 1 GiB or more, more tiles than resident workgroups): the
+// caller (specenh_csd) then runs csd_kernel.
+int stft_csd_amplitude(const specenh_stft_plan* plan, const float* x, const float* y,
+                       long long batch, long long length, long long x_stride, long long y_stride,
+                       float* out, hipStream_t stream, bool* launched);
+}  // namespace specenh
 
 struct specenh_stft_plan {
   int nperseg, noverlap, hop;
@@ -1316,3 +1422,50 @@ int specenh_stft_psd_f16(const specenh_stft_plan* plan, const void* x, long long
 }
 
 }  // extern "C"
+
+namespace specenh {
+
+int stft_csd_amplitude(const specenh_stft_plan* plan, const float* x, const float* y,
+                       long long batch, long long length, long long x_stride, long long y_stride,
+                       float* out, hipStream_t stream, bool* launched) {
+  *launched = false;
+  const int N = plan->nperseg;
+  const long long T = specenh_stft_frames(length, N, plan->noverlap);
+  if (T < 0) return (int)T;
+  if (N > 1024 || batch > (1ll << 30) || (long long)(N / 2 + 1) * T * 4 >= (1ll << 30) ||
+      x_stride * 4 >= (1ll << 31) || y_stride * 4 >= (1ll << 31))
+    return SPECENH_OK;
+  StftArgs a{};
+  a.x = x;
+  a.x_stride = x_stride;
+  a.y = y;
+  a.y_stride = y_stride;
+  a.T = (int)T;
+  a.hop = plan->hop;
+  a.scale = (float)plan->scale;
+  a.eps = 0.f;
+  a.inv_kk = (float)(12.0 / ((double)N * ((double)N * N - 1.0)));
+  a.detrend = plan->detrend;
+  a.flags = 0;
+  a.out = out;
+  a.F_out = N / 2 + 1;
+  a.window = plan->d_window;
+  a.twiddle = plan->d_twiddle;
+  a.dc_alpha = plan->dc_alpha;
+  a.dc_beta = plan->dc_beta;
+  a.dc_coef = plan->d_dc;
+  hipError_t e = hipSuccess;
+  switch (N) {
+    case 64: e = launch_team_mode<64, 3>(a, batch, nullptr, stream, launched); break;
+    case 128: e = launch_team_mode<128, 3>(a, batch, nullptr, stream, launched); break;
+    case 256: e = launch_team_mode<256, 3>(a, batch, nullptr, stream, launched); break;
+    case 512: e = launch_team_mode<512, 3>(a, batch, nullptr, stream, launched); break;
+    case 1024: e = launch_team_mode<1024, 3>(a, batch, nullptr, stream, launched); break;
+    default: break;
+  }
+  if (e != hipSuccess)
+    return set_error(SPECENH_EHIP, std::string("csd team launch: ") + hipGetErrorString(e));
+  return SPECENH_OK;
+}
+
+}  // namespace specenh

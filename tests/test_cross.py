@@ -74,11 +74,42 @@ def test_gpu_batched_pairs_and_amplitude(gpu_device, n, ov):
                                             amplitude=True)
     torch.cuda.synchronize()
     P = P.cpu().numpy()
+    A = A.cpu().numpy()
     for b in range(5):
         _, _, R = ref.cross_spectrogram(xy[b].astype(np.float64), xy[5 + b].astype(np.float64),
                                         5e5, "hann", n, ov, "linear", "density")
         assert _nrel(P[b], R) <= 1e-5
-    assert np.allclose(A.cpu().numpy(), np.abs(P), rtol=1e-6, atol=0)
+        # amplitude: the STFT team schedule (nperseg <= 1024) or csd_kernel (larger)
+        assert _nrel(A[b], np.abs(R)) <= 1e-5
+    assert _nrel(A, np.abs(P)) <= 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,ov,win,det,sc", [(1024, 768, "hamm", "linear", "density"),
+                                             (512, 256, "hann", "constant", "spectrum"),
+                                             (256, 128, "blackman", False, "density"),
+                                             (64, 32, "hann", "linear", "density")])
+def test_gpu_amplitude_team_schedule(gpu_device, n, ov, win, det, sc):
+    """|Pxy| on the STFT team kernel (MODE 3) at many frames per pair, strided rows,
+    against the fp64 oracle: every tile, the ragged last tile and the DC/Nyquist rows."""
+    import torch
+
+    from specenh import cross
+    from specenh.synthetic import plasma_chirps
+
+    hop = n - ov
+    L = 61 * hop + n + 13  # 62 frames: several tiles plus a ragged one
+    xy = plasma_chirps(6, L, seed0=300 + n, dtype=np.float32)
+    big = torch.as_tensor(np.pad(xy, ((0, 0), (0, 40))), device=gpu_device)
+    x, y = big[:3, :L], big[3:, :L]  # row stride L + 40
+    _, _, A = cross.cross_spectrogram_batch(x, y, 5e5, win, n, ov, det, sc, amplitude=True)
+    torch.cuda.synchronize()
+    A = A.cpu().numpy()
+    for b in range(3):
+        _, _, R = ref.cross_spectrogram(xy[b].astype(np.float64), xy[3 + b].astype(np.float64),
+                                        5e5, win, n, ov, det, sc)
+        assert A[b].shape == R.shape
+        assert _nrel(A[b], np.abs(R)) <= 1e-5, (b, _nrel(A[b], np.abs(R)))
 
 
 @pytest.mark.gpu

@@ -1,0 +1,361 @@
+// conv_rows.hip — the encoder's pooled 5 x 5 convolutions as a row sweep (gfx950).
+//
+// VAE/manual_scan_3layers.py:188-193: Conv2D(32, 5, relu, same) + MaxPooling2D(2) on the
+// 64 x 64 x 16 map, Conv2D(64, 5, relu, same) + MaxPooling2D(2) on the 32 x 32 x 32 map.
+// conv_patch_kernel (conv_ae.hip) runs these as 16 x 16 output tiles: every patch fragment
+// feeds the MFMAs of ONE (tap, output row) and every tile re-stages a 2-pixel halo; PMC put
+// both layers at 0.31-0.41 of the MFMA peak with ~5 VALU + 2.5 SALU instructions per MFMA.
+// Here a workgroup walks whole images DOWN, two input rows per step:
+//  * wave (window wx, channel block nb) owns 16 output columns x 16 output channels. Its 25
+//    (CIN = 32) or 13 (CIN = 16, two taps per K = 32 step) weight fragments stay in registers
+//    for the whole launch (the MFMA A operand: 16 output channels x 32 K).
+//  * input row r is read ONCE per (window, tap column): that B fragment (32 K x 16 pixels)
+//    feeds the MFMAs of all five kernel rows, i.e. output rows r + 2 - ky (5 MFMAs per LDS
+//    read). Six accumulators (output rows 2q - 2 .. 2q + 3) rotate down the image.
+//  * CIN = 16 pairs taps (kx, kx + 1) of one input row in a K step (columns 0-1, 2-3); the
+//    fifth column pairs rows: F(r) = (row r, row r + 1) at kx = 4 feeds output rows r + 2
+//    (weights w[0][4], w[1][4]), r (w[2][4], w[3][4]) and r - 2 (w[4][4], 0): 13 MFMAs per
+//    input row for 12.5 taps of work (plus F(-1) once per image for output row 1).
+//  * when output rows 2p, 2p + 1 are complete, the 2 x 2 max-pool runs in registers (rows in
+//    lane, columns across the lane pair m, m ^ 1 by DPP); the bias is the accumulators'
+//    start value and ReLU / rounding commute with the max, so pooled row p is
+//    round_T(relu(max)) and is stored as 8 bytes per even lane.
+//  * input rows arrive by LDS-DMA (global_load_lds, 16 B per lane) into an 8-row ring,
+//    three steps ahead; rows outside the image are zero-filled, as is the 2-pixel halo of
+//    every ring row. One workgroup barrier per step. Workgroups are persistent: the row
+//    stream runs on across the workgroup's images (image i, rows 0 .. H + 1, the last two
+//    zero), so the pipeline never drains between images.
+// 64-byte pixels (CIN = 32) are stored with their 16-byte groups swizzled, g ^ ((p >> 1) & 3)
+// (conflict-free B-fragment reads under the ds_read_b128 lane groups); 32-byte pixels need
+// no swizzle. Host-checked shapes: (CIN, COUT, W) = (16, 32, 64) and (32, 64, 32), H even.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <string>
+#include <type_traits>
+
+#include "lds_dma.hpp"
+#include "specenh.h"
+#include "runtime.hpp"
+
+namespace specenh {
+int set_error(int code, const std::string& msg);  // stft_psd.hip
+
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma(const uint4& a, const uint4& b, f32x4 acc) {
+  if constexpr (__is_same(T, _Float16))
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), acc, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+}
+
+template <typename T>
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  const T a = (T)lo, b = (T)hi;
+  return (uint32_t)__builtin_bit_cast(unsigned short, a) |
+         ((uint32_t)__builtin_bit_cast(unsigned short, b) << 16);
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+
+// max with the neighbouring lane (m ^ 1): DPP quad_perm [1, 0, 3, 2]
+__device__ __forceinline__ float max_pair(float v) {
+  const float o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true));
+  return fmaxf(v, o);
+}
+
+template <int CIN, int COUT, int W>
+struct RC {
+  static constexpr int NWIN = W / 16;                 // 16-column windows
+  static constexpr int NNB = COUT / 16;               // 16-channel blocks
+  static constexpr int WAVES = NWIN * NNB;
+  static constexpr int THREADS = 64 * WAVES;
+  static constexpr int PIX = CIN * 2;                 // bytes per pixel
+  static constexpr int ROWB = (W + 4) * PIX;          // ring row: 2 zero pixels each side
+  static constexpr int RING = 8;                      // rows (4 steps)
+  static constexpr int LDS = RING * ROWB;
+  static constexpr int NW = CIN == 16 ? 13 : 25;      // resident weight fragments
+  static constexpr int CPP = CIN / 8;                 // 16-byte groups per pixel
+  static constexpr int CHUNKS = W * CPP;              // 16-byte chunks per row
+  static constexpr int DMA_WAVES = 2 * CHUNKS / 64;   // waves moving a step's two rows
+  static_assert(WAVES == 8 && CHUNKS % 64 == 0 && DMA_WAVES <= WAVES, "shape");
+  // waves per SIMD the register budget is sized for (CIN = 32 holds 25 fragments)
+  static constexpr int WPE = CIN == 16 ? 4 : 2;
+};
+
+struct CRArgs {
+  const void* x;     // [N][H][W][CIN]
+  const void* w;     // forward GEMM weights [COUT][5][5][CIN]
+  const float* b;    // [COUT]
+  void* out;         // [N][H/2][W/2][COUT]
+  int N, H;
+};
+
+template <typename T, int CIN, int COUT, int W>
+__global__ __launch_bounds__((RC<CIN, COUT, W>::THREADS))
+__attribute__((amdgpu_waves_per_eu(RC<CIN, COUT, W>::WPE)))
+void conv_rows_pool_kernel(CRArgs a) {
+  using C = RC<CIN, COUT, W>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char ring[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = lane & 15, kg = lane >> 4;
+  const int wx = wv % C::NWIN, nb = wv / C::NWIN;
+  const int x0 = 16 * wx;
+  const int H = a.H, SPI = H / 2 + 1;  // steps per image: rows (2q, 2q + 1), q = 0 .. H/2
+  const int G = gridDim.x;
+  const int nimg = ((int)a.N - (int)blockIdx.x + G - 1) / G;
+  const int S = nimg * SPI + 1;  // + 1: the last pair is stored one step after its rows
+
+  {
+    uint4* z = reinterpret_cast<uint4*>(ring);
+    for (int e = tid; e < C::LDS / 16; e += C::THREADS) z[e] = uint4{0u, 0u, 0u, 0u};
+  }
+
+  // ---- resident weights: A operand, lane (m, kg) = output channel 16 nb + m, K 8 kg .. ----
+  uint4 wf[C::NW];
+  {
+    const T* __restrict__ Wg = reinterpret_cast<const T*>(a.w);
+    const int co = 16 * nb + m;
+    auto tap = [&](int ky, int kx, int c8) {
+      return *reinterpret_cast<const uint4*>(Wg + ((co * 5 + ky) * 5 + kx) * CIN + c8);
+    };
+    if constexpr (CIN == 32) {
+#pragma unroll
+      for (int t = 0; t < 25; ++t) wf[t] = tap(t / 5, t % 5, 8 * kg);
+    } else {
+      const int hi = kg >> 1, c8 = 8 * (kg & 1);
+#pragma unroll
+      for (int ky = 0; ky < 5; ++ky) {
+        wf[ky] = tap(ky, hi, c8);          // columns (0, 1)
+        wf[5 + ky] = tap(ky, 2 + hi, c8);  // columns (2, 3)
+      }
+      wf[10] = tap(hi, 4, c8);             // F: (w[0][4], w[1][4])
+      wf[11] = tap(2 + hi, 4, c8);         //    (w[2][4], w[3][4])
+      wf[12] = hi ? uint4{0u, 0u, 0u, 0u} : tap(4, 4, c8);  // (w[4][4], 0)
+    }
+  }
+  const f32x4 bias = f32x4{a.b[16 * nb + 4 * kg], a.b[16 * nb + 4 * kg + 1],
+                           a.b[16 * nb + 4 * kg + 2], a.b[16 * nb + 4 * kg + 3]};
+
+  // ---- this lane's B-fragment byte offsets within a ring row ----
+  int boff[5];
+  int foff = 0, foffw = 0, fo0 = 0;  // CIN = 16: F fragment (next row in the next slot /
+                                     // wrapped), and its offset within one row
+  if constexpr (CIN == 32) {
+#pragma unroll
+    for (int kx = 0; kx < 5; ++kx) {
+      const int ps = x0 + m + kx;  // stored pixel (x + 2)
+      boff[kx] = ps * 64 + 16 * (kg ^ ((ps >> 1) & 3));
+    }
+  } else {
+    boff[0] = (x0 + m + (kg >> 1)) * 32 + 16 * (kg & 1);  // columns (0, 1); (2, 3) at + 64
+    const int fo = (x0 + m + 4) * 32 + 16 * (kg & 1);
+    fo0 = fo;
+    foff = fo + (kg >> 1) * C::ROWB;
+    foffw = fo - (kg >> 1) * 7 * C::ROWB;  // row r in slot 7: row r + 1 in slot 0
+  }
+
+  // ---- row DMA: waves 0 .. DMA_WAVES - 1, wave w moves half (w & 1) of row w >> 1 ----
+  const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
+  const bool dma_wave = wv < C::DMA_WAVES;
+  int dsrc = 0, ddst = 0;
+  if (dma_wave) {
+    const int c = (wv & 1) * 64 + lane;  // chunk of the row
+    const int ps = 2 + c / C::CPP, gs = c % C::CPP;
+    const int g = CIN == 32 ? (gs ^ ((ps >> 1) & 3)) : gs;
+    dsrc = (ps - 2) * CIN + 8 * g;  // element offset within the image row
+    ddst = 2 * C::PIX + (wv & 1) * 1024;
+  }
+  // rows of global step s: image (s / SPI) of this workgroup, rows 2q, 2q + 1 (q = s % SPI)
+  auto stage = [&](int s) -> bool {  // returns whether this wave issued an LDS-DMA
+    if (!dma_wave) return false;
+    const int il = s / SPI, q = s - il * SPI;
+    const int r = 2 * q + (wv >> 1);
+    unsigned char* dst = ring + ((2 * s + (wv >> 1)) & 7) * C::ROWB + ddst;
+    if (s < S && il < nimg && r < H) {
+      const long long n = (long long)blockIdx.x + (long long)il * G;
+      lds_dma16(X + ((n * H + r) * W) * CIN + dsrc, dst);
+      return true;
+    }
+    *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
+    return false;
+  };
+  __syncthreads();  // ring zeroed
+  stage(0);
+  stage(1);
+  stage(2);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+
+  f32x4 acc[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) acc[i] = bias;
+  T* __restrict__ O = reinterpret_cast<T*>(a.out);
+  const int PW = W / 2, PHh = H / 2;
+
+  // step s with I = s % 3 compile-time (the accumulator ring: output row 2q + d -> slot
+  // (2 I + d) mod 6)
+  auto step = [&](auto ic, const int s) {
+    constexpr int I = decltype(ic)::value;
+    auto slot = [](int d) { return (2 * I + d + 12) % 6; };
+    // (1) pair s - 2 (output rows 2q - 4, 2q - 3) is complete: pool, store, reset
+    {
+      const int p = s - 2;
+      f32x4& r0 = acc[slot(-4)];
+      f32x4& r1 = acc[slot(-3)];
+      if (p >= 0) {
+        const int il = p / SPI, q = p - il * SPI;
+        if (il < nimg && q < PHh) {
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = fmaxf(max_pair(fmaxf(r0[i], r1[i])), 0.f);
+          if ((m & 1) == 0) {
+            const long long n = (long long)blockIdx.x + (long long)il * G;
+            const long long o = ((n * PHh + q) * PW + (x0 + m) / 2) * COUT + 16 * nb + 4 * kg;
+            *reinterpret_cast<uint2*>(O + o) = uint2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
+          }
+        }
+      }
+      r0 = bias;
+      r1 = bias;
+    }
+    // (2) rows of step s + 3 into the ring
+    const bool issued = stage(s + 3);
+    // (3) this step's input rows
+    const int il = s / SPI, q = s - il * SPI;
+    if (il < nimg && 2 * q < H) {
+      // every B fragment of the step first (one LDS latency per step, not one per row or
+      // tap column: sched_barrier keeps the compiler from sinking the reads to their MFMAs)
+      constexpr int NB = CIN == 32 ? 5 : 3;
+      uint4 bf[2][NB];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int rs = (2 * s + j) & 7;
+        const unsigned char* rb = ring + rs * C::ROWB;
+        if constexpr (CIN == 32) {
+#pragma unroll
+          for (int kx = 0; kx < 5; ++kx) bf[j][kx] = *reinterpret_cast<const uint4*>(rb + boff[kx]);
+        } else {
+          bf[j][0] = *reinterpret_cast<const uint4*>(rb + boff[0]);
+          bf[j][1] = *reinterpret_cast<const uint4*>(rb + boff[0] + 64);
+          bf[j][2] = *reinterpret_cast<const uint4*>(rb + (rs == 7 ? foffw : foff));
+        }
+      }
+      uint4 bT = uint4{0u, 0u, 0u, 0u};
+      if constexpr (CIN == 16) {
+        if (q == 0) {
+          // F(-1) = (row -1, row 0): output row 1 gets w[1][4] x row 0. Row -1 is zero
+          // padding (not read: its ring slot is being refilled by this step's stage)
+          bT = *reinterpret_cast<const uint4*>(ring + ((2 * s) & 7) * C::ROWB + fo0);
+          if (kg < 2) bT = uint4{0u, 0u, 0u, 0u};
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (CIN == 32) {
+#pragma unroll
+          for (int kx = 0; kx < 5; ++kx)
+#pragma unroll
+            for (int ky = 0; ky < 5; ++ky) {
+              f32x4& ac = acc[slot(j + 2 - ky)];
+              ac = mfma<T>(wf[ky * 5 + kx], bf[j][kx], ac);
+            }
+        } else {
+          // consecutive MFMAs into different accumulators (no back-to-back dependency)
+#pragma unroll
+          for (int ky = 0; ky < 5; ++ky) {
+            f32x4& ac = acc[slot(j + 2 - ky)];
+            ac = mfma<T>(wf[ky], bf[j][0], ac);
+          }
+#pragma unroll
+          for (int ky = 0; ky < 5; ++ky) {
+            f32x4& ac = acc[slot(j + 2 - ky)];
+            ac = mfma<T>(wf[5 + ky], bf[j][1], ac);
+          }
+          acc[slot(j + 2)] = mfma<T>(wf[10], bf[j][2], acc[slot(j + 2)]);
+          acc[slot(j)] = mfma<T>(wf[11], bf[j][2], acc[slot(j)]);
+          acc[slot(j - 2)] = mfma<T>(wf[12], bf[j][2], acc[slot(j - 2)]);
+          if (j == 0 && q == 0) acc[slot(1)] = mfma<T>(wf[10], bT, acc[slot(1)]);
+        }
+      }
+    }
+    // (4) rows of step s + 2 (DMA issued at step s - 1) have landed; this step's stores are
+    // older than its DMA and complete too
+    if (issued) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+  };
+  int s = 0;
+  for (; s + 3 <= S; s += 3) {
+    step(std::integral_constant<int, 0>{}, s);
+    step(std::integral_constant<int, 1>{}, s + 1);
+    step(std::integral_constant<int, 2>{}, s + 2);
+  }
+  if (s < S) step(std::integral_constant<int, 0>{}, s);
+  if (s + 1 < S) step(std::integral_constant<int, 1>{}, s + 1);
+}
+
+template <typename T, int CIN, int COUT, int W>
+hipError_t launch_rows(const CRArgs& a, hipStream_t st) {
+  using C = RC<CIN, COUT, W>;
+  const void* k = reinterpret_cast<const void*>(&conv_rows_pool_kernel<T, CIN, COUT, W>);
+  static int per_cu[64] = {};
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (per_cu[dev] == 0) {
+    int pc = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k, C::THREADS, C::LDS);
+    if (e != hipSuccess) return e;
+    per_cu[dev] = std::max(1, pc);
+  }
+  const long long grid = std::min<long long>(a.N, (long long)per_cu[dev] * device_cus());
+  SPECENH_LAUNCH((conv_rows_pool_kernel<T, CIN, COUT, W>), dim3((unsigned)grid), dim3(C::THREADS),
+                 C::LDS, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// The row-sweep kernel for an inference Conv2D(5, relu, same) + MaxPooling2D(2) when the
+// shape is one it is built for; *launched = false otherwise (the caller runs
+// conv_patch_kernel).
+int conv_rows_pool(int dtype, const void* x, int N, int H, int W, int CI, const void* w,
+                   const float* b, int CO, void* out, hipStream_t st, bool* launched) {
+  *launched = false;
+  if (variant(V_CONV_NO_ROWS) != 0 || N <= 0 || H < 2 || (H & 1) || !b) return SPECENH_OK;
+  if ((long long)N * H * W * CI >= (1ll << 31)) return SPECENH_OK;
+  CRArgs a{};
+  a.x = x; a.w = w; a.b = b; a.out = out; a.N = N; a.H = H;
+  hipError_t e = hipSuccess;
+  const bool f16 = dtype == SPECENH_DTYPE_F16;
+  if (dtype != SPECENH_DTYPE_F16 && dtype != SPECENH_DTYPE_BF16) return SPECENH_OK;
+  if (CI == 16 && CO == 32 && W == 64)
+    e = f16 ? launch_rows<_Float16, 16, 32, 64>(a, st) : launch_rows<__bf16, 16, 32, 64>(a, st);
+  else if (CI == 32 && CO == 64 && W == 32)
+    e = f16 ? launch_rows<_Float16, 32, 64, 32>(a, st) : launch_rows<__bf16, 32, 64, 32>(a, st);
+  else
+    return SPECENH_OK;
+  if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("conv_rows: ") + hipGetErrorString(e));
+  *launched = true;
+  return SPECENH_OK;
+}
+
+}  // namespace specenh

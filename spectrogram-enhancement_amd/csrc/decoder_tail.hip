@@ -38,6 +38,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "lds_dma.hpp"
 #include "specenh.h"
 #include "runtime.hpp"
 
@@ -651,10 +652,6 @@ __device__ __forceinline__ int x1_off(int ps, int g) { return ps * d3::X1ST + 8 
 // consumer 16-byte reads of consecutive pixels conflict-free)
 __device__ __forceinline__ int x2_off(int ps, int g) { return ps * d3::X2ST + 8 * (g ^ ((ps >> 1) & 3)); }
 
-// one 16-byte LDS-DMA per lane: LDS destination = wave-uniform dst + 16 x lane
-__device__ __forceinline__ void lds_dma16(const void* src, void* dst) {
-  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-}
 
 struct D3Args {
   const void* x;     // [N][H][32][64]

@@ -1,0 +1,76 @@
+"""The encoder's pooled 5 x 5 convolutions as a row sweep (csrc/conv_rows.hip
+conv_rows_pool_kernel; VAE/manual_scan_3layers.py:188-193: Conv2D(32, 5, relu, same) +
+MaxPooling2D(2) on 64-wide 16-channel maps, Conv2D(64, 5, ...) on 32-wide 32-channel maps).
+
+Against a float64 torch conv + bias + ReLU + max-pool of the same 16-bit operands, element by
+element: products of 16-bit values are exact in fp32, so the kernel differs from float64 by
+the fp32 summation (bounded by 1e-5 of the sum of |products| of the pooled window) and one
+rounding to the 16-bit type. Batches that give the persistent workgroups unequal image
+counts, heights from 2 (one pooled row) up, and the tile kernel (SPECENH_CONV_NO_ROWS) on
+the same inputs."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import specenh  # noqa: F401  (registers torch.ops.specenh.*)
+from specenh import _lib
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(16, 32, 64), (32, 64, 32)]  # (C, CO, W): the model's conv2 and conv3
+
+
+def _run(x, w, bias, CO, pool_out):
+    N, H, W, C = x.shape
+    torch.ops.specenh.conv2d_out(x, w, bias, 5, 5, CO, 1, 2, 2, 1, H, W, 1, None, None, pool_out,
+                                 True, None)
+
+
+def _ref(x, w, bias):
+    xd = x.double().cpu().permute(0, 3, 1, 2)
+    wd = w.double().cpu().permute(0, 3, 1, 2)
+    b = bias.double().cpu().view(1, -1, 1, 1)
+    ref = F.max_pool2d(torch.relu(F.conv2d(xd, wd, padding=2) + b), 2)
+    mag = F.max_pool2d(F.conv2d(xd.abs(), wd.abs(), padding=2) + b.abs(), 2)
+    return ref.permute(0, 2, 3, 1), mag.permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("C,CO,W", SHAPES)
+@pytest.mark.parametrize("N,H", [(1, 64), (3, 32), (7, 2), (5, 18), (513, 8)])
+def test_rows_vs_float64(gpu_device, dtype, C, CO, W, N, H):
+    rng = np.random.default_rng(C + CO + N + H)
+    x = torch.tensor(rng.standard_normal((N, H, W, C)), dtype=dtype, device=gpu_device)
+    w = torch.tensor(rng.standard_normal((CO, 5, 5, C)) * 0.1, dtype=dtype, device=gpu_device)
+    bias = torch.tensor(rng.standard_normal(CO) * 0.5, dtype=torch.float32, device=gpu_device)
+    out = torch.full((N, H // 2, W // 2, CO), float("nan"), dtype=dtype, device=gpu_device)
+    _run(x, w, bias, CO, out)
+    torch.cuda.synchronize()
+    assert "conv_rows_pool_kernel" in _lib.last_kernel_name()
+    ref, mag = _ref(x, w, bias)
+    got = out.double().cpu()
+    assert bool(torch.isfinite(got).all())
+    eps = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
+    assert torch.all((got - ref).abs() <= eps * ref.abs() + 1e-5 * mag + 1e-30)
+
+
+@pytest.mark.parametrize("C,CO,W", SHAPES)
+def test_rows_matches_tile_kernel(gpu_device, kernel_variant, C, CO, W):
+    """The same layer through conv_patch_kernel (16 x 16 tiles): equal up to fp32 summation
+    order and one 16-bit rounding (the row sweep starts its sums at the bias)."""
+    N, H = 300, 64 if C == 16 else 32
+    rng = np.random.default_rng(5 + C)
+    x = torch.tensor(rng.uniform(0, 1, (N, H, W, C)), dtype=torch.float16, device=gpu_device)
+    w = torch.tensor(rng.standard_normal((CO, 5, 5, C)) * 0.05, dtype=torch.float16,
+                     device=gpu_device)
+    bias = torch.tensor(rng.standard_normal(CO) * 0.1, dtype=torch.float32, device=gpu_device)
+    a = torch.empty((N, H // 2, W // 2, CO), dtype=torch.float16, device=gpu_device)
+    b = torch.empty_like(a)
+    _run(x, w, bias, CO, a)
+    kernel_variant("CONV_NO_ROWS", 1)
+    _run(x, w, bias, CO, b)
+    torch.cuda.synchronize()
+    assert "conv_patch_kernel" in _lib.last_kernel_name()
+    d = (a.float() - b.float()).abs()
+    assert float(d.max()) <= 2.0 ** -10 * float(b.float().abs().max())

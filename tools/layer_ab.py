@@ -3,9 +3,10 @@ the bench's launch shape, for each environment variant given on the command line
 
     python tools/layer_ab.py [--batch 2048] [--reps 20] "" "SPECENH_PATCH_WSPLIT=0" ...
 
-Each variant is a space-separated list of NAME=VALUE settings applied to os.environ (the
-library reads its SPECENH_* switches at every launch). Variants are interleaved per
-repetition so clock drift hits them alike; medians are printed."""
+Each variant is a space-separated list of NAME=VALUE kernel switches (SPECENH_CONV_NO_ROWS=1,
+...), applied through specenh_set_variant (the library reads the environment only once) and
+reset to their defaults between variants. Variants are interleaved per repetition so clock
+drift hits them alike; medians are printed."""
 import argparse
 import os
 import sys
@@ -16,7 +17,7 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "spectrogram-enhancement_amd")]
 import bench  # noqa: E402
-from specenh import ae  # noqa: E402
+from specenh import _lib, ae  # noqa: E402
 
 
 def main():
@@ -35,21 +36,22 @@ def main():
     eng = ae.AutoencoderEngine(ops, (128, 128, 1), compute_dtype="float16", device=dev)
     eng.set_keras_weights(bench.ae_weights())
     x = eng.to_compute(torch.rand(a.batch, 128, 128, 1, device=dev))
-    base = dict(os.environ)
+    names_used = {kv.split("=", 1)[0] for v in variants for kv in v.split()}
+    defaults = {k: _lib.get_variant(k) for k in names_used}
     res = {v: [] for v in variants}
     for rep in range(a.reps + 2):
         for v in variants:
-            os.environ.clear()
-            os.environ.update(base)
+            for k, val in defaults.items():
+                _lib.set_variant(k, val)
             for kv in v.split():
                 k, val = kv.split("=", 1)
-                os.environ[k] = val
+                _lib.set_variant(k, int(val))
             timing = []
             eng.forward(x, timing=timing)
             torch.cuda.synchronize()
             if rep >= 2:
                 res[v].append([s.elapsed_time(e) for s, e in timing])
-    names = bench.LAYER_NAMES_TAIL if eng.tail else bench.LAYER_NAMES
+    names = bench.layer_names(eng)
     print("variant".ljust(40) + "".join(n.rjust(17) for n in names) + "total".rjust(10))
     for v in variants:
         med = np.median(np.array(res[v]), axis=0)

@@ -150,8 +150,21 @@ def fold(src):
 
 
 def main():
-    src, dst = sys.argv[1], sys.argv[2]
+    src, dst = sys.argv[1], sys.argv[2]  # dst is updated in place
     res = fold(src)
+    # targets not profiled in this run keep their earlier records; a re-profiled target is
+    # replaced stage by stage (stages it no longer has are kept, their symbols say what ran)
+    try:
+        with open(dst) as fh:
+            old = json.load(fh)
+    except (OSError, ValueError):
+        old = {}
+    for target, stages in old.items():
+        if target.startswith("_"):
+            continue
+        merged = dict(stages)
+        merged.update(res.get(target, {}))
+        res[target] = merged
     res["_source"] = ("rocprofv3 --pmc passes of tools/pmc_refresh.sh (FETCH_SIZE; WRITE_SIZE; "
                       "SQ waves/waits/MFMA busy + GRBM_GUI_ACTIVE; SQ instruction mix + LDS "
                       "conflicts), one pass each, folded by tools/pmc_fold.py; FETCH_SIZE x2, "

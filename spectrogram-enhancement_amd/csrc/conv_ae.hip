@@ -2347,9 +2347,12 @@ int patch_cc(const ConvArgs& a, int nph) {
   return 0;
 }
 
-// conv_rows.hip: inference Conv2D(5, relu, same) + MaxPooling2D(2) as a row sweep
+// conv_rows.hip: inference Conv2D(5, relu, same) + MaxPooling2D(2) and Conv2DTranspose(5,
+// s2, relu, same) on 64 channels as row sweeps
 int conv_rows_pool(int dtype, const void* x, int N, int H, int W, int CI, const void* w,
                    const float* b, int CO, void* out, hipStream_t st, bool* launched);
+int convt_rows(int dtype, const void* x, int N, int H, int W, int CI, const void* w,
+               const float* b, int CO, void* out, hipStream_t st, bool* launched);
 
 template <typename T>
 int launch_fwd(const ConvArgs& a, int nph, hipStream_t st) {
@@ -2558,6 +2561,14 @@ int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, cons
   if (a.pool && (nph != 1 || (OH & 1) || (OW & 1) || mask || logits || out_f32))
     return set_error(SPECENH_EUNSUPPORTED, "fused max-pool: plain conv with even output only");
   hipStream_t st = (hipStream_t)stream;
+  // Conv2DTranspose(5, s2, relu, same) on 64 channels: the row sweep (conv_rows.hip)
+  if (dtype != SPECENH_DTYPE_F32 && stride == 1 && in_dil == 2 && KH == 5 && KW == 5 &&
+      pad_t == 3 && pad_l == 3 && OH == 2 * IH && OW == 2 * IW && act == 1 && !mask && !logits &&
+      !out_f32 && !pool2 && bias) {
+    bool launched = false;
+    const int rc = convt_rows(dtype, in, N, IH, IW, C, w_gemm, bias, CO, out, st, &launched);
+    if (rc != SPECENH_OK || launched) return rc;
+  }
   // 1 input channel: window rows as MFMA K runs (conv_c1_mfma.hip)
   if (stride == 1 && in_dil == 1 && C == 1 && !(variant(V_CONV_NO_C1MFMA) != 0)) {
     const int r = launch_conv_c1_mfma(dtype, in, N, IH, IW, C, w_gemm, KH, KW, CO, bias, pad_t,

@@ -332,6 +332,198 @@ hipError_t launch_rows(const CRArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ============================================================================ convT rows
+// Conv2DTranspose(CO, 5, strides=2, relu, same) on 64-channel inputs as a row sweep
+// (VAE/manual_scan_3layers.py:196-197: the decoder's 64 -> 64 at 16 x 16 -> 32 x 32 and,
+// outside the fused decoder, 64 -> 32 at 32 x 32 -> 64 x 64). conv_patch_kernel runs the
+// four output phases as dense convs over 16 x 16 tiles (0.20 of the MFMA peak). Here, as in
+// decoder3's producer waves (decoder_tail.hip), input position row s yields output rows
+// 2s, 2s + 1: for each of the 9 neighbourhood offsets (dy, dx) one B fragment pair (input
+// row s + dy shifted by dx, 16 positions x 64 channels, two K = 32 halves) feeds every
+// phase that has the tap — 50 MFMAs from 18 LDS reads per (row, 16 positions, 16 output
+// channels). Output phase (py, px) of position (s, x) is pixel (2s + py, 2x + px), its tap
+// (ky, kx) = (2 dy + 3 - py, 2 dx + 3 - px) when inside the 5 x 5 kernel (pad 3 of the
+// dilated-input conv): 4 / 6 / 6 / 9 taps, exactly the 25 useful ones.
+//  * wave (window wx, channel block nb) holds its 50 tap fragments (A operand) in registers
+//    for the launch; the four phase accumulators start at the bias.
+//  * the input rows are one stream per persistent workgroup: position p = il (H + 1) + 1 + r
+//    holds row r of the workgroup's image il, position il (H + 1) the zero row between
+//    images, so step g (image g / (H + 1), row s = g % (H + 1), s = H a bubble) reads
+//    positions g .. g + 2 and the ring refill is one position per step (LDS-DMA, 3 steps
+//    ahead, 8-row ring).
+//  * the packed outputs of step g are stored at the start of step g + 1, ahead of that
+//    step's DMA, so the end-of-step vmcnt wait (everything but that DMA) never waits on a
+//    store younger than the DMA it needs.
+// Input pixels are 128 B with their 16-byte groups swizzled, g ^ (p & 7) (decoder3's x1_off:
+// conflict-free fragment reads).
+template <int CO, int W>
+struct TC {
+  static constexpr int CI = 64;
+  static constexpr int NWIN = W / 16, NNB = CO / 16;
+  static constexpr int WAVES = NWIN * NNB;
+  static constexpr int THREADS = 64 * WAVES;
+  static constexpr int ROWB = (W + 2) * CI * 2;  // one zero position each side
+  static constexpr int RING = 8;
+  static constexpr int LDS = RING * ROWB;
+  static constexpr int DMA_WAVES = W * CI * 2 / 1024;  // one 1-KB DMA per wave and row
+  static_assert(WAVES == 4 && DMA_WAVES <= WAVES, "shape");
+};
+
+__device__ __forceinline__ constexpr int tky(int py, int dy) { return 2 * dy + 3 - py; }
+__device__ __forceinline__ constexpr bool ttap(int ph, int dy, int dx) {
+  return tky(ph >> 1, dy) >= 0 && tky(ph >> 1, dy) < 5 && tky(ph & 1, dx) >= 0 &&
+         tky(ph & 1, dx) < 5;
+}
+
+template <typename T>
+__device__ __forceinline__ uint2 relu_pack4(const f32x4& v) {
+  return uint2{pack2<T>(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f)),
+               pack2<T>(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f))};
+}
+
+template <typename T, int CO, int W>
+__global__ __launch_bounds__((TC<CO, W>::THREADS)) __attribute__((amdgpu_waves_per_eu(2)))
+void convt_rows_kernel(CRArgs a) {
+  using C = TC<CO, W>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char ring[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = lane & 15, kg = lane >> 4;
+  const int wx = wv % C::NWIN, nb = wv / C::NWIN;
+  const int H = a.H, SPI = H + 1;
+  const int G = gridDim.x;
+  const int nimg = ((int)a.N - (int)blockIdx.x + G - 1) / G;
+  const int S = nimg * SPI;
+
+  {
+    uint4* z = reinterpret_cast<uint4*>(ring);
+    for (int e = tid; e < C::LDS / 16; e += C::THREADS) z[e] = uint4{0u, 0u, 0u, 0u};
+  }
+  // tap fragments [phase][(dy, dx) taps][K half]
+  uint4 wf[50];
+  {
+    const T* __restrict__ Wg = reinterpret_cast<const T*>(a.w);
+    int u = 0;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          if (!ttap(ph, dy, dx)) continue;
+#pragma unroll
+          for (int kh = 0; kh < 2; ++kh)
+            wf[u++] = *reinterpret_cast<const uint4*>(
+                Wg + (((16 * nb + m) * 5 + tky(ph >> 1, dy)) * 5 + tky(ph & 1, dx)) * 64 +
+                32 * kh + 8 * kg);
+        }
+  }
+  const f32x4 bias = f32x4{a.b[16 * nb + 4 * kg], a.b[16 * nb + 4 * kg + 1],
+                           a.b[16 * nb + 4 * kg + 2], a.b[16 * nb + 4 * kg + 3]};
+  int xo[3];  // byte offset of pixel 16 wx + m + dx (stored + 1), group kg, in a ring row
+#pragma unroll
+  for (int dx = -1; dx <= 1; ++dx) {
+    const int ps = 16 * wx + m + dx + 1;
+    xo[dx + 1] = ps * 128 + 16 * (kg ^ (ps & 7));
+  }
+  // ring refill: wave w < DMA_WAVES moves chunks 64 w .. 64 w + 63 of a row
+  const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
+  const bool dma_wave = wv < C::DMA_WAVES;
+  int dsrc = 0;
+  if (dma_wave) {
+    const int c = 64 * wv + lane;
+    const int ps = 1 + c / 8, gs = c & 7;
+    dsrc = (ps - 1) * 64 + 8 * (gs ^ (ps & 7));
+  }
+  auto stage = [&](int p) -> bool {  // stream position p -> ring slot p & 7
+    if (!dma_wave) return false;
+    unsigned char* dst = ring + (p & 7) * C::ROWB + 128 + 1024 * wv;
+    const int il = p / SPI, r = p - il * SPI - 1;
+    if (il < nimg && r >= 0) {
+      const long long n = (long long)blockIdx.x + (long long)il * G;
+      lds_dma16(X + ((n * H + r) * W) * 64 + dsrc, dst);
+      return true;
+    }
+    *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
+    return false;
+  };
+  __syncthreads();  // ring zeroed
+#pragma unroll
+  for (int p = 0; p < 5; ++p) stage(p);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+
+  T* __restrict__ O = reinterpret_cast<T*>(a.out);
+  const int OW = 2 * W;
+  uint2 pk[4];
+  long long po = -1;  // element offset of the held outputs' (2s, 2x) pixel, -1: none
+  auto store_held = [&]() {
+    if (po >= 0) {
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph)
+        *reinterpret_cast<uint2*>(O + po + ((ph >> 1) * OW + (ph & 1)) * CO) = pk[ph];
+    }
+  };
+  for (int g = 0; g < S; ++g) {
+    store_held();
+    po = -1;
+    const bool issued = stage(g + 5);
+    const int il = g / SPI, s = g - il * SPI;
+    if (s < H) {
+      f32x4 acc[4] = {bias, bias, bias, bias};
+      int u0[4] = {0, 8, 20, 32};
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy) {
+        const unsigned char* src = ring + ((g + 1 + dy) & 7) * C::ROWB;
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          // K half 1 (groups kg + 4) sits at the half-0 offset ^ 64 bytes (swizzle bit 2)
+          const uint4 b0 = *reinterpret_cast<const uint4*>(src + xo[dx + 1]);
+          const uint4 b1 = *reinterpret_cast<const uint4*>(src + (xo[dx + 1] ^ 64));
+#pragma unroll
+          for (int ph = 0; ph < 4; ++ph)
+            if (ttap(ph, dy, dx)) acc[ph] = mfma<T>(wf[u0[ph]], b0, acc[ph]);
+#pragma unroll
+          for (int ph = 0; ph < 4; ++ph)
+            if (ttap(ph, dy, dx)) {
+              acc[ph] = mfma<T>(wf[u0[ph] + 1], b1, acc[ph]);
+              u0[ph] += 2;
+            }
+        }
+      }
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) pk[ph] = relu_pack4<T>(acc[ph]);
+      const long long n = (long long)blockIdx.x + (long long)il * G;
+      po = ((n * 2 * H + 2 * s) * OW + 2 * (16 * wx + m)) * CO + 16 * nb + 4 * kg;
+    }
+    if (issued) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+  }
+  store_held();
+}
+
+template <typename T, int CO, int W>
+hipError_t launch_convt_rows(const CRArgs& a, hipStream_t st) {
+  using C = TC<CO, W>;
+  const void* k = reinterpret_cast<const void*>(&convt_rows_kernel<T, CO, W>);
+  static int per_cu[64] = {};
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (per_cu[dev] == 0) {
+    int pc = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k, C::THREADS, C::LDS);
+    if (e != hipSuccess) return e;
+    per_cu[dev] = std::max(1, pc);
+  }
+  const long long grid = std::min<long long>(a.N, (long long)per_cu[dev] * device_cus());
+  SPECENH_LAUNCH((convt_rows_kernel<T, CO, W>), dim3((unsigned)grid), dim3(C::THREADS), C::LDS,
+                 st, a);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 // The row-sweep kernel for an inference Conv2D(5, relu, same) + MaxPooling2D(2) when the
@@ -354,6 +546,33 @@ int conv_rows_pool(int dtype, const void* x, int N, int H, int W, int CI, const 
   else
     return SPECENH_OK;
   if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("conv_rows: ") + hipGetErrorString(e));
+  *launched = true;
+  return SPECENH_OK;
+}
+
+}  // namespace specenh
+
+namespace specenh {
+
+// The row-sweep kernel for Conv2DTranspose(CO, 5, s2, relu, same) on 64-channel inputs of
+// width 16 (CO 64) or 32 (CO 32), forward (any batch); *launched = false otherwise.
+int convt_rows(int dtype, const void* x, int N, int H, int W, int CI, const void* w,
+               const float* b, int CO, void* out, hipStream_t st, bool* launched) {
+  *launched = false;
+  if (variant(V_CONVT_NO_ROWS) != 0 || N <= 0 || H <= 0 || CI != 64 || !b) return SPECENH_OK;
+  if (dtype != SPECENH_DTYPE_F16 && dtype != SPECENH_DTYPE_BF16) return SPECENH_OK;
+  if ((long long)N * 4 * H * W * CO >= (1ll << 31)) return SPECENH_OK;
+  CRArgs a{};
+  a.x = x; a.w = w; a.b = b; a.out = out; a.N = N; a.H = H;
+  const bool f16 = dtype == SPECENH_DTYPE_F16;
+  hipError_t e;
+  if (CO == 64 && W == 16)
+    e = f16 ? launch_convt_rows<_Float16, 64, 16>(a, st) : launch_convt_rows<__bf16, 64, 16>(a, st);
+  else if (CO == 32 && W == 32)
+    e = f16 ? launch_convt_rows<_Float16, 32, 32>(a, st) : launch_convt_rows<__bf16, 32, 32>(a, st);
+  else
+    return SPECENH_OK;
+  if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("convt_rows: ") + hipGetErrorString(e));
   *launched = true;
   return SPECENH_OK;
 }

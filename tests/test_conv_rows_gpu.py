@@ -74,3 +74,64 @@ def test_rows_matches_tile_kernel(gpu_device, kernel_variant, C, CO, W):
     assert "conv_patch_kernel" in _lib.last_kernel_name()
     d = (a.float() - b.float()).abs()
     assert float(d.max()) <= 2.0 ** -10 * float(b.float().abs().max())
+
+
+# ---------------------------------------------------------------- Conv2DTranspose row sweep
+# (csrc/conv_rows.hip convt_rows_kernel; VAE/manual_scan_3layers.py:196-197). The engine's
+# forward GEMM form: a stride-1 conv of the zero-interleaved input (pad 3 top/left, 2
+# bottom/right) with the [CO][5][5][64] GEMM weights.
+def _convt_ref(x, w, bias):
+    N, H, W, C = x.shape
+    xd = torch.zeros((N, C, 2 * H - 1, 2 * W - 1), dtype=torch.float64)
+    xd[:, :, ::2, ::2] = x.double().cpu().permute(0, 3, 1, 2)
+    xd = F.pad(xd, (3, 2, 3, 2))
+    wd = w.double().cpu().permute(0, 3, 1, 2)
+    b = bias.double().cpu().view(1, -1, 1, 1)
+    ref = torch.relu(F.conv2d(xd, wd) + b)
+    mag = F.conv2d(xd.abs(), wd.abs()) + b.abs()
+    return ref.permute(0, 2, 3, 1), mag.permute(0, 2, 3, 1)
+
+
+def _convt_run(x, w, bias, CO, out):
+    N, H, W, C = x.shape
+    torch.ops.specenh.conv2d_out(x, w, bias, 5, 5, CO, 1, 3, 3, 2, 2 * H, 2 * W, 1, None, None,
+                                 out, False, None)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("CO,W", [(64, 16), (32, 32)])
+@pytest.mark.parametrize("N,H", [(1, 16), (3, 1), (5, 7), (300, 4)])
+def test_convt_rows_vs_float64(gpu_device, dtype, CO, W, N, H):
+    rng = np.random.default_rng(CO + W + N + H)
+    x = torch.tensor(np.maximum(rng.standard_normal((N, H, W, 64)), 0), dtype=dtype,
+                     device=gpu_device)
+    w = torch.tensor(rng.standard_normal((CO, 5, 5, 64)) * 0.05, dtype=dtype, device=gpu_device)
+    bias = torch.tensor(rng.standard_normal(CO) * 0.3, dtype=torch.float32, device=gpu_device)
+    out = torch.full((N, 2 * H, 2 * W, CO), float("nan"), dtype=dtype, device=gpu_device)
+    _convt_run(x, w, bias, CO, out)
+    torch.cuda.synchronize()
+    assert "convt_rows_kernel" in _lib.last_kernel_name()
+    ref, mag = _convt_ref(x, w, bias)
+    got = out.double().cpu()
+    assert bool(torch.isfinite(got).all())
+    eps = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
+    assert torch.all((got - ref).abs() <= eps * ref.abs() + 1e-5 * mag + 1e-30)
+
+
+@pytest.mark.parametrize("CO,W", [(64, 16), (32, 32)])
+def test_convt_rows_matches_tile_kernel(gpu_device, kernel_variant, CO, W):
+    N, H = 257, W
+    rng = np.random.default_rng(11 + CO)
+    x = torch.tensor(rng.uniform(0, 1, (N, H, W, 64)), dtype=torch.float16, device=gpu_device)
+    w = torch.tensor(rng.standard_normal((CO, 5, 5, 64)) * 0.03, dtype=torch.float16,
+                     device=gpu_device)
+    bias = torch.tensor(rng.standard_normal(CO) * 0.1, dtype=torch.float32, device=gpu_device)
+    a = torch.empty((N, 2 * H, 2 * W, CO), dtype=torch.float16, device=gpu_device)
+    b = torch.empty_like(a)
+    _convt_run(x, w, bias, CO, a)
+    kernel_variant("CONVT_NO_ROWS", 1)
+    _convt_run(x, w, bias, CO, b)
+    torch.cuda.synchronize()
+    assert "conv_patch_kernel" in _lib.last_kernel_name()
+    d = (a.float() - b.float()).abs()
+    assert float(d.max()) <= 2.0 ** -10 * float(b.float().abs().max())

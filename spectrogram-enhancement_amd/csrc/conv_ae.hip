@@ -2353,6 +2353,8 @@ int conv_rows_pool(int dtype, const void* x, int N, int H, int W, int CI, const 
                    const float* b, int CO, void* out, hipStream_t st, bool* launched);
 int convt_rows(int dtype, const void* x, int N, int H, int W, int CI, const void* w,
                const float* b, int CO, void* out, hipStream_t st, bool* launched);
+int conv1_rows_pool(int dtype, const void* x, int N, int H, int W, const void* w,
+                    const float* b, int CO, void* out, hipStream_t st, bool* launched);
 
 template <typename T>
 int launch_fwd(const ConvArgs& a, int nph, hipStream_t st) {
@@ -2567,6 +2569,14 @@ int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, cons
       !out_f32 && !pool2 && bias) {
     bool launched = false;
     const int rc = convt_rows(dtype, in, N, IH, IW, C, w_gemm, bias, CO, out, st, &launched);
+    if (rc != SPECENH_OK || launched) return rc;
+  }
+  // 1 input channel, pooled inference on 128-wide images: the row sweep (conv_rows.hip)
+  if (stride == 1 && in_dil == 1 && C == 1 && KH == 5 && KW == 5 && pad_t == 2 && pad_l == 2 &&
+      OH == IH && OW == IW && act == 1 && pool2 && !argmax && !mask && !logits && !out_f32 &&
+      bias && dtype != SPECENH_DTYPE_F32) {
+    bool launched = false;
+    const int rc = conv1_rows_pool(dtype, in, N, IH, IW, w_gemm, bias, CO, out, st, &launched);
     if (rc != SPECENH_OK || launched) return rc;
   }
   // 1 input channel: window rows as MFMA K runs (conv_c1_mfma.hip)

@@ -524,6 +524,173 @@ hipError_t launch_convt_rows(const CRArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ============================================================================ C = 1 rows
+// The first Conv2D(16, 5, relu, same) + MaxPooling2D(2) (VAE/manual_scan_3layers.py:187-188)
+// on W = 128 one-channel images, as a row sweep. As in conv_c1_mfma.hip the MFMA K index is
+// (ky, kx) with kx padded to 8: lane group kg's 8 K-elements are one 8-element run of input
+// row y - 2 + kg, so B(r) = rows r .. r + 3 and output row y = A0 x B(y - 2) + A1 x B'(y + 2)
+// (A0: kernel rows 0-3, A1: row 4 in lane group 0; B' = B with lane groups 1-3 zeroed).
+// Lane m of wave w owns output columns x = 32 w + 2 m + cb (cb = 0, 1): the 2 x 2 pool of
+// pooled pixel 16 w + m is in the lane's own four accumulators (rows 2p, 2p + 1 x cb), so a
+// step (pooled row p) is 8 MFMAs per wave, no cross-lane exchange, 8-byte stores of whole
+// 512-byte pixel runs per wave. conv_c1_mfma tiles 32 x 32 with a halo and re-read the
+// input 3.3x (PMC); here every row is read once.
+//  * a staged row holds elements x = -8 .. W + 5 (zero outside the image) twice, as 32-bit
+//    words as loaded (copy 0) and shifted by one element (copy 1), so every run starts on
+//    a word of one copy: a B fragment is 4 word reads (the run of column cb comes from
+//    copy cb);
+//  * the rows are one stream per workgroup: position il (H + 4) + r + 2 holds row r of the
+//    workgroup's image il (two zero rows above and below each image), step g = il (H/2 + 2)
+//    + p reads positions 2g .. 2g + 5 (p >= H/2: bubbles); LDS-DMA 5 steps ahead into a
+//    16-row ring (waited for two steps later), copy 1 built one step ahead of use.
+constexpr int C1W = 128;       // image width
+constexpr int C1CW = 72;       // words per copy (elements x = -8 .. W + 5, even count)
+constexpr int C1ROW = 2 * C1CW;  // words per staged row (copy 0, copy 1): 144 = 16 (mod 32)
+constexpr int C1RING = 16;
+constexpr int C1LDS = C1RING * C1ROW * 4;
+
+template <typename T>
+__global__ __launch_bounds__(256) void conv1_rows_pool_kernel(CRArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char ring_raw[];
+  uint32_t* const ring = reinterpret_cast<uint32_t*>(ring_raw);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = lane & 15, kg = lane >> 4;
+  const int H = a.H, SPI = H / 2 + 2, PPI = H + 4;
+  const int G = gridDim.x;
+  const int nimg = ((int)a.N - (int)blockIdx.x + G - 1) / G;
+  const int S = nimg * SPI;
+
+  for (int e = tid; e < C1RING * C1ROW; e += 256) ring[e] = 0u;
+  // A operand: lane (m, kg) = channel m, K = (kernel row kg, kx 0..7) / (row 4 in group 0)
+  uint4 w0, w1;
+  {
+    const T* __restrict__ Wg = reinterpret_cast<const T*>(a.w);
+    uint32_t q0[4], q1[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v[4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int kx = 2 * i + h;
+        v[2 * h] = kx < 5 ? (float)Wg[(m * 5 + kg) * 5 + kx] : 0.f;
+        v[2 * h + 1] = kx < 5 && kg == 0 ? (float)Wg[(m * 5 + 4) * 5 + kx] : 0.f;
+      }
+      q0[i] = pack2<T>(v[0], v[2]);
+      q1[i] = pack2<T>(v[1], v[3]);
+    }
+    w0 = uint4{q0[0], q0[1], q0[2], q0[3]};
+    w1 = uint4{q1[0], q1[1], q1[2], q1[3]};
+  }
+  const f32x4 bias = f32x4{a.b[4 * kg], a.b[4 * kg + 1], a.b[4 * kg + 2], a.b[4 * kg + 3]};
+
+  // ring refill (wave 0): positions pp, pp + 1 by LDS-DMA, 16 B (8 elements) per lane from
+  // lanes 0-15, into copy 0 words 4 .. 67 (x = 0 .. W - 1); returns the DMAs issued
+  const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
+  auto stage = [&](int pp) -> int {
+    if (wv != 0) return 0;
+    int nd = 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pos = pp + j;
+      const int il = pos / PPI, r = pos - il * PPI - 2;
+      uint32_t* dst = ring + (pos & (C1RING - 1)) * C1ROW + 4;  // x = 0 is word 4
+      if (il < nimg && r >= 0 && r < H) {
+        const long long n = (long long)blockIdx.x + (long long)il * G;
+        if (lane < 16) lds_dma16(X + (n * H + r) * C1W + 8 * lane, dst);
+        ++nd;
+      } else if (lane < 16) {
+        *reinterpret_cast<uint4*>(dst + 4 * lane) = uint4{0u, 0u, 0u, 0u};
+      }
+    }
+    return nd;
+  };
+  // copy 1 of positions pp, pp + 1: word i = elements (2i + 1, 2i + 2) of copy 0
+  auto shift = [&](int pp) {
+    if (tid < 2 * C1CW) {
+      const int j = tid / C1CW, i = tid - j * C1CW;
+      uint32_t* row = ring + ((pp + j) & (C1RING - 1)) * C1ROW;
+      const uint32_t lo = row[i], hi = row[i + 1];  // i = 71 reads copy 1 word 0: unused
+      row[C1CW + i] = __builtin_amdgcn_alignbit(hi, lo, 16);
+    }
+  };
+  __syncthreads();  // ring zeroed
+  for (int pp = 0; pp < 10; pp += 2) stage(pp);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  shift(0); shift(2); shift(4);
+  lds_barrier();
+
+  // B fragment of position pos (rows pos .. pos + 3 in lane groups 0..3), column block cb:
+  // words 16 w + m + 3 .. + 6 of copy cb of row pos + kg
+  const int wbase = 16 * wv + m + 3;
+  auto bfrag = [&](int pos, int cb) -> uint4 {
+    const uint32_t* row = ring + ((pos + kg) & (C1RING - 1)) * C1ROW + cb * C1CW + wbase;
+    return uint4{row[0], row[1], row[2], row[3]};
+  };
+  T* __restrict__ O = reinterpret_cast<T*>(a.out);
+  const int PW = C1W / 2, PH = H / 2;
+  for (int g = 0; g < S; ++g) {
+    // positions 2g + 10, 2g + 11 into the ring (their slots held 2g - 6, 2g - 5: done)
+    const int nd = stage(2 * g + 10);
+    shift(2 * g + 6);  // copy 1 for step g + 1 (positions landed at the end of step g - 1)
+    const int il = g / SPI, p = g - il * SPI;
+    if (p < PH) {
+      const int pb = 2 * g;  // position of input row 2p - 2
+      f32x4 acc[2][2];
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          // output row y = 2p + dy: B(y - 2) at position pb + dy, B'(y + 2) at pb + dy + 4
+          const uint4 b = bfrag(pb + dy, cb);
+          uint4 b4 = bfrag(pb + dy + 4, cb);
+          if (kg != 0) b4 = uint4{0u, 0u, 0u, 0u};
+          acc[dy][cb] = mfma<T>(w0, b, bias);
+          acc[dy][cb] = mfma<T>(w1, b4, acc[dy][cb]);
+        }
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        v[i] = fmaxf(fmaxf(fmaxf(acc[0][0][i], acc[0][1][i]), fmaxf(acc[1][0][i], acc[1][1][i])),
+                     0.f);
+      const long long n = (long long)blockIdx.x + (long long)il * G;
+      *reinterpret_cast<uint2*>(O + ((n * PH + p) * PW + 16 * wv + m) * 16 + 4 * kg) =
+          uint2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
+    }
+    // wave 0: the DMAs of step g - 1 (positions 2g + 8, 2g + 9, shifted at step g + 1) must
+    // land before the barrier; this step's DMAs and its store are the youngest vector-memory
+    // ops, so wait for all but those. The other waves issue only stores: no wait.
+    if (wv == 0) {
+      const int younger = nd + (p < PH ? 1 : 0);
+      if (younger == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else if (younger == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    }
+    lds_barrier();
+  }
+}
+
+template <typename T>
+hipError_t launch_conv1_rows(const CRArgs& a, hipStream_t st) {
+  const void* k = reinterpret_cast<const void*>(&conv1_rows_pool_kernel<T>);
+  static int per_cu[64] = {};
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (per_cu[dev] == 0) {
+    int pc = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k, 256, C1LDS);
+    if (e != hipSuccess) return e;
+    per_cu[dev] = std::max(1, pc);
+  }
+  const long long grid = std::min<long long>(a.N, (long long)per_cu[dev] * device_cus());
+  SPECENH_LAUNCH(conv1_rows_pool_kernel<T>, dim3((unsigned)grid), dim3(256), C1LDS, st, a);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 // The row-sweep kernel for an inference Conv2D(5, relu, same) + MaxPooling2D(2) when the
@@ -573,6 +740,28 @@ int convt_rows(int dtype, const void* x, int N, int H, int W, int CI, const void
   else
     return SPECENH_OK;
   if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("convt_rows: ") + hipGetErrorString(e));
+  *launched = true;
+  return SPECENH_OK;
+}
+
+}  // namespace specenh
+
+namespace specenh {
+
+// The C = 1 row sweep for an inference Conv2D(16, 5, relu, same) + MaxPooling2D(2) on
+// 128-wide images; *launched = false otherwise (the caller runs conv_c1_mfma).
+int conv1_rows_pool(int dtype, const void* x, int N, int H, int W, const void* w,
+                    const float* b, int CO, void* out, hipStream_t st, bool* launched) {
+  *launched = false;
+  if (variant(V_CONV1_NO_ROWS) != 0 || N <= 0 || H < 2 || (H & 1) || W != C1W || CO != 16 || !b)
+    return SPECENH_OK;
+  if (dtype != SPECENH_DTYPE_F16 && dtype != SPECENH_DTYPE_BF16) return SPECENH_OK;
+  if (((uintptr_t)x & 15) || (long long)N * H * W >= (1ll << 31)) return SPECENH_OK;
+  CRArgs a{};
+  a.x = x; a.w = w; a.b = b; a.out = out; a.N = N; a.H = H;
+  const hipError_t e = dtype == SPECENH_DTYPE_F16 ? launch_conv1_rows<_Float16>(a, st)
+                                                  : launch_conv1_rows<__bf16>(a, st);
+  if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("conv1_rows: ") + hipGetErrorString(e));
   *launched = true;
   return SPECENH_OK;
 }

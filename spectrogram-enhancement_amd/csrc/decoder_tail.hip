@@ -679,7 +679,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
   const int m = lane & 15, kg = lane >> 4;
   const int n = blockIdx.x;
   const int H1 = a.H, H2 = 2 * H1, H3 = 4 * H1;
-  const int S = H1 + 2;  // macro steps
+  const int S = H1 + 3;  // macro steps (the consumer's Conv2D(1) runs one tail step behind)
   {
     uint4* z = reinterpret_cast<uint4*>(lds_raw);
     for (int e = tid; e < LDS_BYTES / 16; e += 512) z[e] = uint4{0u, 0u, 0u, 0u};
@@ -797,21 +797,26 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
 #pragma unroll
     for (int dx = -1; dx <= 1; ++dx) xo[dx + 1] = x2_off(16 * w + m + dx + 1, kg);
     lds_barrier();  // macro step -1
-    // tail step t (= 2s - 3 or 2s - 2) with T8 = t & 7 compile-time from s & 3
+    // tail step t (= 2s - 3 or 2s - 2) with T8 = t & 7 compile-time from s & 3. The
+    // Conv2D(1) of step t is for output rows 2t - 4, 2t - 3 (map rows 2t - 6 .. 2t - 1, all
+    // written by earlier steps: the 8-row map ring holds 2t - 6 .. 2t + 1), so it does not
+    // wait for this step's Conv2DTranspose and the two MFMA streams interleave. It is
+    // issued first: its map reads then precede this step's map writes into the slots of
+    // rows 2t - 8, 2t - 7.
     auto tstep = [&](auto ic, const int t, float* scb) {
       constexpr int T8 = decltype(ic)::value;  // t & 7: the tail-input ring slot of row t
       constexpr int T4 = T8 & 3;                // the map ring: rows 2t, 2t + 1 in slots 2 T4 ..
-      if (t < 0 || t > H2) return;
+      if (t < 0 || t > H2 + 1) return;
+      if (t >= 2)
+        tw.conv_out_d([&](int j) { return mr + ((2 * T4 - 6 + j + 8) & 7) * rows::MROW; }, scb,
+                      m);
       T* const m0 = mr + ((2 * T4) & 7) * rows::MROW;
       T* const m1 = mr + ((2 * T4 + 1) & 7) * rows::MROW;
       if (t < H2)
         tw.convt(x2r, [](int dy) { return ((T8 + dy + 8) & 7) * X2ROW; },
                  [&](int dx) { return xo[dx + 1]; }, m0, m1);
-      else
+      else if (t == H2)
         tw.zero_rows(m0, m1);
-      if (t >= 1)
-        tw.conv_out_d([&](int j) { return mr + ((2 * T4 - 4 + j + 8) & 7) * rows::MROW; }, scb,
-                      m);
     };
     auto cstep = [&](auto ic, const int s) {
       constexpr int I = decltype(ic)::value;  // s & 3
@@ -820,8 +825,9 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       tstep(IC<(2 * I + 5) & 7>{}, 2 * s - 3, sc0);  // (2s - 3) & 7 = (2 I - 3) & 7
       tstep(IC<(2 * I + 6) & 7>{}, 2 * s - 2, sc1);
       lds_barrier();
-      if (2 * s - 3 >= 1) tw.conv_out_sums(sc0, O, 2 * (2 * s - 3) - 2, lane);
-      if (2 * s - 2 >= 1) tw.conv_out_sums(sc1, O, 2 * (2 * s - 2) - 2, lane);
+      const int t0 = 2 * s - 3, t1 = 2 * s - 2;
+      if (t0 >= 2 && t0 <= H2 + 1) tw.conv_out_sums(sc0, O, 2 * t0 - 4, lane);
+      if (t1 >= 2 && t1 <= H2 + 1) tw.conv_out_sums(sc1, O, 2 * t1 - 4, lane);
     };
     int s = 0;
     for (; s + 4 <= S; s += 4) {

@@ -24,7 +24,7 @@ constexpr VariantName kVariants[V_COUNT] = {
     {"CONV_NO_C1MFMA", 0},  {"CONV_NO_NARROW", 0},   {"WGRAD_GENERIC", 0},
     {"WGRAD_NO_CO1", 0},    {"WGRAD_PERPHASE", 0},   {"SVD_GRAM_TILES", 0},
     {"TAIL_TILES", 0},      {"DECODER_UNFUSED", 0},  {"SVD_NO_TOP1", 0},
-    {"CONV_NO_ROWS", 0},    {"CONVT_NO_ROWS", 0},
+    {"CONV_NO_ROWS", 0},    {"CONVT_NO_ROWS", 0},    {"CONV1_NO_ROWS", 0},
 };
 
 std::atomic<int> g_variant[V_COUNT];

@@ -29,6 +29,7 @@ enum Variant : int {
   V_SVD_NO_TOP1,      // default kept range [1, r): Gram + subspace + recon instead of top1_kernel
   V_CONV_NO_ROWS,     // pooled encoder convs: conv_patch_kernel tiles instead of the row sweep
   V_CONVT_NO_ROWS,    // Conv2DTranspose on 64 channels: conv_patch_kernel instead of the row sweep
+  V_CONV1_NO_ROWS,    // C = 1 pooled conv: conv_c1_mfma tiles instead of the row sweep
   V_COUNT
 };
 

@@ -135,3 +135,41 @@ def test_convt_rows_matches_tile_kernel(gpu_device, kernel_variant, CO, W):
     assert "conv_patch_kernel" in _lib.last_kernel_name()
     d = (a.float() - b.float()).abs()
     assert float(d.max()) <= 2.0 ** -10 * float(b.float().abs().max())
+
+
+# ---------------------------------------------------------------- C = 1 row sweep
+# (csrc/conv_rows.hip conv1_rows_pool_kernel; VAE/manual_scan_3layers.py:187-188)
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,H", [(1, 128), (3, 2), (5, 10), (300, 64), (2, 130)])
+def test_conv1_rows_vs_float64(gpu_device, dtype, N, H):
+    rng = np.random.default_rng(N + H)
+    x = torch.tensor(rng.uniform(0, 1, (N, H, 128, 1)), dtype=dtype, device=gpu_device)
+    w = torch.tensor(rng.standard_normal((16, 5, 5, 1)) * 0.3, dtype=dtype, device=gpu_device)
+    bias = torch.tensor(rng.standard_normal(16) * 0.2, dtype=torch.float32, device=gpu_device)
+    out = torch.full((N, H // 2, 64, 16), float("nan"), dtype=dtype, device=gpu_device)
+    _run(x, w, bias, 16, out)
+    torch.cuda.synchronize()
+    assert "conv1_rows_pool_kernel" in _lib.last_kernel_name()
+    ref, mag = _ref(x, w, bias)
+    got = out.double().cpu()
+    assert bool(torch.isfinite(got).all())
+    eps = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
+    assert torch.all((got - ref).abs() <= eps * ref.abs() + 1e-5 * mag + 1e-30)
+
+
+def test_conv1_rows_matches_tile_kernel(gpu_device, kernel_variant):
+    N, H = 2048, 128
+    rng = np.random.default_rng(77)
+    x = torch.tensor(rng.uniform(0, 1, (N, H, 128, 1)), dtype=torch.float16, device=gpu_device)
+    w = torch.tensor(rng.standard_normal((16, 5, 5, 1)) * 0.3, dtype=torch.float16,
+                     device=gpu_device)
+    bias = torch.tensor(rng.standard_normal(16) * 0.2, dtype=torch.float32, device=gpu_device)
+    a = torch.full((N, 64, 64, 16), float("nan"), dtype=torch.float16, device=gpu_device)
+    b = torch.empty_like(a)
+    _run(x, w, bias, 16, a)
+    kernel_variant("CONV1_NO_ROWS", 1)
+    _run(x, w, bias, 16, b)
+    torch.cuda.synchronize()
+    assert "conv_c1_mfma_kernel" in _lib.last_kernel_name()
+    d = (a.float() - b.float()).abs()
+    assert float(d.max()) <= 2.0 ** -10 * float(b.float().abs().max())

@@ -124,11 +124,14 @@ LAYER_NAMES_DEC3 = LAYER_NAMES[:4] + ["convT2+convT3+conv_out"]
 
 
 def layer_names(eng):
-    """Names of the forward's launches (the engine's fusions: decoder3 / tail)."""
-    return LAYER_NAMES_DEC3 if eng.dec3 else (LAYER_NAMES_TAIL if eng.tail else LAYER_NAMES)
+    """Names of the forward's launches (the engine's fusions: encoder2 / decoder3 / tail)."""
+    names = LAYER_NAMES_DEC3 if eng.dec3 else (LAYER_NAMES_TAIL if eng.tail else LAYER_NAMES)
+    if getattr(eng, "enc2", False):
+        names = ["conv1+pool+conv2+pool"] + names[2:]
+    return names
 
 
-def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4, tail=False, dec3=False):
+def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4, tail=False, dec3=False, enc2=False):
     """Per launch of the fused forward (conv+pool fused; with ``tail`` the last
     Conv2DTranspose + Conv2D(1) are one launch, csrc/decoder_tail.hip): useful FLOPs and
     algorithmic HBM bytes per sample (activations read once + written once), the weights
@@ -166,6 +169,11 @@ def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4, tail=False, dec3=Fals
                            h * w * out_bytes,
                            "weight_bytes": a["weight_bytes"] + b["weight_bytes"],
                            "unit": "mfma"}]
+    if enc2:  # conv1+pool and conv2+pool as one launch: the pooled 16-channel map stays in LDS
+        a, b = res[0], res[1]
+        res = [{"flops": a["flops"] + b["flops"], "mfma_flops": a["mfma_flops"] + b["mfma_flops"],
+                "bytes": h * w * act_bytes + (h // 4) * (w // 4) * AE_FILTERS[1] * act_bytes,
+                "weight_bytes": a["weight_bytes"] + b["weight_bytes"], "unit": "mfma"}] + res[2:]
     return res
 
 
@@ -667,7 +675,8 @@ def main():
     pmc = load_pmc()
     layers = []
     names = layer_names(eng)
-    for name, c, ms, sym in zip(names, ae_layer_costs(tail=eng.tail, dec3=eng.dec3), layer_ms,
+    for name, c, ms, sym in zip(names, ae_layer_costs(tail=eng.tail, dec3=eng.dec3,
+                                                      enc2=getattr(eng, "enc2", False)), layer_ms,
                                 kernels):
         # compute floor: MFMA FLOPs at the dense fp16 MFMA peak + VALU FLOPs at the dot2 peak
         t_c = c["mfma_flops"] * Hs / (MFMA_PEAK_TFLOPS * 1e12) + \

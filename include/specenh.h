@@ -278,6 +278,19 @@ int specenh_decoder3(int dtype, const void* x, int N, int H, int W, int C,
                      const float* bt, int CO2, const void* wo_gemm, const float* bo, int k,
                      float* out, void* stream);
 
+/* The encoder's first TWO layers in one launch (VAE/manual_scan_3layers.py:187-191, the
+ * inference path of predict :239):
+ *   x [N][H][W][1] -> Conv2D(CO1, k, relu, "same") -> MaxPooling2D(2)
+ *                  -> Conv2D(CO2, k, relu, "same") -> MaxPooling2D(2) -> out [N][H/4][W/4][CO2]
+ * w1_gemm / b1, w2_gemm / b2: the two layers' specenh_conv2d weights (GEMM layout, dtype) and
+ * fp32 biases. The pooled CO1-channel map stays in LDS, rounded to dtype after its ReLU
+ * exactly as the unfused path stores it. dtype BF16 / F16; W = 128, CO1 = 16, CO2 = 32,
+ * k = 5, H a multiple of 4, x 16-byte aligned (the reference model on 128 x 128 inputs),
+ * otherwise SPECENH_EUNSUPPORTED / SPECENH_EINVAL. */
+int specenh_encoder2(int dtype, const void* x, int N, int H, int W, const void* w1_gemm,
+                     const float* b1, int CO1, const void* w2_gemm, const float* b2, int CO2,
+                     int k, void* out, void* stream);
+
 /* ---------------------------------------------------------------- label filters
  * The image-filter helpers of spec_denoising/pipeline_data.py:38-61 (the training-label
  * chain) on a batch of spectrograms, each a rows x cols row-major block at

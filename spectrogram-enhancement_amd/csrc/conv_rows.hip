@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <type_traits>
 
@@ -691,6 +692,277 @@ hipError_t launch_conv1_rows(const CRArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ============================================================================ encoder 1+2
+// The encoder's first two layers in one launch (VAE/manual_scan_3layers.py:187-191):
+// Conv2D(16, 5, relu) + MaxPooling2D(2) on 128 x 128 one-channel images, then Conv2D(32, 5,
+// relu) + MaxPooling2D(2). The 64 x 64 x 16 map between them (128 KB per image, written and
+// read once each by the two-launch path) is produced in conv2's LDS ring and never reaches
+// HBM. The conv2 part is conv_rows_pool_kernel<T, 16, 32, 64> step for step; instead of an
+// LDS-DMA of its input rows, step s computes the two conv2 input rows of step s + 2 with
+// the conv1 row sweep (conv1_rows_pool_kernel: waves 0-3 the first row, 4-7 the second,
+// 16 pooled pixels each) from a 32-row stream of the images' rows (4 per step: H + 4 =
+// 4 (H/4 + 1) positions per image), LDS-DMA 8 steps ahead, copy 1 built 4 steps later.
+struct E2Args {
+  const void* x;    // [N][H][128] (C = 1)
+  const void* w1;   // conv1 GEMM weights [16][5][5]
+  const float* b1;  // [16]
+  const void* w2;   // conv2 GEMM weights [32][5][5][16]
+  const float* b2;  // [32]
+  void* out;        // [N][H/4][32][32]
+  int N, H;
+};
+
+constexpr int E2R1 = 32;  // conv1 input ring rows (positions)
+
+template <typename T>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+void enc2_rows_kernel(E2Args a) {
+  using C = RC<16, 32, 64>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  unsigned char* const ring = lds;                                        // conv2 input rows
+  uint32_t* const ring1 = reinterpret_cast<uint32_t*>(lds + C::LDS);     // image rows
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = lane & 15, kg = lane >> 4;
+  const int wx = wv % C::NWIN, nb = wv / C::NWIN;
+  const int x0 = 16 * wx;
+  const int H1 = a.H, H = H1 / 2;           // conv1 / conv2 input heights
+  const int SPI = H / 2 + 1, PPI = H1 + 4;  // conv2 steps and image-row positions per image
+  const int G = gridDim.x;
+  const int nimg = ((int)a.N - (int)blockIdx.x + G - 1) / G;
+  const int S = nimg * SPI + 1;
+
+  for (int e = tid; e < (C::LDS + E2R1 * C1ROW * 4) / 16; e += 512)
+    reinterpret_cast<uint4*>(lds)[e] = uint4{0u, 0u, 0u, 0u};
+
+  // ---- conv2: resident weight fragments (as conv_rows_pool_kernel, CIN = 16) ----
+  uint4 wf[13];
+  {
+    const T* __restrict__ Wg = reinterpret_cast<const T*>(a.w2);
+    const int co = 16 * nb + m, hi = kg >> 1, c8 = 8 * (kg & 1);
+    auto tap = [&](int ky, int kx) {
+      return *reinterpret_cast<const uint4*>(Wg + ((co * 5 + ky) * 5 + kx) * 16 + c8);
+    };
+#pragma unroll
+    for (int ky = 0; ky < 5; ++ky) {
+      wf[ky] = tap(ky, hi);
+      wf[5 + ky] = tap(ky, 2 + hi);
+    }
+    wf[10] = tap(hi, 4);
+    wf[11] = tap(2 + hi, 4);
+    wf[12] = hi ? uint4{0u, 0u, 0u, 0u} : tap(4, 4);
+  }
+  const f32x4 bias = f32x4{a.b2[16 * nb + 4 * kg], a.b2[16 * nb + 4 * kg + 1],
+                           a.b2[16 * nb + 4 * kg + 2], a.b2[16 * nb + 4 * kg + 3]};
+  const int boff = (x0 + m + (kg >> 1)) * 32 + 16 * (kg & 1);
+  const int fo = (x0 + m + 4) * 32 + 16 * (kg & 1);
+  const int foff = fo + (kg >> 1) * C::ROWB, foffw = fo - (kg >> 1) * 7 * C::ROWB;
+
+  // ---- conv1: A fragments (kernel rows 0-3 / row 4 in lane group 0) ----
+  uint4 v0, v1;
+  {
+    const T* __restrict__ W1 = reinterpret_cast<const T*>(a.w1);
+    uint32_t q0[4], q1[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v[4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int kx = 2 * i + h;
+        v[2 * h] = kx < 5 ? (float)W1[(m * 5 + kg) * 5 + kx] : 0.f;
+        v[2 * h + 1] = kx < 5 && kg == 0 ? (float)W1[(m * 5 + 4) * 5 + kx] : 0.f;
+      }
+      q0[i] = pack2<T>(v[0], v[2]);
+      q1[i] = pack2<T>(v[1], v[3]);
+    }
+    v0 = uint4{q0[0], q0[1], q0[2], q0[3]};
+    v1 = uint4{q1[0], q1[1], q1[2], q1[3]};
+  }
+  const f32x4 bias1 = f32x4{a.b1[4 * kg], a.b1[4 * kg + 1], a.b1[4 * kg + 2], a.b1[4 * kg + 3]};
+  const int w1x = wv & 3, jr = wv >> 2;  // conv1 pixel block, conv2 input row of the pair
+  const int wbase = 16 * w1x + m + 3;
+
+  // image-row stream: position pp = il (H1 + 4) + y + 2; waves 0-3 move positions pp + wv
+  const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
+  auto stage1 = [&](int pp) -> int {
+    if (wv >= 4) return 0;
+    const int pos = pp + wv;
+    const int il = pos / PPI, y = pos - il * PPI - 2;
+    uint32_t* dst = ring1 + (pos & (E2R1 - 1)) * C1ROW + 4;
+    if (il < nimg && y >= 0 && y < H1) {
+      const long long n = (long long)blockIdx.x + (long long)il * G;
+      if (lane < 16) lds_dma16(X + (n * H1 + y) * C1W + 8 * lane, dst);
+      return 1;
+    }
+    if (lane < 16) *reinterpret_cast<uint4*>(dst + 4 * lane) = uint4{0u, 0u, 0u, 0u};
+    return 0;
+  };
+  auto shift1 = [&](int pp) {  // copy 1 of positions pp .. pp + 3
+    if (tid < 4 * C1CW) {
+      const int j = tid / C1CW, i = tid - j * C1CW;
+      uint32_t* row = ring1 + ((pp + j) & (E2R1 - 1)) * C1ROW;
+      row[C1CW + i] = __builtin_amdgcn_alignbit(row[i + 1], row[i], 16);
+    }
+  };
+  auto bfrag = [&](int pos, int cb) -> uint4 {
+    const uint32_t* row = ring1 + ((pos + kg) & (E2R1 - 1)) * C1ROW + cb * C1CW + wbase;
+    return uint4{row[0], row[1], row[2], row[3]};
+  };
+  // conv2 input row 2 q2 + jr of conv2 step g2 (image g2 / SPI) into its ring slot: pooled
+  // pixels 16 w1x + m, channels 4 kg .. 4 kg + 3 (zero rows outside the image)
+  auto produce = [&](int g2) {
+    const int il = g2 / SPI, q2 = g2 - il * SPI;
+    const int r = 2 * q2 + jr;
+    uint2 pk = uint2{0u, 0u};
+    if (il < nimg && r < H) {
+      const int pb = 4 * g2 + 2 * jr;  // position of image row 2r - 2
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const uint4 b = bfrag(pb + dy, cb);
+          uint4 b4 = bfrag(pb + dy + 4, cb);
+          if (kg != 0) b4 = uint4{0u, 0u, 0u, 0u};
+          f32x4 acc = mfma<T>(v0, b, bias1);
+          acc = mfma<T>(v1, b4, acc);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], acc[i]);  // (>= 0: relu folded)
+        }
+      pk = uint2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
+    }
+    *reinterpret_cast<uint2*>(ring + ((2 * g2 + jr) & 7) * C::ROWB + (16 * w1x + m + 2) * 32 +
+                              8 * kg) = pk;
+  };
+
+  __syncthreads();  // rings zeroed
+  for (int pp = 0; pp < 32; pp += 4) stage1(pp);  // positions 0 .. 31 (steps -8 .. -1)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  for (int pp = 0; pp < 16; pp += 4) shift1(pp);
+  lds_barrier();
+  produce(0);
+  produce(1);
+  lds_barrier();
+
+  f32x4 acc[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) acc[i] = bias;
+  T* __restrict__ O = reinterpret_cast<T*>(a.out);
+  const int PW = 32, PHh = H / 2;
+  int c_1 = 0, c_2 = 0;  // this wave's vector-memory ops (store + LDS-DMA) of steps s - 1, s - 2
+
+  auto step = [&](auto ic, const int s) {
+    constexpr int I = decltype(ic)::value;
+    auto slot = [](int d) { return (2 * I + d + 12) % 6; };
+    int ns = 0;  // stores issued by this wave in this step
+    {  // conv2 pair s - 2: pool, store, reset
+      const int p = s - 2;
+      f32x4& r0 = acc[slot(-4)];
+      f32x4& r1 = acc[slot(-3)];
+      if (p >= 0) {
+        const int il = p / SPI, q = p - il * SPI;
+        if (il < nimg && q < PHh) {
+          ns = 1;
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = fmaxf(max_pair(fmaxf(r0[i], r1[i])), 0.f);
+          if ((m & 1) == 0) {
+            const long long n = (long long)blockIdx.x + (long long)il * G;
+            const long long o = ((n * PHh + q) * PW + (x0 + m) / 2) * 32 + 16 * nb + 4 * kg;
+            *reinterpret_cast<uint2*>(O + o) = uint2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
+          }
+        }
+      }
+      r0 = bias;
+      r1 = bias;
+    }
+    // image rows 8 steps ahead (positions 4s + 32 .. 4s + 35: slots of 4s .. 4s + 3, whose
+    // last readers were this step's predecessors), copy 1 of positions 4s + 16 .. 4s + 19
+    // (landed: DMA of step s - 4, waited at the end of step s - 1), conv2 input rows of
+    // step s + 2 (positions 4s + 8 .. 4s + 15)
+    const int nd = stage1(4 * s + 32);
+    shift1(4 * s + 16);
+    produce(s + 2);
+    const int il = s / SPI, q = s - il * SPI;
+    if (il < nimg && 2 * q < H) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int rs = (2 * s + j) & 7;
+        const unsigned char* rb = ring + rs * C::ROWB;
+        const uint4 b0 = *reinterpret_cast<const uint4*>(rb + boff);
+        const uint4 b2 = *reinterpret_cast<const uint4*>(rb + boff + 64);
+        const uint4 bF = *reinterpret_cast<const uint4*>(rb + (rs == 7 ? foffw : foff));
+#pragma unroll
+        for (int ky = 0; ky < 5; ++ky) {
+          f32x4& ac = acc[slot(j + 2 - ky)];
+          ac = mfma<T>(wf[ky], b0, ac);
+        }
+#pragma unroll
+        for (int ky = 0; ky < 5; ++ky) {
+          f32x4& ac = acc[slot(j + 2 - ky)];
+          ac = mfma<T>(wf[5 + ky], b2, ac);
+        }
+        acc[slot(j + 2)] = mfma<T>(wf[10], bF, acc[slot(j + 2)]);
+        acc[slot(j)] = mfma<T>(wf[11], bF, acc[slot(j)]);
+        acc[slot(j - 2)] = mfma<T>(wf[12], bF, acc[slot(j - 2)]);
+        if (j == 0 && q == 0) {
+          uint4 bT = *reinterpret_cast<const uint4*>(ring + ((2 * s) & 7) * C::ROWB + fo);
+          if (kg < 2) bT = uint4{0u, 0u, 0u, 0u};
+          acc[slot(1)] = mfma<T>(wf[10], bT, acc[slot(1)]);
+        }
+      }
+    }
+    // the DMA of step s - 3 (copy-1 shifted at step s + 1) must have landed: wait for all
+    // but this wave's vector-memory ops of steps s - 2 .. s (each step: its store, then its
+    // DMA). Only the DMA waves wait; stores alone are never waited for.
+    if (wv < 4) {
+      const int younger = c_2 + c_1 + ns + nd;
+      switch (younger) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+      }
+    }
+    c_2 = c_1;
+    c_1 = ns + nd;
+    lds_barrier();
+  };
+  int s = 0;
+  for (; s + 3 <= S; s += 3) {
+    step(std::integral_constant<int, 0>{}, s);
+    step(std::integral_constant<int, 1>{}, s + 1);
+    step(std::integral_constant<int, 2>{}, s + 2);
+  }
+  if (s < S) step(std::integral_constant<int, 0>{}, s);
+  if (s + 1 < S) step(std::integral_constant<int, 1>{}, s + 1);
+}
+
+constexpr int E2LDS = RC<16, 32, 64>::LDS + E2R1 * C1ROW * 4;
+
+template <typename T>
+hipError_t launch_enc2(const E2Args& a, hipStream_t st) {
+  const void* k = reinterpret_cast<const void*>(&enc2_rows_kernel<T>);
+  static int per_cu[64] = {};
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (per_cu[dev] == 0) {
+    int pc = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k, 512, E2LDS);
+    if (e != hipSuccess) return e;
+    per_cu[dev] = std::max(1, pc);
+  }
+  const long long grid = std::min<long long>(a.N, (long long)per_cu[dev] * device_cus());
+  SPECENH_LAUNCH(enc2_rows_kernel<T>, dim3((unsigned)grid), dim3(512), E2LDS, st, a);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 // The row-sweep kernel for an inference Conv2D(5, relu, same) + MaxPooling2D(2) when the
@@ -767,3 +1039,36 @@ int conv1_rows_pool(int dtype, const void* x, int N, int H, int W, const void* w
 }
 
 }  // namespace specenh
+
+// Conv2D(16, 5, relu, same) + MaxPooling2D(2) + Conv2D(32, 5, relu, same) + MaxPooling2D(2)
+// on [N][H][128][1] 16-bit images (H a multiple of 4) in one launch (enc2_rows_kernel).
+extern "C" int specenh_encoder2(int dtype, const void* x, int N, int H, int W, const void* w1_gemm,
+                                const float* b1, int CO1, const void* w2_gemm, const float* b2,
+                                int CO2, int k, void* out, void* stream) {
+  using namespace specenh;
+  if (N < 0 || H <= 0 || W <= 0) return set_error(SPECENH_EINVAL, "bad input shape");
+  if (dtype != SPECENH_DTYPE_F16 && dtype != SPECENH_DTYPE_BF16)
+    return set_error(SPECENH_EUNSUPPORTED, "fused encoder: fp16 / bf16 only");
+  if (W != C1W || CO1 != 16 || CO2 != 32 || k != 5 || (H & 3))
+    return set_error(SPECENH_EUNSUPPORTED,
+                     "fused encoder: Conv2D(16, 5) + pool + Conv2D(32, 5) + pool on 128-wide "
+                     "one-channel images, height a multiple of 4");
+  if (N == 0) return SPECENH_OK;
+  if (!x || !w1_gemm || !b1 || !w2_gemm || !b2 || !out) return set_error(SPECENH_EINVAL, "null pointer");
+  if (((uintptr_t)x & 15) || (long long)N * H * W >= (1ll << 31))
+    return set_error(SPECENH_EINVAL, "input must be 16-byte aligned and below 2^31 elements");
+  E2Args a{};
+  a.x = x; a.w1 = w1_gemm; a.b1 = b1; a.w2 = w2_gemm; a.b2 = b2; a.out = out; a.N = N; a.H = H;
+  hipStream_t st = (hipStream_t)stream;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&enc2_rows_kernel<_Float16>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, E2LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&enc2_rows_kernel<__bf16>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, E2LDS);
+  });
+  const hipError_t e = dtype == SPECENH_DTYPE_F16 ? launch_enc2<_Float16>(a, st)
+                                                  : launch_enc2<__bf16>(a, st);
+  if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("encoder2: ") + hipGetErrorString(e));
+  return SPECENH_OK;
+}

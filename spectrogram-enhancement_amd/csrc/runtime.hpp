@@ -30,6 +30,7 @@ enum Variant : int {
   V_CONV_NO_ROWS,     // pooled encoder convs: conv_patch_kernel tiles instead of the row sweep
   V_CONVT_NO_ROWS,    // Conv2DTranspose on 64 channels: conv_patch_kernel instead of the row sweep
   V_CONV1_NO_ROWS,    // C = 1 pooled conv: conv_c1_mfma tiles instead of the row sweep
+  V_ENCODER_UNFUSED,  // engine (Python): no two-layer encoder launch (specenh_encoder2)
   V_COUNT
 };
 

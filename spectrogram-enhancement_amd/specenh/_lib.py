@@ -107,6 +107,9 @@ SIGNATURES = {
                                     _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p, _c.c_void_p,
                                     _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p,
                                     _c.c_void_p]),
+    "specenh_encoder2": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                    _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p, _c.c_void_p,
+                                    _c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p]),
     "specenh_maxpool2_fwd": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
                                         _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p]),
     "specenh_maxpool2_bwd": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p,

@@ -31,7 +31,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .ops import decoder3_supported, ops, tail_supported
+from .ops import decoder3_supported, encoder2_supported, ops, tail_supported
 
 F32, BF16, F16 = 0, 1, 2
 _DTYPES = {"float32": F32, "bfloat16": BF16, "bf16": BF16, "mixed_bfloat16": BF16,
@@ -171,6 +171,18 @@ class AutoencoderEngine:
                                                 o3.k, w_in)
                          and o3.k == self.ops[-2].k == self.ops[-1].k
                          and _lib.get_variant("DECODER_UNFUSED") == 0)
+        # inference: the FIRST two layers (Conv2D + pool, Conv2D + pool) as one launch
+        # (csrc/conv_rows.hip enc2_rows_kernel) on the reference model's 128-wide one-channel
+        # inputs; the pooled 16-channel map between them stays in LDS
+        self.enc2 = False
+        if len(self.ops) >= 4 and 0 in self.fused and 2 in self.fused:
+            o1, o2 = self.ops[0], self.ops[2]
+            self.enc2 = (o1.kind == o2.kind == "conv" and o1.act == o2.act == "relu"
+                         and o1.padding == o2.padding == "same" and o1.k == o2.k
+                         and o2.cin == o1.cout
+                         and encoder2_supported(self.tdt, o1.cin, o1.cout, o2.cout, o1.k,
+                                                self.input_shape[0], self.input_shape[1])
+                         and _lib.get_variant("ENCODER_UNFUSED") == 0)
         self.t = 0  # Adam iterations
         self._bufs = {}
         self._loss = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -235,7 +247,8 @@ class AutoencoderEngine:
             last = i == len(self.ops)
             dtype = torch.float32 if (last and not train) else self.tdt
             tail_map = not train and ((self.tail and i == len(self.ops) - 1) or
-                                      (self.dec3 and i == len(self.ops) - 2))
+                                      (self.dec3 and i == len(self.ops) - 2) or
+                                      (self.enc2 and i == 2))  # maps kept in LDS
             if (i - 1) not in self.fused and not tail_map:  # never-stored fused outputs
                 b["h"][i] = torch.empty((N, H, W, C), dtype=dtype, device=dev)
             if train:
@@ -316,7 +329,23 @@ class AutoencoderEngine:
             self._last_train_N = N
         n_ops = len(self.ops)
         skip = False
+        start = 0
+        if self.enc2 and not train:  # conv1 + pool + conv2 + pool, one launch
+            if timing is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record(torch.cuda.current_stream(self.device))
+            o1, o2 = self.ops[0], self.ops[2]
+            ops.encoder2_out(x, self._wv[0], self._bv[0], o1.cout, self._wv[2], self._bv[2],
+                             o2.cout, o1.k, b["h"][4])
+            if timing is not None:
+                ev[1].record(torch.cuda.current_stream(self.device))
+                timing.append(ev)
+            if kernels is not None:
+                kernels.append(_lib.last_kernel_name())
+            start = 4
         for i, op in enumerate(self.ops):
+            if i < start:
+                continue
             if skip:  # the pool that was fused into the previous conv
                 skip = False
                 continue

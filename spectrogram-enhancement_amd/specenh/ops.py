@@ -389,6 +389,47 @@ _op(f"decoder3({_D3}) -> Tensor", _dec3,
 _op(f"decoder3_out({_D3}, Tensor(a!) out) -> ()", _dec3_out, lambda *a: None)
 
 
+def _enc2_out(x, w1, b1, cout1, w2, b2, cout2, k, out):
+    _need(x, "x")
+    _need(out, "out")
+    N, H, W, C = x.shape
+    if C != 1:
+        raise ValueError("x must be [N, H, W, 1]")
+    if any(t.dtype != x.dtype for t in (w1, w2)) or w1.numel() != cout1 * k * k or \
+            w2.numel() != cout2 * k * k * cout1:
+        raise ValueError("w1 / w2 must be the two layers' GEMM weights in x's dtype")
+    if any(t.dtype != torch.float32 for t in (b1, b2)) or b1.numel() != cout1 or \
+            b2.numel() != cout2:
+        raise ValueError("biases must be float32 [CO1] and [CO2]")
+    if out.dtype != x.dtype or tuple(out.shape) != (N, H // 4, W // 4, cout2):
+        raise ValueError("out must be [N, H/4, W/4, CO2] in x's dtype")
+    _lib.check(_lib.lib().specenh_encoder2(
+        _code(x), _vp(x), N, H, W, _vp(w1), _vp(b1), cout1, _vp(w2), _vp(b2), cout2, k, _vp(out),
+        _st(x)), "encoder2")
+
+
+def _enc2(x, w1, b1, cout1, w2, b2, cout2, k):
+    N, H, W, _ = x.shape
+    out = torch.empty((N, H // 4, W // 4, cout2), dtype=x.dtype, device=x.device)
+    _enc2_out(x, w1, b1, cout1, w2, b2, cout2, k, out)
+    return out
+
+
+_E2 = "Tensor x, Tensor w1, Tensor b1, int cout1, Tensor w2, Tensor b2, int cout2, int k"
+_op(f"encoder2({_E2}) -> Tensor", _enc2,
+    lambda x, w1, b1, cout1, w2, b2, cout2, k:
+    x.new_empty((x.shape[0], x.shape[1] // 4, x.shape[2] // 4, cout2)))
+_op(f"encoder2_out({_E2}, Tensor(a!) out) -> ()", _enc2_out, lambda *a: None)
+
+
+def encoder2_supported(dtype: torch.dtype, cin: int, cout1: int, cout2: int, k: int,
+                       height: int, width: int) -> bool:
+    """specenh_encoder2's configuration: the reference model's first two layers on 128-wide
+    one-channel images."""
+    return dtype in (torch.float16, torch.bfloat16) and (cin, cout1, cout2, k, width) == \
+        (1, 16, 32, 5, 128) and height % 4 == 0
+
+
 def decoder3_supported(dtype: torch.dtype, cin: int, cout1: int, cout2: int, k: int,
                        width: int) -> bool:
     """specenh_decoder3's configuration: the reference model's decoder on 128-wide images."""

@@ -173,3 +173,51 @@ def test_conv1_rows_matches_tile_kernel(gpu_device, kernel_variant):
     assert "conv_c1_mfma_kernel" in _lib.last_kernel_name()
     d = (a.float() - b.float()).abs()
     assert float(d.max()) <= 2.0 ** -10 * float(b.float().abs().max())
+
+
+# ---------------------------------------------------------------- encoder 1 + 2 fused
+# (csrc/conv_rows.hip enc2_rows_kernel, specenh_encoder2; VAE/manual_scan_3layers.py:187-191)
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,H", [(1, 128), (7, 4), (5, 12), (300, 128), (3, 132)])
+def test_encoder2_equals_two_launches(gpu_device, dtype, N, H):
+    """The fused launch runs the two row sweeps' arithmetic step for step: bitwise equal to
+    conv1_rows_pool_kernel + conv_rows_pool_kernel, and within the 16-bit rounding of a
+    float64 composite (the intermediate map rounded to the 16-bit type as stored)."""
+    rng = np.random.default_rng(N + 3 * H)
+    x = torch.tensor(rng.uniform(0, 1, (N, H, 128, 1)), dtype=dtype, device=gpu_device)
+    w1 = torch.tensor(rng.standard_normal((16, 5, 5, 1)) * 0.3, dtype=dtype, device=gpu_device)
+    b1 = torch.tensor(rng.standard_normal(16) * 0.2, dtype=torch.float32, device=gpu_device)
+    w2 = torch.tensor(rng.standard_normal((32, 5, 5, 16)) * 0.08, dtype=dtype, device=gpu_device)
+    b2 = torch.tensor(rng.standard_normal(32) * 0.2, dtype=torch.float32, device=gpu_device)
+    out = torch.full((N, H // 4, 32, 32), float("nan"), dtype=dtype, device=gpu_device)
+    torch.ops.specenh.encoder2_out(x, w1, b1, 16, w2, b2, 32, 5, out)
+    torch.cuda.synchronize()
+    assert "enc2_rows_kernel" in _lib.last_kernel_name()
+    h1 = torch.empty((N, H // 2, 64, 16), dtype=dtype, device=gpu_device)
+    _run(x, w1, b1, 16, h1)
+    two = torch.empty_like(out)
+    _run(h1, w2, b2, 32, two)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(out).all())
+    assert torch.equal(out, two)
+    ref, mag = _ref(h1, w2, b2)  # second layer in float64 on the stored intermediate
+    got = out.double().cpu()
+    eps = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
+    assert torch.all((got - ref).abs() <= eps * ref.abs() + 1e-5 * mag + 1e-30)
+
+
+def test_encoder2_engine_path(gpu_device, kernel_variant):
+    """AutoencoderEngine.forward at the C5 shape takes the fused launch (enc2) and matches
+    the unfused engine (SPECENH_ENCODER_UNFUSED) bitwise."""
+    import bench
+
+    x = torch.rand(64, 128, 128, 1, device=gpu_device).to(torch.float16)
+    eng = bench.make_c5_engine(gpu_device)
+    assert eng.enc2
+    a = eng.forward(x).clone()
+    kernel_variant("ENCODER_UNFUSED", 1)
+    eng2 = bench.make_c5_engine(gpu_device)
+    assert not eng2.enc2
+    b = eng2.forward(x)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)

@@ -34,6 +34,11 @@ def _cases(dev):
     wo, bo = r(25 * 16, dtype=torch.float16, lo=-0.2, hi=0.2), r(1)
     Sp = r(1, 256, 3845)
     x3 = r(2, 3, 32, 64, dtype=torch.float16)
+    xe = torch.rand(2, 12, 128, 1, device=dev, dtype=torch.float16)
+    we1 = (torch.randn(16 * 25, device=dev) * 0.1).to(torch.float16)
+    be1 = torch.randn(16, device=dev)
+    we2 = (torch.randn(32 * 25 * 16, device=dev) * 0.05).to(torch.float16)
+    be2 = torch.randn(32, device=dev)
     w3a, b3a = r(32 * 25 * 64, dtype=torch.float16, lo=-0.05, hi=0.05), r(32, lo=-0.1, hi=0.1)
     ops = torch.ops.specenh
     return [
@@ -66,6 +71,9 @@ def _cases(dev):
         (ops.decoder3, (x3, w3a, b3a, 32, wt, bc16, 16, wo, bo, 5)),
         (ops.decoder3_out, (x3, w3a, b3a, 32, wt, bc16, 16, wo, bo, 5,
                             torch.empty(2, 12, 128, 1, device=dev))),
+        (ops.encoder2, (xe, we1, be1, 16, we2, be2, 32, 5)),
+        (ops.encoder2_out, (xe, we1, be1, 16, we2, be2, 32, 5,
+                            torch.empty(2, 3, 32, 32, device=dev, dtype=torch.float16))),
         (ops.maxpool2, (pin,)),
         (ops.maxpool2_out, (pin, torch.empty_like(pooled), torch.empty_like(am))),
         (ops.maxpool2_bwd, (pooled.clone(), am, pooled)),

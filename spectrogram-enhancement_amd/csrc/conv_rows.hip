@@ -715,7 +715,7 @@ struct E2Args {
 constexpr int E2R1 = 32;  // conv1 input ring rows (positions)
 
 template <typename T>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 void enc2_rows_kernel(E2Args a) {
   using C = RC<16, 32, 64>;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -813,24 +813,25 @@ void enc2_rows_kernel(E2Args a) {
   auto produce = [&](int g2) {
     const int il = g2 / SPI, q2 = g2 - il * SPI;
     const int r = 2 * q2 + jr;
-    uint2 pk = uint2{0u, 0u};
-    if (il < nimg && r < H) {
-      const int pb = 4 * g2 + 2 * jr;  // position of image row 2r - 2
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
+    // branch-free (the step stays one basic block, so the scheduler can interleave these
+    // MFMAs with conv2's): rows past the image are computed from whatever finite rows the
+    // ring holds and replaced by zeros
+    const int pb = 4 * g2 + 2 * jr;  // position of image row 2r - 2
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int dy = 0; dy < 2; ++dy)
+    for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          const uint4 b = bfrag(pb + dy, cb);
-          uint4 b4 = bfrag(pb + dy + 4, cb);
-          if (kg != 0) b4 = uint4{0u, 0u, 0u, 0u};
-          f32x4 acc = mfma<T>(v0, b, bias1);
-          acc = mfma<T>(v1, b4, acc);
+      for (int cb = 0; cb < 2; ++cb) {
+        const uint4 b = bfrag(pb + dy, cb);
+        uint4 b4 = bfrag(pb + dy + 4, cb);
+        if (kg != 0) b4 = uint4{0u, 0u, 0u, 0u};
+        f32x4 acc1 = mfma<T>(v0, b, bias1);
+        acc1 = mfma<T>(v1, b4, acc1);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], acc[i]);  // (>= 0: relu folded)
-        }
-      pk = uint2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
-    }
+        for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], acc1[i]);  // (>= 0: relu folded)
+      }
+    const bool real = il < nimg && r < H;
+    const uint2 pk = real ? uint2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])} : uint2{0u, 0u};
     *reinterpret_cast<uint2*>(ring + ((2 * g2 + jr) & 7) * C::ROWB + (16 * w1x + m + 2) * 32 +
                               8 * kg) = pk;
   };
@@ -884,33 +885,33 @@ void enc2_rows_kernel(E2Args a) {
     const int nd = stage1(4 * s + 32);
     shift1(4 * s + 16);
     produce(s + 2);
-    const int il = s / SPI, q = s - il * SPI;
-    if (il < nimg && 2 * q < H) {
+    // this step's conv2 rows, unconditionally: past an image they are the zero rows the
+    // conv1 stage stored (adding nothing)
+    const int q = s % SPI;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int rs = (2 * s + j) & 7;
-        const unsigned char* rb = ring + rs * C::ROWB;
-        const uint4 b0 = *reinterpret_cast<const uint4*>(rb + boff);
-        const uint4 b2 = *reinterpret_cast<const uint4*>(rb + boff + 64);
-        const uint4 bF = *reinterpret_cast<const uint4*>(rb + (rs == 7 ? foffw : foff));
+    for (int j = 0; j < 2; ++j) {
+      const int rs = (2 * s + j) & 7;
+      const unsigned char* rb = ring + rs * C::ROWB;
+      const uint4 b0 = *reinterpret_cast<const uint4*>(rb + boff);
+      const uint4 b2 = *reinterpret_cast<const uint4*>(rb + boff + 64);
+      const uint4 bF = *reinterpret_cast<const uint4*>(rb + (rs == 7 ? foffw : foff));
 #pragma unroll
-        for (int ky = 0; ky < 5; ++ky) {
-          f32x4& ac = acc[slot(j + 2 - ky)];
-          ac = mfma<T>(wf[ky], b0, ac);
-        }
+      for (int ky = 0; ky < 5; ++ky) {
+        f32x4& ac = acc[slot(j + 2 - ky)];
+        ac = mfma<T>(wf[ky], b0, ac);
+      }
 #pragma unroll
-        for (int ky = 0; ky < 5; ++ky) {
-          f32x4& ac = acc[slot(j + 2 - ky)];
-          ac = mfma<T>(wf[5 + ky], b2, ac);
-        }
-        acc[slot(j + 2)] = mfma<T>(wf[10], bF, acc[slot(j + 2)]);
-        acc[slot(j)] = mfma<T>(wf[11], bF, acc[slot(j)]);
-        acc[slot(j - 2)] = mfma<T>(wf[12], bF, acc[slot(j - 2)]);
-        if (j == 0 && q == 0) {
-          uint4 bT = *reinterpret_cast<const uint4*>(ring + ((2 * s) & 7) * C::ROWB + fo);
-          if (kg < 2) bT = uint4{0u, 0u, 0u, 0u};
-          acc[slot(1)] = mfma<T>(wf[10], bT, acc[slot(1)]);
-        }
+      for (int ky = 0; ky < 5; ++ky) {
+        f32x4& ac = acc[slot(j + 2 - ky)];
+        ac = mfma<T>(wf[5 + ky], b2, ac);
+      }
+      acc[slot(j + 2)] = mfma<T>(wf[10], bF, acc[slot(j + 2)]);
+      acc[slot(j)] = mfma<T>(wf[11], bF, acc[slot(j)]);
+      acc[slot(j - 2)] = mfma<T>(wf[12], bF, acc[slot(j - 2)]);
+      if (j == 0) {  // F(-1) at the top of an image (q == 0), zero otherwise
+        uint4 bT = *reinterpret_cast<const uint4*>(ring + ((2 * s) & 7) * C::ROWB + fo);
+        if (kg < 2 || q != 0) bT = uint4{0u, 0u, 0u, 0u};
+        acc[slot(1)] = mfma<T>(wf[10], bT, acc[slot(1)]);
       }
     }
     // the DMA of step s - 3 (copy-1 shifted at step s + 1) must have landed: wait for all

@@ -894,7 +894,11 @@ void enc2_rows_kernel(E2Args a) {
       const unsigned char* rb = ring + rs * C::ROWB;
       const uint4 b0 = *reinterpret_cast<const uint4*>(rb + boff);
       const uint4 b2 = *reinterpret_cast<const uint4*>(rb + boff + 64);
-      const uint4 bF = *reinterpret_cast<const uint4*>(rb + (rs == 7 ? foffw : foff));
+      uint4 bF = *reinterpret_cast<const uint4*>(rb + (rs == 7 ? foffw : foff));
+      // the bubble step's F(H + 1) would pair the zero row H + 1 with the NEXT image's row 0
+      // (the next ring slot) and add it to that image's output rows 1 / -1 (pair s + 1 is
+      // the next image's rows 0, 1): zero it (the next image's F(-1) adds that term)
+      if (j == 1 && q == SPI - 1) bF = uint4{0u, 0u, 0u, 0u};
 #pragma unroll
       for (int ky = 0; ky < 5; ++ky) {
         f32x4& ac = acc[slot(j + 2 - ky)];

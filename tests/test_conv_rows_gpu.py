@@ -100,7 +100,7 @@ def _convt_run(x, w, bias, CO, out):
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("CO,W", [(64, 16), (32, 32)])
-@pytest.mark.parametrize("N,H", [(1, 16), (3, 1), (5, 7), (300, 4)])
+@pytest.mark.parametrize("N,H", [(1, 16), (3, 1), (5, 7), (300, 4), (1100, 3)])
 def test_convt_rows_vs_float64(gpu_device, dtype, CO, W, N, H):
     rng = np.random.default_rng(CO + W + N + H)
     x = torch.tensor(np.maximum(rng.standard_normal((N, H, W, 64)), 0), dtype=dtype,
@@ -140,7 +140,7 @@ def test_convt_rows_matches_tile_kernel(gpu_device, kernel_variant, CO, W):
 # ---------------------------------------------------------------- C = 1 row sweep
 # (csrc/conv_rows.hip conv1_rows_pool_kernel; VAE/manual_scan_3layers.py:187-188)
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("N,H", [(1, 128), (3, 2), (5, 10), (300, 64), (2, 130)])
+@pytest.mark.parametrize("N,H", [(1, 128), (3, 2), (5, 10), (300, 64), (2, 130), (4200, 4)])
 def test_conv1_rows_vs_float64(gpu_device, dtype, N, H):
     rng = np.random.default_rng(N + H)
     x = torch.tensor(rng.uniform(0, 1, (N, H, 128, 1)), dtype=dtype, device=gpu_device)
@@ -178,11 +178,14 @@ def test_conv1_rows_matches_tile_kernel(gpu_device, kernel_variant):
 # ---------------------------------------------------------------- encoder 1 + 2 fused
 # (csrc/conv_rows.hip enc2_rows_kernel, specenh_encoder2; VAE/manual_scan_3layers.py:187-191)
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("N,H", [(1, 128), (7, 4), (5, 12), (300, 128), (3, 132)])
+@pytest.mark.parametrize("N,H", [(1, 128), (7, 4), (5, 12), (300, 128), (3, 132), (1300, 128),
+                                 (1100, 8)])
 def test_encoder2_equals_two_launches(gpu_device, dtype, N, H):
     """The fused launch runs the two row sweeps' arithmetic step for step: bitwise equal to
     conv1_rows_pool_kernel + conv_rows_pool_kernel, and within the 16-bit rounding of a
-    float64 composite (the intermediate map rounded to the 16-bit type as stored)."""
+    float64 composite (the intermediate map rounded to the 16-bit type as stored). N > 512:
+    several images per persistent workgroup (the image-to-image hand-over of the row
+    streams; a bubble-step F term once leaked into the next image's row 1)."""
     rng = np.random.default_rng(N + 3 * H)
     x = torch.tensor(rng.uniform(0, 1, (N, H, 128, 1)), dtype=dtype, device=gpu_device)
     w1 = torch.tensor(rng.standard_normal((16, 5, 5, 1)) * 0.3, dtype=dtype, device=gpu_device)

@@ -126,5 +126,10 @@ class _BCE(torch.autograd.Function):
 
 def binary_crossentropy_with_logits(z, target):
     """compile(loss="binary_crossentropy") after a sigmoid layer, as Keras evaluates it in graph
-    mode: mean over all elements of max(z, 0) - z t + log1p(exp(-|z|)) from the logits z."""
+    mode: mean over all elements of max(z, 0) - z t + log1p(exp(-|z|)) from the logits z.
+    bfloat16 / float16 logits (a low-precision last layer) are widened to float32 first, as
+    Keras' mixed-precision policy computes the loss in float32; the gradient flows back
+    through the cast in z's dtype."""
+    if z.dtype != torch.float32:
+        z = z.float()
     return _BCE.apply(z, target)

@@ -165,6 +165,54 @@ def test_autograd_model_matches_oracle(gpu_device):
         assert np.linalg.norm(a - b) <= 1e-5 * np.linalg.norm(b)
 
 
+def test_autograd_model_bf16_end_to_end(gpu_device):
+    """The docstring example in bfloat16: a bf16 last layer's logits go
+    straight into binary_crossentropy_with_logits (widened to fp32 inside, the gradient
+    flowing back through the cast). Against fp64 autograd on the same bf16-rounded inputs
+    and weights: loss within 1e-2, logits within 5e-2 normwise, gradients within 0.2 normwise
+    (bf16 activations, output gradients and backward maps: 8-bit mantissas; the small
+    gradients of this 3-image batch measured up to ~0.1 — a missing or mis-signed term
+    gives ~1)."""
+    from specenh import autograd as F
+
+    spec = ora.ae_spec(8, 16, 16, k=5)
+    params = ora.glorot_params(spec, seed=5)
+    rng = np.random.default_rng(6)
+    bf = lambda a: torch.tensor(a).to(torch.bfloat16).float().numpy()  # noqa: E731
+    for p in params:
+        if p is not None:
+            p["W"] = bf(p["W"])
+            p["b"] = (0.05 * rng.standard_normal(p["b"].shape)).astype(np.float32)
+    x = bf(rng.uniform(0, 1, (3, 32, 32, 1)).astype(np.float32))
+    y = rng.uniform(0, 1, (3, 32, 32, 1)).astype(np.float32)
+    ref_loss, ref_z, ref_g = _oracle_grads(spec, params, x, y)
+
+    dev = gpu_device
+    tp = [None if p is None else
+          {"W": torch.tensor(p["W"], device=dev).to(torch.bfloat16).requires_grad_(),
+           "b": torch.tensor(p["b"], device=dev, requires_grad=True)} for p in params]
+    h = torch.tensor(x, device=dev).to(torch.bfloat16)
+    for lay, p in zip(spec, tp):
+        if lay[0] == "pool":
+            h = F.max_pool2(h)
+            continue
+        act = None if lay[4] == "sigmoid" else lay[4]
+        fn = F.conv2d_same if lay[0] == "conv" else F.conv2d_transpose_same
+        h = fn(h, p["W"], p["b"], act)
+    assert h.dtype == torch.bfloat16
+    loss = F.binary_crossentropy_with_logits(h, torch.tensor(y, device=dev))
+    loss.backward()
+    assert abs(float(loss) - ref_loss) <= 1e-2 * ref_loss
+    z = h.detach().float().cpu().numpy()
+    assert np.linalg.norm(z - ref_z) <= 5e-2 * np.linalg.norm(ref_z)
+    got = []
+    for p in tp:
+        if p is not None:
+            got += [p["W"].grad.float().cpu().numpy(), p["b"].grad.cpu().numpy()]
+    for a, b in zip(got, ref_g):
+        assert np.linalg.norm(a - b) <= 0.2 * np.linalg.norm(b)
+
+
 def test_autograd_sigmoid_output_grad(gpu_device):
     """Conv2D with a fused sigmoid: the gradient through the activation."""
     from specenh import autograd as F

@@ -677,9 +677,21 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int m = lane & 15, kg = lane >> 4;
-  const int n = blockIdx.x;
   const int H1 = a.H, H2 = 2 * H1, H3 = 4 * H1;
-  const int S = H1 + 3;  // macro steps (the consumer's Conv2D(1) runs one tail step behind)
+  // Persistent workgroups: one continuous row stream over the workgroup's images
+  // n = blockIdx.x + i G. Per image SPI = H1 + 1 macro steps: producer step s = 0 .. H1 - 1
+  // turns input row s into tail-input rows 2s, 2s + 1, step s = H1 writes the two zero rows
+  // that separate images; the consumer's tail steps then run on, 2 per macro step, with
+  // per-image tail step t = 0 .. 2 H1 + 1 (t >= 2 H1: zero map rows). The input stream has
+  // one zero row between images (position i SPI), so producer step g reads positions
+  // g .. g + 2. Ring slots are global (macro step g, tail step 2g - 3 / 2g - 2), so the
+  // compile-time slot offsets of the unrolled loops are the single-image ones. Round 2/3
+  // launched one workgroup per image: per image the LDS clear, the 50 + 28 fragment loads
+  // and the pipeline fill and drain (3 of 35 macro steps) were paid again.
+  const int SPI = H1 + 1, TPI = 2 * SPI;
+  const int G = gridDim.x;
+  const int nimg = ((int)a.N - (int)blockIdx.x + G - 1) / G;
+  const int S = nimg * SPI + 2;  // + 2: the consumer's last tail steps
   {
     uint4* z = reinterpret_cast<uint4*>(lds_raw);
     for (int e = tid; e < LDS_BYTES / 16; e += 512) z[e] = uint4{0u, 0u, 0u, 0u};
@@ -709,18 +721,20 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
     }
     const f32x4 bias = f32x4{a.b1[16 * nb + 4 * kg], a.b1[16 * nb + 4 * kg + 1],
                              a.b1[16 * nb + 4 * kg + 2], a.b1[16 * nb + 4 * kg + 3]};
-    const T* __restrict__ X = reinterpret_cast<const T*>(a.x) + (long long)n * H1 * W1 * CI1;
-    // input row r -> ring slot r & 3 by LDS-DMA: wave wv moves stored pixels 1 + 8 wv ..
-    // 8 + 8 wv (1 KB, lane-linear); lane i takes stored group i & 7, i.e. source group
-    // (i & 7) ^ (ps & 7)
+    const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
+    // input stream position p (image p / SPI, row p % SPI - 1; row -1 is the zero row) ->
+    // ring slot p & 3 by LDS-DMA: wave wv moves stored pixels 1 + 8 wv .. 8 + 8 wv (1 KB,
+    // lane-linear); lane i takes stored group i & 7, i.e. source group (i & 7) ^ (ps & 7)
     const int dps = 1 + 8 * wv + (lane >> 3);
     const int dsrc = (dps - 1) * CI1 + 8 * ((lane & 7) ^ (dps & 7));
     unsigned char* const ddst = lds_raw + (1 + 8 * wv) * X1ST * 2;
-    auto stage = [&](int row, int slot) {
-      unsigned char* dst = ddst + slot * X1ROW * 2;
-      if (row >= 0 && row < H1) {
-        lds_dma16(X + (long long)row * W1 * CI1 + dsrc, dst);
-      } else {  // outside the image: the zero padding rows
+    auto stage = [&](int p) {
+      unsigned char* dst = ddst + (p & 3) * X1ROW * 2;
+      const int il = p / SPI, row = p - il * SPI - 1;
+      if (il < nimg && row >= 0 && row < H1) {
+        const long long n = (long long)blockIdx.x + (long long)il * G;
+        lds_dma16(X + ((n * H1 + row) * W1) * CI1 + dsrc, dst);
+      } else {  // between / after the images: the zero padding rows
         *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
       }
     };
@@ -735,21 +749,22 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       x2w[px] = x2_off(ps, ch >> 3) + (ch & 7);
     }
 #pragma unroll
-    for (int d = -1; d <= 1; ++d) stage(d, d & 3);
+    for (int p = 0; p < 3; ++p) stage(p);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();  // (macro step -1: the consumers' matching barrier is below)
 
-    auto pstep = [&](auto ic, const int s) {
-      constexpr int I = decltype(ic)::value;  // s & 3
-      stage(s + 2, (I + 2) & 3);  // lands while this row's MFMAs run
+    auto pstep = [&](auto ic, const int g) {
+      constexpr int I = decltype(ic)::value;  // g & 3
+      stage(g + 3);  // lands while this row's MFMAs run
       T* const r0 = x2r + ((2 * I) & 7) * X2ROW;
       T* const r1 = x2r + ((2 * I + 1) & 7) * X2ROW;
-      if (s < H1) {
+      const int il = g / SPI, s = g - il * SPI;
+      if (il < nimg && s < H1) {
         f32x4 acc[4] = {bias, bias, bias, bias};
         int u0[4] = {0, 8, 20, 32};
 #pragma unroll
         for (int dy = -1; dy <= 1; ++dy) {
-          const T* src = x1r + ((I + dy + 4) & 3) * X1ROW;
+          const T* src = x1r + ((I + 1 + dy + 4) & 3) * X1ROW;  // position g + 1 + dy
 #pragma unroll
           for (int dx = -1; dx <= 1; ++dx) {
             // group kg + 4 (the second K-step) sits at the first's offset ^ 32 elements:
@@ -769,76 +784,84 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
 #pragma unroll
         for (int ph = 0; ph < 4; ++ph)
           *reinterpret_cast<uint2*>(((ph >> 1) ? r1 : r0) + x2w[ph & 1]) = relu_pack<T>(acc[ph]);
-      } else if (s == H1) {  // tail-input rows 2 H1, 2 H1 + 1: zero padding
+      } else {  // tail-input rows 2 H1, 2 H1 + 1 (and past the last image): zero padding
 #pragma unroll
         for (int ph = 0; ph < 4; ++ph)
           *reinterpret_cast<uint2*>(((ph >> 1) ? r1 : r0) + x2w[ph & 1]) = uint2{0u, 0u};
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // input row s + 2 has landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // input position g + 3 has landed
       lds_barrier();
     };
-    int s = 0;
-    for (; s + 4 <= S; s += 4) {
-      pstep(IC<0>{}, s);
-      pstep(IC<1>{}, s + 1);
-      pstep(IC<2>{}, s + 2);
-      pstep(IC<3>{}, s + 3);
+    int g = 0;
+    for (; g + 4 <= S; g += 4) {
+      pstep(IC<0>{}, g);
+      pstep(IC<1>{}, g + 1);
+      pstep(IC<2>{}, g + 2);
+      pstep(IC<3>{}, g + 3);
     }
-    if (s < S) pstep(IC<0>{}, s);
-    if (s + 1 < S) pstep(IC<1>{}, s + 1);
-    if (s + 2 < S) pstep(IC<2>{}, s + 2);
+    if (g < S) pstep(IC<0>{}, g);
+    if (g + 1 < S) pstep(IC<1>{}, g + 1);
+    if (g + 2 < S) pstep(IC<2>{}, g + 2);
   } else {
-    // ======================= consumer: the row-sweep tail, tail steps t = 2s - 3, 2s - 2
+    // ======================= consumer: the row-sweep tail, tail steps t = 2g - 3, 2g - 2
     const int w = wv - 4;
     TailWave<T> tw;
     tw.load(a.wt, a.bt, a.wo, a.bo, w, lane);
-    float* __restrict__ O = a.out + (long long)n * H3 * rows::MW;
     int xo[3];  // element offset of pixel 16 w + m + dx (stored + 1), group kg, in a ring row
 #pragma unroll
     for (int dx = -1; dx <= 1; ++dx) xo[dx + 1] = x2_off(16 * w + m + dx + 1, kg);
     lds_barrier();  // macro step -1
-    // tail step t (= 2s - 3 or 2s - 2) with T8 = t & 7 compile-time from s & 3. The
-    // Conv2D(1) of step t is for output rows 2t - 4, 2t - 3 (map rows 2t - 6 .. 2t - 1, all
-    // written by earlier steps: the 8-row map ring holds 2t - 6 .. 2t + 1), so it does not
-    // wait for this step's Conv2DTranspose and the two MFMA streams interleave. It is
-    // issued first: its map reads then precede this step's map writes into the slots of
-    // rows 2t - 8, 2t - 7.
+    // global tail step t (image t / TPI, per-image step tl = t % TPI) with T8 = t & 7
+    // compile-time from g & 3. The Conv2D(1) of step tl is for output rows 2tl - 4, 2tl - 3
+    // (map rows 2tl - 6 .. 2tl - 1, all written by earlier steps: the 8-row map ring holds
+    // 2t - 6 .. 2t + 1), so it does not wait for this step's Conv2DTranspose and the two MFMA
+    // streams interleave. It is issued first: its map reads then precede this step's map
+    // writes into the slots of rows 2t - 8, 2t - 7. Map rows of per-image steps tl >= 2 H1
+    // are zero (the Conv2D(1) padding below one image and above the next).
     auto tstep = [&](auto ic, const int t, float* scb) {
       constexpr int T8 = decltype(ic)::value;  // t & 7: the tail-input ring slot of row t
       constexpr int T4 = T8 & 3;                // the map ring: rows 2t, 2t + 1 in slots 2 T4 ..
-      if (t < 0 || t > H2 + 1) return;
-      if (t >= 2)
+      if (t < 0) return;
+      const int il = t / TPI, tl = t - il * TPI;
+      if (il >= nimg) return;
+      if (tl >= 2)
         tw.conv_out_d([&](int j) { return mr + ((2 * T4 - 6 + j + 8) & 7) * rows::MROW; }, scb,
                       m);
       T* const m0 = mr + ((2 * T4) & 7) * rows::MROW;
       T* const m1 = mr + ((2 * T4 + 1) & 7) * rows::MROW;
-      if (t < H2)
+      if (tl < H2)
         tw.convt(x2r, [](int dy) { return ((T8 + dy + 8) & 7) * X2ROW; },
                  [&](int dx) { return xo[dx + 1]; }, m0, m1);
-      else if (t == H2)
+      else
         tw.zero_rows(m0, m1);
     };
-    auto cstep = [&](auto ic, const int s) {
-      constexpr int I = decltype(ic)::value;  // s & 3
+    auto sums = [&](const float* scb, int t) {
+      if (t < 0) return;
+      const int il = t / TPI, tl = t - il * TPI;
+      if (il >= nimg || tl < 2) return;
+      const long long n = (long long)blockIdx.x + (long long)il * G;
+      tw.conv_out_sums(scb, a.out + n * H3 * rows::MW, 2 * tl - 4, lane);
+    };
+    auto cstep = [&](auto ic, const int g) {
+      constexpr int I = decltype(ic)::value;  // g & 3
       float* const sc0 = sc + ((I & 1) * 2) * (rows::SCR * rows::SCW);
       float* const sc1 = sc0 + rows::SCR * rows::SCW;
-      tstep(IC<(2 * I + 5) & 7>{}, 2 * s - 3, sc0);  // (2s - 3) & 7 = (2 I - 3) & 7
-      tstep(IC<(2 * I + 6) & 7>{}, 2 * s - 2, sc1);
+      tstep(IC<(2 * I + 5) & 7>{}, 2 * g - 3, sc0);  // (2g - 3) & 7 = (2 I - 3) & 7
+      tstep(IC<(2 * I + 6) & 7>{}, 2 * g - 2, sc1);
       lds_barrier();
-      const int t0 = 2 * s - 3, t1 = 2 * s - 2;
-      if (t0 >= 2 && t0 <= H2 + 1) tw.conv_out_sums(sc0, O, 2 * t0 - 4, lane);
-      if (t1 >= 2 && t1 <= H2 + 1) tw.conv_out_sums(sc1, O, 2 * t1 - 4, lane);
+      sums(sc0, 2 * g - 3);
+      sums(sc1, 2 * g - 2);
     };
-    int s = 0;
-    for (; s + 4 <= S; s += 4) {
-      cstep(IC<0>{}, s);
-      cstep(IC<1>{}, s + 1);
-      cstep(IC<2>{}, s + 2);
-      cstep(IC<3>{}, s + 3);
+    int g = 0;
+    for (; g + 4 <= S; g += 4) {
+      cstep(IC<0>{}, g);
+      cstep(IC<1>{}, g + 1);
+      cstep(IC<2>{}, g + 2);
+      cstep(IC<3>{}, g + 3);
     }
-    if (s < S) cstep(IC<0>{}, s);
-    if (s + 1 < S) cstep(IC<1>{}, s + 1);
-    if (s + 2 < S) cstep(IC<2>{}, s + 2);
+    if (g < S) cstep(IC<0>{}, g);
+    if (g + 1 < S) cstep(IC<1>{}, g + 1);
+    if (g + 2 < S) cstep(IC<2>{}, g + 2);
   }
 }
 
@@ -939,10 +962,12 @@ extern "C" int specenh_decoder3(int dtype, const void* x, int N, int H, int W, i
     (void)hipFuncSetAttribute(k16, hipFuncAttributeMaxDynamicSharedMemorySize, d3::LDS_BYTES);
     (void)hipFuncSetAttribute(kb16, hipFuncAttributeMaxDynamicSharedMemorySize, d3::LDS_BYTES);
   });
+  // persistent: one workgroup per CU (105 KB of LDS, 256 VGPRs at 2 waves per SIMD)
+  const unsigned grid = (unsigned)std::min<long long>(N, device_cus());
   if (dtype == SPECENH_DTYPE_F16)
-    SPECENH_LAUNCH(decoder3_kernel<_Float16>, dim3((unsigned)N), dim3(512), d3::LDS_BYTES, st, a);
+    SPECENH_LAUNCH(decoder3_kernel<_Float16>, dim3(grid), dim3(512), d3::LDS_BYTES, st, a);
   else
-    SPECENH_LAUNCH(decoder3_kernel<__bf16>, dim3((unsigned)N), dim3(512), d3::LDS_BYTES, st, a);
+    SPECENH_LAUNCH(decoder3_kernel<__bf16>, dim3(grid), dim3(512), d3::LDS_BYTES, st, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("decoder3: ") + hipGetErrorString(e));
   return SPECENH_OK;

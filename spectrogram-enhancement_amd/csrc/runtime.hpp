@@ -31,6 +31,7 @@ enum Variant : int {
   V_CONVT_NO_ROWS,    // Conv2DTranspose on 64 channels: conv_patch_kernel instead of the row sweep
   V_CONV1_NO_ROWS,    // C = 1 pooled conv: conv_c1_mfma tiles instead of the row sweep
   V_ENCODER_UNFUSED,  // engine (Python): no two-layer encoder launch (specenh_encoder2)
+  V_STFT_NO_HOLD,     // per-shot normalised STFT: raw rows + re-read sweep, not held tiles
   V_COUNT
 };
 

@@ -180,15 +180,18 @@ __device__ __forceinline__ int tile_swz(int k) {
 
 // min/max of three floats as one instruction each (plain fminf/fmaxf get NaN-quieting
 // canonicalisation v_max ops on every operand). Operands are finite here or NaN only
-// when the input itself is NaN.
+// when the input itself is NaN. hipcc pads no hazard inside an asm statement, and the
+// operands come straight from v_log_f32 (a transcendental: a VALU read of its result
+// needs wait states), so the pad is in the string: without it the max read a stale
+// register in some schedules (the held-tile kernel's extremes came out O(1) wrong).
 __device__ __forceinline__ float fmin3(float a, float b, float c) {
   float r;
-  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  asm("s_nop 1\n\tv_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
 __device__ __forceinline__ float fmax3(float a, float b, float c) {
   float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  asm("s_nop 1\n\tv_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
 
@@ -710,7 +713,15 @@ __device__ __forceinline__ double dc_lane_base(const StftArgs& a, int gl) {
 // frequency-row segments of TF frames. With NORMALIZE the workgroup knows the whole
 // spectrogram's min/max at the end and rescales its own output in a final sweep
 // (the rows were written moments ago and are re-read from the on-die caches).
-template <int N, bool XH = false>
+// HOLD (NORMALIZE, a spectrogram of HOLD <= 2 tiles: the C5 stream's 128 frames at
+// nperseg 256): every tile's values stay in the lane groups' registers (HOLD x IB pairs)
+// until the extremes are known, and each tile is stored once, normalised on its way through
+// the LDS tile — no raw store, no re-read, no second write. PMC had the sweep at 454 MB per
+// 2048 C5 shots for 202 MB of algorithmic traffic: the raw rows of the 2 x 32 resident shots
+// per XCD (4 MB) do not stay in its 4 MB L2. Same arithmetic ((v - mn) * inv); the two
+// instantiations' FFT code is scheduled differently, so values agree to an ulp or so of the
+// log2 PSD (<= 1e-6 on [0, 1], measured; N = 512 bitwise), not bit for bit.
+template <int N, bool XH = false, int HOLD = 0>
 __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_kernel(
     StftArgs a) {
   using C = Cfg<N>;
@@ -751,6 +762,38 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
   if constexpr (C::PF) load_pair<N, XH>(s0, xr, xr, a.hop, 2 * fi, a.T, gl);
   __syncthreads();
 
+  if constexpr (HOLD > 0) {  // (host-checked: NORMALIZE, ntiles == HOLD)
+    f2v pv[HOLD][IB];
+#pragma unroll
+    for (int tile = 0; tile < HOLD; ++tile) {
+      const int fa = tile * Lo::TF + 2 * fi;
+      if constexpr (!C::PF) load_pair<N, XH>(s0, xr, xr, a.hop, fa, a.T, gl);
+      pair_spectrum<N, XH>(a, s0, s0, s_tw, s_win, s_dc, buf, gl, dcb, xr, xr, fa + Lo::TF,
+                           C::PF != 0 && tile + 1 < HOLD, true, true, pv[tile], lmin, lmax);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      lmin = fminf(lmin, __shfl_xor(lmin, m));
+      lmax = fmaxf(lmax, __shfl_xor(lmax, m));
+    }
+    if (lane == 0) {
+      s_red[wave] = lmin;
+      s_red[C::WAVES + wave] = lmax;
+    }
+    __syncthreads();  // s_red complete; every group is done with its FFT buffer
+    float mn = s_red[0], mx = s_red[C::WAVES];
+#pragma unroll
+    for (int w = 1; w < C::WAVES; ++w) {
+      mn = fminf(mn, s_red[w]);
+      mx = fmaxf(mx, s_red[C::WAVES + w]);
+    }
+    const float inv = 1.0f / (mx - mn);  // max == min -> NaN, as the reference's 0/0
+#pragma unroll
+    for (int tile = 0; tile < HOLD; ++tile)
+      tile_store<N>(a, s_tile, pv[tile], gl, fi, tid, orr, tile * Lo::TF, mn, inv, true,
+                    tile > 0);
+    return;
+  }
   for (int tile = 0; tile < ntiles; ++tile) {
     const int t0 = tile * Lo::TF;
     const int fa = t0 + 2 * fi;  // tail frames are clamped duplicates (load_pair)
@@ -806,11 +849,31 @@ hipError_t launch_stft(const StftArgs& a, long long batch, hipStream_t stream) {
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)stft_psd_kernel<N, XH>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, Lo::BYTES);
+    if constexpr (N <= 512)
+      for (const void* k : {(const void*)stft_psd_kernel<N, XH, 1>, (const void*)stft_psd_kernel<N, XH, 2>})
+        if (e == hipSuccess)
+          e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, Lo::BYTES);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
+  // held tiles: normalised spectrograms of one or two tiles (larger N hold more bins per
+  // lane: the second tile's values would spill)
+  if constexpr (N <= 512) {
+    const int ntiles = (a.T + Lo::TF - 1) / Lo::TF;
+    const bool hold = (a.flags & SPECENH_STFT_NORMALIZE) && !(a.flags & SPECENH_STFT_DEV_NOSTORE) &&
+                      ntiles <= 2 && variant(V_STFT_NO_HOLD) == 0;
+    if (hold) {
+      if (ntiles == 2)
+        SPECENH_LAUNCH((stft_psd_kernel<N, XH, 2>), dim3((unsigned)batch), dim3(Lo::THREADS),
+                       Lo::BYTES, stream, a);
+      else
+        SPECENH_LAUNCH((stft_psd_kernel<N, XH, 1>), dim3((unsigned)batch), dim3(Lo::THREADS),
+                       Lo::BYTES, stream, a);
+      return hipGetLastError();
+    }
+  }
   SPECENH_LAUNCH((stft_psd_kernel<N, XH>), dim3((unsigned)batch), dim3(Lo::THREADS),
-                     Lo::BYTES, stream, a);
+                 Lo::BYTES, stream, a);
   return hipGetLastError();
 }
 

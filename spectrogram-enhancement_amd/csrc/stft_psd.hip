@@ -769,7 +769,8 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
       const int fa = tile * Lo::TF + 2 * fi;
       if constexpr (!C::PF) load_pair<N, XH>(s0, xr, xr, a.hop, fa, a.T, gl);
       pair_spectrum<N, XH>(a, s0, s0, s_tw, s_win, s_dc, buf, gl, dcb, xr, xr, fa + Lo::TF,
-                           C::PF != 0 && tile + 1 < HOLD, true, true, pv[tile], lmin, lmax);
+                           C::PF != 0 && tile + 1 < HOLD, want_log, log2_out, pv[tile], lmin,
+                           lmax);
     }
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {

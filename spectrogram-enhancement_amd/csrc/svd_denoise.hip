@@ -203,6 +203,124 @@ __global__ __launch_bounds__(256) void gram_lds_kernel(XView x, int K, int r, fl
   }
 }
 
+// 128 < r <= 256 (r % 4 == 0; C3: 513 x 256): one workgroup of 4 waves per matrix, X read
+// from HBM once. gram_kernel (one wave per 32x32 tile, operands straight from global) read
+// every X element 9 times, 5.5x the input from HBM by PMC (11.9 GB per 4096 C3 matrices).
+// Here X is staged through LDS in chunks of G2_KC rows (the next chunk in registers while
+// the current one is used; row pitch G2_LD = 288 words: the two half-waves' rows land 32
+// banks apart); the 36 upper-triangle 32x32 tiles of G go 9 to each wave. Per pair of rows a
+// wave reads the 8 column-panel fragments once: tile (ti, tj) takes fragment ti as the MFMA's
+// A operand and fragment tj as its B operand (same v_mfma_f32_32x32x2_f32 as gram_kernel,
+// whose lane layout is documented there), so 8 LDS reads feed 9 MFMAs. Columns r .. 255 of
+// the chunk stay zero; rows past K are fetched as zeros (exact +0 products).
+constexpr int G2_KC = 16, G2_LD = 288;
+// row-major upper triangle of the 8 x 8 tile grid: tile t -> (ti, tj)
+__device__ constexpr int kG2TI[36] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2,
+                                      2, 2, 2, 3, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 6, 6, 7};
+__device__ constexpr int kG2TJ[36] = {0, 1, 2, 3, 4, 5, 6, 7, 1, 2, 3, 4, 5, 6, 7, 2, 3, 4,
+                                      5, 6, 7, 3, 4, 5, 6, 7, 4, 5, 6, 7, 5, 6, 7, 6, 7, 7};
+
+template <int W>  // the wave's tiles are W, W + 4, ..., W + 32: compile-time panel indices
+__device__ __forceinline__ void gram256_wave(const XView& x, int K, int r, float* sX,
+                                             float* Gb) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const float* X = x.base + (long long)blockIdx.x * x.batch_stride;
+  const bool rowmaj = x.si == 1;
+  const int nvec = G2_KC * r / 4;
+  constexpr int NV = G2_KC * 256 / 4 / 256;  // float4 per thread per chunk (r = 256)
+  float4 reg[NV];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int e = tid + 256 * u;
+      reg[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < nvec) {
+        if (rowmaj) {
+          const int kk = e / (r / 4), i4 = e - kk * (r / 4);
+          if (k0 + kk < K)
+            reg[u] = *reinterpret_cast<const float4*>(X + (long long)(k0 + kk) * x.sk + 4 * i4);
+        } else {  // X[k][i] = base[k + i * si]: 4 consecutive k of one column i
+          const int i = e / (G2_KC / 4), k4 = e - i * (G2_KC / 4);
+          const float* src = X + (long long)i * x.si + k0 + 4 * k4;
+          float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (k0 + 4 * k4 + c < K) v[c] = src[c];
+          reg[u] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int e = tid + 256 * u;
+      if (e >= nvec) continue;
+      if (rowmaj) {
+        const int kk = e / (r / 4), i4 = e - kk * (r / 4);
+        *reinterpret_cast<float4*>(sX + kk * G2_LD + 4 * i4) = reg[u];
+      } else {
+        const int i = e / (G2_KC / 4), k4 = e - i * (G2_KC / 4);
+        sX[(4 * k4 + 0) * G2_LD + i] = reg[u].x;
+        sX[(4 * k4 + 1) * G2_LD + i] = reg[u].y;
+        sX[(4 * k4 + 2) * G2_LD + i] = reg[u].z;
+        sX[(4 * k4 + 3) * G2_LD + i] = reg[u].w;
+      }
+    }
+  };
+  f32x16 acc[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) acc[q] = f32x16{};
+  const int c = lane & 31, kh = lane >> 5;
+  fetch(0);
+  for (int k0 = 0; k0 < K; k0 += G2_KC) {
+    __syncthreads();  // previous chunk fully consumed
+    store();
+    __syncthreads();
+    if (k0 + G2_KC < K) fetch(k0 + G2_KC);
+#pragma unroll 4
+    for (int s2 = 0; s2 < G2_KC / 2; ++s2) {
+      const float* row = sX + (2 * s2 + kh) * G2_LD + c;
+      float f[8];
+#pragma unroll
+      for (int p = 0; p < 8; ++p) f[p] = row[32 * p];
+#pragma unroll
+      for (int q = 0; q < 9; ++q)
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(f[kG2TI[W + 4 * q]], f[kG2TJ[W + 4 * q]],
+                                                      acc[q], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    const int ti = kG2TI[W + 4 * q], tj = kG2TJ[W + 4 * q];
+#pragma unroll
+    for (int reg16 = 0; reg16 < 16; ++reg16) {
+      const int row = ti * 32 + (reg16 & 3) + 8 * (reg16 >> 2) + 4 * kh;
+      const int col = tj * 32 + c;
+      if (row < r && col < r) {
+        Gb[(long long)row * r + col] = acc[q][reg16];
+        Gb[(long long)col * r + row] = acc[q][reg16];
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void gram256_kernel(XView x, int K, int r, float* G) {
+  __shared__ __attribute__((aligned(16))) float sX[G2_KC * G2_LD];
+  // columns r .. 255 stay zero (the stores only write i < r)
+  for (int e = threadIdx.x; e < G2_KC * (256 - r); e += 256) {
+    const int kk = e / (256 - r), i = r + e - kk * (256 - r);
+    sX[kk * G2_LD + i] = 0.f;
+  }
+  float* Gb = G + (long long)blockIdx.x * r * r;
+  switch (threadIdx.x >> 6) {
+    case 0: gram256_wave<0>(x, K, r, sX, Gb); break;
+    case 1: gram256_wave<1>(x, K, r, sX, Gb); break;
+    case 2: gram256_wave<2>(x, K, r, sX, Gb); break;
+    default: gram256_wave<3>(x, K, r, sX, Gb); break;
+  }
+}
+
 // ---------------------------------------------------------------- 2. subspace
 constexpr int SS_THREADS = 256;
 #ifndef SPECENH_SS_SINGLE_QR
@@ -230,8 +348,28 @@ __device__ void gemm_GZ(const float* G, int r, const float* sZ, float* sY) {
     float acc[P];
 #pragma unroll
     for (int c = 0; c < P; ++c) acc[c] = 0.f;
-#pragma unroll 8
-    for (int j = 0; j < r; ++j) {
+    // G rows in batches of GB loads in flight (G comes from L2 / HBM: one batch per round
+    // trip), then the batch's FMAs in the same j order
+    constexpr int GB = 16;
+    int j = 0;
+    for (; j + GB <= r; j += GB) {
+      float g[GB];
+#pragma unroll
+      for (int u = 0; u < GB; ++u) g[u] = G[(long long)(j + u) * r + i];
+#pragma unroll
+      for (int u = 0; u < GB; ++u) {
+        const float4* zj = reinterpret_cast<const float4*>(sZ + (j + u) * P);
+#pragma unroll
+        for (int c4 = 0; c4 < P / 4; ++c4) {
+          const float4 z = zj[c4];
+          acc[4 * c4 + 0] = fmaf(g[u], z.x, acc[4 * c4 + 0]);
+          acc[4 * c4 + 1] = fmaf(g[u], z.y, acc[4 * c4 + 1]);
+          acc[4 * c4 + 2] = fmaf(g[u], z.z, acc[4 * c4 + 2]);
+          acc[4 * c4 + 3] = fmaf(g[u], z.w, acc[4 * c4 + 3]);
+        }
+      }
+    }
+    for (; j < r; ++j) {
       const float g = G[(long long)j * r + i];
       const float4* zj = reinterpret_cast<const float4*>(sZ + j * P);
 #pragma unroll
@@ -660,34 +798,82 @@ __global__ __launch_bounds__(256) void recon_kernel(XView x, int Kr, int r, cons
   const int tid = threadIdx.x;
   const float* X = x.base + b * x.batch_stride;
   const float* Vb = V + b * (long long)r * K;
-  for (int idx = tid; idx < r * KP; idx += 256) {
-    const int i = idx / KP, c = idx % KP;
-    sV[idx] = (c >= lo && c < hi) ? Vb[(long long)i * K + c] : 0.f;  // only used columns
+  // Staging in batches of UB loads per thread, all in flight before their LDS writes (a
+  // plain strided loop waits for each load in turn: ~50 HBM round trips per workgroup).
+  constexpr int UB = 8;
+  for (int i0 = tid; i0 < r * KP; i0 += 256 * UB) {
+    float t[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = i0 + 256 * u, i = idx / KP, c = idx % KP;
+      t[u] = (idx < r * KP && c >= lo && c < hi) ? Vb[(long long)i * K + c] : 0.f;  // used columns
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u)
+      if (i0 + 256 * u < r * KP) sV[i0 + 256 * u] = t[u];
   }
   const int rows = min(RB, Kr - k0);
-  if (x.si == 1) {
-    for (int idx = tid; idx < RB * r; idx += 256) {
-      const int kk = idx / r, i = idx % r;
-      sX[kk * (r + 1) + i] = kk < rows ? X[(long long)(k0 + kk) * x.sk + i] : 0.f;
+  const bool tr = x.si != 1;  // transposed view: walk the contiguous k direction
+  for (int i0 = tid; i0 < RB * r; i0 += 256 * UB) {
+    float t[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = i0 + 256 * u;
+      const int kk = tr ? idx % RB : idx / r, i = tr ? idx / RB : idx % r;
+      t[u] = (idx < RB * r && kk < rows) ? X[(long long)(k0 + kk) * x.sk + (long long)i * x.si] : 0.f;
     }
-  } else {  // transposed view: read along the contiguous k direction
-    for (int idx = tid; idx < RB * r; idx += 256) {
-      const int i = idx / RB, kk = idx % RB;
-      sX[kk * (r + 1) + i] = kk < rows ? X[(long long)(k0 + kk) * x.sk + (long long)i * x.si] : 0.f;
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = i0 + 256 * u;
+      const int kk = tr ? idx % RB : idx / r, i = tr ? idx / RB : idx % r;
+      if (idx < RB * r) sX[kk * (r + 1) + i] = t[u];
     }
   }
   __syncthreads();
-  // phase 1: RB x KP entries of Y, 256 threads
-  for (int e = tid; e < RB * KP; e += 256) {
-    const int kk = e / KP, c = e % KP;
-    float s = 0.f;
-    if (c >= lo && c < hi)
-      for (int i = 0; i < r; ++i) s = fmaf(sX[kk * (r + 1) + i], sV[i * KP + c], s);
-    sY[e] = s;
+  // phase 1: RB x KP entries of Y, a quad of columns per thread (one X read and one 16-byte
+  // V read per 4 FMAs; unused columns of sV are zero, so their Y entries are +0)
+  for (int e = tid; e < RB * (KP / 4); e += 256) {
+    const int kk = e / (KP / 4), c4 = e % (KP / 4);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (4 * c4 + 3 >= lo && 4 * c4 < hi)
+      for (int i = 0; i < r; ++i) {
+        const float xv = sX[kk * (r + 1) + i];
+        const float4 v = *reinterpret_cast<const float4*>(sV + i * KP + 4 * c4);
+        s.x = fmaf(xv, v.x, s.x);
+        s.y = fmaf(xv, v.y, s.y);
+        s.z = fmaf(xv, v.z, s.z);
+        s.w = fmaf(xv, v.w, s.w);
+      }
+    *reinterpret_cast<float4*>(sY + kk * KP + 4 * c4) = s;
   }
   __syncthreads();
   // phase 2: out rows, thread per column i (coalesced along i for m >= n)
   TO* Ob = out + b * out_bstride;
+  if (osi == 1) {  // column i's V row stays in registers over the block's rows; Y rows are
+                   // wave-wide broadcasts
+    for (int i = tid; i < r; i += 256) {
+      float v[KP];
+#pragma unroll
+      for (int c4 = 0; c4 < KP / 4; ++c4) {
+        const float4 t = *reinterpret_cast<const float4*>(sV + i * KP + 4 * c4);
+        v[4 * c4] = t.x; v[4 * c4 + 1] = t.y; v[4 * c4 + 2] = t.z; v[4 * c4 + 3] = t.w;
+      }
+      for (int kk = 0; kk < rows; ++kk) {
+        float s = 0.f;
+#pragma unroll
+        for (int c4 = 0; c4 < KP / 4; ++c4) {
+          const float4 y = *reinterpret_cast<const float4*>(sY + kk * KP + 4 * c4);
+          s = fmaf(y.x, v[4 * c4], s);
+          s = fmaf(y.y, v[4 * c4 + 1], s);
+          s = fmaf(y.z, v[4 * c4 + 2], s);
+          s = fmaf(y.w, v[4 * c4 + 3], s);
+        }
+        const float o = complement ? sX[kk * (r + 1) + i] - s : s;
+        Ob[(long long)(k0 + kk) * osk + i] = to_out<TO>(o);
+      }
+    }
+    return;
+  }
   for (int e = tid; e < RB * r; e += 256) {
     int kk, i;
     if (osi == 1) { kk = e / r; i = e % r; } else { i = e / RB; kk = e % RB; }
@@ -1831,7 +2017,12 @@ namespace {
 // G = X^T X for every matrix: the LDS-chunked kernel for r <= 128 (r % 4 == 0), else
 // one wave per 32x32 tile.
 void launch_gram(const XView& xv, int Kr, int r, float* G, long long batch, hipStream_t st) {
+  // float4 row loads need 16-B aligned rows when X is row-major
+  const bool vec_ok = xv.si != 1 || (xv.sk % 4 == 0 && xv.batch_stride % 4 == 0 &&
+                                     (reinterpret_cast<uintptr_t>(xv.base) & 15) == 0);
   const bool lds = r <= 128 && r % 4 == 0 && variant(V_SVD_GRAM_TILES) == 0;
+  const bool lds256 = r > 128 && r <= 256 && r % 4 == 0 && vec_ok &&
+                      variant(V_SVD_GRAM_TILES) == 0;
   const int nts = (r + 31) / 32;
   const int ntri = nts * (nts + 1) / 2;
   for (long long b0 = 0; b0 < batch; b0 += 65535) {
@@ -1841,6 +2032,9 @@ void launch_gram(const XView& xv, int Kr, int r, float* G, long long batch, hipS
     if (lds)
       SPECENH_LAUNCH(gram_lds_kernel, dim3((unsigned)nb), dim3(256), 0, st, xb, Kr, r,
                          G + b0 * (long long)r * r);
+    else if (lds256)
+      SPECENH_LAUNCH(gram256_kernel, dim3((unsigned)nb), dim3(256), 0, st, xb, Kr, r,
+                     G + b0 * (long long)r * r);
     else
       SPECENH_LAUNCH(gram_kernel, dim3((ntri + 3) / 4, (unsigned)nb), dim3(256), 0, st, xb,
                          Kr, r, G + b0 * (long long)r * r, nts);

@@ -245,11 +245,13 @@ def test_rank_deficient_complement(gpu_device):
         assert _range_err(got, ref.denoiseSignal(A64, *args), A64) <= TOL, args
 
 
-@pytest.mark.parametrize("shape", [(128, 128), (96, 128), (128, 40), (52, 100)])
+@pytest.mark.parametrize("shape", [(128, 128), (96, 128), (128, 40), (52, 100),
+                                   (513, 256), (256, 513), (300, 200), (201, 132), (140, 301)])
 def test_gram_paths_agree(gpu_device, shape, kernel_variant):
-    """The LDS-chunked Gram (r <= 128: row-major and transposed X, ragged chunks and tiles)
-    and the one-wave-per-tile Gram give the same reconstruction to fp32 rounding, and both
-    match the oracle on a gapped matrix."""
+    """The LDS-chunked Grams (gram_lds_kernel for r <= 128, gram256_kernel for 128 < r <= 256:
+    row-major and transposed X, ragged chunks, odd K, r not a multiple of 32) and the
+    one-wave-per-tile Gram give the same reconstruction to fp32 rounding, and both match the
+    oracle on a gapped matrix. (513, 256) is BASELINE config 3's geometry."""
     import os
     import sys
 

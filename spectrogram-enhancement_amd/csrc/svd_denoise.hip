@@ -464,26 +464,48 @@ __device__ void gemm_GZ8(const float* G, int r, const float* sZ, float* sY, floa
   __syncthreads();
 }
 
+// out[a][c] = sum_i A[i][a] B[i][c] in fp64 for all P x P (a, c); A, B r x P fp32 in LDS.
+// On the fp64 matrix cores: (P rounded up to 16)^2 / 256 tiles of v_mfma_f64_16x16x4_f64,
+// dealt to the 4 waves, r / 4 MFMAs each (the fp32 values are exact in fp64, products exact,
+// sums in fp64). A per-thread walk over all r rows was a serial chain of r dependent fp64
+// adds per entry (the subspace kernel's Rayleigh-Ritz and CholeskyQR Grams). Lane l supplies
+// A[i = i0 + (l >> 4)][a = 16 ta + (l & 15)] and B[i][c = 16 tb + (l & 15)]; D holds
+// (row (l >> 4) + 4 reg, col l & 15) of the tile. Ends with out visible to all threads.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+template <int P>
+__device__ void prodP(const float* sA, const float* sB, int r, double* out) {
+  constexpr int NT = (P + 15) / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m = lane & 15, kq = lane >> 4;
+  for (int t = wave; t < NT * NT; t += SS_THREADS / 64) {  // wave-uniform
+    const int ta = t / NT, tb = t % NT;
+    const int a = 16 * ta + m, c = 16 * tb + m;
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int i0 = 0; i0 < r; i0 += 4) {
+      const int i = i0 + kq;
+      const double av = (i < r && a < P) ? (double)sA[i * P + a] : 0.0;
+      const double bv = (i < r && c < P) ? (double)sB[i * P + c] : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int row = 16 * ta + kq + 4 * reg, col = 16 * tb + m;
+      if (row < P && col < P) out[row * P + col] = acc[reg];
+    }
+  }
+  __syncthreads();
+}
+
 // Orthonormalise the columns of Y (r x P, LDS) into Z with CholeskyQR in fp64:
 // S = Y^T Y, S = R^T R, Z = Y R^-1. fp64 keeps the Gram of Y (condition up to ~1e12
 // here) factorisable; callers run it twice (CholeskyQR2) for fp32-level orthogonality.
 template <int P>
 __device__ void cholqr(const float* sY, float* sZ, int r, double* sS, double* sRi) {
   const int tid = threadIdx.x;
-  constexpr int NPAIRS = P * (P + 1) / 2;
   if constexpr (P == 8) {
     prod8(sY, sY, r, sS + 2 * P * P, sS);  // scratch [4][64] past sS, sRi (SsLayout)
-  } else
-  for (int q = tid; q < NPAIRS; q += SS_THREADS) {
-    int a = 0, rem = q;
-    while (rem >= P - a) {
-      rem -= P - a;
-      ++a;
-    }
-    const int bcol = a + rem;
-    double s = 0.0;
-    for (int i = 0; i < r; ++i) s += (double)sY[i * P + a] * (double)sY[i * P + bcol];
-    sS[a * P + bcol] = s;
+  } else {
+    prodP<P>(sY, sY, r, sS);  // (full P x P; the factorisation reads the upper triangle)
   }
   __syncthreads();
   if (tid < 64) {  // Cholesky S = R^T R (R upper, in place), one wave
@@ -698,12 +720,8 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
       prod8(sZ, sY, r, sPart, sS);
       if (tid < 64) sH[tid] = (float)sS[tid];
     } else {
-      for (int q = tid; q < P * P; q += SS_THREADS) {
-        const int a = q / P, c = q % P;
-        double s = 0.0;
-        for (int i = 0; i < r; ++i) s += (double)sZ[i * P + a] * (double)sY[i * P + c];
-        sH[q] = (float)s;
-      }
+      prodP<P>(sZ, sY, r, sS);
+      for (int q = tid; q < P * P; q += SS_THREADS) sH[q] = (float)sS[q];
     }
     __syncthreads();
     for (int q = tid; q < P * P; q += SS_THREADS) {  // symmetrise

@@ -844,9 +844,10 @@ __global__ __launch_bounds__(256) void recon_kernel(XView x, int Kr, int r, cons
   const int tid = threadIdx.x;
   const float* X = x.base + b * x.batch_stride;
   const float* Vb = V + b * (long long)r * K;
-  // Staging in batches of UB loads per thread, all in flight before their LDS writes (a
+  // Staging in batches of loads per thread, all in flight before their LDS writes (a
   // plain strided loop waits for each load in turn: ~50 HBM round trips per workgroup).
-  constexpr int UB = 8;
+  // (batches of 16 for V and 32 for X: one round trip each at C3's r = 256, K = 16)
+  constexpr int UB = 16, UBX = 32;
   for (int i0 = tid; i0 < r * KP; i0 += 256 * UB) {
     float t[UB];
 #pragma unroll
@@ -860,16 +861,16 @@ __global__ __launch_bounds__(256) void recon_kernel(XView x, int Kr, int r, cons
   }
   const int rows = min(RB, Kr - k0);
   const bool tr = x.si != 1;  // transposed view: walk the contiguous k direction
-  for (int i0 = tid; i0 < RB * r; i0 += 256 * UB) {
-    float t[UB];
+  for (int i0 = tid; i0 < RB * r; i0 += 256 * UBX) {
+    float t[UBX];
 #pragma unroll
-    for (int u = 0; u < UB; ++u) {
+    for (int u = 0; u < UBX; ++u) {
       const int idx = i0 + 256 * u;
       const int kk = tr ? idx % RB : idx / r, i = tr ? idx / RB : idx % r;
       t[u] = (idx < RB * r && kk < rows) ? X[(long long)(k0 + kk) * x.sk + (long long)i * x.si] : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < UB; ++u) {
+    for (int u = 0; u < UBX; ++u) {
       const int idx = i0 + 256 * u;
       const int kk = tr ? idx % RB : idx / r, i = tr ? idx / RB : idx % r;
       if (idx < RB * r) sX[kk * (r + 1) + i] = t[u];

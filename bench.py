@@ -349,7 +349,22 @@ def svd_c3_stage(dev, B=4096, m=513, n=256, k=16, reps=5):
         ms = e0.elapsed_time(e1) / reps
         fl = flop if name == "rank16" else 2.0 * m * n * n + 4.0 * m * n  # K = 1
         ach = fl * B / (ms * 1e-3) / 1e12
-        res[name] = {"ms": ms, "matrices_per_s": B / (ms * 1e-3),
+        # accuracy on sampled matrices of the timed batch: the notebook's arithmetic
+        # (numpy thin SVD in float64, components [lo, hi); denoising_by_svd.ipynb:209-228)
+        # on the same fp32 matrices vs the output of the last timed launch
+        rels = []
+        for b in np.linspace(0, B - 1, 6).astype(int):
+            a64 = A[b].double().cpu().numpy()
+            u, sv, vh = np.linalg.svd(a64, full_matrices=False)
+            l0, h0 = (0, 16) if name == "rank16" else (1, len(sv))
+            ref = (u[:, l0:h0] * sv[l0:h0]) @ vh[l0:h0]
+            rels.append(float(np.linalg.norm(out[b].double().cpu().numpy() - ref) /
+                              np.linalg.norm(ref)))
+        acc = {"rel_fro_max": max(rels), "tol": 1e-5, "pass": max(rels) <= 1e-5,
+               "matrices": 6, "reference": "numpy float64 thin SVD of the same fp32 matrices"}
+        if not acc["pass"]:
+            print(f"[bench] C3 {name} ACCURACY CHECK FAILED: {max(rels):.3e}", file=sys.stderr)
+        res[name] = {"ms": ms, "matrices_per_s": B / (ms * 1e-3), "accuracy": acc,
                      "roofline": {"bound": "mfma_fp32", "achieved": ach,
                                   "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                                   "frac": ach / FP32_MFMA_PEAK_TFLOPS,
@@ -386,7 +401,8 @@ def c4_engine_and_batch(dev, batch=128, n=None, seed=4):
     return eng, X, Y, X[:batch], Y[:batch]
 
 
-def ae_train_c4_stage(dev, dist=None, batch=128, steps=20, n_local=4096, seed=4):
+def ae_train_c4_stage(dev, dist=None, batch=128, steps=20, n_local=4096, seed=4, make=None,
+                      sync=None):
     """BASELINE config 4: Keras fit() steps of the 3-layer model on the C4 workload (SURVEY
     §8 d: C1 spectrograms of seeded noisy chirps -> the noise-free chirps' spectrograms,
     generated on the device), mixed_bfloat16 (bf16 MFMA, fp32 master weights + Adam):
@@ -399,12 +415,21 @@ def ae_train_c4_stage(dev, dist=None, batch=128, steps=20, n_local=4096, seed=4)
     configuration) and global batch ``batch`` (batch / world per rank: Keras parity).
     Reported: global samples/s (all ranks' samples / max-over-ranks time), ms per step, and
     the standalone all-reduce time of the gradient buffer with its share of the step.
-    1.494 GFLOP per sample (SURVEY §8 d C4: forward x 3) at the dense bf16 MFMA peak."""
+    1.494 GFLOP per sample (SURVEY §8 d C4: forward x 3) at the dense bf16 MFMA peak.
+
+    ``make(rank) -> (engine, X, Y)`` and ``sync()`` replace the HIP engine / C4 pairs and
+    torch.cuda.synchronize (tests/test_bench_dist_cpu.py runs this orchestration on gloo
+    with the oracle's CPU engine)."""
     import torch
     world = dist.get_world_size() if dist else 1
     rank = dist.get_rank() if dist else 0
     group = dist.group.WORLD if dist else None
-    eng, X, Y, _, _ = c4_engine_and_batch(dev, batch, n=n_local, seed=seed + 7919 * rank)
+    if make is None:
+        eng, X, Y, _, _ = c4_engine_and_batch(dev, batch, n=n_local, seed=seed + 7919 * rank)
+    else:
+        eng, X, Y = make(rank)
+    n_local = X.shape[0]
+    sync = sync or torch.cuda.synchronize
     if dist:
         eng.sync_state(group)
     g = torch.Generator(device=dev)
@@ -425,10 +450,10 @@ def ae_train_c4_stage(dev, dist=None, batch=128, steps=20, n_local=4096, seed=4)
         run(per_rank, 3)
         if dist:
             dist.barrier()
-        torch.cuda.synchronize()
+        sync()
         t0 = time.perf_counter()
         run(per_rank, steps)
-        torch.cuda.synchronize()
+        sync()
         el = max_over_ranks(time.perf_counter() - t0, dist, dev)
         return el / steps
 
@@ -451,11 +476,11 @@ def ae_train_c4_stage(dev, dist=None, batch=128, steps=20, n_local=4096, seed=4)
     if dist:  # the gradient exchange alone (both buckets, the flat fp32 buffer)
         for _ in range(3):
             dist.all_reduce(eng.g)
-        torch.cuda.synchronize()
+        sync()
         t0 = time.perf_counter()
         for _ in range(20):
             dist.all_reduce(eng.g)
-        torch.cuda.synchronize()
+        sync()
         ar = max_over_ranks(time.perf_counter() - t0, dist, dev) / 20
         res["allreduce"] = {"bytes": eng.g.numel() * 4, "ms": ar * 1e3,
                             "share_of_step": ar * 1e3 / res["per_gpu_batch"]["ms_per_step"]}
@@ -573,8 +598,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
+    # rank 0 times the CPU reference at every world size, before anything touches the GPU
+    # (the other ranks wait in the process-group rendezvous), so a scaling line at N > 1
+    # carries the same baseline as N = 1
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_shots)
 
     import torch

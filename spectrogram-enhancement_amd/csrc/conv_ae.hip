@@ -179,11 +179,12 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 }
 
 // max(a, b) without the NaN-quieting canonicalisation fmaxf gets (operands are
-// accumulators: finite unless the inputs hold NaN/Inf)
+// accumulators: finite unless the inputs hold NaN/Inf) as v_med3_f32(a, b, +inf): a
+// builtin, not inline asm, so the compiler's hazard recognizer sees the read of an MFMA
+// result and pads the XDL-write -> VALU-read wait states (inside an asm statement it
+// does not)
 __device__ __forceinline__ float vmax(float a, float b) {
-  float r;
-  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
+  return __builtin_amdgcn_fmed3f(a, b, __builtin_inff());
 }
 
 // 8 GEMM-K elements k .. k+7 of one output pixel (by, bx = top-left of its window, nb =

@@ -251,6 +251,11 @@ int specenh_csd(const specenh_csd_plan* plan, const float* x, const float* y, lo
     return set_error(SPECENH_EUNSUPPORTED, "cross spectrum: batch <= 65535 signal pairs per call");
   if (x_stride < length || y_stride < length) return set_error(SPECENH_EINVAL, "stride < length");
   if (mode == SPECENH_CSD_AMPLITUDE && plan->stft) {
+    // Per-frame amplitude, no segment averaging: |Pxy(f, t)| = sqrt(PSD_x(f, t) PSD_y(f, t))
+    // holds frame by frame only. crosspowerspec.py:39 takes its amplitude from ae_co2
+    // (co2_deps, not in the reference), so treating ae_co2's amplitude as this per-frame
+    // |Pxy| is an assumption: parity with ae_co2 itself is unpinned; the
+    // tests pin it against the scipy two-signal restatement (tests/golden/csd.npz).
     bool launched = false;
     const int rc = specenh::stft_csd_amplitude(plan->stft, x, y, batch, length, x_stride, y_stride,
                                                reinterpret_cast<float*>(out), (hipStream_t)stream,

@@ -665,6 +665,35 @@ struct D3Args {
   int N, H;
 };
 
+#ifdef SPECENH_D3_STATS  // development build (tools/d3_stats.py): per-wave barrier clocks
+__device__ unsigned long long d3_stats[1024 * 8 * 4];
+struct D3Clock {
+  long long last = 0, busy = 0, wait = 0, n = 0;
+  __device__ __forceinline__ void barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const long long t0 = __builtin_amdgcn_s_memtime();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (last) busy += t0 - last;
+    wait += t1 - t0;
+    ++n;
+    last = t1;
+  }
+  __device__ void flush(int wv) {
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) {
+      unsigned long long* p = d3_stats + (blockIdx.x * 8 + wv) * 4;
+      p[0] = busy; p[1] = wait; p[2] = n; p[3] = 0;
+    }
+  }
+};
+#define D3_BARRIER() clk.barrier()
+#else
+#define D3_BARRIER() lds_barrier()
+#endif
+
 template <typename T>
 __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
   using namespace d3;
@@ -678,6 +707,9 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int m = lane & 15, kg = lane >> 4;
   const int H1 = a.H, H2 = 2 * H1, H3 = 4 * H1;
+#ifdef SPECENH_D3_STATS
+  D3Clock clk;
+#endif
   // Persistent workgroups: one continuous row stream over the workgroup's images
   // n = blockIdx.x + i G. Per image SPI = H1 + 1 macro steps: producer step s = 0 .. H1 - 1
   // turns input row s into tail-input rows 2s, 2s + 1, step s = H1 writes the two zero rows
@@ -751,7 +783,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
 #pragma unroll
     for (int p = 0; p < 3; ++p) stage(p);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();  // (macro step -1: the consumers' matching barrier is below)
+    D3_BARRIER();  // (macro step -1: the consumers' matching barrier is below)
 
     auto pstep = [&](auto ic, const int g) {
       constexpr int I = decltype(ic)::value;  // g & 3
@@ -790,7 +822,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
           *reinterpret_cast<uint2*>(((ph >> 1) ? r1 : r0) + x2w[ph & 1]) = uint2{0u, 0u};
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // input position g + 3 has landed
-      lds_barrier();
+      D3_BARRIER();
     };
     int g = 0;
     for (; g + 4 <= S; g += 4) {
@@ -802,6 +834,9 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
     if (g < S) pstep(IC<0>{}, g);
     if (g + 1 < S) pstep(IC<1>{}, g + 1);
     if (g + 2 < S) pstep(IC<2>{}, g + 2);
+#ifdef SPECENH_D3_STATS
+    clk.flush(wv);
+#endif
   } else {
     // ======================= consumer: the row-sweep tail, tail steps t = 2g - 3, 2g - 2
     const int w = wv - 4;
@@ -810,7 +845,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
     int xo[3];  // element offset of pixel 16 w + m + dx (stored + 1), group kg, in a ring row
 #pragma unroll
     for (int dx = -1; dx <= 1; ++dx) xo[dx + 1] = x2_off(16 * w + m + dx + 1, kg);
-    lds_barrier();  // macro step -1
+    D3_BARRIER();  // macro step -1
     // global tail step t (image t / TPI, per-image step tl = t % TPI) with T8 = t & 7
     // compile-time from g & 3. The Conv2D(1) of step tl is for output rows 2tl - 4, 2tl - 3
     // (map rows 2tl - 6 .. 2tl - 1, all written by earlier steps: the 8-row map ring holds
@@ -848,7 +883,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       float* const sc1 = sc0 + rows::SCR * rows::SCW;
       tstep(IC<(2 * I + 5) & 7>{}, 2 * g - 3, sc0);  // (2g - 3) & 7 = (2 I - 3) & 7
       tstep(IC<(2 * I + 6) & 7>{}, 2 * g - 2, sc1);
-      lds_barrier();
+      D3_BARRIER();
       sums(sc0, 2 * g - 3);
       sums(sc1, 2 * g - 2);
     };
@@ -862,6 +897,9 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
     if (g < S) cstep(IC<0>{}, g);
     if (g + 1 < S) cstep(IC<1>{}, g + 1);
     if (g + 2 < S) cstep(IC<2>{}, g + 2);
+#ifdef SPECENH_D3_STATS
+    clk.flush(wv);
+#endif
   }
 }
 
@@ -932,6 +970,12 @@ extern "C" int specenh_convt_conv_out(int dtype, const void* x, int N, int H, in
                                                           hipGetErrorString(e));
   return SPECENH_OK;
 }
+
+#ifdef SPECENH_D3_STATS
+extern "C" int specenh_d3_stats(void* host, int bytes) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(d3_stats), bytes) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int specenh_decoder3(int dtype, const void* x, int N, int H, int W, int C,
                                 const void* w1_gemm, const float* b1, int CO1, const void* wt_gemm,

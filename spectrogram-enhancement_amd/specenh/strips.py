@@ -35,7 +35,13 @@ def patch_batch(S: torch.Tensor, dtype=torch.float32, rows=ROWS, width=WIDTH,
     from .ops import ops
     if out is None:
         return ops.strips_pack(S, rows, width, n_strips, dtype)
-    ops.strips_pack_out(S, rows, width, n_strips, out)  # straight into the caller's buffer
+    B = S.shape[0]
+    if (out.dtype in (torch.float32, torch.bfloat16, torch.float16) and out.is_contiguous()
+            and out.numel() == B * n_strips * rows * width and out.device == S.device):
+        ops.strips_pack_out(S, rows, width, n_strips, out)  # straight into the caller's buffer
+    else:  # strided / other dtype: pack, then copy_ (casts and strides as torch does)
+        res = ops.strips_pack(S, rows, width, n_strips, dtype)
+        out.copy_(res.view(out.shape) if out.numel() == res.numel() else res)
     return out
 
 

@@ -106,10 +106,15 @@ def optimal_batch(A: torch.Tensor, mode: int = _lib.SVD_OPTIMAL, out: torch.Tens
     from .ops import ops
     if out is None:
         out, ns, med = ops.svd_denoise_optimal(A, int(mode))
-    else:  # straight into the caller's buffer
+    elif (out.dtype == torch.float32 and out.is_contiguous() and out.numel() == B * m * n
+          and out.device == A.device):  # straight into the caller's buffer
         ns = torch.empty(B, dtype=torch.int32, device=A.device)
         med = torch.empty(B, dtype=torch.float64, device=A.device)
         ops.svd_denoise_optimal_out(A, int(mode), out.view(B, m, n), ns, med)
+    else:  # strided / other dtype: compute, then copy_ (casts and strides as torch does)
+        res, ns, med = ops.svd_denoise_optimal(A, int(mode))
+        out.copy_(res.view(out.shape) if out.shape != res.shape and out.numel() == res.numel()
+                  else res)
     res = out[0] if squeeze else out
     return (res, ns, med) if return_rank else res
 

@@ -1,0 +1,209 @@
+"""The reference's own production shapes on the GPU.
+
+``pipeline_data.py:31-35,77-84`` (and the BES variant, ``denoising_by_svd.ipynb:49-52``)
+cut a shot to ``cut_shot * fs`` = 2 x 500,000 = 1,000,000 samples and run a 512-point
+Hamming spectrogram with hop 256: 257 x 3905 PSD, (256, 3905) after the Nyquist row is
+dropped. The notebook's loop (``denoising_by_svd.ipynb:250-263``) then calls
+``denoiseSignal(s)`` on each channel's (256, 3905) spectrogram.
+
+Tolerances (the contract of tests/test_stft_gpu.py and tests/test_svd_gpu.py):
+  * specgr: f / t bit-exact, max |GPU - fp64 truth| <= 1e-5 (fp32 samples on both sides);
+  * denoiseSignal: ||GPU - ref||_F / ||ref||_F <= 1e-5 where the kept range has a spectral
+    gap (default [1, r): sigma_1 / sigma_2 ~ 60 on these spectrograms; use_optimal).
+    The (0, 16) cut of a log spectrogram of chirps + noise has NO gap (sigma_16 / sigma_17 =
+    1.003 here): the 16th / 17th singular directions are then not determined to fp32 by any
+    method, so that range is pinned through rotation-invariant properties — the kept energy
+    ||out||_F^2 = sum_{i<16} sigma_i^2, the Eckart-Young residual ||A - out||_F^2 =
+    sum_{i>=16} sigma_i^2, out's singular values = sigma_0..15, and the part of out inside the
+    gapped top-15 subspace (the directions the cut does determine) to 1e-5.
+"""
+import pickle
+
+import numpy as np
+import pytest
+
+from oracle import spectrogram as ref
+from oracle import svd as osvd
+
+pytestmark = pytest.mark.gpu
+
+FS = 500000
+SPEC = {"nperseg": 512, "noverlap": 256, "fs": FS, "window": "hamm", "scaling": "density",
+        "detrend": "linear", "eps": 1e-11}          # pipeline_data.py:77-84
+L_SHOT = 2 * FS                                     # cut_shot = 2 (pipeline_data.py:28)
+TOL_NORM = 1e-5
+TOL_SVD = 1e-5
+
+
+def _rel(a, b):
+    return np.linalg.norm(a - b) / np.linalg.norm(b)
+
+
+@pytest.fixture(scope="module")
+def shots():
+    from specenh.synthetic import plasma_chirps
+    # 3 channels of 1.2 s each (the cut keeps the first 2 s worth of a longer record in the
+    # reference; here the record is 1.2 M samples and the cut keeps 1 M)
+    return plasma_chirps(3, 1_200_000, seed0=11, dtype=np.float32)
+
+
+@pytest.fixture(scope="module")
+def truth(shots):
+    out = []
+    for x in shots:
+        S, f, t = ref.specgr_arrays(x[:L_SHOT].astype(np.float64), SPEC)
+        out.append((S, f, t))
+    return out
+
+
+def test_specgr_reference_entry_production_shot(shots, truth, tmp_path, gpu_device):
+    """The reference entry itself: specgr(fname, ecen, spec_params, cut_shot=2) on a pickle
+    of channel records (pipeline_data.py:28-36; the file is written by this test)."""
+    from specenh import pipeline_data
+
+    fname = tmp_path / "shot_ECE.pkl"
+    with open(fname, "wb") as fh:
+        pickle.dump({"\\tecef%.2i" % (c + 1): shots[c].astype(np.float64) for c in range(3)}, fh)
+    for c in range(3):
+        S, f, t = pipeline_data.specgr(str(fname), c + 1, SPEC)
+        St, ft, tt = truth[c]
+        assert S.shape == (256, 3905) and S.dtype == np.float64
+        assert np.array_equal(f, ft) and np.array_equal(t, tt)
+        err = np.abs(S - St).max()
+        assert err <= TOL_NORM, (c, err)
+
+
+def test_specgr_bes_variant_production_shot(shots, truth, tmp_path, gpu_device):
+    """denoising_by_svd.ipynb:49-52: key 'besfu%02d', field 'data.BES'."""
+    from specenh import pipeline_data
+
+    fname = tmp_path / "shot_BES"
+    with open(fname, "wb") as fh:
+        pickle.dump({"besfu01": {"data.BES": shots[1].astype(np.float64)}}, fh)
+    S, f, t = pipeline_data.specgr(str(fname), 1, SPEC, 2, key_format="besfu%02d",
+                                   field="data.BES")
+    St, ft, tt = truth[1]
+    assert S.shape == (256, 3905)
+    assert np.array_equal(f, ft) and np.array_equal(t, tt)
+    assert np.abs(S - St).max() <= TOL_NORM
+
+
+def test_specgr_batch_production_shots(shots, truth, gpu_device):
+    """The same three channels in one launch, cut on the device (specgr_batch cut_shot)."""
+    import torch
+
+    from specenh import pipeline_data
+
+    x = torch.as_tensor(shots, device=gpu_device)
+    S = pipeline_data.specgr_batch(x, SPEC, cut_shot=2).double().cpu().numpy()
+    assert S.shape == (3, 256, 3905)
+    for c in range(3):
+        assert np.abs(S[c] - truth[c][0]).max() <= TOL_NORM
+
+
+@pytest.fixture(scope="module")
+def spectrogram(truth):
+    """The notebook's denoiseSignal input: channel 0's (256, 3905) spectrogram, fp32-cast
+    (the GPU path computes from fp32; the reference's float64 output on the same values)."""
+    return truth[0][0].astype(np.float32).astype(np.float64)
+
+
+@pytest.fixture(scope="module")
+def svd_ref(spectrogram):
+    u, s, vh = np.linalg.svd(spectrogram, full_matrices=False)
+    return u, s, vh
+
+
+def _check_ungapped(out, A, svd_ref, lo, hi, ref_out):
+    """Rotation-invariant checks of a kept range [lo, hi) whose end has no spectral gap."""
+    u, s, vh = svd_ref
+    kept = np.sqrt(np.sum(s[lo:hi] ** 2))
+    assert abs(np.linalg.norm(out) - kept) / kept <= TOL_SVD, "kept energy"
+    if lo == 0:  # Eckart-Young: A - out is the best rank-(r - hi) remainder
+        resid = np.sqrt(np.sum(s[hi:] ** 2))
+        assert abs(np.linalg.norm(A - out) - resid) / resid <= 1e-4, "residual"
+    so = np.linalg.svd(out, compute_uv=False)
+    assert np.max(np.abs(so[:hi - lo] - s[lo:hi])) <= 1e-4 * s[0], "singular values"
+    assert np.max(so[hi - lo:], initial=0.0) <= 1e-5 * s[0], "rank"
+    # the part of out inside the gapped top-j subspace (j = the largest gap below the cut):
+    # directions the cut does determine
+    j = int(np.argmax(s[lo + 1:hi] / s[lo + 2:hi + 1])) + lo + 2
+    P = lambda X: u[:, lo:j].T @ X @ vh[lo:j].T  # noqa: E731
+    e = _rel(P(out), P(ref_out))
+    assert e <= TOL_SVD, ("determined part", j, e, "normwise", _rel(out, ref_out))
+
+
+def test_denoise_default_production_shape(spectrogram, svd_ref, gpu_device):
+    """denoising_by_svd.ipynb:263 — svd = denoiseSignal(s): components [1, r)."""
+    from specenh import svd
+
+    _, s, _ = svd_ref
+    assert s[0] / s[1] > 10  # the gap the default cut relies on
+    out = svd.denoiseSignal(spectrogram)
+    assert out.shape == (256, 3905) and out.dtype == np.float64
+    e = _rel(out, osvd.denoiseSignal(spectrogram))
+    assert e <= TOL_SVD, e
+
+
+def test_denoise_optimal_production_shape(spectrogram, svd_ref, gpu_device):
+    """use_optimal (:210-217): [0, num_sing - 1) at the Gavish-Donoho threshold."""
+    import torch
+
+    from specenh import svd
+
+    _, s, _ = svd_ref
+    out = svd.denoiseSignal(spectrogram, use_optimal=True)
+    e = _rel(out, osvd.denoiseSignal(spectrogram, use_optimal=True))
+    _, ns, med = svd.optimal_batch(torch.as_tensor(spectrogram.astype(np.float32),
+                                                   device=gpu_device), return_rank=True)
+    k = osvd.optimal_rank(s, spectrogram.shape)
+    assert int(ns[0]) == k
+    assert float(med[0]) == pytest.approx(float(np.median(s)), rel=1e-5)
+    # the kept range [0, k - 1) ends inside the noise bulk (sigma ratios ~1.003 there)
+    gap = s[k - 2] / s[k - 1]
+    if gap > 1.05:
+        assert e <= TOL_SVD, e
+    else:
+        _check_ungapped(out, spectrogram, svd_ref, 0, k - 1,
+                        osvd.denoiseSignal(spectrogram, use_optimal=True))
+
+
+def test_denoise_rank16_production_shape(spectrogram, svd_ref, gpu_device):
+    """denoiseSignal(s, 0, 16) on the ungapped spectrogram: rotation-invariant checks."""
+    from specenh import svd
+
+    A = spectrogram
+    out = svd.denoiseSignal(A, 0, 16)
+    _check_ungapped(out, A, svd_ref, 0, 16, osvd.denoiseSignal(A, 0, 16))
+
+
+def test_compute_signal_production_shape(spectrogram, svd_ref, gpu_device):
+    """computeSignal (:161-186): components [1, 2 num_sing), projected on the determined
+    (gapped) part as in tests/test_svd_gpu.py::test_compute_signal_matches_notebook."""
+    from specenh import svd
+
+    u, s, vh = svd_ref
+    out = svd.computeSignal(spectrogram)
+    ref_out = osvd.computeSignal(spectrogram)
+    k = osvd.optimal_rank(s, spectrogram.shape)
+    hi = 2 * k
+    band_noise = np.sqrt(np.sum(s[max(1, hi - 4):hi + 4] ** 2))
+    assert np.linalg.norm(out - ref_out) <= 2 * band_noise
+    P = lambda X: u[:, 1:2].T @ X @ vh[1:2].T  # noqa: E731  (sigma_1 / sigma_2 gapped)
+    assert _rel(P(out), P(ref_out)) <= TOL_SVD
+
+
+def test_notebook_loop_batched(shots, truth, gpu_device):
+    """denoising_by_svd.ipynb:250-263 for three channels as one device batch: specgr ->
+    denoiseSignal default, spectrograms never leave the GPU."""
+    import torch
+
+    from specenh import pipeline_data, svd
+
+    x = torch.as_tensor(shots, device=gpu_device)
+    S = pipeline_data.specgr_batch(x, SPEC, cut_shot=2)
+    D = svd.denoise_batch(S).double().cpu().numpy()
+    for c in range(3):
+        Sc = S[c].double().cpu().numpy()
+        e = _rel(D[c], osvd.denoiseSignal(Sc))
+        assert e <= TOL_SVD, (c, e)

@@ -30,11 +30,8 @@ def _both(x, nperseg, noverlap, window):
         # the sweep kernel proper (short shots would otherwise take its held-tile
         # instantiation, whose FFT code is scheduled differently: equal to ~1e-5 only,
         # tests/test_stft_gpu.py::test_held_tiles_match_sweep)
-        _lib.set_variant("STFT_NO_HOLD", 1)
-        try:
+        with _lib.variant("STFT_NO_HOLD", 1):  # restores the caller's value
             stft._launch(plan, x, out, flags | extra, workspace=ws)
-        finally:
-            _lib.set_variant("STFT_NO_HOLD", 0)
         outs.append(out)
         torch.cuda.synchronize()
         tmo = int(ws[:4].view(torch.int32)[0])

@@ -14,6 +14,7 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "spectrogram-enhancement_amd"))
 import specenh  # noqa: E402,F401
+from specenh import _lib  # noqa: E402
 
 
 def timeit(fn, reps):
@@ -45,10 +46,9 @@ def main():
         out = torch.empty(N, OH, OH, CO, device=dev, dtype=dt)
         for masked in (False, True):
             for generic in ((False, True) if s == 2 else (False,)):
-                if generic:
-                    os.environ["SPECENH_CONV_NO_S2"] = "1"
-                else:
-                    os.environ.pop("SPECENH_CONV_NO_S2", None)
+                # the variant switches are read from the environment once per process:
+                # select through the library, not os.environ
+                _lib.set_variant("CONV_NO_S2", 1 if generic else 0)
 
                 def run():
                     torch.ops.specenh.conv2d_out(x, w, None, 5, 5, CO, s, 2 if s == 2 else 2, 2, 1,
@@ -58,7 +58,7 @@ def main():
                 gb = (x.numel() + out.numel() * (2 if masked else 1)) * 2 / 1e9
                 print(f"{name:22s} mask={int(masked)} generic={int(generic)} {us:8.1f} us "
                       f"({gb / us * 1e3:6.0f} GB/s)")
-    os.environ.pop("SPECENH_CONV_NO_S2", None)
+    _lib.set_variant("CONV_NO_S2", 0)
 
 
 if __name__ == "__main__":

@@ -382,9 +382,16 @@ __device__ __forceinline__ uint2 relu_pack4(const f32x4& v) {
                pack2<T>(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f))};
 }
 
-template <typename T, int CO, int W>
+// LEAD: ring refills in flight beyond the one a step waits for. Step g needs positions
+// g + 1 .. g + 3 after its barrier, so it waits for the DMA of position g + 3 only, issued LEAD
+// steps earlier; the wave's ledger of its vector-memory ops (LDS-DMAs, and the output stores,
+// which vmcnt counts too on gfx9) turns that into the count of younger ops. Round 3 waited
+// with vmcnt(1) for everything but the DMA just issued, i.e. for the previous step's DMA and
+// this step's own stores.
+template <typename T, int CO, int W, int LEAD>
 __global__ __launch_bounds__((TC<CO, W>::THREADS)) __attribute__((amdgpu_waves_per_eu(2)))
 void convt_rows_kernel(CRArgs a) {
+  static_assert(LEAD >= 1 && LEAD <= 4, "8-row ring: positions g .. g + 3 + LEAD live");
   using C = TC<CO, W>;
   extern __shared__ __attribute__((aligned(16))) unsigned char ring[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -450,7 +457,7 @@ void convt_rows_kernel(CRArgs a) {
   };
   __syncthreads();  // ring zeroed
 #pragma unroll
-  for (int p = 0; p < 5; ++p) stage(p);
+  for (int p = 0; p < 3 + LEAD; ++p) stage(p);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_barrier();
 
@@ -458,17 +465,22 @@ void convt_rows_kernel(CRArgs a) {
   const int OW = 2 * W;
   uint2 pk[4];
   long long po = -1;  // element offset of the held outputs' (2s, 2x) pixel, -1: none
+  int vmn = 0;        // this wave's vector-memory ops issued in the loop
+  int mk[LEAD + 1];   // vmn right after the DMA of position g + 3 + i (-1: none in flight)
+#pragma unroll
+  for (int i = 0; i <= LEAD; ++i) mk[i] = -1;
   auto store_held = [&]() {
     if (po >= 0) {
 #pragma unroll
       for (int ph = 0; ph < 4; ++ph)
-        *reinterpret_cast<uint2*>(O + po + ((ph >> 1) * OW + (ph & 1)) * CO) = pk[ph];
+        gstore8(O + po + ((ph >> 1) * OW + (ph & 1)) * CO, pk[ph]);
+      vmn += 4;
     }
   };
   for (int g = 0; g < S; ++g) {
     store_held();
     po = -1;
-    const bool issued = stage(g + 5);
+    mk[LEAD] = stage(g + 3 + LEAD) ? ++vmn : -1;
     const int il = g / SPI, s = g - il * SPI;
     if (s < H) {
       f32x4 acc[4] = {bias, bias, bias, bias};
@@ -497,17 +509,18 @@ void convt_rows_kernel(CRArgs a) {
       const long long n = (long long)blockIdx.x + (long long)il * G;
       po = ((n * 2 * H + 2 * s) * OW + 2 * (16 * wx + m)) * CO + 16 * nb + 4 * kg;
     }
-    if (issued) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (mk[0] >= 0) wait_vmcnt(vmn - mk[0]);  // position g + 3 has landed
     lds_barrier();
+#pragma unroll
+    for (int i = 0; i < LEAD; ++i) mk[i] = mk[i + 1];
   }
   store_held();
 }
 
-template <typename T, int CO, int W>
-hipError_t launch_convt_rows(const CRArgs& a, hipStream_t st) {
+template <typename T, int CO, int W, int LEAD>
+hipError_t launch_convt_rows_lead(const CRArgs& a, hipStream_t st) {
   using C = TC<CO, W>;
-  const void* k = reinterpret_cast<const void*>(&convt_rows_kernel<T, CO, W>);
+  const void* k = reinterpret_cast<const void*>(&convt_rows_kernel<T, CO, W, LEAD>);
   static int per_cu[64] = {};
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -520,9 +533,15 @@ hipError_t launch_convt_rows(const CRArgs& a, hipStream_t st) {
     per_cu[dev] = std::max(1, pc);
   }
   const long long grid = std::min<long long>(a.N, (long long)per_cu[dev] * device_cus());
-  SPECENH_LAUNCH((convt_rows_kernel<T, CO, W>), dim3((unsigned)grid), dim3(C::THREADS), C::LDS,
-                 st, a);
+  SPECENH_LAUNCH((convt_rows_kernel<T, CO, W, LEAD>), dim3((unsigned)grid), dim3(C::THREADS),
+                 C::LDS, st, a);
   return hipGetLastError();
+}
+
+template <typename T, int CO, int W>
+hipError_t launch_convt_rows(const CRArgs& a, hipStream_t st) {
+  return variant(V_ROWS_SHORT_LEAD) ? launch_convt_rows_lead<T, CO, W, 1>(a, st)
+                               : launch_convt_rows_lead<T, CO, W, 3>(a, st);
 }
 
 // ============================================================================ C = 1 rows

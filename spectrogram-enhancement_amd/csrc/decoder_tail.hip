@@ -631,7 +631,7 @@ constexpr int CI1 = 64, CO1 = 32;     // the first Conv2DTranspose
 constexpr int W1 = 32;                // its input positions per row
 constexpr int X1ST = CI1;             // its input pixels: dense 128 B, 16-B groups swizzled
 constexpr int X1ROW = (W1 + 2) * X1ST;
-constexpr int NX1 = 4;
+constexpr int NX1 = 8;                // input ring rows (positions g .. g + 3 + LEAD live)
 constexpr int X2ST = 32;              // tail input pixel stride (elements): dense 64 B, swizzled
 constexpr int X2ROW = (2 * W1 + 2) * X2ST;
 constexpr int NX2 = 8;
@@ -639,7 +639,12 @@ constexpr int LDS_X1 = NX1 * X1ROW * 2;
 constexpr int LDS_X2 = NX2 * X2ROW * 2;
 constexpr int LDS_M = rows::NMR * rows::MROW * 2;
 constexpr int LDS_S = 4 * rows::SCR * rows::SCW * 4;
-constexpr int LDS_BYTES = LDS_X1 + LDS_X2 + LDS_M + LDS_S;  // 105,728 B: one workgroup per CU
+constexpr int LDS_BYTES = LDS_X1 + LDS_X2 + LDS_M + LDS_S;  // 123,136 B: one workgroup per CU
+// map-free consumer: per (macro-step parity, tail step of the pair) the column-boundary sums
+// of the 4 consumer waves, slots 1 .. 4 (0 and 5: the image's zero borders), 2 sides x 4
+// lane groups
+constexpr int NBND = 6 * 2 * 4;
+constexpr int LDS_BYTES_NM = LDS_X1 + LDS_X2 + 4 * NBND * 4;  // 69,376 B
 }  // namespace d3
 
 // first Conv2DTranspose input pixel ps (x = ps - 1), 16-byte group g of its 8: group g sits
@@ -694,14 +699,27 @@ struct D3Clock {
 #define D3_BARRIER() lds_barrier()
 #endif
 
-template <typename T>
+// MAP = false (the default since round 4): the consumer never writes the 16-channel map. Its
+// Conv2D(1) runs as MFMAs on the Conv2DTranspose's own packed accumulators (the B operand of
+// v_mfma_f32_16x16x32 is exactly what the ReLU-packed 16x16 accumulators of one phase pair hold:
+// 8 channels-by-column values of one position per lane), into three rolling accumulators of
+// output-row PAIRS; only the column shifts of the 5 x 5 window cross lanes (DPP row shifts) and,
+// at the 16-position block edges, waves (8 floats through LDS per tail step). MAP = true keeps
+// the round-3 consumer (map ring + D scratch + diagonal sums; V_D3_MAP) for A/B.
+// LEAD: the producer's input-ring refills in flight beyond the one a macro step waits for
+// (step g needs position g + 3 after its barrier and waits for that DMA only, issued LEAD steps
+// earlier; round 3: LEAD 0, the DMA issued by the same step).
+template <typename T, bool MAP, int LEAD>
 __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
+  static_assert(LEAD >= 0 && LEAD <= 4, "8-row input ring");
   using namespace d3;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  constexpr int LB = MAP ? LDS_BYTES : LDS_BYTES_NM;
   T* const x1r = reinterpret_cast<T*>(lds_raw);
   T* const x2r = reinterpret_cast<T*>(lds_raw + LDS_X1);
   T* const mr = reinterpret_cast<T*>(lds_raw + LDS_X1 + LDS_X2);
   float* const sc = reinterpret_cast<float*>(lds_raw + LDS_X1 + LDS_X2 + LDS_M);
+  float* const bnd = reinterpret_cast<float*>(lds_raw + LDS_X1 + LDS_X2);  // !MAP
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -726,7 +744,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
   const int S = nimg * SPI + 2;  // + 2: the consumer's last tail steps
   {
     uint4* z = reinterpret_cast<uint4*>(lds_raw);
-    for (int e = tid; e < LDS_BYTES / 16; e += 512) z[e] = uint4{0u, 0u, 0u, 0u};
+    for (int e = tid; e < LB / 16; e += 512) z[e] = uint4{0u, 0u, 0u, 0u};
   }
   __syncthreads();
 
@@ -760,15 +778,17 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
     const int dps = 1 + 8 * wv + (lane >> 3);
     const int dsrc = (dps - 1) * CI1 + 8 * ((lane & 7) ^ (dps & 7));
     unsigned char* const ddst = lds_raw + (1 + 8 * wv) * X1ST * 2;
-    auto stage = [&](int p) {
-      unsigned char* dst = ddst + (p & 3) * X1ROW * 2;
+    auto stage = [&](int p) -> bool {  // whether this wave issued an LDS-DMA
+      unsigned char* dst = ddst + (p & (NX1 - 1)) * X1ROW * 2;
       const int il = p / SPI, row = p - il * SPI - 1;
       if (il < nimg && row >= 0 && row < H1) {
         const long long n = (long long)blockIdx.x + (long long)il * G;
         lds_dma16(X + ((n * H1 + row) * W1) * CI1 + dsrc, dst);
-      } else {  // between / after the images: the zero padding rows
-        *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
+        return true;
       }
+      // between / after the images: the zero padding rows
+      *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
+      return false;
     };
     // this lane's B-fragment offsets (pixel 16 wx + m + dx, group kg) in an input ring row,
     // and its tail-input write offsets (pixel 2 (16 wx + m) + px, channels 16 nb + 4 kg ..)
@@ -781,14 +801,18 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       x2w[px] = x2_off(ps, ch >> 3) + (ch & 7);
     }
 #pragma unroll
-    for (int p = 0; p < 3; ++p) stage(p);
+    for (int p = 0; p < 3 + LEAD; ++p) stage(p);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     D3_BARRIER();  // (macro step -1: the consumers' matching barrier is below)
+    int vmn = 0;       // this wave's LDS-DMAs issued in the loop (its only vector-memory ops)
+    int mk[LEAD + 1];  // vmn right after the DMA of position g + 3 + i (-1: none in flight)
+#pragma unroll
+    for (int i = 0; i <= LEAD; ++i) mk[i] = -1;
 
     auto pstep = [&](auto ic, const int g) {
-      constexpr int I = decltype(ic)::value;  // g & 3
-      stage(g + 3);  // lands while this row's MFMAs run
-      T* const r0 = x2r + ((2 * I) & 7) * X2ROW;
+      constexpr int I = decltype(ic)::value;  // g & 7 (the input ring's period)
+      mk[LEAD] = stage(g + 3 + LEAD) ? ++vmn : -1;
+      T* const r0 = x2r + ((2 * I) & 7) * X2ROW;  // (tail ring: period 4 macro steps)
       T* const r1 = x2r + ((2 * I + 1) & 7) * X2ROW;
       const int il = g / SPI, s = g - il * SPI;
       if (il < nimg && s < H1) {
@@ -796,7 +820,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
         int u0[4] = {0, 8, 20, 32};
 #pragma unroll
         for (int dy = -1; dy <= 1; ++dy) {
-          const T* src = x1r + ((I + 1 + dy + 4) & 3) * X1ROW;  // position g + 1 + dy
+          const T* src = x1r + ((I + 1 + dy + NX1) & (NX1 - 1)) * X1ROW;  // position g + 1 + dy
 #pragma unroll
           for (int dx = -1; dx <= 1; ++dx) {
             // group kg + 4 (the second K-step) sits at the first's offset ^ 32 elements:
@@ -821,19 +845,181 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
         for (int ph = 0; ph < 4; ++ph)
           *reinterpret_cast<uint2*>(((ph >> 1) ? r1 : r0) + x2w[ph & 1]) = uint2{0u, 0u};
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // input position g + 3 has landed
+      if (mk[0] >= 0) wait_vmcnt(vmn - mk[0]);  // input position g + 3 has landed
       D3_BARRIER();
+#pragma unroll
+      for (int i = 0; i < LEAD; ++i) mk[i] = mk[i + 1];
     };
     int g = 0;
-    for (; g + 4 <= S; g += 4) {
+    for (; g + 8 <= S; g += 8) {
       pstep(IC<0>{}, g);
       pstep(IC<1>{}, g + 1);
       pstep(IC<2>{}, g + 2);
       pstep(IC<3>{}, g + 3);
+      pstep(IC<4>{}, g + 4);
+      pstep(IC<5>{}, g + 5);
+      pstep(IC<6>{}, g + 6);
+      pstep(IC<7>{}, g + 7);
     }
     if (g < S) pstep(IC<0>{}, g);
     if (g + 1 < S) pstep(IC<1>{}, g + 1);
     if (g + 2 < S) pstep(IC<2>{}, g + 2);
+    if (g + 3 < S) pstep(IC<3>{}, g + 3);
+    if (g + 4 < S) pstep(IC<4>{}, g + 4);
+    if (g + 5 < S) pstep(IC<5>{}, g + 5);
+    if (g + 6 < S) pstep(IC<6>{}, g + 6);
+#ifdef SPECENH_D3_STATS
+    clk.flush(wv);
+#endif
+  } else if constexpr (!MAP) {
+    // ======================= map-free consumer, tail steps t = 2g - 3, 2g - 2 per macro step g
+    // Tail step t (per-image tl) turns tail-input rows t - 1 .. t + 1 into the Conv2DTranspose
+    // accumulators of map rows 2tl, 2tl + 1 (16 positions x 16 channels x 4 phases per wave),
+    // packs them after bias + ReLU exactly as the map would hold them, and adds their Conv2D(1)
+    // contributions to output-row pairs tl - 1, tl, tl + 1 (P0, P1, P2). Pair tl - 1 is then
+    // complete (map rows 2tl - 4 .. 2tl + 1) and is emitted after the macro step's barrier.
+    const int w = wv - 4;
+    uint4 wt[25];  // Conv2DTranspose taps (A: co = m, ci = 8 kg ..), phase-major, (dy, dx) order
+    {
+      const T* __restrict__ Wt = reinterpret_cast<const T*>(a.wt);
+      int u = 0;
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+          for (int dx = -1; dx <= 1; ++dx) {
+            const int ky = ky_of(ph >> 1, dy), kx = ky_of(ph & 1, dx);
+            if (ky < 0 || ky >= KT || kx < 0 || kx >= KT) continue;
+            wt[u++] = *reinterpret_cast<const uint4*>(Wt + ((m * KT + ky) * KT + kx) * CI + 8 * kg);
+          }
+    }
+    const f32x4 bias = f32x4{a.bt[4 * kg], a.bt[4 * kg + 1], a.bt[4 * kg + 2], a.bt[4 * kg + 3]};
+    // Conv2D(1) A fragments wd[d][py] for pair tl + d - 1 and map row 2tl + py. Result row
+    // i = 4 gO + j (gO = i >> 2: output row r = gO >> 1 of the pair, column parity o = gO & 1)
+    // holds output column 2 m' + ox of position m', ox = o + {0, 2, -2}[j] (j = 3 unused), so
+    // lane group g of the result owns output (r, o) = (g >> 1, g & 1) of its position and
+    // receives the ox = o + 2 / o - 2 parts from positions m - 1 / m + 1. K = 8 kA + 4 px + c:
+    // channel 4 kA + c of map column 2 m' + px (the packed B layout below).
+    // ky = py + 2 - 2 (d - 1) - r, kx = px + 2 - ox.
+    uint4 wd[3][2];
+    {
+      const T* __restrict__ Wo = reinterpret_cast<const T*>(a.wo);
+      const int i = lane & 15, kA = lane >> 4;
+      const int gO = i >> 2, j = i & 3, r = gO >> 1, o = gO & 1;
+      const int ox = o + (j == 1 ? 2 : (j == 2 ? -2 : 0));
+#pragma unroll
+      for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int py = 0; py < 2; ++py) {
+          const int ky = py + 2 - 2 * (d - 1) - r;
+          uint32_t e[4];
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            uint32_t v2 = 0;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+              const int el = 2 * h + s2, px = el >> 2, c = el & 3, kx = px + 2 - ox;
+              unsigned short bits = 0;
+              if (j < 3 && ky >= 0 && ky < KO && kx >= 0 && kx < KO)
+                bits = __builtin_bit_cast(unsigned short, Wo[(ky * KO + kx) * CO + 4 * kA + c]);
+              v2 |= (uint32_t)bits << (16 * s2);
+            }
+            e[h] = v2;
+          }
+          wd[d][py] = uint4{e[0], e[1], e[2], e[3]};
+        }
+    }
+    const float bo = a.bo[0];
+    int xo[3];  // element offset of pixel 16 w + m + dx (stored + 1), group kg, in a ring row
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) xo[dx + 1] = x2_off(16 * w + m + dx + 1, kg);
+    // this lane's output pixel of a pair: row kg >> 1, column 32 w + 2 m + (kg & 1); block-edge
+    // exchange: lane m = 15 publishes E[1] (column 2 m + o + 2: the next wave's m = 0) in slot
+    // w + 1 side 0, lane m = 0 publishes E[2] in side 1; m = 0 / 15 read the neighbours' slots,
+    // every other lane a never-written zero word
+    const int orow = kg >> 1, ocol = 32 * w + 2 * m + (kg & 1);
+    const int bwi = ((w + 1) * 2 + (m == 0 ? 1 : 0)) * 4 + kg;
+    const int bri = m == 0 ? (w * 2 + 0) * 4 + kg : (m == 15 ? ((w + 2) * 2 + 1) * 4 + kg : 0);
+    D3_BARRIER();  // macro step -1
+
+    f32x4 P0 = f32x4{0.f, 0.f, 0.f, 0.f}, P1 = P0, P2 = P0;
+    int il = -1, tl = TPI - 3;  // tail step t = -3
+    auto tstep = [&](auto ic, float* bb, f32x4& E, int& eil, int& etl) -> bool {
+      constexpr int T8 = decltype(ic)::value;  // t & 7: the tail-input ring slot of row t
+      eil = il;
+      etl = tl;
+      if (++tl == TPI) { tl = 0; ++il; }
+      if (eil < 0 || eil >= nimg) return false;
+      f32x4 acc[4] = {bias, bias, bias, bias};
+      int u0[4] = {0, 4, 10, 16};  // first tap register of each phase (4 / 6 / 6 / 9 taps)
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          const uint4 b = *reinterpret_cast<const uint4*>(x2r + ((T8 + dy + 8) & 7) * X2ROW + xo[dx + 1]);
+#pragma unroll
+          for (int ph = 0; ph < 4; ++ph) {
+            const int ky = ky_of(ph >> 1, dy), kx = ky_of(ph & 1, dx);
+            if (ky < 0 || ky >= KT || kx < 0 || kx >= KT) continue;
+            acc[ph] = mfma<T>(wt[u0[ph]++], b, acc[ph]);
+          }
+        }
+      // map rows 2tl, 2tl + 1 as the Conv2D(1)'s B operands (zero below the image)
+      const uint32_t keep = etl < H2 ? 0xffffffffu : 0u;
+      uint4 bv[2];
+#pragma unroll
+      for (int py = 0; py < 2; ++py) {
+        const uint2 lo = relu_pack<T>(acc[2 * py]), hi = relu_pack<T>(acc[2 * py + 1]);
+        bv[py] = uint4{lo.x & keep, lo.y & keep, hi.x & keep, hi.y & keep};
+      }
+#pragma unroll
+      for (int py = 0; py < 2; ++py) {
+        P0 = mfma<T>(wd[0][py], bv[py], P0);
+        P1 = mfma<T>(wd[1][py], bv[py], P1);
+        P2 = mfma<T>(wd[2][py], bv[py], P2);
+      }
+      E = P0;
+      P0 = P1;
+      P1 = P2;
+      P2 = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (etl < 1 || etl > H2) return false;  // pair tl - 1 is not an output row pair
+      if (m == 0 || m == 15) bb[bwi] = m == 0 ? E[2] : E[1];
+      return true;
+    };
+    auto emit = [&](const f32x4& E, const float* bb, int eil, int etl) {
+      float s = bo + E[0];
+      s += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                         0, __builtin_bit_cast(int, E[1]), 0x111, 0xf, 0xf, false));
+      s += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                         0, __builtin_bit_cast(int, E[2]), 0x101, 0xf, 0xf, false));
+      s += bb[bri];
+      const long long n = (long long)blockIdx.x + (long long)eil * G;
+      a.out[(n * H3 + 2 * (etl - 1) + orow) * rows::MW + ocol] =
+          __builtin_amdgcn_rcpf(1.f + __expf(-s));
+    };
+    auto cstep = [&](auto ic) {
+      constexpr int I = decltype(ic)::value;  // g & 3
+      float* const b0 = bnd + ((I & 1) * 2) * NBND;
+      float* const b1 = b0 + NBND;
+      f32x4 E0, E1;
+      int il0, tl0, il1, tl1;
+      const bool e0 = tstep(IC<(2 * I + 5) & 7>{}, b0, E0, il0, tl0);  // (2g - 3) & 7
+      const bool e1 = tstep(IC<(2 * I + 6) & 7>{}, b1, E1, il1, tl1);
+      D3_BARRIER();
+      if (e0) emit(E0, b0, il0, tl0);
+      if (e1) emit(E1, b1, il1, tl1);
+    };
+    int g = 0;
+    for (; g + 4 <= S; g += 4) {
+      cstep(IC<0>{});
+      cstep(IC<1>{});
+      cstep(IC<2>{});
+      cstep(IC<3>{});
+    }
+    if (g < S) cstep(IC<0>{});
+    if (g + 1 < S) cstep(IC<1>{});
+    if (g + 2 < S) cstep(IC<2>{});
 #ifdef SPECENH_D3_STATS
     clk.flush(wv);
 #endif
@@ -999,19 +1185,39 @@ extern "C" int specenh_decoder3(int dtype, const void* x, int N, int H, int W, i
   hipStream_t st = (hipStream_t)stream;
   // (the kernels are named here, outside the lambda, so the device compilation instantiates
   // them)
-  const void* const k16 = reinterpret_cast<const void*>(&decoder3_kernel<_Float16>);
-  const void* const kb16 = reinterpret_cast<const void*>(&decoder3_kernel<__bf16>);
+  const void* const k16 = reinterpret_cast<const void*>(&decoder3_kernel<_Float16, true, 0>);
+  const void* const kb16 = reinterpret_cast<const void*>(&decoder3_kernel<__bf16, true, 0>);
   static std::once_flag attr_once;
   std::call_once(attr_once, [k16, kb16] {
     (void)hipFuncSetAttribute(k16, hipFuncAttributeMaxDynamicSharedMemorySize, d3::LDS_BYTES);
     (void)hipFuncSetAttribute(kb16, hipFuncAttributeMaxDynamicSharedMemorySize, d3::LDS_BYTES);
+    const void* const nm[4] = {reinterpret_cast<const void*>(&decoder3_kernel<_Float16, false, 3>),
+                               reinterpret_cast<const void*>(&decoder3_kernel<__bf16, false, 3>),
+                               reinterpret_cast<const void*>(&decoder3_kernel<_Float16, false, 0>),
+                               reinterpret_cast<const void*>(&decoder3_kernel<__bf16, false, 0>)};
+    for (const void* k : nm)
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, d3::LDS_BYTES_NM);
   });
-  // persistent: one workgroup per CU (105 KB of LDS, 256 VGPRs at 2 waves per SIMD)
+  // persistent: one workgroup per CU (256 VGPRs at 2 waves per SIMD; 68 KB of LDS, 120 KB with
+  // the map ring)
   const unsigned grid = (unsigned)std::min<long long>(N, device_cus());
-  if (dtype == SPECENH_DTYPE_F16)
-    SPECENH_LAUNCH(decoder3_kernel<_Float16>, dim3(grid), dim3(512), d3::LDS_BYTES, st, a);
-  else
-    SPECENH_LAUNCH(decoder3_kernel<__bf16>, dim3(grid), dim3(512), d3::LDS_BYTES, st, a);
+  const bool map = variant(V_D3_MAP) != 0, short_lead = variant(V_ROWS_SHORT_LEAD) != 0;
+  const dim3 gd(grid), bd(512);
+  if (dtype == SPECENH_DTYPE_F16) {
+    if (map)
+      SPECENH_LAUNCH((decoder3_kernel<_Float16, true, 0>), gd, bd, d3::LDS_BYTES, st, a);
+    else if (short_lead)
+      SPECENH_LAUNCH((decoder3_kernel<_Float16, false, 0>), gd, bd, d3::LDS_BYTES_NM, st, a);
+    else
+      SPECENH_LAUNCH((decoder3_kernel<_Float16, false, 3>), gd, bd, d3::LDS_BYTES_NM, st, a);
+  } else {
+    if (map)
+      SPECENH_LAUNCH((decoder3_kernel<__bf16, true, 0>), gd, bd, d3::LDS_BYTES, st, a);
+    else if (short_lead)
+      SPECENH_LAUNCH((decoder3_kernel<__bf16, false, 0>), gd, bd, d3::LDS_BYTES_NM, st, a);
+    else
+      SPECENH_LAUNCH((decoder3_kernel<__bf16, false, 3>), gd, bd, d3::LDS_BYTES_NM, st, a);
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("decoder3: ") + hipGetErrorString(e));
   return SPECENH_OK;

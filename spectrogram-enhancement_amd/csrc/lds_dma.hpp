@@ -25,4 +25,34 @@ __device__ __forceinline__ void lds_dma16(const void* src, void* dst) {
                : "m0");
 }
 
+// one 8-byte global store per lane as exactly ONE vector-memory instruction, so a kernel that
+// keeps a ledger of its own vector-memory ops (vmcnt counts stores as well as loads on gfx9)
+// knows how many were issued after a given DMA
+__device__ __forceinline__ void gstore8(void* dst, uint2 v) {
+  asm volatile("global_store_dwordx2 %0, %1, off" : : "v"(dst), "v"(v) : "memory");
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n: wait until at most n of this wave's
+// vector-memory ops are outstanding (n > 15 waits as for 15: stricter, never laxer)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+  }
+}
+
 }  // namespace specenh

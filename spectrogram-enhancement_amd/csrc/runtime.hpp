@@ -32,6 +32,8 @@ enum Variant : int {
   V_CONV1_NO_ROWS,    // C = 1 pooled conv: conv_c1_mfma tiles instead of the row sweep
   V_ENCODER_UNFUSED,  // engine (Python): no two-layer encoder launch (specenh_encoder2)
   V_STFT_NO_HOLD,     // per-shot normalised STFT: raw rows + re-read sweep, not held tiles
+  V_D3_MAP,           // decoder3: Conv2D(1) from a 16-channel map ring in LDS (round-3 consumer)
+  V_ROWS_SHORT_LEAD,  // convT rows / decoder3 producer: the round-3 ring refill lead (1 / 0 steps, not 3)
   V_COUNT
 };
 

@@ -137,6 +137,27 @@ def test_convt_rows_matches_tile_kernel(gpu_device, kernel_variant, CO, W):
     assert float(d.max()) <= 2.0 ** -10 * float(b.float().abs().max())
 
 
+@pytest.mark.parametrize("CO,W", [(64, 16), (32, 32)])
+@pytest.mark.parametrize("N,H", [(1, 5), (700, 16)])
+def test_convt_rows_lead_bitwise(gpu_device, kernel_variant, CO, W, N, H):
+    """Three ring refills in flight (default) vs the round-3 one-step lead: the waits differ,
+    the arithmetic does not (several images per persistent workgroup at N = 700)."""
+    rng = np.random.default_rng(5 + CO + N)
+    x = torch.tensor(rng.uniform(0, 1, (N, H, W, 64)), dtype=torch.float16, device=gpu_device)
+    w = torch.tensor(rng.standard_normal((CO, 5, 5, 64)) * 0.03, dtype=torch.float16,
+                     device=gpu_device)
+    bias = torch.tensor(rng.standard_normal(CO) * 0.1, dtype=torch.float32, device=gpu_device)
+    a = torch.full((N, 2 * H, 2 * W, CO), float("nan"), dtype=torch.float16, device=gpu_device)
+    b = torch.full_like(a, float("nan"))
+    _convt_run(x, w, bias, CO, a)
+    kernel_variant("ROWS_SHORT_LEAD", 1)
+    _convt_run(x, w, bias, CO, b)
+    torch.cuda.synchronize()
+    assert "convt_rows_kernel" in _lib.last_kernel_name()
+    assert bool(torch.isfinite(a).all())
+    assert torch.equal(a, b)
+
+
 # ---------------------------------------------------------------- C = 1 row sweep
 # (csrc/conv_rows.hip conv1_rows_pool_kernel; VAE/manual_scan_3layers.py:187-188)
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])

@@ -116,13 +116,16 @@ def _dec3_model(dtype, hw, seed):
 @pytest.mark.parametrize("dtype", ["float16", "mixed_bfloat16"])
 @pytest.mark.parametrize("hw,n", [((32, 32), 3), ((8, 32), 2), ((5, 32), 1), ((64, 32), 2),
                                   ((1, 32), 2), ((32, 32), 600), ((3, 32), 1000)])
-def test_decoder3_matches_unfused_and_oracle(gpu_device, dtype, hw, n, kernel_variant):
+@pytest.mark.parametrize("d3map", [0, 1])
+def test_decoder3_matches_unfused_and_oracle(gpu_device, dtype, hw, n, d3map, kernel_variant):
     """decoder3_kernel (Conv2DTranspose(32) + Conv2DTranspose(16) + Conv2D(1), both maps in
     LDS) vs the same engine with the decoder unfused (DECODER_UNFUSED=1: convT2 through
     conv_patch + the row-sweep tail) and the fp64 oracle; output NaN-poisoned first. The
     32-channel map is rounded to T in both paths after its ReLU, so they differ only by
     accumulation order (and the fp16 roundings that follow from it). n > 256: several images
-    per persistent workgroup (the row stream's image-to-image hand-over)."""
+    per persistent workgroup (the row stream's image-to-image hand-over). d3map = 1: the
+    round-3 consumer (16-channel map ring in LDS) instead of the map-free Conv2D(1)."""
+    kernel_variant("D3_MAP", d3map)
     eng, ops_, ws = _dec3_model(dtype, hw, seed=hw[0] * 13 + n)
     assert eng.dec3
     x = np.random.default_rng(n + 5).uniform(0, 1, (n,) + hw + (1,)).astype(np.float32)
@@ -151,3 +154,21 @@ def test_decoder3_matches_unfused_and_oracle(gpu_device, dtype, hw, n, kernel_va
         ref = ora.forward(spec, params, torch.tensor(x[idx], dtype=torch.float64)).numpy()
     err = checks.out_rel(fused.cpu().numpy()[idx], ref)
     assert err <= checks.TOL[dtype]["out_rel"], err
+
+
+@pytest.mark.parametrize("hw,n", [((32, 32), 3), ((32, 32), 600), ((3, 32), 1000)])
+def test_decoder3_lead_bitwise(gpu_device, hw, n, kernel_variant):
+    """decoder3's producer with three input-ring refills in flight (default) vs the round-3
+    wait for the refill issued in the same macro step: only the waits differ."""
+    from specenh import _lib
+    eng, ops_, ws = _dec3_model("float16", hw, seed=n + 3)
+    x = np.random.default_rng(n + 9).uniform(0, 1, (n,) + hw + (1,)).astype(np.float32)
+    xd = eng.to_compute(torch.from_numpy(x))
+    a = eng.forward(xd).clone()
+    kernel_variant("ROWS_SHORT_LEAD", 1)
+    eng._buffers(n, False)["h"][len(ops_)].fill_(float("nan"))
+    b = eng.forward(xd).clone()
+    torch.cuda.synchronize()
+    assert "decoder3_kernel" in _lib.last_kernel_name()
+    assert not torch.isnan(a).any()
+    assert torch.equal(a, b)

@@ -1,6 +1,7 @@
 """The C5 decoder's last three layers at the bench's launch shape (2048 x 32 x 32 x 64 fp16):
-decoder3_kernel (one launch) vs the unfused engine path (convT2 conv_patch launch + the
-row-sweep tail), interleaved rounds in one process, HIP events.  python tools/dec3_bench.py [N]"""
+decoder3_kernel map-free (default) vs its round-3 map-ring consumer (D3_MAP=1) vs the unfused
+engine path (convT2 conv_patch launch + the row-sweep tail), interleaved rounds in one
+process, HIP events.  python tools/dec3_bench.py [N]"""
 import os
 import sys
 
@@ -25,23 +26,31 @@ def main():
         e.set_keras_weights(w)
         engs[v] = e
     _lib.set_variant("DECODER_UNFUSED", 0)
+    arms = {"mapfree": (engs[0], 0), "map": (engs[0], 1), "unfused": (engs[1], 0)}
     x = (torch.rand(N, 32, 32, 64, device=dev) * 0.5).half()
-    res = {0: [], 1: []}
+    res = {k: [] for k in arms}
+    outs = {}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for rnd in range(6):
-        for v in (0, 1):
-            engs[v].forward(x)
+        for name, (eng, mp) in arms.items():
+            _lib.set_variant("D3_MAP", mp)
+            outs[name] = eng.forward(x).clone()
             e0.record()
             for _ in range(10):
-                engs[v].forward(x)
+                eng.forward(x)
             e1.record()
             e1.synchronize()
             if rnd:
-                res[v].append(e0.elapsed_time(e1) / 10)
-    d = (engs[0].forward(x) - engs[1].forward(x)).abs().max().item()
-    for v, name in ((0, "decoder3"), (1, "unfused")):
-        print(f"{name:9s} N={N}: median {np.median(res[v]):.4f} ms  min {min(res[v]):.4f}", flush=True)
-    print(f"max |fused - unfused| = {d:.2e}")
+                res[name].append(e0.elapsed_time(e1) / 10)
+    _lib.set_variant("D3_MAP", 0)
+    flop = 2.0 * N * (32 * 32 * 25 * 64 * 32 + 64 * 64 * 25 * 32 * 16 + 128 * 128 * 25 * 16)
+    for name in arms:
+        med = float(np.median(res[name]))
+        print(f"{name:8s} N={N}: median {med:.4f} ms  min {min(res[name]):.4f}  "
+              f"({flop / med / 1e9:.0f} TF/s = {flop / med / 1e9 / 2500:.3f} of 2.5 PF)", flush=True)
+    for name in ("map", "unfused"):
+        d = (outs["mapfree"] - outs[name]).abs().max().item()
+        print(f"max |mapfree - {name}| = {d:.2e}")
 
 
 if __name__ == "__main__":

@@ -733,8 +733,10 @@ struct E2Args {
 
 constexpr int E2R1 = 32;  // conv1 input ring rows (positions)
 
-template <typename T>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+// WPE: waves per SIMD the register budget is cut for (4: two workgroups per CU, 128 VGPRs;
+// 2: one workgroup, 256 VGPRs)
+template <typename T, int WPE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE)))
 void enc2_rows_kernel(E2Args a) {
   using C = RC<16, 32, 64>;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -751,8 +753,14 @@ void enc2_rows_kernel(E2Args a) {
   const int nimg = ((int)a.N - (int)blockIdx.x + G - 1) / G;
   const int S = nimg * SPI + 1;
 
-  for (int e = tid; e < (C::LDS + E2R1 * C1ROW * 4) / 16; e += 512)
+  for (int e = tid; e < (C::LDS + (E2R1 + 1) * C1ROW * 4) / 16; e += 512)
     reinterpret_cast<uint4*>(lds)[e] = uint4{0u, 0u, 0u, 0u};
+  // both layers' biases in LDS (read where used: as resident f32x4s they cost the 8 VGPRs
+  // that made the 4-waves-per-SIMD build spill)
+  float* const btab = reinterpret_cast<float*>(lds + C::LDS + (E2R1 + 1) * C1ROW * 4);
+  if (tid < 16) btab[tid] = a.b1[tid];
+  else if (tid < 48) btab[tid] = a.b2[tid - 16];
+  auto bias2_ld = [&]() { return *reinterpret_cast<const f32x4*>(btab + 16 + 16 * nb + 4 * kg); };
 
   // ---- conv2: resident weight fragments (as conv_rows_pool_kernel, CIN = 16) ----
   uint4 wf[13];
@@ -771,8 +779,7 @@ void enc2_rows_kernel(E2Args a) {
     wf[11] = tap(2 + hi, 4);
     wf[12] = hi ? uint4{0u, 0u, 0u, 0u} : tap(4, 4);
   }
-  const f32x4 bias = f32x4{a.b2[16 * nb + 4 * kg], a.b2[16 * nb + 4 * kg + 1],
-                           a.b2[16 * nb + 4 * kg + 2], a.b2[16 * nb + 4 * kg + 3]};
+
   const int boff = (x0 + m + (kg >> 1)) * 32 + 16 * (kg & 1);
   const int fo = (x0 + m + 4) * 32 + 16 * (kg & 1);
   const int foff = fo + (kg >> 1) * C::ROWB, foffw = fo - (kg >> 1) * 7 * C::ROWB;
@@ -797,16 +804,15 @@ void enc2_rows_kernel(E2Args a) {
     v0 = uint4{q0[0], q0[1], q0[2], q0[3]};
     v1 = uint4{q1[0], q1[1], q1[2], q1[3]};
   }
-  const f32x4 bias1 = f32x4{a.b1[4 * kg], a.b1[4 * kg + 1], a.b1[4 * kg + 2], a.b1[4 * kg + 3]};
+
   const int w1x = wv & 3, jr = wv >> 2;  // conv1 pixel block, conv2 input row of the pair
   const int wbase = 16 * w1x + m + 3;
 
-  // image-row stream: position pp = il (H1 + 4) + y + 2; waves 0-3 move positions pp + wv
+  // image-row stream: position pp = il (H1 + 4) + y + 2; waves 0-3 move positions pp + wv.
+  // The loop keeps (image, row) of its positions and steps as scalar counters advanced per
+  // step (a run-time division per use had cost ~25 SALU + a VALU reciprocal each).
   const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
-  auto stage1 = [&](int pp) -> int {
-    if (wv >= 4) return 0;
-    const int pos = pp + wv;
-    const int il = pos / PPI, y = pos - il * PPI - 2;
+  auto stage1_at = [&](int pos, int il, int y) -> int {  // position pos = il PPI + y + 2
     uint32_t* dst = ring1 + (pos & (E2R1 - 1)) * C1ROW + 4;
     if (il < nimg && y >= 0 && y < H1) {
       const long long n = (long long)blockIdx.x + (long long)il * G;
@@ -815,6 +821,12 @@ void enc2_rows_kernel(E2Args a) {
     }
     if (lane < 16) *reinterpret_cast<uint4*>(dst + 4 * lane) = uint4{0u, 0u, 0u, 0u};
     return 0;
+  };
+  auto stage1 = [&](int pp) -> int {  // (prologue)
+    if (wv >= 4) return 0;
+    const int pos = pp + wv;
+    const int il = pos / PPI;
+    return stage1_at(pos, il, pos - il * PPI - 2);
   };
   auto shift1 = [&](int pp) {  // copy 1 of positions pp .. pp + 3
     if (tid < 4 * C1CW) {
@@ -827,23 +839,29 @@ void enc2_rows_kernel(E2Args a) {
     const uint32_t* row = ring1 + ((pos + kg) & (E2R1 - 1)) * C1ROW + cb * C1CW + wbase;
     return uint4{row[0], row[1], row[2], row[3]};
   };
+  // B' (kernel row 4 only): lane group 0 reads row pos, groups 1-3 the zero row past the ring
+  // (an address select instead of zeroing 4 data registers)
+  const uint32_t* const zrow = ring1 + E2R1 * C1ROW + wbase;
+  auto bfrag4 = [&](int pos, int cb) -> uint4 {
+    const uint32_t* row = kg == 0 ? ring1 + (pos & (E2R1 - 1)) * C1ROW + cb * C1CW + wbase : zrow;
+    return uint4{row[0], row[1], row[2], row[3]};
+  };
   // conv2 input row 2 q2 + jr of conv2 step g2 (image g2 / SPI) into its ring slot: pooled
   // pixels 16 w1x + m, channels 4 kg .. 4 kg + 3 (zero rows outside the image)
-  auto produce = [&](int g2) {
-    const int il = g2 / SPI, q2 = g2 - il * SPI;
+  auto produce = [&](int g2, int il, int q2) {  // g2 = il SPI + q2
     const int r = 2 * q2 + jr;
     // branch-free (the step stays one basic block, so the scheduler can interleave these
     // MFMAs with conv2's): rows past the image are computed from whatever finite rows the
     // ring holds and replaced by zeros
     const int pb = 4 * g2 + 2 * jr;  // position of image row 2r - 2
     float v[4] = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 bias1 = *reinterpret_cast<const f32x4*>(btab + 4 * kg);
 #pragma unroll
     for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         const uint4 b = bfrag(pb + dy, cb);
-        uint4 b4 = bfrag(pb + dy + 4, cb);
-        if (kg != 0) b4 = uint4{0u, 0u, 0u, 0u};
+        const uint4 b4 = bfrag4(pb + dy + 4, cb);
         f32x4 acc1 = mfma<T>(v0, b, bias1);
         acc1 = mfma<T>(v1, b4, acc1);
 #pragma unroll
@@ -861,28 +879,38 @@ void enc2_rows_kernel(E2Args a) {
   lds_barrier();
   for (int pp = 0; pp < 16; pp += 4) shift1(pp);
   lds_barrier();
-  produce(0);
-  produce(1);
+  produce(0, 0, 0);
+  produce(1, 1 / SPI, 1 % SPI);
   lds_barrier();
 
   f32x4 acc[6];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) acc[i] = bias;
+  for (int i = 0; i < 6; ++i) acc[i] = bias2_ld();
   T* __restrict__ O = reinterpret_cast<T*>(a.out);
   const int PW = 32, PHh = H / 2;
   int c_1 = 0, c_2 = 0;  // this wave's vector-memory ops (store + LDS-DMA) of steps s - 1, s - 2
+  // scalar counters: steps s - 2 (pool), s (conv2), s + 2 (conv1) as (image, step in image),
+  // and this wave's stage-1 position 4 s + 32 + wv as (image, row); floor division once here
+  auto fdiv = [](int x, int d) { return x >= 0 ? x / d : -((-x + d - 1) / d); };
+  int ilA = fdiv(-2, SPI), qA = -2 - ilA * SPI;
+  int qC = 0;
+  int ilB = 2 / SPI, qB = 2 - ilB * SPI;
+  int ilD = (32 + wv) / PPI, rD = 32 + wv - ilD * PPI;  // row y = rD - 2
+  auto adv = [](int& il, int& q, int by, int per) {
+    q += by;
+    if (q >= per) { q -= per; ++il; }
+  };
 
   auto step = [&](auto ic, const int s) {
     constexpr int I = decltype(ic)::value;
     auto slot = [](int d) { return (2 * I + d + 12) % 6; };
     int ns = 0;  // stores issued by this wave in this step
     {  // conv2 pair s - 2: pool, store, reset
-      const int p = s - 2;
       f32x4& r0 = acc[slot(-4)];
       f32x4& r1 = acc[slot(-3)];
-      if (p >= 0) {
-        const int il = p / SPI, q = p - il * SPI;
-        if (il < nimg && q < PHh) {
+      {
+        const int il = ilA, q = qA;
+        if (il >= 0 && il < nimg && q < PHh) {
           ns = 1;
           float v[4];
 #pragma unroll
@@ -894,6 +922,7 @@ void enc2_rows_kernel(E2Args a) {
           }
         }
       }
+      const f32x4 bias = bias2_ld();
       r0 = bias;
       r1 = bias;
     }
@@ -901,12 +930,12 @@ void enc2_rows_kernel(E2Args a) {
     // last readers were this step's predecessors), copy 1 of positions 4s + 16 .. 4s + 19
     // (landed: DMA of step s - 4, waited at the end of step s - 1), conv2 input rows of
     // step s + 2 (positions 4s + 8 .. 4s + 15)
-    const int nd = stage1(4 * s + 32);
+    const int nd = wv < 4 ? stage1_at(4 * s + 32 + wv, ilD, rD - 2) : 0;
     shift1(4 * s + 16);
-    produce(s + 2);
+    produce(s + 2, ilB, qB);
     // this step's conv2 rows, unconditionally: past an image they are the zero rows the
     // conv1 stage stored (adding nothing)
-    const int q = s % SPI;
+    const int q = qC;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int rs = (2 * s + j) & 7;
@@ -954,6 +983,10 @@ void enc2_rows_kernel(E2Args a) {
     }
     c_2 = c_1;
     c_1 = ns + nd;
+    adv(ilA, qA, 1, SPI);
+    qC = qC + 1 == SPI ? 0 : qC + 1;
+    adv(ilB, qB, 1, SPI);
+    adv(ilD, rD, 4, PPI);
     lds_barrier();
   };
   int s = 0;
@@ -966,11 +999,11 @@ void enc2_rows_kernel(E2Args a) {
   if (s + 1 < S) step(std::integral_constant<int, 1>{}, s + 1);
 }
 
-constexpr int E2LDS = RC<16, 32, 64>::LDS + E2R1 * C1ROW * 4;
+constexpr int E2LDS = RC<16, 32, 64>::LDS + (E2R1 + 1) * C1ROW * 4 + 48 * 4;
 
-template <typename T>
-hipError_t launch_enc2(const E2Args& a, hipStream_t st) {
-  const void* k = reinterpret_cast<const void*>(&enc2_rows_kernel<T>);
+template <typename T, int WPE>
+hipError_t launch_enc2_wpe(const E2Args& a, hipStream_t st) {
+  const void* k = reinterpret_cast<const void*>(&enc2_rows_kernel<T, WPE>);
   static int per_cu[64] = {};
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -983,8 +1016,13 @@ hipError_t launch_enc2(const E2Args& a, hipStream_t st) {
     per_cu[dev] = std::max(1, pc);
   }
   const long long grid = std::min<long long>(a.N, (long long)per_cu[dev] * device_cus());
-  SPECENH_LAUNCH(enc2_rows_kernel<T>, dim3((unsigned)grid), dim3(512), E2LDS, st, a);
+  SPECENH_LAUNCH((enc2_rows_kernel<T, WPE>), dim3((unsigned)grid), dim3(512), E2LDS, st, a);
   return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_enc2(const E2Args& a, hipStream_t st) {
+  return variant(V_ENC2_WPE2) ? launch_enc2_wpe<T, 2>(a, st) : launch_enc2_wpe<T, 4>(a, st);
 }
 
 }  // namespace
@@ -1086,10 +1124,12 @@ extern "C" int specenh_encoder2(int dtype, const void* x, int N, int H, int W, c
   hipStream_t st = (hipStream_t)stream;
   static std::once_flag once;
   std::call_once(once, [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&enc2_rows_kernel<_Float16>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, E2LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&enc2_rows_kernel<__bf16>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, E2LDS);
+    const void* const ks[4] = {reinterpret_cast<const void*>(&enc2_rows_kernel<_Float16, 4>),
+                               reinterpret_cast<const void*>(&enc2_rows_kernel<__bf16, 4>),
+                               reinterpret_cast<const void*>(&enc2_rows_kernel<_Float16, 2>),
+                               reinterpret_cast<const void*>(&enc2_rows_kernel<__bf16, 2>)};
+    for (const void* k : ks)
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, E2LDS);
   });
   const hipError_t e = dtype == SPECENH_DTYPE_F16 ? launch_enc2<_Float16>(a, st)
                                                   : launch_enc2<__bf16>(a, st);

@@ -201,12 +201,15 @@ def test_conv1_rows_matches_tile_kernel(gpu_device, kernel_variant):
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("N,H", [(1, 128), (7, 4), (5, 12), (300, 128), (3, 132), (1300, 128),
                                  (1100, 8)])
-def test_encoder2_equals_two_launches(gpu_device, dtype, N, H):
+@pytest.mark.parametrize("wpe2", [0, 1])
+def test_encoder2_equals_two_launches(gpu_device, dtype, N, H, wpe2, kernel_variant):
     """The fused launch runs the two row sweeps' arithmetic step for step: bitwise equal to
     conv1_rows_pool_kernel + conv_rows_pool_kernel, and within the 16-bit rounding of a
     float64 composite (the intermediate map rounded to the 16-bit type as stored). N > 512:
     several images per persistent workgroup (the image-to-image hand-over of the row
-    streams; a bubble-step F term once leaked into the next image's row 1)."""
+    streams; a bubble-step F term once leaked into the next image's row 1). wpe2: the
+    one-workgroup-per-CU build (256 VGPRs)."""
+    kernel_variant("ENC2_WPE2", wpe2)
     rng = np.random.default_rng(N + 3 * H)
     x = torch.tensor(rng.uniform(0, 1, (N, H, 128, 1)), dtype=dtype, device=gpu_device)
     w1 = torch.tensor(rng.standard_normal((16, 5, 5, 1)) * 0.3, dtype=dtype, device=gpu_device)

@@ -443,10 +443,10 @@ void convt_rows_kernel(CRArgs a) {
     const int ps = 1 + c / 8, gs = c & 7;
     dsrc = (ps - 1) * 64 + 8 * (gs ^ (ps & 7));
   }
-  auto stage = [&](int p) -> bool {  // stream position p -> ring slot p & 7
+  // stream position p = il SPI + r + 1 -> ring slot p & 7
+  auto stage_at = [&](int p, int il, int r) -> bool {
     if (!dma_wave) return false;
     unsigned char* dst = ring + (p & 7) * C::ROWB + 128 + 1024 * wv;
-    const int il = p / SPI, r = p - il * SPI - 1;
     if (il < nimg && r >= 0) {
       const long long n = (long long)blockIdx.x + (long long)il * G;
       lds_dma16(X + ((n * H + r) * W) * 64 + dsrc, dst);
@@ -454,6 +454,10 @@ void convt_rows_kernel(CRArgs a) {
     }
     *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
     return false;
+  };
+  auto stage = [&](int p) -> bool {  // (prologue)
+    const int il = p / SPI;
+    return stage_at(p, il, p - il * SPI - 1);
   };
   __syncthreads();  // ring zeroed
 #pragma unroll
@@ -477,11 +481,13 @@ void convt_rows_kernel(CRArgs a) {
       vmn += 4;
     }
   };
+  // scalar counters (image, step in image) of step g and of its refill position g + 3 + LEAD
+  int il = 0, s = 0;
+  int ilp = (3 + LEAD) / SPI, sp = 3 + LEAD - ilp * SPI;
   for (int g = 0; g < S; ++g) {
     store_held();
     po = -1;
-    mk[LEAD] = stage(g + 3 + LEAD) ? ++vmn : -1;
-    const int il = g / SPI, s = g - il * SPI;
+    mk[LEAD] = stage_at(g + 3 + LEAD, ilp, sp - 1) ? ++vmn : -1;
     if (s < H) {
       f32x4 acc[4] = {bias, bias, bias, bias};
       int u0[4] = {0, 8, 20, 32};
@@ -513,6 +519,8 @@ void convt_rows_kernel(CRArgs a) {
     lds_barrier();
 #pragma unroll
     for (int i = 0; i < LEAD; ++i) mk[i] = mk[i + 1];
+    if (++s == SPI) { s = 0; ++il; }
+    if (++sp == SPI) { sp = 0; ++ilp; }
   }
   store_held();
 }

@@ -531,6 +531,19 @@ struct TailWave {
 template <int I>
 using IC = std::integral_constant<int, I>;
 
+// v (this lane's value) moved within 16-lane rows by the DPP control CTRL (0 where the source
+// lane is outside the row). The value first passes through an empty asm statement: applied
+// directly to an element of an MFMA result vector, hipcc (ROCm 7.2) folds the DPP move into its
+// user with the vector's FIRST register as the source (element 1 or 2 read element 0: the
+// map-free decoder3 was wrong in every column but the first until this; the same happens with
+// __builtin_amdgcn_mov_dpp). A plain 32-bit VGPR source is folded correctly.
+template <int CTRL>
+__device__ __forceinline__ float dpp_shift(float v) {
+  int x = __builtin_bit_cast(int, v);
+  asm volatile("" : "+v"(x));
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false));
+}
+
 template <typename T>
 __global__ __launch_bounds__(256, 2) void tail_rows_kernel(RowsArgs a) {
   using namespace rows;
@@ -778,9 +791,9 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
     const int dps = 1 + 8 * wv + (lane >> 3);
     const int dsrc = (dps - 1) * CI1 + 8 * ((lane & 7) ^ (dps & 7));
     unsigned char* const ddst = lds_raw + (1 + 8 * wv) * X1ST * 2;
-    auto stage = [&](int p) -> bool {  // whether this wave issued an LDS-DMA
+    // position p = il SPI + row + 1; returns whether this wave issued an LDS-DMA
+    auto stage_at = [&](int p, int il, int row) -> bool {
       unsigned char* dst = ddst + (p & (NX1 - 1)) * X1ROW * 2;
-      const int il = p / SPI, row = p - il * SPI - 1;
       if (il < nimg && row >= 0 && row < H1) {
         const long long n = (long long)blockIdx.x + (long long)il * G;
         lds_dma16(X + ((n * H1 + row) * W1) * CI1 + dsrc, dst);
@@ -789,6 +802,10 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       // between / after the images: the zero padding rows
       *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
       return false;
+    };
+    auto stage = [&](int p) -> bool {  // (prologue)
+      const int il = p / SPI;
+      return stage_at(p, il, p - il * SPI - 1);
     };
     // this lane's B-fragment offsets (pixel 16 wx + m + dx, group kg) in an input ring row,
     // and its tail-input write offsets (pixel 2 (16 wx + m) + px, channels 16 nb + 4 kg ..)
@@ -809,13 +826,15 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
 #pragma unroll
     for (int i = 0; i <= LEAD; ++i) mk[i] = -1;
 
+    // scalar counters (image, step in image) of macro step g and of its refill position
+    int ilg = 0, sg = 0;
+    int ilp = (3 + LEAD) / SPI, sp = 3 + LEAD - ilp * SPI;
     auto pstep = [&](auto ic, const int g) {
       constexpr int I = decltype(ic)::value;  // g & 7 (the input ring's period)
-      mk[LEAD] = stage(g + 3 + LEAD) ? ++vmn : -1;
+      mk[LEAD] = stage_at(g + 3 + LEAD, ilp, sp - 1) ? ++vmn : -1;
       T* const r0 = x2r + ((2 * I) & 7) * X2ROW;  // (tail ring: period 4 macro steps)
       T* const r1 = x2r + ((2 * I + 1) & 7) * X2ROW;
-      const int il = g / SPI, s = g - il * SPI;
-      if (il < nimg && s < H1) {
+      if (ilg < nimg && sg < H1) {
         f32x4 acc[4] = {bias, bias, bias, bias};
         int u0[4] = {0, 8, 20, 32};
 #pragma unroll
@@ -849,6 +868,8 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       D3_BARRIER();
 #pragma unroll
       for (int i = 0; i < LEAD; ++i) mk[i] = mk[i + 1];
+      if (++sg == SPI) { sg = 0; ++ilg; }
+      if (++sp == SPI) { sp = 0; ++ilp; }
     };
     int g = 0;
     for (; g + 8 <= S; g += 8) {
@@ -989,10 +1010,8 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
     };
     auto emit = [&](const f32x4& E, const float* bb, int eil, int etl) {
       float s = bo + E[0];
-      s += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                                         0, __builtin_bit_cast(int, E[1]), 0x111, 0xf, 0xf, false));
-      s += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                                         0, __builtin_bit_cast(int, E[2]), 0x101, 0xf, 0xf, false));
+      s += dpp_shift<0x111>(E[1]);  // row_shr:1: lane m reads lane m - 1
+      s += dpp_shift<0x101>(E[2]);  // row_shl:1: lane m reads lane m + 1
       s += bb[bri];
       const long long n = (long long)blockIdx.x + (long long)eil * G;
       a.out[(n * H3 + 2 * (etl - 1) + orow) * rows::MW + ocol] =

@@ -428,6 +428,7 @@ void convt_rows_kernel(CRArgs a) {
   }
   const f32x4 bias = f32x4{a.b[16 * nb + 4 * kg], a.b[16 * nb + 4 * kg + 1],
                            a.b[16 * nb + 4 * kg + 2], a.b[16 * nb + 4 * kg + 3]};
+  resident_loads_landed();
   int xo[3];  // byte offset of pixel 16 wx + m + dx (stored + 1), group kg, in a ring row
 #pragma unroll
   for (int dx = -1; dx <= 1; ++dx) {
@@ -812,7 +813,7 @@ void enc2_rows_kernel(E2Args a) {
     v0 = uint4{q0[0], q0[1], q0[2], q0[3]};
     v1 = uint4{q1[0], q1[1], q1[2], q1[3]};
   }
-
+  resident_loads_landed();
   const int w1x = wv & 3, jr = wv >> 2;  // conv1 pixel block, conv2 input row of the pair
   const int wbase = 16 * w1x + m + 3;
 

@@ -657,7 +657,7 @@ constexpr int LDS_BYTES = LDS_X1 + LDS_X2 + LDS_M + LDS_S;  // 123,136 B: one wo
 // of the 4 consumer waves, slots 1 .. 4 (0 and 5: the image's zero borders), 2 sides x 4
 // lane groups
 constexpr int NBND = 6 * 2 * 4;
-constexpr int LDS_BYTES_NM = LDS_X1 + LDS_X2 + 4 * NBND * 4;  // 69,376 B
+constexpr int LDS_BYTES_NM = LDS_X1 + LDS_X2 + (4 * NBND + 64) * 4;  // 69,632 B (+ 64 dump words)
 }  // namespace d3
 
 // first Conv2DTranspose input pixel ps (x = ps - 1), 16-byte group g of its 8: group g sits
@@ -670,6 +670,13 @@ __device__ __forceinline__ int x1_off(int ps, int g) { return ps * d3::X1ST + 8 
 // consumer 16-byte reads of consecutive pixels conflict-free)
 __device__ __forceinline__ int x2_off(int ps, int g) { return ps * d3::X2ST + 8 * (g ^ ((ps >> 1) & 3)); }
 
+
+#ifndef SPECENH_D3_CPRIO
+#define SPECENH_D3_CPRIO 0  // measured +4 % (tools/lib_ab.sh, profiles/r04_d3_ab.txt)
+#endif
+#ifndef SPECENH_D3_BRANCHFREE
+#define SPECENH_D3_BRANCHFREE 1
+#endif
 
 struct D3Args {
   const void* x;     // [N][H][32][64]
@@ -784,6 +791,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
     }
     const f32x4 bias = f32x4{a.b1[16 * nb + 4 * kg], a.b1[16 * nb + 4 * kg + 1],
                              a.b1[16 * nb + 4 * kg + 2], a.b1[16 * nb + 4 * kg + 3]};
+    resident_loads_landed();
     const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
     // input stream position p (image p / SPI, row p % SPI - 1; row -1 is the zero row) ->
     // ring slot p & 3 by LDS-DMA: wave wv moves stored pixels 1 + 8 wv .. 8 + 8 wv (1 KB,
@@ -952,6 +960,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
         }
     }
     const float bo = a.bo[0];
+    resident_loads_landed();
     int xo[3];  // element offset of pixel 16 w + m + dx (stored + 1), group kg, in a ring row
 #pragma unroll
     for (int dx = -1; dx <= 1; ++dx) xo[dx + 1] = x2_off(16 * w + m + dx + 1, kg);
@@ -960,8 +969,16 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
     // w + 1 side 0, lane m = 0 publishes E[2] in side 1; m = 0 / 15 read the neighbours' slots,
     // every other lane a never-written zero word
     const int orow = kg >> 1, ocol = 32 * w + 2 * m + (kg & 1);
+    // every lane stores its word each tail step (no exec-mask branch): lanes other than
+    // m = 0 / 15 into their own word of a dump area past the four exchange buffers
+    float* const dump = bnd + 4 * NBND + lane;
     const int bwi = ((w + 1) * 2 + (m == 0 ? 1 : 0)) * 4 + kg;
     const int bri = m == 0 ? (w * 2 + 0) * 4 + kg : (m == 15 ? ((w + 2) * 2 + 1) * 4 + kg : 0);
+#if SPECENH_D3_CPRIO
+    // the consumer waves are the macro step's critical path (barrier clocks, tools/d3_stats.py:
+    // busy 95 % of the step vs the producers' 81 %): they win the SIMD's issue arbitration
+    __builtin_amdgcn_s_setprio(1);
+#endif
     D3_BARRIER();  // macro step -1
 
     f32x4 P0 = f32x4{0.f, 0.f, 0.f, 0.f}, P1 = P0, P2 = P0;
@@ -971,7 +988,13 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       eil = il;
       etl = tl;
       if (++tl == TPI) { tl = 0; ++il; }
-      if (eil < 0 || eil >= nimg) return false;
+      const bool img = eil >= 0 && eil < nimg;
+#if !SPECENH_D3_BRANCHFREE
+      if (!img) return false;
+#endif
+      // (branch-free: before the first / past the last image the ring rows are zero rows and
+      // the results are masked, so both tail steps of a macro step form one basic block and
+      // the scheduler can interleave their MFMA chains)
       f32x4 acc[4] = {bias, bias, bias, bias};
       int u0[4] = {0, 4, 10, 16};  // first tap register of each phase (4 / 6 / 6 / 9 taps)
 #pragma unroll
@@ -987,7 +1010,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
           }
         }
       // map rows 2tl, 2tl + 1 as the Conv2D(1)'s B operands (zero below the image)
-      const uint32_t keep = etl < H2 ? 0xffffffffu : 0u;
+      const uint32_t keep = img && etl < H2 ? 0xffffffffu : 0u;
       uint4 bv[2];
 #pragma unroll
       for (int py = 0; py < 2; ++py) {
@@ -1004,9 +1027,14 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       P0 = P1;
       P1 = P2;
       P2 = f32x4{0.f, 0.f, 0.f, 0.f};
+#if SPECENH_D3_BRANCHFREE
+      *(m == 0 || m == 15 ? bb + bwi : dump) = m == 0 ? E[2] : E[1];
+      return img && etl >= 1 && etl <= H2;  // pair tl - 1 is an output row pair
+#else
       if (etl < 1 || etl > H2) return false;  // pair tl - 1 is not an output row pair
       if (m == 0 || m == 15) bb[bwi] = m == 0 ? E[2] : E[1];
       return true;
+#endif
     };
     auto emit = [&](const f32x4& E, const float* bb, int eil, int etl) {
       float s = bo + E[0];

@@ -32,6 +32,12 @@ __device__ __forceinline__ void gstore8(void* dst, uint2 v) {
   asm volatile("global_store_dwordx2 %0, %1, off" : : "v"(dst), "v"(v) : "memory");
 }
 
+// The launch-resident fragments (weights, biases) loaded before a step loop have landed:
+// s_waitcnt vmcnt(0) as the builtin, which the compiler's wait insertion sees. Without it the
+// compiler puts its wait for those loads at their first use INSIDE the loop, where it runs
+// every step and drains every LDS-DMA and store in flight (vmcnt counts both on gfx9).
+__device__ __forceinline__ void resident_loads_landed() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // s_waitcnt vmcnt(n) for a wave-uniform run-time n: wait until at most n of this wave's
 // vector-memory ops are outstanding (n > 15 waits as for 15: stricter, never laxer)
 __device__ __forceinline__ void wait_vmcnt(int n) {

@@ -1,7 +1,7 @@
 """The C5 decoder's last three layers at the bench's launch shape (2048 x 32 x 32 x 64 fp16):
 decoder3_kernel map-free (default) vs its round-3 map-ring consumer (D3_MAP=1) vs the unfused
 engine path (convT2 conv_patch launch + the row-sweep tail), interleaved rounds in one
-process, HIP events.  python tools/dec3_bench.py [N]"""
+process, HIP events.  python tools/dec3_bench.py [N] [arm,arm...]"""
 import os
 import sys
 
@@ -27,6 +27,8 @@ def main():
         engs[v] = e
     _lib.set_variant("DECODER_UNFUSED", 0)
     arms = {"mapfree": (engs[0], 0), "map": (engs[0], 1), "unfused": (engs[1], 0)}
+    if len(sys.argv) > 2:
+        arms = {k: v for k, v in arms.items() if k in sys.argv[2].split(",")}
     x = (torch.rand(N, 32, 32, 64, device=dev) * 0.5).half()
     res = {k: [] for k in arms}
     outs = {}
@@ -49,6 +51,8 @@ def main():
         print(f"{name:8s} N={N}: median {med:.4f} ms  min {min(res[name]):.4f}  "
               f"({flop / med / 1e9:.0f} TF/s = {flop / med / 1e9 / 2500:.3f} of 2.5 PF)", flush=True)
     for name in ("map", "unfused"):
+        if name not in outs or "mapfree" not in outs:
+            continue
         d = (outs["mapfree"] - outs[name]).abs().max().item()
         print(f"max |mapfree - {name}| = {d:.2e}")
 

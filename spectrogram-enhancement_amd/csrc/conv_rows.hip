@@ -526,6 +526,173 @@ void convt_rows_kernel(CRArgs a) {
   store_held();
 }
 
+// convt_rows_pw_kernel: convT1 (CO = 64 on 16-position rows), every wave with its OWN input
+// ring. The four waves of convt_rows_kernel<T, 64, 16> (one per 16-channel block) all read the
+// whole input row, so they shared one ring filled by two of them and met at a workgroup barrier
+// every step. Here each wave LDS-DMAs the row (2 x 1 KB) into its own 8-row ring (18 KB; 72 KB
+// per workgroup, two workgroups per CU) and waits only for its own refill: no barrier in the
+// step loop, the two waves of a SIMD drift freely against each other. The input is read from
+// L2 four times instead of once (it is 32 KB per image against 128 KB of output).
+template <typename T, int LEAD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void convt_rows_pw_kernel(CRArgs a) {
+  static_assert(LEAD >= 1 && LEAD <= 4, "8-row ring: positions g .. g + 3 + LEAD live");
+  using C = TC<64, 16>;
+  constexpr int CO = 64, W = 16;
+  constexpr int WR = C::RING * C::ROWB;  // bytes per wave ring
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_pw[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = lane & 15, kg = lane >> 4;
+  const int nb = wv;
+  unsigned char* const ring = lds_pw + wv * WR;
+  const int H = a.H, SPI = H + 1;
+  const int G = gridDim.x;
+  const int nimg = ((int)a.N - (int)blockIdx.x + G - 1) / G;
+  const int S = nimg * SPI;
+
+  for (int e = lane; e < WR / 16; e += 64) reinterpret_cast<uint4*>(ring)[e] = uint4{0u, 0u, 0u, 0u};
+  uint4 wf[50];  // tap fragments [phase][(dy, dx) taps][K half]
+  {
+    const T* __restrict__ Wg = reinterpret_cast<const T*>(a.w);
+    int u = 0;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          if (!ttap(ph, dy, dx)) continue;
+#pragma unroll
+          for (int kh = 0; kh < 2; ++kh)
+            wf[u++] = *reinterpret_cast<const uint4*>(
+                Wg + (((16 * nb + m) * 5 + tky(ph >> 1, dy)) * 5 + tky(ph & 1, dx)) * 64 +
+                32 * kh + 8 * kg);
+        }
+  }
+  const f32x4 bias = f32x4{a.b[16 * nb + 4 * kg], a.b[16 * nb + 4 * kg + 1],
+                           a.b[16 * nb + 4 * kg + 2], a.b[16 * nb + 4 * kg + 3]};
+  resident_loads_landed();
+  int xo[3];  // byte offset of pixel m + dx (stored + 1), group kg, in a ring row
+#pragma unroll
+  for (int dx = -1; dx <= 1; ++dx) {
+    const int ps = m + dx + 1;
+    xo[dx + 1] = ps * 128 + 16 * (kg ^ (ps & 7));
+  }
+  // refill: 16-byte chunks c = lane and 64 + lane of a row (pixel 1 + c / 8, swizzled group)
+  const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
+  int dsrc[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = 64 * h + lane;
+    const int ps = 1 + c / 8, gs = c & 7;
+    dsrc[h] = (ps - 1) * 64 + 8 * (gs ^ (ps & 7));
+  }
+  // stream position p = il SPI + r + 1 -> ring slot p & 7; returns the DMAs issued
+  auto stage_at = [&](int p, int il, int r) -> int {
+    unsigned char* dst = ring + (p & 7) * C::ROWB + 128;
+    if (il < nimg && r >= 0) {
+      const long long n = (long long)blockIdx.x + (long long)il * G;
+      const T* src = X + ((n * H + r) * W) * 64;
+      lds_dma16(src + dsrc[0], dst);
+      lds_dma16(src + dsrc[1], dst + 1024);
+      return 2;
+    }
+    *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
+    *reinterpret_cast<uint4*>(dst + 1024 + 16 * lane) = uint4{0u, 0u, 0u, 0u};
+    return 0;
+  };
+#pragma unroll
+  for (int p = 0; p < 3 + LEAD; ++p) {
+    const int il = p / SPI;
+    stage_at(p, il, p - il * SPI - 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+  T* __restrict__ O = reinterpret_cast<T*>(a.out);
+  constexpr int OW = 2 * W;
+  uint2 pk[4];
+  long long po = -1;  // element offset of the held outputs' (2s, 2x) pixel, -1: none
+  int vmn = 0;        // this wave's vector-memory ops issued in the loop
+  int mk[LEAD + 1];   // vmn right after the DMAs of position g + 3 + i (-1: none in flight)
+#pragma unroll
+  for (int i = 0; i <= LEAD; ++i) mk[i] = -1;
+  auto store_held = [&]() {
+    if (po >= 0) {
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph)
+        gstore8(O + po + ((ph >> 1) * OW + (ph & 1)) * CO, pk[ph]);
+      vmn += 4;
+    }
+  };
+  int il = 0, s = 0;
+  int ilp = (3 + LEAD) / SPI, sp = 3 + LEAD - ilp * SPI;
+  for (int g = 0; g < S; ++g) {
+    store_held();
+    po = -1;
+    const int nd = stage_at(g + 3 + LEAD, ilp, sp - 1);
+    vmn += nd;
+    mk[LEAD] = nd ? vmn : -1;
+    if (s < H) {
+      f32x4 acc[4] = {bias, bias, bias, bias};
+      int u0[4] = {0, 8, 20, 32};
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy) {
+        const unsigned char* src = ring + ((g + 1 + dy) & 7) * C::ROWB;
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          const uint4 b0 = *reinterpret_cast<const uint4*>(src + xo[dx + 1]);
+          const uint4 b1 = *reinterpret_cast<const uint4*>(src + (xo[dx + 1] ^ 64));
+#pragma unroll
+          for (int ph = 0; ph < 4; ++ph)
+            if (ttap(ph, dy, dx)) acc[ph] = mfma<T>(wf[u0[ph]], b0, acc[ph]);
+#pragma unroll
+          for (int ph = 0; ph < 4; ++ph)
+            if (ttap(ph, dy, dx)) {
+              acc[ph] = mfma<T>(wf[u0[ph] + 1], b1, acc[ph]);
+              u0[ph] += 2;
+            }
+        }
+      }
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) pk[ph] = relu_pack4<T>(acc[ph]);
+      const long long n = (long long)blockIdx.x + (long long)il * G;
+      po = ((n * 2 * H + 2 * s) * OW + 2 * m) * CO + 16 * nb + 4 * kg;
+    }
+    // this wave's refill of position g + 3 (both DMAs) has landed; LDS reads are in order
+    // within a wave, so the zero-filled rows need no wait
+    if (mk[0] >= 0) wait_vmcnt(vmn - mk[0]);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < LEAD; ++i) mk[i] = mk[i + 1];
+    if (++s == SPI) { s = 0; ++il; }
+    if (++sp == SPI) { sp = 0; ++ilp; }
+  }
+  store_held();
+}
+
+template <typename T>
+hipError_t launch_convt_rows_pw(const CRArgs& a, hipStream_t st) {
+  using C = TC<64, 16>;
+  constexpr int LDS = 4 * C::RING * C::ROWB;
+  const void* k = reinterpret_cast<const void*>(&convt_rows_pw_kernel<T, 3>);
+  static int per_cu[64] = {};
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (per_cu[dev] == 0) {
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    int pc = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k, 256, LDS);
+    if (e != hipSuccess) return e;
+    per_cu[dev] = std::max(1, pc);
+  }
+  const long long grid = std::min<long long>(a.N, (long long)per_cu[dev] * device_cus());
+  SPECENH_LAUNCH((convt_rows_pw_kernel<T, 3>), dim3((unsigned)grid), dim3(256), LDS, st, a);
+  return hipGetLastError();
+}
+
 template <typename T, int CO, int W, int LEAD>
 hipError_t launch_convt_rows_lead(const CRArgs& a, hipStream_t st) {
   using C = TC<CO, W>;
@@ -1076,7 +1243,9 @@ int convt_rows(int dtype, const void* x, int N, int H, int W, int CI, const void
   a.x = x; a.w = w; a.b = b; a.out = out; a.N = N; a.H = H;
   const bool f16 = dtype == SPECENH_DTYPE_F16;
   hipError_t e;
-  if (CO == 64 && W == 16)
+  if (CO == 64 && W == 16 && variant(V_CONVT_SHARED_RING) == 0)
+    e = f16 ? launch_convt_rows_pw<_Float16>(a, st) : launch_convt_rows_pw<__bf16>(a, st);
+  else if (CO == 64 && W == 16)
     e = f16 ? launch_convt_rows<_Float16, 64, 16>(a, st) : launch_convt_rows<__bf16, 64, 16>(a, st);
   else if (CO == 32 && W == 32)
     e = f16 ? launch_convt_rows<_Float16, 32, 32>(a, st) : launch_convt_rows<__bf16, 32, 32>(a, st);

@@ -110,7 +110,7 @@ def test_convt_rows_vs_float64(gpu_device, dtype, CO, W, N, H):
     out = torch.full((N, 2 * H, 2 * W, CO), float("nan"), dtype=dtype, device=gpu_device)
     _convt_run(x, w, bias, CO, out)
     torch.cuda.synchronize()
-    assert "convt_rows_kernel" in _lib.last_kernel_name()
+    assert "convt_rows" in _lib.last_kernel_name()
     ref, mag = _convt_ref(x, w, bias)
     got = out.double().cpu()
     assert bool(torch.isfinite(got).all())
@@ -137,6 +137,28 @@ def test_convt_rows_matches_tile_kernel(gpu_device, kernel_variant, CO, W):
     assert float(d.max()) <= 2.0 ** -10 * float(b.float().abs().max())
 
 
+@pytest.mark.parametrize("N,H", [(1, 5), (3, 1), (700, 16), (1100, 3)])
+def test_convt_rows_per_wave_ring_bitwise(gpu_device, kernel_variant, N, H):
+    """convT1 (CO 64 on 16-wide rows): per-wave input rings, no step barrier (default) vs the
+    shared ring (CONVT_SHARED_RING): the same MFMA order, bitwise equal; several images per
+    persistent workgroup at N = 700 / 1100."""
+    rng = np.random.default_rng(17 + N + H)
+    x = torch.tensor(rng.uniform(0, 1, (N, H, 16, 64)), dtype=torch.float16, device=gpu_device)
+    w = torch.tensor(rng.standard_normal((64, 5, 5, 64)) * 0.03, dtype=torch.float16,
+                     device=gpu_device)
+    bias = torch.tensor(rng.standard_normal(64) * 0.1, dtype=torch.float32, device=gpu_device)
+    a = torch.full((N, 2 * H, 32, 64), float("nan"), dtype=torch.float16, device=gpu_device)
+    b = torch.full_like(a, float("nan"))
+    _convt_run(x, w, bias, 64, a)
+    assert "convt_rows_pw_kernel" in _lib.last_kernel_name()
+    kernel_variant("CONVT_SHARED_RING", 1)
+    _convt_run(x, w, bias, 64, b)
+    torch.cuda.synchronize()
+    assert "convt_rows_kernel" in _lib.last_kernel_name()
+    assert bool(torch.isfinite(a).all())
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("CO,W", [(64, 16), (32, 32)])
 @pytest.mark.parametrize("N,H", [(1, 5), (700, 16)])
 def test_convt_rows_lead_bitwise(gpu_device, kernel_variant, CO, W, N, H):
@@ -149,11 +171,12 @@ def test_convt_rows_lead_bitwise(gpu_device, kernel_variant, CO, W, N, H):
     bias = torch.tensor(rng.standard_normal(CO) * 0.1, dtype=torch.float32, device=gpu_device)
     a = torch.full((N, 2 * H, 2 * W, CO), float("nan"), dtype=torch.float16, device=gpu_device)
     b = torch.full_like(a, float("nan"))
+    kernel_variant("CONVT_SHARED_RING", 1)  # (the LEAD variants are the shared-ring kernel's)
     _convt_run(x, w, bias, CO, a)
     kernel_variant("ROWS_SHORT_LEAD", 1)
     _convt_run(x, w, bias, CO, b)
     torch.cuda.synchronize()
-    assert "convt_rows_kernel" in _lib.last_kernel_name()
+    assert "convt_rows" in _lib.last_kernel_name()
     assert bool(torch.isfinite(a).all())
     assert torch.equal(a, b)
 

@@ -242,6 +242,15 @@ int specenh_bce_logits(const float* z, const void* target, int target_dtype, lon
 int specenh_adam_step(float* w, const float* g, float* m, float* v, long long n, float lr_t,
                       float b1, float b2, float eps, float grad_scale, void* w_lowp,
                       int lowp_dtype, void* stream);
+/* specenh_adam_step, and in the same pass the input-gradient GEMM weights of nseg (<= 8)
+ * layers from the updated weights: segment s is w[seg_off[s] .. + k k ci co) as forward GEMM
+ * weights [co][k][k][ci] (seg_kcc[3s .. 3s+2] = k, ci, co); seg_dst[s] ([ci][k][k][co], in
+ * lowp_dtype, fp32 when w_lowp is NULL) receives specenh_weight_flip_transpose of the updated
+ * copy. One launch instead of an Adam launch plus one flip launch per layer. */
+int specenh_adam_step_flip(float* w, const float* g, float* m, float* v, long long n, float lr_t,
+                           float b1, float b2, float eps, float grad_scale, void* w_lowp,
+                           int lowp_dtype, int nseg, const long long* seg_off, const int* seg_kcc,
+                           void* const* seg_dst, void* stream);
 /* bd[i][a][b][o] = bt[o][k-1-a][k-1-b][i] (bt: [co][k][k][ci], bd: [ci][k][k][co]):
  * the GEMM weights of a convolution's input gradient from its forward GEMM weights. */
 int specenh_weight_flip_transpose(int dtype, const void* bt, int k, int ci, int co, void* bd,

@@ -2075,6 +2075,49 @@ __global__ void adam_kernel(float* __restrict__ w, const float* __restrict__ g, 
   }
 }
 
+// Adam (as adam_kernel) with the input-gradient GEMM weights of up to 8 layers written from
+// the updated weights in the same pass: element i of segment s (w[off .. off + k k ci co) =
+// bt[co][ky][kx][ci]) also goes to bd[ci][k-1-ky][k-1-kx][co] (flip_transpose_kernel's map),
+// as T — the value w_lowp receives, or fp32 for fp32 training. Replaces the per-layer
+// flip_transpose launches that followed every optimizer step.
+struct FlipSegs {
+  long long off[8];
+  int k[8], ci[8], co[8];
+  void* dst[8];
+  int n;
+};
+
+template <typename T, bool LOWP>
+__global__ void adam_flip_kernel(float* __restrict__ w, const float* __restrict__ g,
+                                 float* __restrict__ m, float* __restrict__ v, long long n,
+                                 float lr_t, float b1, float b2, float eps, float gscale,
+                                 T* __restrict__ w_lowp, FlipSegs fs) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const float gi = g[i] * gscale;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float wi = w[i] - lr_t * mi / (sqrtf(vi) + eps);
+    w[i] = wi;
+    const T wt = from_f<T>(wi);
+    if (LOWP) w_lowp[i] = wt;
+    for (int s = 0; s < fs.n; ++s) {
+      const int k = fs.k[s], CI = fs.ci[s], CO = fs.co[s];
+      const long long r = i - fs.off[s];
+      if (r < 0 || r >= (long long)k * k * CI * CO) continue;
+      const int ci = (int)(r % CI);
+      long long t = r / CI;
+      const int kx = (int)(t % k);
+      t /= k;
+      const int ky = (int)(t % k);
+      const int co = (int)(t / k);
+      reinterpret_cast<T*>(fs.dst[s])[(((long long)ci * k + (k - 1 - ky)) * k + (k - 1 - kx)) * CO + co] = wt;
+    }
+  }
+}
+
 // bd[ci][a][b][co] = bt[co][k-1-a][k-1-b][ci]
 template <typename T>
 __global__ void flip_transpose_kernel(const T* __restrict__ bt, int k, int CI, int CO,
@@ -2724,6 +2767,41 @@ int specenh_adam_step(float* w, const float* g, float* m, float* v, long long n,
   else
     return set_error(SPECENH_EINVAL, "adam: low-precision copy must be bf16 or f16");
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "adam");
+}
+
+int specenh_adam_step_flip(float* w, const float* g, float* m, float* v, long long n, float lr_t,
+                           float b1, float b2, float eps, float grad_scale, void* w_lowp,
+                           int lowp_dtype, int nseg, const long long* seg_off, const int* seg_kcc,
+                           void* const* seg_dst, void* stream) {
+  if (!w || !g || !m || !v || n <= 0) return set_error(SPECENH_EINVAL, "adam args");
+  if (nseg < 0 || nseg > 8 || (nseg > 0 && (!seg_off || !seg_kcc || !seg_dst)))
+    return set_error(SPECENH_EINVAL, "adam_flip: 0..8 segments");
+  FlipSegs fs{};
+  fs.n = nseg;
+  for (int s = 0; s < nseg; ++s) {
+    const long long sz = (long long)seg_kcc[3 * s] * seg_kcc[3 * s] * seg_kcc[3 * s + 1] *
+                         seg_kcc[3 * s + 2];
+    if (!seg_dst[s] || sz <= 0 || seg_off[s] < 0 || seg_off[s] + sz > n)
+      return set_error(SPECENH_EINVAL, "adam_flip: segment outside w");
+    fs.off[s] = seg_off[s];
+    fs.k[s] = seg_kcc[3 * s];
+    fs.ci[s] = seg_kcc[3 * s + 1];
+    fs.co[s] = seg_kcc[3 * s + 2];
+    fs.dst[s] = seg_dst[s];
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (!w_lowp)
+    SPECENH_LAUNCH((adam_flip_kernel<float, false>), dim3(grid1d(n)), dim3(256), 0, st, w, g, m, v,
+                   n, lr_t, b1, b2, eps, grad_scale, (float*)nullptr, fs);
+  else if (lowp_dtype == SPECENH_DTYPE_F16)
+    SPECENH_LAUNCH((adam_flip_kernel<_Float16, true>), dim3(grid1d(n)), dim3(256), 0, st, w, g, m,
+                   v, n, lr_t, b1, b2, eps, grad_scale, (_Float16*)w_lowp, fs);
+  else if (lowp_dtype == SPECENH_DTYPE_BF16)
+    SPECENH_LAUNCH((adam_flip_kernel<__bf16, true>), dim3(grid1d(n)), dim3(256), 0, st, w, g, m,
+                   v, n, lr_t, b1, b2, eps, grad_scale, (__bf16*)w_lowp, fs);
+  else
+    return set_error(SPECENH_EINVAL, "adam: low-precision copy must be bf16 or f16");
+  return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "adam_flip");
 }
 
 int specenh_weight_flip_transpose(int dtype, const void* bt, int k, int ci, int co, void* bd,

@@ -121,6 +121,10 @@ SIGNATURES = {
                                      _c.c_longlong, _c.c_float, _c.c_float, _c.c_float,
                                      _c.c_float, _c.c_float, _c.c_void_p, _c.c_int,
                                      _c.c_void_p]),
+    "specenh_adam_step_flip": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                          _c.c_longlong, _c.c_float, _c.c_float, _c.c_float,
+                                          _c.c_float, _c.c_float, _c.c_void_p, _c.c_int, _c.c_int,
+                                          _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p]),
     "specenh_weight_flip_transpose": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int,
                                                  _c.c_int, _c.c_void_p, _c.c_void_p]),
     "specenh_cast": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_void_p, _c.c_longlong,

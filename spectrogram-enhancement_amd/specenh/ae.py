@@ -493,8 +493,18 @@ class AutoencoderEngine:
                        act=None, mask=relu_mask, bias=False, out_shape=(IH, IW), cout=op.cin)
 
     def adam(self, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7, grad_scale=1.0):
+        """Keras Adam on the fp32 master weights; the low-precision copy and every layer's
+        flipped input-gradient weights are written by the same launch (adam_step_flip_)."""
         self.t += 1
         lr_t = lr * math.sqrt(1.0 - beta_2 ** self.t) / (1.0 - beta_1 ** self.t)
+        if len(self.w_d) <= 8:
+            seg = sorted(self.w_d.items())
+            ops.adam_step_flip_(self.w, self.g, self.m, self.v, lr_t, beta_1, beta_2, epsilon,
+                                grad_scale, self.w_lp, [self.ops[i].off_w for i, _ in seg],
+                                [x for i, _ in seg for x in (self.ops[i].k, self.ops[i].cin,
+                                                              self.ops[i].cout)],
+                                [wd for _, wd in seg])
+            return
         ops.adam_step_(self.w, self.g, self.m, self.v, lr_t, beta_1, beta_2, epsilon, grad_scale,
                        self.w_lp)
         for i, wd in self.w_d.items():

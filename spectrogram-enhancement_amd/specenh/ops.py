@@ -537,6 +537,40 @@ _op("adam_step_(Tensor(a!) w, Tensor g, Tensor(b!) m, Tensor(c!) v, float lr_t, 
     lambda *a: None)
 
 
+def _adam_flip(w, g, m, v, lr_t, beta_1, beta_2, epsilon, grad_scale, w_lowp, seg_off, seg_kcc,
+               seg_dst):
+    """adam_step_ plus the flipped input-gradient weights of len(seg_dst) layers in the same
+    launch (specenh_adam_step_flip): seg_off[s] is the layer's flat weight offset in w,
+    seg_kcc[3s:3s+3] = (k, ci, co), seg_dst[s] its [ci][k][k][co] buffer."""
+    import ctypes
+    n = w.numel()
+    for t, nm in ((g, "g"), (m, "m"), (v, "v")):
+        if t.numel() != n or t.dtype != torch.float32:
+            raise ValueError(f"{nm} must be float32 like w")
+    if w_lowp is not None and w_lowp.numel() != n:
+        raise ValueError("w_lowp must have w's size")
+    ns = len(seg_dst)
+    if len(seg_off) != ns or len(seg_kcc) != 3 * ns:
+        raise ValueError("segment lists")
+    want = w_lowp.dtype if w_lowp is not None else torch.float32
+    for s, d in enumerate(seg_dst):
+        k, ci, co = seg_kcc[3 * s:3 * s + 3]
+        if d.dtype != want or d.numel() != k * k * ci * co or not d.is_contiguous():
+            raise ValueError(f"segment {s}: destination must be contiguous {want} [{ci}][{k}][{k}][{co}]")
+    off = (ctypes.c_longlong * max(ns, 1))(*seg_off)
+    kcc = (ctypes.c_int * max(3 * ns, 1))(*seg_kcc)
+    dst = (ctypes.c_void_p * max(ns, 1))(*[d.data_ptr() for d in seg_dst])
+    _lib.check(_lib.lib().specenh_adam_step_flip(
+        _vp(w), _vp(g), _vp(m), _vp(v), n, lr_t, beta_1, beta_2, epsilon, grad_scale,
+        _vp(w_lowp), _code(w_lowp) if w_lowp is not None else F32, ns, off, kcc, dst, _st(w)),
+        "adam_step_flip")
+
+
+_op("adam_step_flip_(Tensor(a!) w, Tensor g, Tensor(b!) m, Tensor(c!) v, float lr_t, "
+    "float beta_1, float beta_2, float epsilon, float grad_scale, Tensor(d!)? w_lowp, "
+    "int[] seg_off, int[] seg_kcc, Tensor(e!)[] seg_dst) -> ()", _adam_flip, lambda *a: None)
+
+
 def _flip_out(bt, k, ci, co, out):
     if bt.numel() != co * k * k * ci or out.numel() != bt.numel() or out.dtype != bt.dtype:
         raise ValueError("bt / out sizes")

@@ -299,6 +299,40 @@ def test_adam_kernel_formula(gpu_device):
     assert torch.equal(wb, d[0].to(torch.bfloat16))
 
 
+@pytest.mark.parametrize("lowp", [None, torch.bfloat16, torch.float16])
+def test_adam_flip_equals_adam_then_flips(gpu_device, lowp):
+    """specenh_adam_step_flip (one launch) == specenh_adam_step + one
+    specenh_weight_flip_transpose per layer, bitwise, on the C4 model's weight layout."""
+    import bench
+    from specenh import ae, ops
+    dt = {None: "float32", torch.bfloat16: "mixed_bfloat16", torch.float16: "float16"}[lowp]
+    engs = []
+    for _ in range(2):
+        e = ae.AutoencoderEngine(bench.ae_ops(), (128, 128, 1), compute_dtype=dt, device=gpu_device)
+        e.set_keras_weights(bench.ae_weights())
+        gen = torch.Generator(device=gpu_device).manual_seed(3)
+        e.g.copy_(torch.randn(e.g.shape, device=gpu_device, generator=gen))
+        e.m.copy_(torch.randn(e.m.shape, device=gpu_device, generator=gen))
+        e.v.copy_(torch.rand(e.v.shape, device=gpu_device, generator=gen))
+        engs.append(e)
+    assert len(engs[0].w_d) == 6
+    engs[0].adam(1e-3, grad_scale=0.5)                   # fused
+    e = engs[1]                                           # reference: the two-step path
+    e.t += 1
+    lr_t = 1e-3 * math.sqrt(1.0 - 0.999 ** e.t) / (1.0 - 0.9 ** e.t)
+    ops.adam_step_(e.w, e.g, e.m, e.v, lr_t, 0.9, 0.999, 1e-7, 0.5, e.w_lp)
+    for i, wd in e.w_d.items():
+        op = e.ops[i]
+        ops.weight_flip_transpose_out(e._wv[i], op.k, op.cin, op.cout, wd)
+    torch.cuda.synchronize()
+    for a, b in ((engs[0].w, e.w), (engs[0].m, e.m), (engs[0].v, e.v)):
+        assert torch.equal(a, b)
+    if lowp is not None:
+        assert torch.equal(engs[0].w_lp, e.w_lp)
+    for i in e.w_d:
+        assert torch.equal(engs[0].w_d[i], e.w_d[i]), i
+
+
 # ----------------------------------------------------------------------------- facade
 def _small_model(policy="float32"):
     from specenh.keras import layers, mixed_precision

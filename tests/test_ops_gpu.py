@@ -83,6 +83,11 @@ def _cases(dev):
                               torch.zeros(1, dtype=torch.float64, device=dev))),
         (ops.adam_step_, (w, gr, m, v, 1e-3, 0.9, 0.999, 1e-7, 0.5,
                           torch.empty(1000, dtype=torch.bfloat16, device=dev))),
+        (ops.adam_step_flip_, (w, gr, m, v, 1e-3, 0.9, 0.999, 1e-7, 0.5,
+                               torch.empty(1000, dtype=torch.bfloat16, device=dev), [8, 300],
+                               [3, 4, 8, 5, 2, 3],
+                               [torch.empty(288, dtype=torch.bfloat16, device=dev),
+                                torch.empty(150, dtype=torch.bfloat16, device=dev)])),
         (ops.weight_flip_transpose, (wc, 3, 4, 8)),
         (ops.weight_flip_transpose_out, (wc, 3, 4, 8, torch.empty_like(wc))),
         (ops.cast, (xc, torch.float16)),

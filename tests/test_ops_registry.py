@@ -10,7 +10,7 @@ OPS = ["stft_psd", "stft_psd_out", "csd", "svd_denoise", "svd_denoise_out", "svd
        "conv2d", "conv2d_out", "conv2d_wgrad", "conv2d_wgrad_out", "convt_conv_out",
        "convt_conv_out_out", "decoder3", "decoder3_out", "encoder2", "encoder2_out", "maxpool2",
        "maxpool2_out",
-       "maxpool2_bwd", "maxpool2_bwd_out", "bce_logits", "bce_logits_out", "adam_step_",
+       "maxpool2_bwd", "maxpool2_bwd_out", "bce_logits", "bce_logits_out", "adam_step_", "adam_step_flip_",
        "weight_flip_transpose", "weight_flip_transpose_out", "cast", "cast_out", "label_filter",
        "quantfilt", "gaussblr", "morph", "strips_pack", "strips_unpack", "strips_pack_out",
        "strips_unpack_out", "svd_denoise_optimal_out"]
@@ -24,7 +24,8 @@ CABI = {"specenh_stft_psd": "stft_psd_out", "specenh_stft_psd_f16": "stft_psd_ou
         "specenh_encoder2": "encoder2_out",
         "specenh_maxpool2_fwd": "maxpool2_out",
         "specenh_maxpool2_bwd": "maxpool2_bwd_out", "specenh_bce_logits": "bce_logits_out",
-        "specenh_adam_step": "adam_step_", "specenh_weight_flip_transpose":
+        "specenh_adam_step": "adam_step_", "specenh_adam_step_flip": "adam_step_flip_",
+        "specenh_weight_flip_transpose":
         "weight_flip_transpose_out", "specenh_cast": "cast_out", "specenh_filter": "label_filter",
         "specenh_quantfilt": "quantfilt", "specenh_gaussblr": "gaussblr",
         "specenh_morph": "morph", "specenh_strips_pack": "strips_pack_out",

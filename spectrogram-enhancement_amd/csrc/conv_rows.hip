@@ -59,11 +59,13 @@ __device__ __forceinline__ f32x4 mfma(const uint4& a, const uint4& b, f32x4 acc)
                                                    __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
 }
 
+// two fp32 -> one packed pair of T (round to nearest even) as ONE v_cvt_pk_{f16,bf16}_f32;
+// the element-wise form became two converts plus a shift and an or
 template <typename T>
 __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  const T a = (T)lo, b = (T)hi;
-  return (uint32_t)__builtin_bit_cast(unsigned short, a) |
-         ((uint32_t)__builtin_bit_cast(unsigned short, b) << 16);
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{lo, hi}, t2));
 }
 
 __device__ __forceinline__ void lds_barrier() {
@@ -376,10 +378,26 @@ __device__ __forceinline__ constexpr bool ttap(int ph, int dy, int dx) {
          tky(ph & 1, dx) < 5;
 }
 
+// bias + ReLU of four fp32 accumulators -> four T in 8 bytes. ReLU commutes with the monotone
+// rounding, so it runs on the packed 16-bit pairs: v_pk_max_f16 for fp16; for bf16 each half's
+// sign is spread over the half by a packed arithmetic shift and cleared with one bitfield select
+// (-0 -> +0 as max(x, 0) gives it). fmaxf on the fp32 accumulators cost 32 VALU per 16 values
+// (the max and a NaN-quieting max per element), these 4-6.
+template <typename T>
+__device__ __forceinline__ uint32_t relu2(uint32_t p) {
+  if constexpr (__is_same(T, _Float16)) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 z = h2{(_Float16)0.f, (_Float16)0.f};
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(h2, p), z));
+  } else {
+    typedef short s2 __attribute__((ext_vector_type(2)));
+    const uint32_t neg = __builtin_bit_cast(uint32_t, __builtin_bit_cast(s2, p) >> (short)15);
+    return p & ~neg;
+  }
+}
 template <typename T>
 __device__ __forceinline__ uint2 relu_pack4(const f32x4& v) {
-  return uint2{pack2<T>(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f)),
-               pack2<T>(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f))};
+  return uint2{relu2<T>(pack2<T>(v[0], v[1])), relu2<T>(pack2<T>(v[2], v[3]))};
 }
 
 // LEAD: ring refills in flight beyond the one a step waits for. Step g needs positions

@@ -41,7 +41,9 @@ __device__ __forceinline__ void resident_loads_landed() { __builtin_amdgcn_s_wai
 // s_waitcnt vmcnt(n) for a wave-uniform run-time n: wait until at most n of this wave's
 // vector-memory ops are outstanding (n > 15 waits as for 15: stricter, never laxer)
 __device__ __forceinline__ void wait_vmcnt(int n) {
-  switch (n) {
+  // (readfirstlane: the count is wave-uniform, but the compiler cannot always prove it and
+  // then compiled the switch into a ladder of VALU compares)
+  switch (__builtin_amdgcn_readfirstlane(n)) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
     case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;

@@ -304,7 +304,8 @@ def test_adam_flip_equals_adam_then_flips(gpu_device, lowp):
     """specenh_adam_step_flip (one launch) == specenh_adam_step + one
     specenh_weight_flip_transpose per layer, bitwise, on the C4 model's weight layout."""
     import bench
-    from specenh import ae, ops
+    from specenh import ae
+    from specenh.ops import ops  # the torch.ops.specenh namespace, as specenh.ae uses it
     dt = {None: "float32", torch.bfloat16: "mixed_bfloat16", torch.float16: "float16"}[lowp]
     engs = []
     for _ in range(2):

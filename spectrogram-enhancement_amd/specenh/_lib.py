@@ -165,7 +165,10 @@ def lib():
             h = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         except OSError as e:
             raise ExtensionNotLoaded(f"failed to load {LIB_PATH}: {e}") from e
+        dev_build = bool(os.environ.get("SPECENH_LIB"))
         for name, (res, args) in SIGNATURES.items():
+            if dev_build and not hasattr(h, name):
+                continue  # an older revision's build for an A/B run (tools/build_rev_lib.sh)
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args

@@ -3,7 +3,7 @@
 # (LIB "main" = the in-tree library; others: tools/variants/libspecenh_NAME.so). Two rounds.
 TOOL=$1; shift
 ARGS=()
-while [ "$1" != "--" ] && [ -n "$1" ]; do ARGS+=("$1"); shift; done
+while [ $# -gt 0 ] && [ "$1" != "--" ]; do ARGS+=("$1"); shift; done
 shift
 for rnd in 1 2; do
   for L in "$@"; do

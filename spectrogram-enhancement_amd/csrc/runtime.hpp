@@ -35,6 +35,7 @@ enum Variant : int {
   V_D3_MAP,           // decoder3: Conv2D(1) from a 16-channel map ring in LDS (round-3 consumer)
   V_ENC2_WPE2,        // fused encoder: one workgroup per CU (256 VGPRs) instead of two
   V_CONVT_SHARED_RING, // convT1 row sweep: one shared input ring + per-step barrier (round 3)
+  V_SVD_RECON_VALU,   // SVD reconstruction with scalar FMAs (round 3) instead of fp32 MFMA
   V_ROWS_SHORT_LEAD,  // convT rows / decoder3 producer: the round-3 ring refill lead (1 / 0 steps, not 3)
   V_COUNT
 };

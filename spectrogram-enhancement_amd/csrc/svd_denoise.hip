@@ -933,6 +933,119 @@ __global__ __launch_bounds__(256) void recon_kernel(XView x, int Kr, int r, cons
   }
 }
 
+// recon_mfma_kernel: the same reconstruction with both products on the fp32 matrix cores
+// (v_mfma_f32_16x16x4_f32). recon_kernel's scalar FMAs needed one or two LDS reads per four
+// FMAs plus their address arithmetic: 954 M VALU instructions for C3's rank-16 pass, 3.6x the
+// FMAs themselves (PMC, profiles/pmc_r04.json). Per workgroup (matrix, RB = 32 rows):
+//   phase 1  Y (32 x KPP) = X_blk (32 x RP) V (RP x KPP): 2 x NT tiles of 16 x 16, the r-long
+//            K loop split over two waves when there are fewer than four tiles (partials summed
+//            in LDS);
+//   phase 2  out (32 x RP) = [X_blk -] Y V^T: 2 x RP/16 tiles dealt to the 4 waves, K = KPP.
+// Operand layout (16x16x4 f32): lane l supplies A[l & 15][l >> 4] and B[l >> 4][l & 15], and
+// holds D[4 (l >> 4) + j][l & 15]. LDS pitches: X rows RP + 2 words (A reads: 16 rows x 2 k per
+// 32-lane group on distinct banks), V rows KPP + 1 (odd: conflict-free both as phase 1's B, rows
+// k, and as phase 2's B, rows i), Y rows KPP + 1. Columns r .. RP - 1 and K .. KPP - 1 are zero.
+template <int KP, typename TO>
+__global__ __launch_bounds__(256) void recon_mfma_kernel(XView x, int Kr, int r, const float* V,
+                                                         int K, int lo, int hi, int complement,
+                                                         const int* only, TO* out,
+                                                         long long out_bstride, long long osk,
+                                                         long long osi) {
+  constexpr int NT = (KP + 15) / 16, KPP = 16 * NT, PV = KPP + 1, PY = KPP + 1;
+  constexpr int KS = 2 * NT < 4 ? 2 : 1;  // K split of phase 1
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int RP = (r + 15) & ~15, PX = RP + 2;
+  float* sV = reinterpret_cast<float*>(smem);  // RP x PV
+  float* sX = sV + RP * PV;                     // RB x PX
+  float* sY = sX + RB * PX;                     // KS x RB x PY
+  const long long b = blockIdx.y;
+  if (only && !only[b]) return;
+  const int k0 = blockIdx.x * RB;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int cl = lane & 15, kr = lane >> 4;
+  const float* X = x.base + b * x.batch_stride;
+  const float* Vb = V + b * (long long)r * K;
+  constexpr int UB = 16, UBX = 32;
+  for (int i0 = tid; i0 < RP * KPP; i0 += 256 * UB) {
+    float t[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = i0 + 256 * u, i = idx / KPP, c = idx % KPP;
+      t[u] = (idx < RP * KPP && i < r && c >= lo && c < hi) ? Vb[(long long)i * K + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = i0 + 256 * u;
+      if (idx < RP * KPP) sV[(idx / KPP) * PV + idx % KPP] = t[u];
+    }
+  }
+  const int rows = min(RB, Kr - k0);
+  const bool tr = x.si != 1;
+  for (int i0 = tid; i0 < RB * RP; i0 += 256 * UBX) {
+    float t[UBX];
+#pragma unroll
+    for (int u = 0; u < UBX; ++u) {
+      const int idx = i0 + 256 * u;
+      const int kk = tr ? idx % RB : idx / RP, i = tr ? idx / RB : idx % RP;
+      t[u] = (idx < RB * RP && kk < rows && i < r)
+                 ? X[(long long)(k0 + kk) * x.sk + (long long)i * x.si] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < UBX; ++u) {
+      const int idx = i0 + 256 * u;
+      const int kk = tr ? idx % RB : idx / RP, i = tr ? idx / RB : idx % RP;
+      if (idx < RB * RP) sX[kk * PX + i] = t[u];
+    }
+  }
+  __syncthreads();
+  // ---- phase 1: Y = X_blk V
+  {
+    const int klen = RP / KS;
+    for (int t = wave; t < 2 * NT * KS; t += 4) {
+      const int tile = t % (2 * NT), part = t / (2 * NT);
+      const int rt = tile & 1, ct = tile >> 1;
+      const float* a_p = sX + (16 * rt + cl) * PX + part * klen + kr;
+      const float* b_p = sV + (part * klen + kr) * PV + 16 * ct + cl;
+      f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < klen; k += 4)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a_p[k], b_p[k * PV], acc, 0, 0, 0);
+      float* yp = sY + part * RB * PY + (16 * rt + 4 * kr) * PY + 16 * ct + cl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) yp[j * PY] = acc[j];
+    }
+  }
+  __syncthreads();
+  if constexpr (KS == 2) {
+    for (int e = tid; e < RB * KPP; e += 256) {
+      const int row = e / KPP, c = e % KPP;
+      sY[row * PY + c] += sY[RB * PY + row * PY + c];
+    }
+    __syncthreads();
+  }
+  // ---- phase 2: out = [X_blk -] Y V^T
+  TO* Ob = out + b * out_bstride;
+  const int nit = RP / 16;
+  for (int t = wave; t < 2 * nit; t += 4) {
+    const int rt = t & 1, it = t >> 1;
+    const float* a_p = sY + (16 * rt + cl) * PY + kr;
+    const float* b_p = sV + (16 * it + cl) * PV + kr;
+    f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KPP; k += 4)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a_p[k], b_p[k], acc, 0, 0, 0);
+    const int col = 16 * it + cl;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = 16 * rt + 4 * kr + j;
+      if (row < rows && col < r) {
+        const float v = complement ? sX[row * PX + col] - acc[j] : acc[j];
+        Ob[(long long)(k0 + row) * osk + (long long)col * osi] = to_out<TO>(v);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- 2'. top-1 complement
 // The default kept range of denoiseSignal (denoising_by_svd.ipynb:188-229 with start = 1,
 // stop = None: every component but the first) is out = X - (X v1) v1^T. For Kr, r <= 128
@@ -2121,6 +2234,21 @@ template <int KP, typename TO>
 hipError_t launch_recon_t(XView xb, int Kr, int r, const float* V, int K, int lo, int hi,
                           int comp, const int* only, void* out, long long ob, long long osk,
                           long long osi, long long nb, hipStream_t st) {
+  if (variant(V_SVD_RECON_VALU) == 0) {  // the matrix-core reconstruction
+    constexpr int NT = (KP + 15) / 16, KPP = 16 * NT, KS = 2 * NT < 4 ? 2 : 1;
+    const int RP = (r + 15) & ~15;
+    const size_t lm = ((size_t)RP * (KPP + 1) + (size_t)RB * (RP + 2) +
+                       (size_t)KS * RB * (KPP + 1)) * 4;
+    if (lm <= 160 * 1024) {
+      hipError_t e = hipFuncSetAttribute((const void*)recon_mfma_kernel<KP, TO>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lm);
+      if (e != hipSuccess) return e;
+      SPECENH_LAUNCH((recon_mfma_kernel<KP, TO>), dim3((Kr + RB - 1) / RB, (unsigned)nb),
+                     dim3(256), lm, st, xb, Kr, r, V, K, lo, hi, comp, only,
+                     reinterpret_cast<TO*>(out), ob, osk, osi);
+      return hipGetLastError();
+    }
+  }
   const size_t lds = (size_t)r * KP * 4 + (size_t)RB * (r + 1) * 4 + (size_t)RB * KP * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipError_t e = hipFuncSetAttribute((const void*)recon_kernel<KP, TO>,

@@ -295,3 +295,38 @@ def test_half_precision_output_is_rounded_fp32(gpu_device, args):
         svd.denoise_batch(A, *args, out=out)
         torch.cuda.synchronize()
         assert torch.equal(out, ref32.to(dt)), dt
+
+
+@pytest.mark.parametrize("m,n", [(513, 256), (100, 72), (48, 64), (130, 200), (256, 100)])
+@pytest.mark.parametrize("rng_k", [(None, None), (0, 16), (2, 30), (0, 40)])
+def test_recon_mfma_matches_scalar_recon(gpu_device, kernel_variant, m, n, rng_k):
+    """recon_mfma_kernel (fp32 matrix cores, default) vs recon_kernel (scalar FMAs,
+    SVD_RECON_VALU=1): the same subspace, products summed in another order — equal to fp32
+    rounding (1e-6 relative Frobenius), across both orientations, r not a multiple of 16 and
+    kept ranges that need 8 .. 48 padded columns."""
+    import os
+    import sys
+
+    import torch
+
+    from specenh import _lib, svd
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import gapped_matrix
+    start, stop = rng_k
+    r = min(m, n)
+    if stop is not None and stop > r:
+        pytest.skip("range beyond the rank")
+    A = np.stack([gapped_matrix(900 + i, m, n, k=min(48, r - 2)) for i in range(5)]).astype(np.float32)
+    At = torch.as_tensor(A, device=gpu_device)
+    n0 = _lib.launch_count()
+    a = svd.denoise_batch(At, start, stop).double().cpu().numpy()
+    names = " ".join(_lib.kernel_names(n0, _lib.launch_count()))
+    kernel_variant("SVD_RECON_VALU", 1)
+    n1 = _lib.launch_count()
+    b = svd.denoise_batch(At, start, stop).double().cpu().numpy()
+    names_b = " ".join(_lib.kernel_names(n1, _lib.launch_count()))
+    if "recon" in names_b:  # (the top-1 path of small default ranges has no recon launch)
+        assert "recon_mfma_kernel" in names and "recon_mfma_kernel" not in names_b
+    for i in range(len(A)):
+        e = np.linalg.norm(a[i] - b[i]) / max(np.linalg.norm(b[i]), 1e-30)
+        assert e <= 1e-6, (i, e)

@@ -524,32 +524,24 @@ __device__ void cholqr(const float* sY, float* sZ, int r, double* sS, double* sR
       wave_lds_sync();
     }
   }
-  // R^-1 (upper) into sRi, one wave, one column per lane:
-  //   Rinv[j][j] = 1/R[j][j];  Rinv[i][j] = -(sum_{k=i+1..j} R[i][k] Rinv[k][j]) / R[i][i]
-  // (lane j reads only R and its own column of Rinv).
-  if (tid < 64) {
-    for (int idx = tid; idx < P * P; idx += 64) sRi[idx] = 0.0;
-    wave_lds_sync();
-    for (int j = tid; j < P; j += 64) {
-      sRi[j * P + j] = 1.0 / sS[j * P + j];
-      for (int i = j - 1; i >= 0; --i) {
-        double acc = 0.0;
-        for (int k = i + 1; k <= j; ++k) acc += sS[i * P + k] * sRi[k * P + j];
-        sRi[i * P + j] = -acc / sS[i * P + i];
-      }
-    }
-  }
+  // Z = Y R^-1 row by row as the forward substitution z R = y (R upper):
+  //   z_c = (y_c - sum_{d<c} z_d R[d][c]) / R[c][c],
+  // P (P - 1) / 2 fp64 FMAs per row on broadcast LDS reads of R. Round 3 formed R^-1 first
+  // with one wave (a serial chain of dependent fp64 LDS round trips per column) and then
+  // multiplied by it (P^2 FMAs per row).
+  if (tid < P) sRi[tid] = 1.0 / sS[tid * P + tid];
   __syncthreads();
-  for (int i = tid; i < r; i += SS_THREADS) {  // z = y R^-1 (row times upper triangle)
+  for (int i = tid; i < r; i += SS_THREADS) {
     double z[P];
 #pragma unroll
-    for (int c = 0; c < P; ++c) z[c] = 0.0;
-#pragma unroll 1
-    for (int d = 0; d < P; ++d) {
-      const double yd = sY[i * P + d];
-      const double* rd = sRi + d * P;
+    for (int c = 0; c < P; ++c) z[c] = sY[i * P + c];
 #pragma unroll
-      for (int c = 0; c < P; ++c) z[c] = fma(yd, rd[c], z[c]);  // rd[c] = 0 for c < d
+    for (int d = 0; d < P; ++d) {  // pivot d: z_d final, eliminate it from the later columns
+      z[d] *= sRi[d];
+      const double* rd = sS + d * P;
+#pragma unroll
+      for (int c = d + 1; c < P; ++c) z[c] = fma(-z[d], rd[c], z[c]);
+      __builtin_amdgcn_sched_barrier(0);  // (one pivot row of R in flight: no hoisted reads)
     }
 #pragma unroll
     for (int c = 0; c < P; ++c) sZ[i * P + c] = (float)z[c];

@@ -37,6 +37,7 @@ enum Variant : int {
   V_CONVT_SHARED_RING, // convT1 row sweep: one shared input ring + per-step barrier (round 3)
   V_SVD_RECON_VALU,   // SVD reconstruction with scalar FMAs (round 3) instead of fp32 MFMA
   V_ROWS_SHORT_LEAD,  // convT rows / decoder3 producer: the round-3 ring refill lead (1 / 0 steps, not 3)
+  V_SVD_GRAM_F32,     // 128 < r <= 256 Gram on fp32 MFMA (round 3) instead of the fp16 hi/lo split
   V_COUNT
 };
 

@@ -321,6 +321,195 @@ __global__ __launch_bounds__(256, 2) void gram256_kernel(XView x, int K, int r, 
   }
 }
 
+// 128 < r <= 256, on the fp16 matrix cores. gram256_kernel runs at ~0.5 of the fp32 MFMA
+// peak (1.9 ms per 4096 C3 matrices, 7x the HBM time of reading X). Here every element is
+// split as 2^e x = hi + lo, two fp16 numbers (hi = fp16(2^e x), lo = fp16(2^e x - hi): 22
+// significant bits, the residual below 2^-22 |x|), and each 32x32 tile of G takes three
+// v_mfma_f32_32x32x16_f16 products per 16 rows, hi^T hi + hi^T lo + lo^T hi (the dropped
+// lo^T lo is below 2^-22 of the product), fp32 accumulation: the products' error is ~20x
+// below the fp32 Gram's own rounding (tools/gram_split_sim.py), at 16x the fp32 MFMA rate.
+// Scale: e is one per matrix, the running minimum of 15 - exponent(chunk max |x|), so every
+// scaled value stays below 2^15 (fp16 max 65504); when a chunk lowers e, the accumulators are
+// rescaled by 2^(2 de) (exact), and G = acc * 2^-2e at the end. Chunk = GS_KC = 16 rows of X:
+// thread t stages column t (16 values; rows past K and columns past r are zero), its wave's
+// max goes to LDS before the barrier that precedes the chunk's conversion, so the scale costs
+// no extra barrier. LDS holds hi and lo as [k-half][column][8 halves]: lane l's MFMA operand
+// for column panel p (A[i][k] = X[k][32p + i], B[k][j] = X[k][32p + j], the same fragment)
+// is one ds_read_b128 at [l >> 5][32p + (l & 31)], and the staging writes are 16 B per thread
+// at consecutive addresses (both conflict-free). Tiles: with panels A = 0..3 and B = 4..7,
+// wave 0 takes A x A (10 upper-triangle tiles), wave 1 B x B (10), waves 2 and 3 {0,1} x B
+// and {2,3} x B (8 each), so a wave holds 4 or 6 panels' fragments (32 / 48 VGPRs) instead
+// of all 8 (64: the 9-per-wave deal spilled at two waves per SIMD).
+constexpr int GS_KC = 16;
+__device__ constexpr int kGSTI[4][10] = {{0, 0, 0, 0, 1, 1, 1, 2, 2, 3},
+                                         {4, 4, 4, 4, 5, 5, 5, 6, 6, 7},
+                                         {0, 0, 0, 0, 1, 1, 1, 1, 0, 0},
+                                         {2, 2, 2, 2, 3, 3, 3, 3, 0, 0}};
+__device__ constexpr int kGSTJ[4][10] = {{0, 1, 2, 3, 1, 2, 3, 2, 3, 3},
+                                         {4, 5, 6, 7, 5, 6, 7, 6, 7, 7},
+                                         {4, 5, 6, 7, 4, 5, 6, 7, 0, 0},
+                                         {4, 5, 6, 7, 4, 5, 6, 7, 0, 0}};
+typedef _Float16 gs_f16x8 __attribute__((ext_vector_type(8)));
+typedef float gs_f32x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float wave_max64(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+template <int W>  // NT = tiles of this wave
+__device__ __forceinline__ void gram256s_wave(const XView& x, int K, int r, gs_f16x8* sH,
+                                              gs_f16x8* sL, float* sMax, float* Gb) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* X = x.base + (long long)blockIdx.x * x.batch_stride;
+  const bool rowmaj = x.si == 1;
+  const bool vec4 = !rowmaj && x.sk == 1 && (x.si & 3) == 0 && (x.batch_stride & 3) == 0 &&
+                    (reinterpret_cast<uintptr_t>(x.base) & 15) == 0;
+  const bool col_ok = tid < r;
+  const float* pc = X + (long long)(col_ok ? tid : 0) * x.si;
+  float v[GS_KC];
+  auto fetch = [&](int k0) {
+    if (!col_ok) {
+#pragma unroll
+      for (int kk = 0; kk < GS_KC; ++kk) v[kk] = 0.f;
+      return;
+    }
+    const float* p = pc + (long long)k0 * x.sk;
+    if (k0 + GS_KC <= K) {
+      if (vec4) {
+#pragma unroll
+        for (int u = 0; u < GS_KC / 4; ++u) {
+          const float4 q = *reinterpret_cast<const float4*>(p + 4 * u);
+          v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < GS_KC; ++kk) v[kk] = p[(long long)kk * x.sk];
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < GS_KC; ++kk) v[kk] = k0 + kk < K ? p[(long long)kk * x.sk] : 0.f;
+    }
+  };
+  auto post_max = [&]() {
+    float m = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < GS_KC; ++kk) m = fmaxf(m, fabsf(v[kk]));
+    m = wave_max64(m);
+    if (lane == 0) sMax[wave] = m;
+  };
+  constexpr int NT = W < 2 ? 10 : 8;
+  f32x16 acc[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) acc[q] = f32x16{};
+  int e_run = 110;  // lowered by the first chunk with a nonzero finite max
+  const int c = lane & 31, kh = lane >> 5;
+  fetch(0);
+  post_max();
+  for (int k0 = 0; k0 < K; k0 += GS_KC) {
+    __syncthreads();  // previous chunk consumed; the chunk's wave maxima visible
+    {
+      const float4 mw = *reinterpret_cast<const float4*>(sMax);
+      const float M = fmaxf(fmaxf(mw.x, mw.y), fmaxf(mw.z, mw.w));
+      if (M > 0.f && M <= 3.0e38f) {  // (Inf / NaN chunks keep the scale)
+        const int et = 15 - __builtin_amdgcn_frexp_expf(M);  // M * 2^et in [2^14, 2^15)
+        if (et < e_run) {  // wave-uniform
+          const int d = 2 * (max(et, -110) - e_run);
+#pragma unroll
+          for (int q = 0; q < NT; ++q)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) acc[q][j] = __builtin_ldexpf(acc[q][j], d);
+          e_run = max(et, -110);
+        }
+      }
+      gs_f32x8 y0, y1;
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        y0[kk] = __builtin_ldexpf(v[kk], e_run);
+        y1[kk] = __builtin_ldexpf(v[8 + kk], e_run);
+      }
+      const gs_f16x8 h0 = __builtin_convertvector(y0, gs_f16x8);
+      const gs_f16x8 h1 = __builtin_convertvector(y1, gs_f16x8);
+      const gs_f16x8 l0 = __builtin_convertvector(y0 - __builtin_convertvector(h0, gs_f32x8), gs_f16x8);
+      const gs_f16x8 l1 = __builtin_convertvector(y1 - __builtin_convertvector(h1, gs_f32x8), gs_f16x8);
+      sH[tid] = h0;
+      sH[256 + tid] = h1;
+      sL[tid] = l0;
+      sL[256 + tid] = l1;
+    }
+    __syncthreads();  // chunk visible; sMax read by every wave
+    const bool more = k0 + GS_KC < K;
+    if (more) fetch(k0 + GS_KC);
+    gs_f16x8 fh[8], fl[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      fh[p] = sH[256 * kh + 32 * p + c];
+      fl[p] = sL[256 * kh + 32 * p + c];
+    }
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+      acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[kGSTI[W][q]], fh[kGSTJ[W][q]],
+                                                      acc[q], 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+      acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[kGSTI[W][q]], fl[kGSTJ[W][q]],
+                                                      acc[q], 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+      acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fl[kGSTI[W][q]], fh[kGSTJ[W][q]],
+                                                      acc[q], 0, 0, 0);
+    if (more) post_max();  // (after the MFMAs: the loads had their time to land)
+  }
+  // D[row][col]: col = c, rows 4 kh + (reg & 3) + 8 (reg >> 2). The mirrored tile is stored as
+  // float4 runs: regs 4g .. 4g + 3 of a lane are four consecutive rows = four consecutive
+  // columns of G's row `col` (4 wide stores per tile instead of 16 single-word scatters).
+  const int ex = -2 * e_run;
+#pragma unroll
+  for (int q = 0; q < NT; ++q) {
+    const int ti = kGSTI[W][q], tj = kGSTJ[W][q];
+    const int col = tj * 32 + c;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int row0 = ti * 32 + 8 * g + 4 * kh;
+      float4 o;
+      o.x = __builtin_ldexpf(acc[q][4 * g], ex);
+      o.y = __builtin_ldexpf(acc[q][4 * g + 1], ex);
+      o.z = __builtin_ldexpf(acc[q][4 * g + 2], ex);
+      o.w = __builtin_ldexpf(acc[q][4 * g + 3], ex);
+      if (col < r) {
+        if (row0 + 3 < r && (r & 3) == 0) {
+          *reinterpret_cast<float4*>(Gb + (long long)col * r + row0) = o;
+        } else {
+          if (row0 < r) Gb[(long long)col * r + row0] = o.x;
+          if (row0 + 1 < r) Gb[(long long)col * r + row0 + 1] = o.y;
+          if (row0 + 2 < r) Gb[(long long)col * r + row0 + 2] = o.z;
+          if (row0 + 3 < r) Gb[(long long)col * r + row0 + 3] = o.w;
+        }
+        if (ti != tj) {
+          if (row0 < r) Gb[(long long)row0 * r + col] = o.x;
+          if (row0 + 1 < r) Gb[(long long)(row0 + 1) * r + col] = o.y;
+          if (row0 + 2 < r) Gb[(long long)(row0 + 2) * r + col] = o.z;
+          if (row0 + 3 < r) Gb[(long long)(row0 + 3) * r + col] = o.w;
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void gram256s_kernel(XView x, int K, int r, float* G) {
+  __shared__ __attribute__((aligned(16))) gs_f16x8 sH[2 * 256];
+  __shared__ __attribute__((aligned(16))) gs_f16x8 sL[2 * 256];
+  __shared__ __attribute__((aligned(16))) float sMax[4];
+  float* Gb = G + (long long)blockIdx.x * r * r;
+  switch (threadIdx.x >> 6) {
+    case 0: gram256s_wave<0>(x, K, r, sH, sL, sMax, Gb); break;
+    case 1: gram256s_wave<1>(x, K, r, sH, sL, sMax, Gb); break;
+    case 2: gram256s_wave<2>(x, K, r, sH, sL, sMax, Gb); break;
+    default: gram256s_wave<3>(x, K, r, sH, sL, sMax, Gb); break;
+  }
+}
+
 // ---------------------------------------------------------------- 2. subspace
 constexpr int SS_THREADS = 256;
 #ifndef SPECENH_SS_SINGLE_QR
@@ -2173,6 +2362,8 @@ void launch_gram(const XView& xv, int Kr, int r, float* G, long long batch, hipS
   const bool vec_ok = xv.si != 1 || (xv.sk % 4 == 0 && xv.batch_stride % 4 == 0 &&
                                      (reinterpret_cast<uintptr_t>(xv.base) & 15) == 0);
   const bool lds = r <= 128 && r % 4 == 0 && variant(V_SVD_GRAM_TILES) == 0;
+  const bool split = r > 128 && r <= 256 && variant(V_SVD_GRAM_TILES) == 0 &&
+                     variant(V_SVD_GRAM_F32) == 0;
   const bool lds256 = r > 128 && r <= 256 && r % 4 == 0 && vec_ok &&
                       variant(V_SVD_GRAM_TILES) == 0;
   const int nts = (r + 31) / 32;
@@ -2181,7 +2372,10 @@ void launch_gram(const XView& xv, int Kr, int r, float* G, long long batch, hipS
     const long long nb = std::min<long long>(65535, batch - b0);
     XView xb = xv;
     xb.base = xv.base + b0 * xv.batch_stride;
-    if (lds)
+    if (split)
+      SPECENH_LAUNCH(gram256s_kernel, dim3((unsigned)nb), dim3(256), 0, st, xb, Kr, r,
+                     G + b0 * (long long)r * r);
+    else if (lds)
       SPECENH_LAUNCH(gram_lds_kernel, dim3((unsigned)nb), dim3(256), 0, st, xb, Kr, r,
                          G + b0 * (long long)r * r);
     else if (lds256)

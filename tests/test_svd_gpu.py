@@ -248,10 +248,11 @@ def test_rank_deficient_complement(gpu_device):
 @pytest.mark.parametrize("shape", [(128, 128), (96, 128), (128, 40), (52, 100),
                                    (513, 256), (256, 513), (300, 200), (201, 132), (140, 301)])
 def test_gram_paths_agree(gpu_device, shape, kernel_variant):
-    """The LDS-chunked Grams (gram_lds_kernel for r <= 128, gram256_kernel for 128 < r <= 256:
-    row-major and transposed X, ragged chunks, odd K, r not a multiple of 32) and the
-    one-wave-per-tile Gram give the same reconstruction to fp32 rounding, and both match the
-    oracle on a gapped matrix. (513, 256) is BASELINE config 3's geometry."""
+    """The LDS-chunked Grams (gram_lds_kernel for r <= 128; for 128 < r <= 256 the fp16
+    hi/lo split gram256s_kernel and the fp32 gram256_kernel: row-major and transposed X,
+    ragged chunks, odd K, r not a multiple of 32) and the one-wave-per-tile Gram give the
+    same reconstruction to fp32 rounding, and all match the oracle on a gapped matrix.
+    (513, 256) is BASELINE config 3's geometry."""
     import os
     import sys
 
@@ -264,14 +265,59 @@ def test_gram_paths_agree(gpu_device, shape, kernel_variant):
     m, n = shape
     A = np.stack([gapped_matrix(700 + i, m, n, dtype=np.float32) for i in range(3)])
     outs = []
-    for flag in ("0", "1"):
-        kernel_variant("SVD_GRAM_TILES", int(flag))
+    for tiles, f32 in ((0, 0), (1, 0), (0, 1)):
+        kernel_variant("SVD_GRAM_TILES", tiles)
+        kernel_variant("SVD_GRAM_F32", f32)
         outs.append(svd.denoise_batch(torch.as_tensor(A, device=gpu_device), 0, 16).double().cpu().numpy())
     for b in range(3):
         truth = ref.denoiseSignal(A[b].astype(np.float64), 0, 16)
-        assert _rel(outs[0][b], truth) <= TOL
-        assert _rel(outs[1][b], truth) <= TOL
-        assert _rel(outs[0][b], outs[1][b]) <= 1e-6
+        for o in outs:
+            assert _rel(o[b], truth) <= TOL
+        assert _rel(outs[1][b], outs[2][b]) <= 1e-6  # fp32 Grams: same products, other order
+        # the split Gram (default; other arithmetic) no further from the truth than fp32's
+        assert _rel(outs[0][b], truth) <= _rel(outs[2][b], truth) + 1e-6
+
+
+@pytest.mark.parametrize("case", ["tiny", "huge", "late_rows", "zero_head", "col_range",
+                                  "transposed_rows"])
+def test_split_gram_scale(gpu_device, case, kernel_variant):
+    """gram256s_kernel's running power-of-two scale (fp16 hi/lo split, 128 < r <= 256): the
+    reconstruction matches float64 numpy and the fp32 Gram path for magnitudes far outside
+    fp16's range (1e-15, 1e15), rows that grow 1e6-fold after the first chunks (accumulators
+    rescaled mid-matrix), leading all-zero chunks, and columns 1e-4 / 1e4 apart."""
+    import os
+    import sys
+
+    import torch
+
+    from specenh import svd
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import gapped_matrix
+
+    m, n = (256, 300) if case == "transposed_rows" else (300, 200)
+    A = np.stack([gapped_matrix(900 + i, m, n) for i in range(2)])
+    if case == "tiny":
+        A = A * 1e-15
+    elif case == "huge":
+        A = A * 1e15
+    elif case == "late_rows":  # the first 40 rows 1e-6 of the rest: rescale in chunk 3
+        A[:, :40] *= 1e-6
+    elif case == "zero_head":
+        A[:, :37] = 0.0
+    elif case == "col_range":  # (row scalings keep the rank-16 + noise gap; so do these)
+        A[:, :, ::2] *= 1e4
+        A[:, :, 1::2] *= 1e-4
+    elif case == "transposed_rows":  # m < n: X = A^T, K = 300 rows of X are A's columns
+        A[:, :, 100:] *= 1e5
+    A = A.astype(np.float32)
+    outs = []
+    for f32 in (0, 1):
+        kernel_variant("SVD_GRAM_F32", f32)
+        outs.append(svd.denoise_batch(torch.as_tensor(A, device=gpu_device), 0, 16).double().cpu().numpy())
+    for b in range(2):
+        truth = ref.denoiseSignal(A[b].astype(np.float64), 0, 16)
+        assert _rel(outs[0][b], truth) <= TOL, (case, b, _rel(outs[0][b], truth))
+        assert _rel(outs[0][b], truth) <= max(2 * _rel(outs[1][b], truth), 1e-6), case
 
 
 @pytest.mark.parametrize("args", [(), (0, 16), (0, 10_000), (5, 2)])

@@ -742,11 +742,12 @@ __device__ void cholqr(const float* sY, float* sZ, int r, double* sS, double* sR
 // LDS, one wave: each round rotates P/2 disjoint (a, b) pairs at once; Q accumulates
 // the eigenvectors. Angles in fp64.
 template <int P>
-__device__ void jacobi(float* sH, float* sQ, float* sCS, int* sPair) {
+__device__ int jacobi(float* sH, float* sQ, float* sCS, int* sPair) {  // -> sweeps run
   const int lane = threadIdx.x;  // wave 0
   for (int idx = lane; idx < P * P; idx += 64) sQ[idx] = (idx / P == idx % P) ? 1.f : 0.f;
   wave_lds_sync();
-  for (int sweep = 0; sweep < 15; ++sweep) {
+  int sweep = 0;
+  for (; sweep < 15; ++sweep) {
     double off = 0.0, diag = 0.0;
     for (int idx = lane; idx < P * P; idx += 64) {
       const double h = sH[idx];
@@ -830,6 +831,7 @@ __device__ void jacobi(float* sH, float* sQ, float* sCS, int* sPair) {
       wave_lds_sync();
     }
   }
+  return sweep;
 }
 
 // P = 8 adds the prod8 scratch ([4][64] doubles after sRi) and gemm_GZ8's sT (r x 8).
@@ -872,6 +874,20 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
   const long long b = blockIdx.x;
   const float* Gb = G + b * (long long)r * r;
   const int tid = threadIdx.x;
+#ifdef SPECENH_SS_STATS  // development build (tools/ss_stats.py): shader clocks per phase
+  long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
+  int sweeps = 0;
+#define SS_MARK(slot)                                    \
+  do {                                                   \
+    const long long now_ = __builtin_amdgcn_s_memtime(); \
+    tacc[slot] += now_ - tlast;                          \
+    tlast = now_;                                        \
+  } while (0)
+#else
+#define SS_MARK(slot) \
+  do {                \
+  } while (0)
+#endif
 
   auto GZ = [&](const float* z, float* y) {
     if constexpr (P == 8) gemm_GZ8(Gb, r, z, y, sT);
@@ -883,6 +899,7 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
   __syncthreads();
   GZ(sZ, sY);
   __syncthreads();
+  SS_MARK(0);
   auto bsum = [&](double v) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
@@ -911,14 +928,18 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
         // re-amplifies the dominant directions anyway): one CholeskyQR pass. The basis
         // that feeds the Rayleigh-Ritz step below gets the full CholeskyQR2.
         cholqr<P>(sY, sZ, r, sS, sRi);  // Z = orth(Y) to ~cond(Y) * eps
+        SS_MARK(1);
         GZ(sZ, sY);                     // Y = G Z
         __syncthreads();
+        SS_MARK(2);
         continue;
       }
       cholqr<P>(sY, sZ, r, sS, sRi);  // Z = orth(Y)
       cholqr<P>(sZ, sY, r, sS, sRi);  // second pass into Y ...
+      SS_MARK(1);
       GZ(sY, sZ);                     // ... Z = G * orth(Y)
       __syncthreads();
+      SS_MARK(2);
       // swap names: basis in sY, product in sZ -> keep (Y := product, Z := basis)
       float* t = sY;
       sY = sZ;
@@ -942,7 +963,11 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
       }
     }
     __syncthreads();
+    SS_MARK(3);
     if (tid < 64) {
+#ifdef SPECENH_SS_STATS
+      sweeps +=
+#endif
       jacobi<P>(sH, sQ, sCS, sPair);
       if (tid == 0) {  // sort Ritz values descending (insertion sort, P <= 64)
         for (int c = 0; c < P; ++c) sOrd[c] = c;
@@ -958,6 +983,7 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
       }
     }
     __syncthreads();
+    SS_MARK(4);
     bad = 0;
     if (flags) {
       for (int which = 0; which < 2; ++which) {
@@ -982,6 +1008,7 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
         if (!(sqrt(fmax(th, 0.0)) * res <= (double)tolv * gap * sqrt(fmax(tr, 0.0)))) bad = 1;
       }
     }
+    SS_MARK(5);
     if (!bad || stage1 >= iters) break;  // uniform: converged, or no second stage
   }
   if (flags && tid == 0) flags[b] = bad;
@@ -995,6 +1022,16 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
     Vb[(long long)i * K + c] = (float)s;
   }
   if (tid < K) theta[b * K + tid] = sH[sOrd[tid] * P + sOrd[tid]];
+#ifdef SPECENH_SS_STATS  // (into this matrix's Gram: dead once V is out, no flagged reruns here)
+  SS_MARK(6);
+  __syncthreads();
+  if (tid == 0) {
+    long long* o = reinterpret_cast<long long*>(const_cast<float*>(Gb));
+    for (int q = 0; q < 7; ++q) o[q] = tacc[q];
+    o[7] = sweeps;
+  }
+#endif
+#undef SS_MARK
 }
 
 // ---------------------------------------------------------------- 3. reconstruction
@@ -1222,6 +1259,151 @@ __global__ __launch_bounds__(256) void recon_mfma_kernel(XView x, int Kr, int r,
       if (row < rows && col < r) {
         const float v = complement ? sX[row * PX + col] - acc[j] : acc[j];
         Ob[(long long)(k0 + row) * osk + (long long)col * osi] = to_out<TO>(v);
+      }
+    }
+  }
+}
+
+// recon_stream_kernel: recon_mfma_kernel's two products, with a workgroup walking a run of
+// `bps` consecutive row blocks of one matrix (all of them when the batch fills the chip:
+// C3's 4096 matrices, 17 blocks each). recon_mfma_kernel's workgroups each staged V (16 KB at
+// K = 16, half the X block's bytes) and one X block, then computed, then stored: nothing in
+// flight while computing, ~2 workgroups per CU, 4.3x the HBM time of reading X and writing
+// the output. Here V is staged once per run, and the next X block's loads are issued before
+// the current block's products, so they are in flight behind the MFMAs and the stores.
+// Staging without run-time divisions: row-major X (TRANS = false) as float4s, thread t ->
+// float4 column t & 63 of rows t >> 6, + 4, ... (8 per block; columns >= r zero); transposed X
+// (TRANS, X[k][i] = base[k + i si]) as thread t -> column t, 32 consecutive k (float4s when
+// aligned). Phase 2's tiles put the output's contiguous direction along the lanes: D = Y V^T
+// tiles for row-major output, D = V Y^T (the same two LDS operands, swapped) for transposed.
+template <int KP, typename TO, bool TRANS>
+__global__ __launch_bounds__(256, 2) void recon_stream_kernel(
+    XView x, int Kr, int r, const float* V, int K, int lo, int hi, int complement,
+    const int* only, TO* out, long long out_bstride, long long osk, long long osi, int bps) {
+  constexpr int NT = (KP + 15) / 16, KPP = 16 * NT, PV = KPP + 1, PY = KPP + 1;
+  constexpr int KS = 2 * NT < 4 ? 2 : 1;  // K split of phase 1
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int RP = (r + 15) & ~15, PX = RP + 2;
+  float* sV = reinterpret_cast<float*>(smem);  // RP x PV
+  float* sX = sV + RP * PV;                     // RB x PX
+  float* sY = sX + RB * PX;                     // KS x RB x PY
+  const long long b = blockIdx.y;
+  if (only && !only[b]) return;
+  const int nblk = (Kr + RB - 1) / RB;
+  const int blk0 = blockIdx.x * bps, blk1 = min(nblk, blk0 + bps);
+  if (blk0 >= blk1) return;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int cl = lane & 15, kr = lane >> 4;
+  const float* X = x.base + b * x.batch_stride;
+  const float* Vb = V + b * (long long)r * K;
+  for (int idx = tid; idx < RP * KPP; idx += 256) {  // (KPP: a power-of-two multiple of 16)
+    const int i = idx / KPP, c = idx % KPP;
+    sV[i * PV + c] = (i < r && c >= lo && c < hi) ? Vb[(long long)i * K + c] : 0.f;
+  }
+  float4 st[8];
+  const bool vec_t = TRANS && (x.si & 3) == 0 && (x.batch_stride & 3) == 0 &&
+                     (reinterpret_cast<uintptr_t>(x.base) & 15) == 0;
+  auto fetch = [&](int k0) {
+    const int rows = min(RB, Kr - k0);
+    if constexpr (!TRANS) {
+      const int c4 = tid & 63, rs = tid >> 6;
+      const bool cv = 4 * c4 < r;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int kk = rs + 4 * u;
+        st[u] = (cv && kk < rows)
+                    ? *reinterpret_cast<const float4*>(X + (long long)(k0 + kk) * x.sk + 4 * c4)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else {
+      const float* p = X + (long long)(tid < r ? tid : 0) * x.si + k0;
+      if (vec_t && rows == RB && tid < r) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) st[u] = *reinterpret_cast<const float4*>(p + 4 * u);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          float e[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) e[q] = (tid < r && 4 * u + q < rows) ? p[4 * u + q] : 0.f;
+          st[u] = make_float4(e[0], e[1], e[2], e[3]);
+        }
+      }
+    }
+  };
+  auto stage = [&]() {
+    if constexpr (!TRANS) {
+      const int c4 = tid & 63, rs = tid >> 6;
+      if (4 * c4 < RP) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          float* d = sX + (rs + 4 * u) * PX + 4 * c4;  // (PX even: 8-byte aligned)
+          *reinterpret_cast<float2*>(d) = make_float2(st[u].x, st[u].y);
+          *reinterpret_cast<float2*>(d + 2) = make_float2(st[u].z, st[u].w);
+        }
+      }
+    } else if (tid < RP) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        sX[(4 * u) * PX + tid] = st[u].x;
+        sX[(4 * u + 1) * PX + tid] = st[u].y;
+        sX[(4 * u + 2) * PX + tid] = st[u].z;
+        sX[(4 * u + 3) * PX + tid] = st[u].w;
+      }
+    }
+  };
+  TO* Ob = out + b * out_bstride;
+  const int nit = RP / 16;
+  fetch(blk0 * RB);
+  for (int blk = blk0; blk < blk1; ++blk) {
+    const int k0 = blk * RB, rows = min(RB, Kr - k0);
+    __syncthreads();  // the previous block's products are done with sX / sY (and sV staged)
+    stage();
+    __syncthreads();
+    if (blk + 1 < blk1) fetch(k0 + RB);  // in flight behind this block's products
+    // ---- phase 1: Y = X_blk V
+    {
+      const int klen = RP / KS;
+      for (int t = wave; t < 2 * NT * KS; t += 4) {
+        const int tile = t % (2 * NT), part = t / (2 * NT);
+        const int rt = tile & 1, ct = tile >> 1;
+        const float* a_p = sX + (16 * rt + cl) * PX + part * klen + kr;
+        const float* b_p = sV + (part * klen + kr) * PV + 16 * ct + cl;
+        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < klen; k += 4)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a_p[k], b_p[k * PV], acc, 0, 0, 0);
+        float* yp = sY + part * RB * PY + (16 * rt + 4 * kr) * PY + 16 * ct + cl;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) yp[j * PY] = acc[j];
+      }
+    }
+    __syncthreads();
+    if constexpr (KS == 2) {
+      for (int e = tid; e < RB * KPP; e += 256) {
+        const int row = e / KPP, c = e % KPP;
+        sY[row * PY + c] += sY[RB * PY + row * PY + c];
+      }
+      __syncthreads();
+    }
+    // ---- phase 2: out = [X_blk -] Y V^T
+    for (int t = wave; t < 2 * nit; t += 4) {
+      const int rt = t & 1, it = t >> 1;
+      const float* y_p = sY + (16 * rt + cl) * PY + kr;
+      const float* v_p = sV + (16 * it + cl) * PV + kr;
+      f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < KPP; k += 4)
+        acc = TRANS ? __builtin_amdgcn_mfma_f32_16x16x4f32(v_p[k], y_p[k], acc, 0, 0, 0)
+                    : __builtin_amdgcn_mfma_f32_16x16x4f32(y_p[k], v_p[k], acc, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = TRANS ? 16 * rt + cl : 16 * rt + 4 * kr + j;
+        const int col = TRANS ? 16 * it + 4 * kr + j : 16 * it + cl;
+        if (row < rows && col < r) {
+          const float v = complement ? sX[row * PX + col] - acc[j] : acc[j];
+          Ob[(long long)(k0 + row) * osk + (long long)col * osi] = to_out<TO>(v);
+        }
       }
     }
   }
@@ -2425,6 +2607,32 @@ hipError_t launch_recon_t(XView xb, int Kr, int r, const float* V, int K, int lo
     const int RP = (r + 15) & ~15;
     const size_t lm = ((size_t)RP * (KPP + 1) + (size_t)RB * (RP + 2) +
                        (size_t)KS * RB * (KPP + 1)) * 4;
+    // runs of row blocks per workgroup: row-major X with 16-byte rows, or transposed X
+    const bool rowmaj16 = xb.si == 1 && r % 4 == 0 && xb.sk % 4 == 0 &&
+                          xb.batch_stride % 4 == 0 && (reinterpret_cast<uintptr_t>(xb.base) & 15) == 0;
+    const bool trans = xb.sk == 1 && xb.si != 1;
+    if (lm <= 160 * 1024 && r <= 256 && (rowmaj16 || trans) &&
+        variant(V_SVD_RECON_BLOCKS) == 0) {
+      const int nblk = (Kr + RB - 1) / RB;
+      // enough workgroups for ~4 per CU, each a run of consecutive blocks of one matrix
+      const long long want = 4LL * device_cus();
+      const int segs = (int)std::max(1LL, std::min<long long>(nblk, (want + nb - 1) / nb));
+      const int bps = (nblk + segs - 1) / segs;
+      const int grid_x = (nblk + bps - 1) / bps;
+      const void* kfn = trans ? (const void*)recon_stream_kernel<KP, TO, true>
+                              : (const void*)recon_stream_kernel<KP, TO, false>;
+      hipError_t e = hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lm);
+      if (e != hipSuccess) return e;
+      if (trans)
+        SPECENH_LAUNCH((recon_stream_kernel<KP, TO, true>), dim3(grid_x, (unsigned)nb), dim3(256),
+                       lm, st, xb, Kr, r, V, K, lo, hi, comp, only, reinterpret_cast<TO*>(out),
+                       ob, osk, osi, bps);
+      else
+        SPECENH_LAUNCH((recon_stream_kernel<KP, TO, false>), dim3(grid_x, (unsigned)nb), dim3(256),
+                       lm, st, xb, Kr, r, V, K, lo, hi, comp, only, reinterpret_cast<TO*>(out),
+                       ob, osk, osi, bps);
+      return hipGetLastError();
+    }
     if (lm <= 160 * 1024) {
       hipError_t e = hipFuncSetAttribute((const void*)recon_mfma_kernel<KP, TO>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lm);

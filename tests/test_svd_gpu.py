@@ -346,10 +346,11 @@ def test_half_precision_output_is_rounded_fp32(gpu_device, args):
 @pytest.mark.parametrize("m,n", [(513, 256), (100, 72), (48, 64), (130, 200), (256, 100)])
 @pytest.mark.parametrize("rng_k", [(None, None), (0, 16), (2, 30), (0, 40)])
 def test_recon_mfma_matches_scalar_recon(gpu_device, kernel_variant, m, n, rng_k):
-    """recon_mfma_kernel (fp32 matrix cores, default) vs recon_kernel (scalar FMAs,
-    SVD_RECON_VALU=1): the same subspace, products summed in another order — equal to fp32
-    rounding (1e-6 relative Frobenius), across both orientations, r not a multiple of 16 and
-    kept ranges that need 8 .. 48 padded columns."""
+    """The matrix-core reconstructions — recon_stream_kernel (default: runs of row blocks per
+    workgroup) and recon_mfma_kernel (SVD_RECON_BLOCKS=1: one block per workgroup) — vs
+    recon_kernel (scalar FMAs, SVD_RECON_VALU=1): the same subspace, products summed in another
+    order — equal to fp32 rounding (1e-6 relative Frobenius), across both orientations, r not
+    a multiple of 16 and kept ranges that need 8 .. 48 padded columns."""
     import os
     import sys
 
@@ -364,15 +365,50 @@ def test_recon_mfma_matches_scalar_recon(gpu_device, kernel_variant, m, n, rng_k
         pytest.skip("range beyond the rank")
     A = np.stack([gapped_matrix(900 + i, m, n, k=min(48, r - 2)) for i in range(5)]).astype(np.float32)
     At = torch.as_tensor(A, device=gpu_device)
+    outs, names = [], []
+    for var in (None, "SVD_RECON_BLOCKS", "SVD_RECON_VALU"):
+        if var:
+            kernel_variant(var, 1)
+        n0 = _lib.launch_count()
+        outs.append(svd.denoise_batch(At, start, stop).double().cpu().numpy())
+        names.append(" ".join(_lib.kernel_names(n0, _lib.launch_count())))
+    if "12recon_kernel" in names[2]:  # (top-1 / eigen paths have no subspace reconstruction)
+        assert "recon_stream_kernel" in names[0] and "recon_mfma_kernel" in names[1]
+    for a in outs[:2]:
+        for i in range(len(A)):
+            e = np.linalg.norm(a[i] - outs[2][i]) / max(np.linalg.norm(outs[2][i]), 1e-30)
+            assert e <= 1e-6, (i, e)
+
+
+@pytest.mark.parametrize("m,n", [(513, 256), (256, 300), (300, 132)])
+@pytest.mark.parametrize("rng_k", [(None, None), (0, 16)])
+def test_recon_stream_runs(gpu_device, kernel_variant, m, n, rng_k):
+    """A batch that fills the chip (1100 matrices: 5 distinct ones tiled) puts every row block
+    of a matrix in one recon_stream_kernel workgroup (V staged once, the next block's loads in
+    flight): equal to recon_mfma_kernel's one-block workgroups — bitwise for row-major X (the
+    same products per block), to 1e-6 for transposed X (MFMA operands swapped) — and every
+    copy of a matrix gets the same output."""
+    import os
+    import sys
+
+    import torch
+
+    from specenh import _lib, svd
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import gapped_matrix
+    A = np.stack([gapped_matrix(950 + i, m, n) for i in range(5)]).astype(np.float32)
+    At = torch.as_tensor(np.tile(A, (220, 1, 1)), device=gpu_device)
     n0 = _lib.launch_count()
-    a = svd.denoise_batch(At, start, stop).double().cpu().numpy()
-    names = " ".join(_lib.kernel_names(n0, _lib.launch_count()))
-    kernel_variant("SVD_RECON_VALU", 1)
-    n1 = _lib.launch_count()
-    b = svd.denoise_batch(At, start, stop).double().cpu().numpy()
-    names_b = " ".join(_lib.kernel_names(n1, _lib.launch_count()))
-    if "12recon_kernel" in names_b:  # (top-1 / eigen paths have no subspace reconstruction)
-        assert "recon_mfma_kernel" in names and "recon_mfma_kernel" not in names_b
-    for i in range(len(A)):
-        e = np.linalg.norm(a[i] - b[i]) / max(np.linalg.norm(b[i]), 1e-30)
-        assert e <= 1e-6, (i, e)
+    a = svd.denoise_batch(At, *rng_k)
+    assert "recon_stream_kernel" in " ".join(_lib.kernel_names(n0, _lib.launch_count()))
+    kernel_variant("SVD_RECON_BLOCKS", 1)
+    b = svd.denoise_batch(At, *rng_k)
+    if m >= n:
+        assert torch.equal(a, b)
+    else:
+        assert float((a - b).norm() / b.norm()) <= 1e-6
+    a5 = a.view(220, 5, m, n)
+    assert torch.equal(a5, a5[:1].expand_as(a5))
+    for i in range(5):
+        truth = ref.denoiseSignal(A[i].astype(np.float64), *[v for v in rng_k if v is not None])
+        assert _rel(a[i].double().cpu().numpy(), truth) <= TOL

@@ -322,7 +322,7 @@ def c3_matrices(dev, B=4096, m=513, n=256, k=16, seed=3):
     return A
 
 
-def svd_c3_stage(dev, B=4096, m=513, n=256, k=16, reps=5):
+def svd_c3_stage(dev, B=4096, m=513, n=256, k=16, reps=5, pmc=None):
     """BASELINE config 3: denoiseSignal on 4096 gapped 513 x 256 fp32 matrices, rank-16
     (start 0, stop 16) and the default (1, r). Matrices: 16 signal components 10 * 0.8^i
     along random orthonormal directions + Gaussian noise of
@@ -331,7 +331,7 @@ def svd_c3_stage(dev, B=4096, m=513, n=256, k=16, reps=5):
     (SURVEY §8 d C3): 2mn^2 + 4mnk = 75.6 MFLOP per matrix at the fp32 MFMA peak; HBM floor
     8mn bytes (read A, write the reconstruction)."""
     import torch
-    from specenh import svd
+    from specenh import _lib, svd
     A = c3_matrices(dev, B, m, n, k)
     out = torch.empty_like(A)
     st = torch.cuda.current_stream(dev)
@@ -339,7 +339,9 @@ def svd_c3_stage(dev, B=4096, m=513, n=256, k=16, reps=5):
     flop = 2.0 * m * n * n + 4.0 * m * n * k
     for name, (lo, hi) in {"rank16": (0, 16), "default": (None, None)}.items():
         for _ in range(2):
+            c0 = _lib.launch_count()
             svd.denoise_batch(A, lo, hi, out=out)
+            syms = _lib.kernel_names(c0, _lib.launch_count())
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
         for _ in range(reps):
@@ -364,7 +366,13 @@ def svd_c3_stage(dev, B=4096, m=513, n=256, k=16, reps=5):
                "matrices": 6, "reference": "numpy float64 thin SVD of the same fp32 matrices"}
         if not acc["pass"]:
             print(f"[bench] C3 {name} ACCURACY CHECK FAILED: {max(rels):.3e}", file=sys.stderr)
+        # measured HBM bytes of the whole denoise call (tools/pmc_refresh.sh c3), vs the
+        # 8 m n B floor of reading A and writing the reconstruction
+        tr, why = pmc_traffic(pmc or {}, "c3", f"svd_c3_{name}", syms, B)
         res[name] = {"ms": ms, "matrices_per_s": B / (ms * 1e-3), "accuracy": acc,
+                     "kernels": sorted(set(syms), key=syms.index),
+                     "traffic": tr, "traffic_floor": 8.0 * m * n * B,
+                     **({"traffic_note": why} if why else {}),
                      "roofline": {"bound": "mfma_fp32", "achieved": ach,
                                   "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                                   "frac": ach / FP32_MFMA_PEAK_TFLOPS,
@@ -813,7 +821,7 @@ def main():
                          "frac": achc / HBM_PEAK_GBPS, "alg_bytes_per_launch": algc,
                          "traffic": trc, "traffic_note": whyc}}
         del x2, oc
-        stages["svd_c3"] = svd_c3_stage(dev)
+        stages["svd_c3"] = svd_c3_stage(dev, pmc=pmc)
         stages["ae_train_c4"] = c4
         stages["c5_host_stream"] = c5_host_stream_stage(dev, lambda: make_c5_engine(dev))
 

@@ -685,6 +685,14 @@ __device__ void prodP(const float* sA, const float* sB, int r, double* out) {
   __syncthreads();
 }
 
+// lane `src`'s v (wave-uniform src, a compile-time constant at the call sites)
+__device__ __forceinline__ double readlane_f64(double v, int src) {
+  const long long u = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)u, src);
+  const int hi = __builtin_amdgcn_readlane((int)(u >> 32), src);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
 // Orthonormalise the columns of Y (r x P, LDS) into Z with CholeskyQR in fp64:
 // S = Y^T Y, S = R^T R, Z = Y R^-1. fp64 keeps the Gram of Y (condition up to ~1e12
 // here) factorisable; callers run it twice (CholeskyQR2) for fp32-level orthogonality.
@@ -697,7 +705,7 @@ __device__ void cholqr(const float* sY, float* sZ, int r, double* sS, double* sR
     prodP<P>(sY, sY, r, sS);  // (full P x P; the factorisation reads the upper triangle)
   }
   __syncthreads();
-  if (tid < 64) {  // Cholesky S = R^T R (R upper, in place), one wave
+  if (tid < 64 && P > 24) {  // Cholesky S = R^T R (R upper, in place), one wave, in LDS
     for (int k = 0; k < P; ++k) {
       double d = sS[k * P + k];
       d = d > 0.0 ? sqrt(d) : 1e-300;  // rank-deficient: keep going, column ~ 0
@@ -712,6 +720,28 @@ __device__ void cholqr(const float* sY, float* sZ, int r, double* sS, double* sR
       }
       wave_lds_sync();
     }
+  } else if (tid < 64) {  // P <= 24: the same factorisation in registers, lane j holding
+                          // column j of S; row k of R reaches the lanes by readlane (no LDS
+                          // round trips or wave syncs per pivot; larger P would spill)
+    const int j = tid;
+    double col[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) col[i] = (j < P && i <= j) ? sS[i * P + j] : 0.0;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      double d = readlane_f64(col[k], k);
+      d = d > 0.0 ? sqrt(d) : 1e-300;  // rank-deficient: keep going, column ~ 0
+      col[k] = j == k ? d : col[k] / d;  // row k of R (lanes j > k; j < k hold zeros)
+#pragma unroll
+      for (int i = k + 1; i < P; ++i) {  // trailing S[i][j] -= R[k][i] R[k][j], j >= i
+        const double rki = readlane_f64(col[k], i);
+        if (j >= i) col[i] -= rki * col[k];
+      }
+    }
+    if (j < P)
+#pragma unroll
+      for (int i = 0; i < P; ++i)
+        if (i <= j) sS[i * P + j] = col[i];
   }
   // Z = Y R^-1 row by row as the forward substitution z R = y (R upper):
   //   z_c = (y_c - sum_{d<c} z_d R[d][c]) / R[c][c],
@@ -798,36 +828,44 @@ __device__ int jacobi(float* sH, float* sQ, float* sCS, int* sPair) {  // -> swe
           if (a > b) { const int t = a; a = b; b = t; }
         }
       };
+      // (each pass reads all its items before writing any: the items touch disjoint
+      // elements, and the compiler, unable to prove that, kept every item's reads behind
+      // the previous item's writes — NIT dependent LDS round trips per pass)
+      int ia[NIT], ib[NIT], ik[NIT];
+      float cc[NIT], ss[NIT], xa[NIT], xb[NIT], qa[NIT], qb[NIT];
 #pragma unroll
       for (int u = 0; u < NIT; ++u) {  // rows a, b of every pair
         const int idx = lane + 64 * u;
-        if (idx < (P / 2) * P) {
-          const int j = idx / P, k = idx % P;
-          int a, b;
-          pair_of(j, a, b);
-          const float c = sCS[2 * j], s = sCS[2 * j + 1];
-          const float xa = sH[a * P + k], xb = sH[b * P + k];
-          sH[a * P + k] = c * xa - s * xb;
-          sH[b * P + k] = s * xa + c * xb;
-        }
+        const int j = idx < (P / 2) * P ? idx / P : 0;
+        ik[u] = idx % P;
+        pair_of(j, ia[u], ib[u]);
+        cc[u] = sCS[2 * j];
+        ss[u] = sCS[2 * j + 1];
+        xa[u] = sH[ia[u] * P + ik[u]];
+        xb[u] = sH[ib[u] * P + ik[u]];
       }
+#pragma unroll
+      for (int u = 0; u < NIT; ++u)
+        if (lane + 64 * u < (P / 2) * P) {
+          sH[ia[u] * P + ik[u]] = cc[u] * xa[u] - ss[u] * xb[u];
+          sH[ib[u] * P + ik[u]] = ss[u] * xa[u] + cc[u] * xb[u];
+        }
       wave_lds_sync();
 #pragma unroll
       for (int u = 0; u < NIT; ++u) {  // columns a, b; Q columns
-        const int idx = lane + 64 * u;
-        if (idx < (P / 2) * P) {
-          const int j = idx / P, k = idx % P;
-          int a, b;
-          pair_of(j, a, b);
-          const float c = sCS[2 * j], s = sCS[2 * j + 1];
-          const float xa = sH[k * P + a], xb = sH[k * P + b];
-          sH[k * P + a] = c * xa - s * xb;
-          sH[k * P + b] = s * xa + c * xb;
-          const float qa = sQ[k * P + a], qb = sQ[k * P + b];
-          sQ[k * P + a] = c * qa - s * qb;
-          sQ[k * P + b] = s * qa + c * qb;
-        }
+        xa[u] = sH[ik[u] * P + ia[u]];
+        xb[u] = sH[ik[u] * P + ib[u]];
+        qa[u] = sQ[ik[u] * P + ia[u]];
+        qb[u] = sQ[ik[u] * P + ib[u]];
       }
+#pragma unroll
+      for (int u = 0; u < NIT; ++u)
+        if (lane + 64 * u < (P / 2) * P) {
+          sH[ik[u] * P + ia[u]] = cc[u] * xa[u] - ss[u] * xb[u];
+          sH[ik[u] * P + ib[u]] = ss[u] * xa[u] + cc[u] * xb[u];
+          sQ[ik[u] * P + ia[u]] = cc[u] * qa[u] - ss[u] * qb[u];
+          sQ[ik[u] * P + ib[u]] = ss[u] * qa[u] + cc[u] * qb[u];
+        }
       wave_lds_sync();
     }
   }
@@ -969,17 +1007,23 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
       sweeps +=
 #endif
       jacobi<P>(sH, sQ, sCS, sPair);
-      if (tid == 0) {  // sort Ritz values descending (insertion sort, P <= 64)
-        for (int c = 0; c < P; ++c) sOrd[c] = c;
-        for (int c = 1; c < P; ++c) {
-          const int key = sOrd[c];
-          int d = c - 1;
-          while (d >= 0 && sH[sOrd[d] * P + sOrd[d]] < sH[key * P + key]) {
-            sOrd[d + 1] = sOrd[d];
-            --d;
-          }
-          sOrd[d + 1] = key;
+      // Ritz values descending, ties in index order (a stable sort), as ranks: lane c counts
+      // the values ahead of its own (thread 0's insertion sort was a serial chain of LDS
+      // reads); NaN sorts last
+      wave_lds_sync();
+      if (tid < P) {
+        auto key = [&](int c) {
+          const float v = sH[c * P + c];
+          return v == v ? v : -INFINITY;
+        };
+        const float t = key(tid);
+        int rank = 0;
+#pragma unroll
+        for (int d = 0; d < P; ++d) {
+          const float u = key(d);
+          rank += (u > t || (u == t && d < tid)) ? 1 : 0;
         }
+        sOrd[rank] = tid;
       }
     }
     __syncthreads();
@@ -1301,11 +1345,12 @@ __global__ __launch_bounds__(256, 2) void recon_stream_kernel(
     const int i = idx / KPP, c = idx % KPP;
     sV[i * PV + c] = (i < r && c >= lo && c < hi) ? Vb[(long long)i * K + c] : 0.f;
   }
-  float4 st[8];
+  float4 stA[8], stB[8];  // two blocks in flight: the next two blocks' X
   const bool vec_t = TRANS && (x.si & 3) == 0 && (x.batch_stride & 3) == 0 &&
                      (reinterpret_cast<uintptr_t>(x.base) & 15) == 0;
-  auto fetch = [&](int k0) {
-    const int rows = min(RB, Kr - k0);
+  // rows = 0: no loads (zeros), so a refill past the run is a predicated no-op rather than
+  // a branch around the loads (a conditional refill keeps the batches out of registers)
+  auto fetch = [&](float4 (&st)[8], int k0, int rows) {
     if constexpr (!TRANS) {
       const int c4 = tid & 63, rs = tid >> 6;
       const bool cv = 4 * c4 < r;
@@ -1332,7 +1377,7 @@ __global__ __launch_bounds__(256, 2) void recon_stream_kernel(
       }
     }
   };
-  auto stage = [&]() {
+  auto stage = [&](const float4 (&st)[8]) {
     if constexpr (!TRANS) {
       const int c4 = tid & 63, rs = tid >> 6;
       if (4 * c4 < RP) {
@@ -1355,13 +1400,13 @@ __global__ __launch_bounds__(256, 2) void recon_stream_kernel(
   };
   TO* Ob = out + b * out_bstride;
   const int nit = RP / 16;
-  fetch(blk0 * RB);
-  for (int blk = blk0; blk < blk1; ++blk) {
+  auto block = [&](int blk, float4 (&st)[8]) {
     const int k0 = blk * RB, rows = min(RB, Kr - k0);
     __syncthreads();  // the previous block's products are done with sX / sY (and sV staged)
-    stage();
+    stage(st);
     __syncthreads();
-    if (blk + 1 < blk1) fetch(k0 + RB);  // in flight behind this block's products
+    // block blk + 2 into the registers just staged: in flight behind two blocks' products
+    fetch(st, k0 + 2 * RB, blk + 2 < blk1 ? min(RB, Kr - k0 - 2 * RB) : 0);
     // ---- phase 1: Y = X_blk V
     {
       const int klen = RP / KS;
@@ -1370,9 +1415,27 @@ __global__ __launch_bounds__(256, 2) void recon_stream_kernel(
         const int rt = tile & 1, ct = tile >> 1;
         const float* a_p = sX + (16 * rt + cl) * PX + part * klen + kr;
         const float* b_p = sV + (part * klen + kr) * PV + 16 * ct + cl;
-        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-        for (int k = 0; k < klen; k += 4)
+        // two accumulators, 8 k-steps per batch of LDS reads (one dependent chain of
+        // read -> MFMA -> MFMA per k-step left the chain's latency exposed); klen % 32 == 0
+        // when RP % 64 == 0 (C3), else the tail loop
+        f4 acc = f4{0.f, 0.f, 0.f, 0.f}, acc2 = f4{0.f, 0.f, 0.f, 0.f};
+        int k = 0;
+        for (; k + 32 <= klen; k += 32) {
+          float av[8], bv[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            av[q] = a_p[k + 4 * q];
+            bv[q] = b_p[(k + 4 * q) * PV];
+          }
+#pragma unroll
+          for (int q = 0; q < 8; q += 2) {
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bv[q], acc, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q + 1], bv[q + 1], acc2, 0, 0, 0);
+          }
+        }
+        for (; k < klen; k += 4)
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a_p[k], b_p[k * PV], acc, 0, 0, 0);
+        acc += acc2;
         float* yp = sY + part * RB * PY + (16 * rt + 4 * kr) * PY + 16 * ct + cl;
 #pragma unroll
         for (int j = 0; j < 4; ++j) yp[j * PY] = acc[j];
@@ -1406,6 +1469,12 @@ __global__ __launch_bounds__(256, 2) void recon_stream_kernel(
         }
       }
     }
+  };
+  fetch(stA, blk0 * RB, min(RB, Kr - blk0 * RB));
+  fetch(stB, (blk0 + 1) * RB, blk0 + 1 < blk1 ? min(RB, Kr - (blk0 + 1) * RB) : 0);
+  for (int blk = blk0; blk < blk1; blk += 2) {
+    block(blk, stA);
+    if (blk + 1 < blk1) block(blk + 1, stB);
   }
 }
 

@@ -385,9 +385,8 @@ def test_recon_mfma_matches_scalar_recon(gpu_device, kernel_variant, m, n, rng_k
 def test_recon_stream_runs(gpu_device, kernel_variant, m, n, rng_k):
     """A batch that fills the chip (1100 matrices: 5 distinct ones tiled) puts every row block
     of a matrix in one recon_stream_kernel workgroup (V staged once, the next block's loads in
-    flight): equal to recon_mfma_kernel's one-block workgroups — bitwise for row-major X (the
-    same products per block), to 1e-6 for transposed X (MFMA operands swapped) — and every
-    copy of a matrix gets the same output."""
+    flight): equal to recon_mfma_kernel's one-block workgroups to fp32 rounding (1e-6; the
+    products are summed in another order), and every copy of a matrix gets the same output."""
     import os
     import sys
 
@@ -403,10 +402,7 @@ def test_recon_stream_runs(gpu_device, kernel_variant, m, n, rng_k):
     assert "recon_stream_kernel" in " ".join(_lib.kernel_names(n0, _lib.launch_count()))
     kernel_variant("SVD_RECON_BLOCKS", 1)
     b = svd.denoise_batch(At, *rng_k)
-    if m >= n:
-        assert torch.equal(a, b)
-    else:
-        assert float((a - b).norm() / b.norm()) <= 1e-6
+    assert float((a - b).norm() / b.norm()) <= 1e-6
     a5 = a.view(220, 5, m, n)
     assert torch.equal(a5, a5[:1].expand_as(a5))
     for i in range(5):

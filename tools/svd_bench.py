@@ -10,4 +10,5 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-print(json.dumps(bench.svd_c3_stage(torch.device("cuda"), B=int(os.environ.get("B", 4096)))))
+print(json.dumps(bench.svd_c3_stage(torch.device("cuda"), B=int(os.environ.get("B", 4096)),
+                                     pmc=bench.load_pmc())))

@@ -1078,6 +1078,15 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
 #undef SS_MARK
 }
 
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations, not for
+// its global loads (__syncthreads' release fence would also drain vmcnt, i.e. wait for the
+// next matrix's prefetch at the first barrier after it is issued).
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // ---------------------------------------------------------------- 3. reconstruction
 // Workgroup = (matrix, block of RB X-rows). With X_blk (RB x r), V (r x K):
 //   Y = X_blk V_K                       (RB x K)      phase 1
@@ -1308,6 +1317,28 @@ __global__ __launch_bounds__(256) void recon_mfma_kernel(XView x, int Kr, int r,
   }
 }
 
+// V (r x K, the kept columns [lo, hi)) into LDS as RP x KPP with row pitch PV, zero-padded:
+// batches of 16 loads per thread in flight before their LDS writes (a plain strided loop
+// waited a full round trip for each of its RP KPP / 256 loads)
+template <int KPP, int PV>
+__device__ __forceinline__ void stage_v(const float* Vb, int r, int K, int lo, int hi, int RP,
+                                        float* sV) {
+  constexpr int UB = 16;
+  for (int i0 = threadIdx.x; i0 < RP * KPP; i0 += 256 * UB) {
+    float t[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = i0 + 256 * u, i = idx / KPP, c = idx % KPP;
+      t[u] = (idx < RP * KPP && i < r && c >= lo && c < hi) ? Vb[(long long)i * K + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = i0 + 256 * u;
+      if (idx < RP * KPP) sV[(idx / KPP) * PV + idx % KPP] = t[u];
+    }
+  }
+}
+
 // recon_stream_kernel: recon_mfma_kernel's two products, with a workgroup walking a run of
 // `bps` consecutive row blocks of one matrix (all of them when the batch fills the chip:
 // C3's 4096 matrices, 17 blocks each). recon_mfma_kernel's workgroups each staged V (16 KB at
@@ -1341,10 +1372,7 @@ __global__ __launch_bounds__(256, 2) void recon_stream_kernel(
   const int cl = lane & 15, kr = lane >> 4;
   const float* X = x.base + b * x.batch_stride;
   const float* Vb = V + b * (long long)r * K;
-  for (int idx = tid; idx < RP * KPP; idx += 256) {  // (KPP: a power-of-two multiple of 16)
-    const int i = idx / KPP, c = idx % KPP;
-    sV[i * PV + c] = (i < r && c >= lo && c < hi) ? Vb[(long long)i * K + c] : 0.f;
-  }
+  stage_v<KPP, PV>(Vb, r, K, lo, hi, RP, sV);
   float4 stA[8], stB[8];  // two blocks in flight: the next two blocks' X
   const bool vec_t = TRANS && (x.si & 3) == 0 && (x.batch_stride & 3) == 0 &&
                      (reinterpret_cast<uintptr_t>(x.base) & 15) == 0;
@@ -1402,9 +1430,11 @@ __global__ __launch_bounds__(256, 2) void recon_stream_kernel(
   const int nit = RP / 16;
   auto block = [&](int blk, float4 (&st)[8]) {
     const int k0 = blk * RB, rows = min(RB, Kr - k0);
-    __syncthreads();  // the previous block's products are done with sX / sY (and sV staged)
+    // (LDS-only barriers: __syncthreads' release fence drains vmcnt, i.e. it waited for the
+    // prefetched blocks at the first barrier after their loads were issued)
+    lds_sync();  // the previous block's products are done with sX / sY (and sV staged)
     stage(st);
-    __syncthreads();
+    lds_sync();
     // block blk + 2 into the registers just staged: in flight behind two blocks' products
     fetch(st, k0 + 2 * RB, blk + 2 < blk1 ? min(RB, Kr - k0 - 2 * RB) : 0);
     // ---- phase 1: Y = X_blk V
@@ -1441,13 +1471,13 @@ __global__ __launch_bounds__(256, 2) void recon_stream_kernel(
         for (int j = 0; j < 4; ++j) yp[j * PY] = acc[j];
       }
     }
-    __syncthreads();
+    lds_sync();
     if constexpr (KS == 2) {
       for (int e = tid; e < RB * KPP; e += 256) {
         const int row = e / KPP, c = e % KPP;
         sY[row * PY + c] += sY[RB * PY + row * PY + c];
       }
-      __syncthreads();
+      lds_sync();
     }
     // ---- phase 2: out = [X_blk -] Y V^T
     for (int t = wave; t < 2 * nit; t += 4) {
@@ -1497,14 +1527,6 @@ constexpr int MAX_ROUNDS = 24;
 // X | Zt (4 x N, basis transposed) | U (N x 4) | part (4 waves x N x 4) | reduction scratch
 constexpr size_t LDS_BYTES = (size_t)N * LD * 4 + 4 * N * 4 + N * 4 * 4 + 4 * N * 4 * 4 + 64 * 8;
 
-// Workgroup barrier that orders LDS only: waits for this wave's LDS operations, not for
-// its global loads (__syncthreads' release fence would also drain vmcnt, i.e. wait for the
-// next matrix's prefetch at the first barrier after it is issued).
-__device__ __forceinline__ void lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 
 // 1/sqrt(d) for d > 0: v_rsq_f64 plus one Newton step (the factors below only need to be
 // consistent with each other, not correctly rounded)

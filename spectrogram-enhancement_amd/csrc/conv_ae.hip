@@ -2046,11 +2046,28 @@ __global__ __launch_bounds__(256) void bce_logits_kernel(const float* __restrict
   __shared__ double red[4];
   double acc = 0.0;
   const float inv = 1.0f / (float)n;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
-    const float zi = z[i], ti = to_f(t[i]);
-    acc += (double)(fmaxf(zi, 0.f) - zi * ti + log1pf(__expf(-fabsf(zi))));
-    if (grad) grad[i] = from_f<TG>((1.f / (1.f + __expf(-zi)) - ti) * inv);
+  // BCE_U elements per thread per pass with all their loads issued first (a grid-stride loop
+  // of one element waited a full round trip per element: 22 us at C4's 2 M elements)
+  constexpr int BCE_U = 8;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i0 = blockIdx.x * (long long)blockDim.x + threadIdx.x; i0 < n;
+       i0 += BCE_U * stride) {
+    float zv[BCE_U], tv[BCE_U];
+#pragma unroll
+    for (int u = 0; u < BCE_U; ++u) {
+      const long long i = i0 + u * stride;
+      zv[u] = i < n ? z[i] : 0.f;
+      tv[u] = i < n ? to_f(t[i]) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < BCE_U; ++u) {
+      const long long i = i0 + u * stride;
+      if (i < n) {
+        const float zi = zv[u], ti = tv[u];
+        acc += (double)(fmaxf(zi, 0.f) - zi * ti + log1pf(__expf(-fabsf(zi))));
+        if (grad) grad[i] = from_f<TG>((1.f / (1.f + __expf(-zi)) - ti) * inv);
+      }
+    }
   }
   for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;

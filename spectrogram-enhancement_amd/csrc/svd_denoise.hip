@@ -2779,8 +2779,12 @@ struct EigLayout {
   size_t per_matrix() const {
     return (size_t)r * r * 8 + 3 * (size_t)r * 8 + 4 * (size_t)r * ld * 8 + 4 * 4 + 8;
   }
-  long long chunk(long long batch) const {  // matrices per pass, <= ~512 MB of workspace
-    const long long c = (long long)((512ull << 20) / per_matrix());
+  // matrices per pass, <= 8 GB of workspace. Every pass is 4 launches even when the pass
+  // only re-does flagged matrices (the fallback after top1 / subspace: the others return at
+  // once), and at 512 MB C3's 4096 x 513 x 256 took 13 passes (240 us of empty launches per
+  // call) and C5's 4096 x 128 x 128 four; 8 GB is one pass for both (288 GB per GPU).
+  long long chunk(long long batch) const {
+    const long long c = (long long)((8ull << 30) / per_matrix());
     return std::max(1LL, std::min(batch, c));
   }
   size_t bytes(long long batch) const { return (size_t)chunk(batch) * per_matrix() + 256; }

@@ -202,8 +202,11 @@ def pmc_traffic(pmc, target, stage, symbols, launch_batch):
     if rec is None:
         return None, f"no PMC record for {target}/{stage}"
     if list(rec.get("symbols", [])) != list(symbols):
-        msg = (f"PMC record for {target}/{stage} is of {rec.get('symbols')}, the timed launch "
-               f"ran {list(symbols)}: traffic withheld (rerun tools/pmc_refresh.sh)")
+        rs = list(rec.get("symbols", []))
+        uniq = lambda xs: sorted(set(xs), key=xs.index)  # noqa: E731
+        msg = (f"PMC record for {target}/{stage} is of {len(rs)} launches {uniq(rs)}, the timed "
+               f"run made {len(symbols)} launches {uniq(list(symbols))}: traffic withheld "
+               f"(rerun tools/pmc_refresh.sh)")
         print(f"[bench] WARNING: {msg}", file=sys.stderr)
         return None, msg
     return rec["hbm_bytes"] * launch_batch / rec["batch"], None

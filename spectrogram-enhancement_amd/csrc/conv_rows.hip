@@ -1165,7 +1165,9 @@ void enc2_rows_kernel(E2Args a) {
     // DMA). Only the DMA waves wait; stores alone are never waited for.
     if (wv < 4) {
       const int younger = c_2 + c_1 + ns + nd;
-      switch (younger) {
+      if (younger >= 6) {  // (steady state: store + DMA in each of the three steps)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else switch (younger) {
         case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
         case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
         case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;

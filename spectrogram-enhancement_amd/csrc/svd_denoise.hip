@@ -2080,17 +2080,15 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
 
 // fp64 Gram G = X^T X: 64x64 tile per workgroup (upper-triangle tiles, mirrored), 16 rows
 // of X per LDS stage, 4x4 outputs per thread. Products of fp32 inputs are exact in fp64.
-__global__ __launch_bounds__(256) void gram64_kernel(XView x, int K, int r, double* G, int nts,
-                                                     const int* only) {
+__device__ __forceinline__ void gram64_one(XView x, int K, int r, double* G, int nts,
+                                           long long b) {
   __shared__ double sa[16][65], sb[16][65];
-  if (only && !only[blockIdx.y]) return;  // uniform: matrix not selected
   int t = blockIdx.x, ti = 0;
   while (t >= nts - ti) {
     t -= nts - ti;
     ++ti;
   }
   const int tj = ti + t;
-  const long long b = blockIdx.y;
   const float* X = x.base + b * x.batch_stride;
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   double acc[4][4];
@@ -2141,6 +2139,20 @@ __global__ __launch_bounds__(256) void gram64_kernel(XView x, int K, int r, doub
     }
 }
 
+// The fallback kernels below loop over matrices b = blockIdx.y (.x), + gridDim: as the fp64
+// path behind top1 / the subspace kernels (`only`: the few flagged matrices) they launch a
+// small grid, not one workgroup per matrix that mostly returns at once (four such launches
+// cost ~25 us per 4096-matrix C5 step); without `only` the grid covers every matrix.
+__global__ __launch_bounds__(256) void gram64_kernel(XView x, int K, int r, double* G, int nts,
+                                                     const int* only, long long nmat) {
+  for (long long b = blockIdx.y; b < nmat; b += gridDim.y) {
+    if (only && !only[b]) continue;  // uniform: matrix not selected
+    gram64_one(x, K, r, G, nts, b);
+    __syncthreads();  // (LDS reused by the next matrix)
+  }
+}
+
+
 __device__ __forceinline__ double block_sum256(double v, double* red) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
@@ -2157,11 +2169,9 @@ __device__ __forceinline__ double block_sum256(double v, double* red) {
 // With taug, the reflectors are kept for the eigenvector back-transform: v_k (v_k[0] = 1
 // implicit) overwrites row k right of the diagonal (never read again), tau_k -> taug[k];
 // G = Q T Q^T with Q = H_0 H_1 ... H_{n-3}.
-__global__ __launch_bounds__(256) void tridiag_kernel(double* G, int n, double* dg, double* eg,
-                                                      double* taug, const int* only) {
+__device__ __forceinline__ void tridiag_one(double* G, int n, double* dg, double* eg,
+                                            double* taug, long long b) {
   __shared__ double sv[256], sw[256], red[4];
-  const long long b = blockIdx.x;
-  if (only && !only[b]) return;
   double* A = G + b * (long long)n * n;
   double* d = dg + b * n;
   double* e = eg + b * n;
@@ -2218,6 +2228,17 @@ __global__ __launch_bounds__(256) void tridiag_kernel(double* G, int n, double* 
     d[n - 1] = A[(long long)(n - 1) * n + n - 1];
   }
 }
+
+__global__ __launch_bounds__(256) void tridiag_kernel(double* G, int n, double* dg, double* eg,
+                                                      double* taug, const int* only,
+                                                      long long nmat) {
+  for (long long b = blockIdx.x; b < nmat; b += gridDim.x) {
+    if (only && !only[b]) continue;
+    tridiag_one(G, n, dg, eg, taug, b);
+    __syncthreads();
+  }
+}
+
 
 // Number of eigenvalues < x of the symmetric tridiagonal (d, e2 = e^2) (Sturm sequence,
 // LAPACK dstebz pivmin guard).
@@ -2404,17 +2425,15 @@ __device__ void col_normalize(double* y, int n, long long ld) {
 // One workgroup per matrix. ranges (device int[2 * batch]) gives a per-matrix kept [lo, hi),
 // else the uniform (lo, hi). Writes the selected eigenvectors of G (Q z, fp64) to
 // Z[b][i][j] (row stride ld) and kinfo[b] = {count, complement}.
-__global__ __launch_bounds__(256) void eigvec_kernel(const double* G, const double* dg,
+__device__ __forceinline__ void eigvec_one(const double* G, const double* dg,
                                                      const double* eg, const double* taug, int n,
                                                      int lo, int hi, const int* ranges, double* Z,
                                                      double* fac, long long ld, int* kinfo,
-                                                     const int* only) {
+                                                     long long b) {
   __shared__ double sd[EIG_MAXN], se[EIG_MAXN], se2[EIG_MAXN], slam[EIG_MAXN], sv[EIG_MAXN];
   __shared__ int sidx[EIG_MAXN], slead[EIG_MAXN];
   __shared__ double red[4];
-  const long long b = blockIdx.x;
   const int tid = threadIdx.x;
-  if (only && !only[b]) return;
   if (ranges) {
     lo = ranges[2 * b];
     hi = ranges[2 * b + 1];
@@ -2528,6 +2547,19 @@ __global__ __launch_bounds__(256) void eigvec_kernel(const double* G, const doub
   }
 }
 
+__global__ __launch_bounds__(256) void eigvec_kernel(const double* G, const double* dg,
+                                                     const double* eg, const double* taug, int n,
+                                                     int lo, int hi, const int* ranges, double* Z,
+                                                     double* fac, long long ld, int* kinfo,
+                                                     const int* only, long long nmat) {
+  for (long long b = blockIdx.x; b < nmat; b += gridDim.x) {
+    if (only && !only[b]) continue;
+    eigvec_one(G, dg, eg, taug, n, lo, hi, ranges, Z, fac, ld, kinfo, b);
+    __syncthreads();
+  }
+}
+
+
 // Per-matrix kept ranges of the optimal modes from num_sing, with the notebook's slicing:
 // use_optimal keeps u[:, 0:num_sing-1] (:216-228; num_sing == 0 -> stop = -1 -> [0, r-1)),
 // computeSignal keeps [1, 2 num_sing) (:181-185; 2 num_sing > r is an IndexError, flagged).
@@ -2557,16 +2589,14 @@ __global__ void optimal_ranges_kernel(const int* num, long long batch, int r, in
 // (fp64, cast to fp32 in LDS). Workgroup = (matrix, RB rows of X); thread i owns column i
 // of the row block (r <= 256), V streams through LDS 32 columns at a time.
 template <typename TO>
-__global__ __launch_bounds__(256) void recon_eig_kernel(XView x, int Kr, int r, const double* Z,
-                                                        long long ld, const int* kinfo, TO* out,
-                                                        long long out_bstride, long long osk,
-                                                        long long osi, const int* only) {
+__device__ __forceinline__ void recon_eig_one(XView x, int Kr, int r, const double* Z,
+                                              long long ld, const int* kinfo, TO* out,
+                                              long long out_bstride, long long osk,
+                                              long long osi, long long b) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* sX = reinterpret_cast<float*>(smem);  // RB x (r + 1)
   float* sV = sX + RB * (r + 1);                // r x 33
   float* sY = sV + r * 33;                      // RB x 33
-  const long long b = blockIdx.y;
-  if (only && !only[b]) return;
   const int kc = kinfo[2 * b], comp = kinfo[2 * b + 1];
   const int k0 = blockIdx.x * RB, tid = threadIdx.x;
   const int rows = min(RB, Kr - k0);
@@ -2621,6 +2651,20 @@ __global__ __launch_bounds__(256) void recon_eig_kernel(XView x, int Kr, int r, 
     }
   }
 }
+
+template <typename TO>
+__global__ __launch_bounds__(256) void recon_eig_kernel(XView x, int Kr, int r, const double* Z,
+                                                        long long ld, const int* kinfo, TO* out,
+                                                        long long out_bstride, long long osk,
+                                                        long long osi, const int* only,
+                                                        long long nmat) {
+  for (long long b = blockIdx.y; b < nmat; b += gridDim.y) {
+    if (only && !only[b]) continue;
+    recon_eig_one<TO>(x, Kr, r, Z, ld, kinfo, out, out_bstride, osk, osi, b);
+    __syncthreads();
+  }
+}
+
 
 }  // namespace specenh
 
@@ -2799,8 +2843,9 @@ hipError_t launch_recon_eig_t(XView xb, int Kr, int r, const double* Z, long lon
   hipError_t e = hipFuncSetAttribute((const void*)recon_eig_kernel<TO>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  SPECENH_LAUNCH(recon_eig_kernel<TO>, dim3((Kr + RB - 1) / RB, (unsigned)nb), dim3(256), lds,
-                     st, xb, Kr, r, Z, ld, kinfo, reinterpret_cast<TO*>(out), ob, osk, osi, only);
+  const unsigned gm = only ? (unsigned)std::min<long long>(nb, 2LL * device_cus()) : (unsigned)nb;
+  SPECENH_LAUNCH(recon_eig_kernel<TO>, dim3((Kr + RB - 1) / RB, gm), dim3(256), lds, st, xb, Kr,
+                 r, Z, ld, kinfo, reinterpret_cast<TO*>(out), ob, osk, osi, only, nb);
   return hipGetLastError();
 }
 
@@ -2857,10 +2902,12 @@ int eig_denoise(const float* A, long long batch, int m, int n, long long a_strid
     const long long nb = std::min(ch, batch - b0);
     xv.base = A + b0 * a_stride;
     const int* on = only ? only + b0 : nullptr;
-    SPECENH_LAUNCH(gram64_kernel, dim3(ntri64, (unsigned)nb), dim3(256), 0, st, xv, Kr, r,
-                       G64, nts64, on);
-    SPECENH_LAUNCH(tridiag_kernel, dim3((unsigned)nb), dim3(256), 0, st, G64, r, dd, ee, tau,
-                       on);
+    // fallback (on: the flagged few): a grid of at most two workgroups per CU looping over
+    // the matrices instead of one per matrix (gram64_kernel's comment)
+    const unsigned gm = on ? (unsigned)std::min<long long>(nb, 2LL * device_cus()) : (unsigned)nb;
+    SPECENH_LAUNCH(gram64_kernel, dim3(ntri64, gm), dim3(256), 0, st, xv, Kr, r, G64, nts64, on,
+                   nb);
+    SPECENH_LAUNCH(tridiag_kernel, dim3(gm), dim3(256), 0, st, G64, r, dd, ee, tau, on, nb);
     const int* rg = nullptr;
     if (opt_mode >= 0) {
       SPECENH_LAUNCH(optimal_rank_kernel, dim3((unsigned)nb), dim3(64), 0, st, dd, ee, r,
@@ -2875,8 +2922,8 @@ int eig_denoise(const float* A, long long batch, int m, int n, long long a_strid
         return set_error(SPECENH_EHIP, "median copy");
       rg = ranges;
     }
-    SPECENH_LAUNCH(eigvec_kernel, dim3((unsigned)nb), dim3(256), 0, st, G64, dd, ee, tau, r,
-                       lo, hi, rg, Z, fac, L.ld, kinfo, on);
+    SPECENH_LAUNCH(eigvec_kernel, dim3(gm), dim3(256), 0, st, G64, dd, ee, tau, r, lo, hi, rg,
+                   Z, fac, L.ld, kinfo, on, nb);
     if (hipGetLastError() != hipSuccess) return set_error(SPECENH_EHIP, "eigen path launch");
     const hipError_t e = launch_recon_eig(odt, xv, Kr, r, Z, L.ld, kinfo,
                                           static_cast<char*>(out) + (size_t)(b0 * ob) * osz, ob,

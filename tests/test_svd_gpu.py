@@ -408,3 +408,19 @@ def test_recon_stream_runs(gpu_device, kernel_variant, m, n, rng_k):
     for i in range(5):
         truth = ref.denoiseSignal(A[i].astype(np.float64), *[v for v in rng_k if v is not None])
         assert _rel(a[i].double().cpu().numpy(), truth) <= TOL
+
+
+@pytest.mark.parametrize("shape,args", [((64, 48), ()), ((300, 200), (0, 16))])
+def test_fallback_loops_over_many_flagged(gpu_device, shape, args):
+    """Ungapped (pure noise) matrices at a batch larger than the fp64 fallback's grid (two
+    workgroups per CU): most are flagged by top1 / the subspace check and redone by the eigen
+    path, whose kernels then loop over several matrices per workgroup."""
+    import torch
+
+    from specenh import svd
+    rng = np.random.default_rng(11)
+    A = rng.standard_normal((600,) + shape).astype(np.float32)
+    out = svd.denoise_batch(torch.as_tensor(A, device=gpu_device), *args).double().cpu().numpy()
+    for b in (0, 1, 299, 511, 512, 599):
+        truth = ref.denoiseSignal(A[b].astype(np.float64), *args)
+        assert _range_err(out[b], truth, A[b].astype(np.float64)) <= TOL, b

@@ -539,7 +539,9 @@ __device__ void gemm_GZ(const float* G, int r, const float* sZ, float* sY) {
     for (int c = 0; c < P; ++c) acc[c] = 0.f;
     // G rows in batches of GB loads in flight (G comes from L2 / HBM: one batch per round
     // trip), then the batch's FMAs in the same j order
-    constexpr int GB = 16;
+    // G loads per batch: 8 for P <= 24 (C3 rank-16 5.05 -> 4.84 ms vs 16; 32: 6.2 ms, 64:
+    // slower still — more rows in flight per thread congest L2 / the memory pipeline)
+    constexpr int GB = P <= 24 ? 8 : 16;
     int j = 0;
     for (; j + GB <= r; j += GB) {
       float g[GB];

@@ -570,6 +570,9 @@ void convt_rows_pw_kernel(CRArgs a) {
   const int S = nimg * SPI;
 
   for (int e = lane; e < WR / 16; e += 64) reinterpret_cast<uint4*>(ring)[e] = uint4{0u, 0u, 0u, 0u};
+  // the zero fill's ds_writes and the prologue's LDS-DMA writes into the same ring take
+  // different paths with no mutual ordering: the writes complete before any DMA is issued
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   uint4 wf[50];  // tap fragments [phase][(dy, dx) taps][K half]
   {
     const T* __restrict__ Wg = reinterpret_cast<const T*>(a.w);

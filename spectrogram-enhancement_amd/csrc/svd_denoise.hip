@@ -2825,12 +2825,15 @@ struct EigLayout {
   size_t per_matrix() const {
     return (size_t)r * r * 8 + 3 * (size_t)r * 8 + 4 * (size_t)r * ld * 8 + 4 * 4 + 8;
   }
-  // matrices per pass, <= 8 GB of workspace. Every pass is 4 launches even when the pass
+  // matrices per pass, <= 1 GiB of workspace (the caller allocates it on every call, so it
+  // is bounded independently of the batch). Every pass is 4 launches even when the pass
   // only re-does flagged matrices (the fallback after top1 / subspace: the others return at
-  // once), and at 512 MB C3's 4096 x 513 x 256 took 13 passes (240 us of empty launches per
-  // call) and C5's 4096 x 128 x 128 four; 8 GB is one pass for both (288 GB per GPU).
+  // once, ~5 us per mostly-empty pass measured): C3's 4096 x 513 x 256 takes 7 passes
+  // (650 matrices of 1.6 MB each), the C5 stream's 2048 x 128 x 128 slices one. Round 4 ran
+  // an 8 GB cap (one pass for C3): 60 us faster at C3 for 6.5 GB of workspace per call.
+  static constexpr size_t kCapBytes = 1ull << 30;
   long long chunk(long long batch) const {
-    const long long c = (long long)((8ull << 30) / per_matrix());
+    const long long c = (long long)(kCapBytes / per_matrix());
     return std::max(1LL, std::min(batch, c));
   }
   size_t bytes(long long batch) const { return (size_t)chunk(batch) * per_matrix() + 256; }

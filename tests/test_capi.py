@@ -87,6 +87,36 @@ def test_host_frequency_and_time_grids_bit_exact():
     assert np.array_equal(stft.get_window("hamm", 512), scipy.signal.get_window("hamm", 512))
 
 
+@pytest.mark.parametrize("batch,m,n,start,stop,path", [
+    (4096, 513, 256, 0, 16, "subspace"),      # C3 rank-16
+    (4096, 513, 256, 1, 256, "subspace"),     # C3 default range
+    (4096, 128, 128, 1, 128, "top1"),         # C5 default range, whole batch
+    (2048, 128, 128, 1, 128, "top1"),         # the bench's C5 slice
+    (4096, 513, 256, 0, 200, "eigen"),        # wide kept range: every matrix on the eigen path
+    (1 << 16, 256, 3905, 1, 256, "subspace"),  # many production-shape spectrograms
+])
+def test_svd_workspace_bounded(batch, m, n, start, stop, path):
+    """The eigen-path part of the SVD workspace is capped at 1 GiB whatever the batch
+    (an 8 GB cap made C3 calls reserve 6.5 GB); the rest is the subspace path's
+    G / V / theta (batch x r x r fp32) and per-matrix flags."""
+    from specenh import _lib
+
+    L = _lib.lib()
+    r = min(m, n)
+    ws = L.specenh_svd_denoise_workspace_bytes(batch, m, n, start, stop)
+    per_matrix = r * r * 8 + 3 * r * 8 + 4 * r * (r // 2 + 2) * 8 + 24
+    eig = min(batch, max(1, (1 << 30) // per_matrix)) * per_matrix + 256
+    assert eig <= (1 << 30) + 256
+    if path == "eigen":
+        assert ws == eig
+    elif path == "top1":  # top1 flags + eigen fallback (r = 128: the subspace layout)
+        assert eig < ws <= eig + batch * (r * r + 8 * r + 8) * 4 + 8 * batch + 1024
+    else:
+        K = 16 if start == 0 else 1
+        sub = batch * (r * r + r * K + K) * 4
+        assert sub + eig <= ws <= sub + eig + 8 * batch + 1024
+
+
 def test_python_boundary_rejects_cpu_tensors():
     import torch
 

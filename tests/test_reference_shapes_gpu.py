@@ -8,14 +8,17 @@ dropped. The notebook's loop (``denoising_by_svd.ipynb:250-263``) then calls
 
 Tolerances (the contract of tests/test_stft_gpu.py and tests/test_svd_gpu.py):
   * specgr: f / t bit-exact; normalised log output vs the fp64 truth (fp32 samples on both
-    sides): 99.99th percentile of |GPU - truth| <= 2e-6 and max <= 2e-5. The 1e-5 max bound of
-    tests/test_stft_gpu.py (set from scipy's fp32 5.5e-6 on 16k-sample cases) sits at the fp32
-    noise floor here: 1M outputs per spectrogram, and the largest error is a single bin whose
-    PSD is ~7 eps (7e-11, 1e-8 of its frame's peak), measured on MI355X at 4.3e-6 / 1.02e-5 /
-    4.8e-6 for the three channels (p99.99 1.2e-6 .. 1.3e-6; tools/diag_prodshot.py). scipy's
-    own fp32 spectrogram of the same shots is off by 3.7e-5 .. 1.1e-4 (its fp32 detrend of
-    the DC row);
-  * denoiseSignal: ||GPU - ref||_F / ||ref||_F <= 1e-5 where the kept range has a spectral
+    sides). EXPLICIT EXCEPTION to SURVEY §8(d)'s 1e-5 max: on these 1M-value
+    production spectrograms the bound is max <= 2e-5 and 99.99th percentile <= 2e-6, AND
+    both no larger than scipy's own fp32 spectrogram of the same samples (the reference's
+    path when a shot is stored as float32: scipy computes in the input's precision). Measured
+    on MI355X: max 4.3e-6 / 1.02e-5 / 4.8e-6 for the three channels, p99.99 1.2e-6 .. 1.3e-6
+    (tools/diag_prodshot.py); scipy fp32: max 2.9e-5 / 6.7e-5 / 3.0e-5, p99.99 2.5e-6 ..
+    8.0e-6. The 1e-5 case is one bin at a spectral null (PSD 1e-6 of its neighbours): the
+    two-for-one FFT (two real frames in one complex FFT) leaks the partner frame's fp32
+    rounding at the same bin into it. tools/stft_pair_error.py emulates the kernel's fp32
+    arithmetic: ln-PSD error 3.4e-5 at that bin with one frame per FFT, 1.5e-4 paired;
+    * denoiseSignal: ||GPU - ref||_F / ||ref||_F <= 1e-5 where the kept range has a spectral
     gap (default [1, r): sigma_1 / sigma_2 ~ 60 on these spectrograms; use_optimal).
     The (0, 16) cut of a log spectrogram of chirps + noise has NO gap (sigma_16 / sigma_17 =
     1.003 here): the 16th / 17th singular directions are then not determined to fp32 by any
@@ -39,14 +42,19 @@ SPEC = {"nperseg": 512, "noverlap": 256, "fs": FS, "window": "hamm", "scaling": 
         "detrend": "linear", "eps": 1e-11}          # pipeline_data.py:77-84
 L_SHOT = 2 * FS                                     # cut_shot = 2 (pipeline_data.py:28)
 TOL_NORM = 2e-5      # max |GPU - truth| on a 1M-value spectrogram (module docstring)
-TOL_NORM_P = 2e-6    # its 99.99th percentile
+TOL_NORM_P = 2e-6    # its 99.99th percentile (both also <= scipy fp32's, _check_specgr)
 TOL_SVD = 1e-5
 
 
-def _check_specgr(S, St):
+def _check_specgr(S, St, S32):
+    """GPU S vs the fp64 truth St, next to scipy's fp32 spectrogram S32 of the same samples."""
     e = np.abs(S - St)
+    e32 = np.abs(S32 - St)
+    q, q32 = np.quantile(e, 0.9999), np.quantile(e32, 0.9999)
     assert e.max() <= TOL_NORM, e.max()
-    assert np.quantile(e, 0.9999) <= TOL_NORM_P, np.quantile(e, 0.9999)
+    assert q <= TOL_NORM_P, q
+    assert e.max() <= e32.max(), ("worse than scipy fp32", e.max(), e32.max())
+    assert q <= q32, ("p99.99 worse than scipy fp32", q, q32)
 
 
 def _rel(a, b):
@@ -66,7 +74,8 @@ def truth(shots):
     out = []
     for x in shots:
         S, f, t = ref.specgr_arrays(x[:L_SHOT].astype(np.float64), SPEC)
-        out.append((S, f, t))
+        S32, _, _ = ref.specgr_scipy(x[:L_SHOT], SPEC)  # scipy in fp32 (fp32 input)
+        out.append((S, f, t, S32.astype(np.float64)))
     return out
 
 
@@ -80,10 +89,10 @@ def test_specgr_reference_entry_production_shot(shots, truth, tmp_path, gpu_devi
         pickle.dump({"\\tecef%.2i" % (c + 1): shots[c].astype(np.float64) for c in range(3)}, fh)
     for c in range(3):
         S, f, t = pipeline_data.specgr(str(fname), c + 1, SPEC)
-        St, ft, tt = truth[c]
+        St, ft, tt, S32 = truth[c]
         assert S.shape == (256, 3905) and S.dtype == np.float64
         assert np.array_equal(f, ft) and np.array_equal(t, tt)
-        _check_specgr(S, St)
+        _check_specgr(S, St, S32)
 
 
 def test_specgr_bes_variant_production_shot(shots, truth, tmp_path, gpu_device):
@@ -95,10 +104,10 @@ def test_specgr_bes_variant_production_shot(shots, truth, tmp_path, gpu_device):
         pickle.dump({"besfu01": {"data.BES": shots[1].astype(np.float64)}}, fh)
     S, f, t = pipeline_data.specgr(str(fname), 1, SPEC, 2, key_format="besfu%02d",
                                    field="data.BES")
-    St, ft, tt = truth[1]
+    St, ft, tt, S32 = truth[1]
     assert S.shape == (256, 3905)
     assert np.array_equal(f, ft) and np.array_equal(t, tt)
-    _check_specgr(S, St)
+    _check_specgr(S, St, S32)
 
 
 def test_specgr_batch_production_shots(shots, truth, gpu_device):
@@ -111,7 +120,7 @@ def test_specgr_batch_production_shots(shots, truth, gpu_device):
     S = pipeline_data.specgr_batch(x, SPEC, cut_shot=2).double().cpu().numpy()
     assert S.shape == (3, 256, 3905)
     for c in range(3):
-        _check_specgr(S[c], truth[c][0])
+        _check_specgr(S[c], truth[c][0], truth[c][3])
 
 
 @pytest.fixture(scope="module")

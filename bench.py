@@ -392,11 +392,16 @@ def ae_ops():
             for lay in ae_layers()]
 
 
-def make_c5_engine(dev, dtype="float16"):
-    """The C5 model (manual_scan_3layers.py:186-199) with the trained weights."""
+def make_c5_engine(dev, dtype="float16", out_fp16=True):
+    """The C5 model (manual_scan_3layers.py:186-199) with the trained weights. Inference
+    output: fp16 reconstructions (32,768 B out per shot), stored by the
+    fused three-layer decoder."""
+    import torch
     from specenh import ae
     eng = ae.AutoencoderEngine(ae_ops(), (HW5, HW5, 1), compute_dtype=dtype, device=dev)
     eng.set_keras_weights(ae_weights())
+    if out_fp16 and eng.dec3:
+        eng.set_inference_output_dtype(torch.float16)
     return eng
 
 
@@ -499,7 +504,7 @@ def ae_train_c4_stage(dev, dist=None, batch=128, steps=20, n_local=4096, seed=4,
     return res
 
 
-def c5_host_stream_stage(dev, make_engine, shots=32768, chunk=2048, slots=3):
+def c5_host_stream_stage(dev, make_engine, shots=32768, chunk=2048, slots=4):
     """BASELINE config 5 as a stream from host memory (SURVEY.md §7 item 7, §8 d C5: "1M
     shots streamed"): fp16 samples in pinned host memory -> H2D -> specgr -> denoiseSignal
     -> fp16 autoencoder -> D2H of the fp32 reconstructions into pinned host memory.
@@ -513,7 +518,9 @@ def c5_host_stream_stage(dev, make_engine, shots=32768, chunk=2048, slots=3):
     n_chunks = shots // chunk
     shots = n_chunks * chunk
     host_x = torch.empty((shots, L5), dtype=torch.float16, pin_memory=True)
-    host_y = torch.empty((shots, HW5, HW5, 1), dtype=torch.float32, pin_memory=True)
+    probe = make_engine()
+    host_y = torch.empty((shots, HW5, HW5, 1), dtype=probe.infer_out_dtype, pin_memory=True)
+    del probe
     for c in range(n_chunks):  # distinct seeded shots, synthesised on the device
         host_x[c * chunk:(c + 1) * chunk].copy_(
             plasma_chirps_torch(chunk, L5, seed=5000 + c, device=dev).to(torch.float16))
@@ -545,7 +552,7 @@ def c5_host_stream_stage(dev, make_engine, shots=32768, chunk=2048, slots=3):
 
     # the two copy directions alone, for the PCIe context of the figure above
     dx = torch.empty((chunk * 4, L5), dtype=torch.float16, device=dev)
-    dy = torch.empty((chunk * 4, HW5 * HW5), dtype=torch.float32, device=dev)
+    dy = torch.empty((chunk * 4, HW5 * HW5), dtype=host_y.dtype, device=dev)
     bw = {}
     for name, (dst, src) in {"h2d": (dx, host_x[:chunk * 4]),
                              "d2h": (host_y[:chunk * 4].view(chunk * 4, -1), dy)}.items():
@@ -556,16 +563,33 @@ def c5_host_stream_stage(dev, make_engine, shots=32768, chunk=2048, slots=3):
             dst.copy_(src, non_blocking=True)
         torch.cuda.synchronize()
         bw[name] = 5 * src.numel() * src.element_size() / (time.perf_counter() - t1) / 1e9
-    in_b, out_b = 2 * L5, 4 * HW5 * HW5
+    # both directions at once on two streams (the stream's real copy ceiling: the shots'
+    # H2D and D2H bytes move concurrently)
+    in_b, out_b = 2 * L5, host_y.element_size() * HW5 * HW5
+    s_in, s_out = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    hx, hy = host_x[:chunk * 4], host_y[:chunk * 4].view(chunk * 4, -1)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(5):
+        with torch.cuda.stream(s_in):
+            dx.copy_(hx, non_blocking=True)
+        with torch.cuda.stream(s_out):
+            hy.copy_(dy, non_blocking=True)
+    torch.cuda.synchronize()
+    t_bi = (time.perf_counter() - t1) / 5
+    bw["h2d_with_d2h"] = hx.numel() * hx.element_size() / t_bi / 1e9
+    bw["d2h_with_h2d"] = hy.numel() * hy.element_size() / t_bi / 1e9
+    ceiling = chunk * 4 / t_bi  # shots/s the copies alone allow, both directions concurrent
     rate = shots / dt
     del sl, dx, dy
     return {"workload": f"{shots} shots streamed from pinned host memory in {chunk}-shot "
-                        f"chunks over {slots} HIP streams (H2D fp16 samples, chain, D2H fp32 "
-                        f"reconstructions)",
+                        f"chunks over {slots} HIP streams (H2D fp16 samples, chain, D2H "
+                        f"{str(host_y.dtype).replace('torch.', '')} reconstructions)",
             "spectrograms_per_s": rate, "ms": dt * 1e3,
             "h2d_bytes_per_shot": in_b, "d2h_bytes_per_shot": out_b,
             "h2d_GBps_achieved": rate * in_b / 1e9, "d2h_GBps_achieved": rate * out_b / 1e9,
-            "copy_only_GBps": bw}
+            "copy_only_GBps": bw, "copy_ceiling_shots_per_s": ceiling,
+            "frac_of_copy_ceiling": rate / ceiling}
 
 
 # ------------------------------------------------------------------ multi-GPU plumbing
@@ -714,7 +738,9 @@ def main():
     pmc = load_pmc()
     layers = []
     names = layer_names(eng)
-    for name, c, ms, sym in zip(names, ae_layer_costs(tail=eng.tail, dec3=eng.dec3,
+    out_bytes = torch.empty((), dtype=eng.infer_out_dtype).element_size()
+    for name, c, ms, sym in zip(names, ae_layer_costs(out_bytes=out_bytes, tail=eng.tail,
+                                                      dec3=eng.dec3,
                                                       enc2=getattr(eng, "enc2", False)), layer_ms,
                                 kernels):
         # compute floor: MFMA FLOPs at the dense fp16 MFMA peak + VALU FLOPs at the dot2 peak
@@ -891,7 +917,7 @@ def main():
                                "autoencoder-denoise inference stream, 16,512-sample fp16 "
                                "shots -> specgr 128x128 (256 hann / hop 128) -> "
                                "denoiseSignal default -> 3-layer conv AE (16/32/64, 5x5) "
-                               "fp16 forward",
+                               "fp16 forward -> fp16 reconstructions (32,768 B per shot)",
                    "shots_per_step": B, "shots_per_launch": Hs, "samples": L5, "stft_dtype": "fp32",
                    "svd_dtype": "fp32 (fp64 small algebra)", "ae_dtype": "fp16",
                    "parallelism": f"shot-sharded x{world}", "streams_per_gpu": NS},

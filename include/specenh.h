@@ -286,6 +286,13 @@ int specenh_decoder3(int dtype, const void* x, int N, int H, int W, int C,
                      const void* w1_gemm, const float* b1, int CO1, const void* wt_gemm,
                      const float* bt, int CO2, const void* wo_gemm, const float* bo, int k,
                      float* out, void* stream);
+/* specenh_decoder3 with the output precision selectable: out_dtype F32 (float [N][4H][4W]) or
+ * F16 (_Float16, the sigmoid rounded once: BASELINE config 5's 32,768-byte fp16
+ * reconstruction per 128 x 128 shot). */
+int specenh_decoder3_ex(int dtype, const void* x, int N, int H, int W, int C,
+                        const void* w1_gemm, const float* b1, int CO1, const void* wt_gemm,
+                        const float* bt, int CO2, const void* wo_gemm, const float* bo, int k,
+                        void* out, int out_dtype, void* stream);
 
 /* The encoder's first TWO layers in one launch (VAE/manual_scan_3layers.py:187-191, the
  * inference path of predict :239):

@@ -2039,16 +2039,19 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_vec_kernel(const T* __restri
 // Keras BCE after a sigmoid (graph mode): sigmoid_cross_entropy_with_logits; the grad of
 // the mean is (sigmoid(z) - t) / n. One fp64 atomic per workgroup.
 template <typename TT, typename TG>
-__global__ __launch_bounds__(256) void bce_logits_kernel(const float* __restrict__ z,
+__global__ __launch_bounds__(512) void bce_logits_kernel(const float* __restrict__ z,
                                                           const TT* __restrict__ t, long long n,
                                                           TG* __restrict__ grad,
                                                           double* __restrict__ loss) {
-  __shared__ double red[4];
+  __shared__ double red[8];
   double acc = 0.0;
   const float inv = 1.0f / (float)n;
   // BCE_U elements per thread per pass with all their loads issued first (a grid-stride loop
-  // of one element waited a full round trip per element: 22 us at C4's 2 M elements)
-  constexpr int BCE_U = 8;
+  // of one element waited a full round trip per element: 22 us at C4's 2 M elements). The
+  // grid is at most 128 workgroups: every workgroup ends in one device-scope fp64 atomic on
+  // the same word, and those serialise at the memory side (~20 ns each: 1024 of them were
+  // 21 us of C4's 1.0 ms step, round 4)
+  constexpr int BCE_U = 32;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i0 = blockIdx.x * (long long)blockDim.x + threadIdx.x; i0 < n;
        i0 += BCE_U * stride) {
@@ -2072,7 +2075,8 @@ __global__ __launch_bounds__(256) void bce_logits_kernel(const float* __restrict
   for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0 && loss) atomicAdd(loss, (red[0] + red[1]) + (red[2] + red[3]));
+  if (threadIdx.x == 0 && loss)
+    atomicAdd(loss, ((red[0] + red[1]) + (red[2] + red[3])) + ((red[4] + red[5]) + (red[6] + red[7])));
 }
 
 template <typename T>
@@ -2754,9 +2758,9 @@ int specenh_bce_logits(const float* z, const void* target, int target_dtype, lon
                        void* grad, int grad_dtype, double* loss_sum, void* stream) {
   if (!z || !target || n <= 0) return set_error(SPECENH_EINVAL, "bce args");
   hipStream_t st = (hipStream_t)stream;
-  const unsigned gx = std::min<unsigned>(grid1d(n), 1024);
+  const unsigned gx = (unsigned)std::max<long long>(1, std::min<long long>((n + 512 * 32 - 1) / (512 * 32), 128));
 #define SPECENH_BCE(TT, TG)                                                                   \
-  SPECENH_LAUNCH((bce_logits_kernel<TT, TG>), dim3(gx), dim3(256), 0, st, z,             \
+  SPECENH_LAUNCH((bce_logits_kernel<TT, TG>), dim3(gx), dim3(512), 0, st, z,             \
                      (const TT*)target, n, (TG*)grad, loss_sum)
   if (target_dtype == 0 && grad_dtype == 0) SPECENH_BCE(float, float);
   else if (target_dtype == 0 && grad_dtype == 1) SPECENH_BCE(float, __bf16);

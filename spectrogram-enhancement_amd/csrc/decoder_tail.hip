@@ -686,8 +686,9 @@ struct D3Args {
   const float* bt;   // [16]
   const void* wo;    // Conv2D(1) [5][5][16]
   const float* bo;   // [1]
-  float* out;        // [N][4H][128]
+  void* out;         // [N][4H][128], fp32 or (out_f16) fp16
   int N, H;
+  int out_f16;       // store the sigmoid outputs as fp16 (the C5 stream's 32,768 B per shot)
 };
 
 #ifdef SPECENH_D3_STATS  // development build (tools/d3_stats.py): per-wave barrier clocks
@@ -816,15 +817,24 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       return stage_at(p, il, p - il * SPI - 1);
     };
     // this lane's B-fragment offsets (pixel 16 wx + m + dx, group kg) in an input ring row,
-    // and its tail-input write offsets (pixel 2 (16 wx + m) + px, channels 16 nb + 4 kg ..)
-    int xo[3], x2w[2];
+    // and its 16-byte tail-input write offset: after the row-pair swap (store_pair below) a
+    // lane of an even row kg holds phase px = 0's channels 16 nb + 4 kg .. + 7 and a lane of an
+    // odd row phase px = 1's channels 16 nb + 4 (kg - 1) .. + 7, i.e. 16-byte group
+    // 2 nb + kg / 2 of pixel 2 (16 wx + m) + 1 + (kg & 1)
+    int xo[3];
 #pragma unroll
     for (int dx = -1; dx <= 1; ++dx) xo[dx + 1] = x1_off(16 * wx + m + dx + 1, kg);
-#pragma unroll
-    for (int px = 0; px < 2; ++px) {
-      const int ps = 2 * (16 * wx + m) + px + 1, ch = 16 * nb + 4 * kg;
-      x2w[px] = x2_off(ps, ch >> 3) + (ch & 7);
-    }
+    const int x2w16 = x2_off(2 * (16 * wx + m) + 1 + (kg & 1), 2 * nb + (kg >> 1));
+    // One tail-input row's two phases (px = 0, 1) as ONE ds_write_b128 per lane instead of two
+    // 4-way conflicted ds_write_b64: v_permlane16_swap exchanges odd rows of the first operand
+    // with even rows of the second, so rows kg, kg ^ 1 trade the halves they do not keep (PMC
+    // round 4: the 8-byte writes were 0.24 of the LDS-array cycles in bank conflicts; the
+    // 16-byte writes are 2-way at most, under their transfer cycles)
+    auto store_pair = [&](T* row, uint2 p0, uint2 p1) {
+      const auto sx = __builtin_amdgcn_permlane16_swap(p0.x, p1.x, false, false);
+      const auto sy = __builtin_amdgcn_permlane16_swap(p0.y, p1.y, false, false);
+      *reinterpret_cast<uint4*>(row + x2w16) = uint4{sx[0], sy[0], sx[1], sy[1]};
+    };
 #pragma unroll
     for (int p = 0; p < 3 + LEAD; ++p) stage(p);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -864,13 +874,11 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
             }
           }
         }
-#pragma unroll
-        for (int ph = 0; ph < 4; ++ph)
-          *reinterpret_cast<uint2*>(((ph >> 1) ? r1 : r0) + x2w[ph & 1]) = relu_pack<T>(acc[ph]);
+        store_pair(r0, relu_pack<T>(acc[0]), relu_pack<T>(acc[1]));
+        store_pair(r1, relu_pack<T>(acc[2]), relu_pack<T>(acc[3]));
       } else {  // tail-input rows 2 H1, 2 H1 + 1 (and past the last image): zero padding
-#pragma unroll
-        for (int ph = 0; ph < 4; ++ph)
-          *reinterpret_cast<uint2*>(((ph >> 1) ? r1 : r0) + x2w[ph & 1]) = uint2{0u, 0u};
+        *reinterpret_cast<uint4*>(r0 + x2w16) = uint4{0u, 0u, 0u, 0u};
+        *reinterpret_cast<uint4*>(r1 + x2w16) = uint4{0u, 0u, 0u, 0u};
       }
       if (mk[0] >= 0) wait_vmcnt(vmn - mk[0]);  // input position g + 3 has landed
       D3_BARRIER();
@@ -1042,8 +1050,12 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       s += dpp_shift<0x101>(E[2]);  // row_shl:1: lane m reads lane m + 1
       s += bb[bri];
       const long long n = (long long)blockIdx.x + (long long)eil * G;
-      a.out[(n * H3 + 2 * (etl - 1) + orow) * rows::MW + ocol] =
-          __builtin_amdgcn_rcpf(1.f + __expf(-s));
+      const long long o = (n * H3 + 2 * (etl - 1) + orow) * rows::MW + ocol;
+      const float y = __builtin_amdgcn_rcpf(1.f + __expf(-s));
+      if (a.out_f16)  // (uniform)
+        reinterpret_cast<_Float16*>(a.out)[o] = (_Float16)y;
+      else
+        reinterpret_cast<float*>(a.out)[o] = y;
     };
     auto cstep = [&](auto ic) {
       constexpr int I = decltype(ic)::value;  // g & 3
@@ -1108,7 +1120,8 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       const int il = t / TPI, tl = t - il * TPI;
       if (il >= nimg || tl < 2) return;
       const long long n = (long long)blockIdx.x + (long long)il * G;
-      tw.conv_out_sums(scb, a.out + n * H3 * rows::MW, 2 * tl - 4, lane);
+      tw.conv_out_sums(scb, reinterpret_cast<float*>(a.out) + n * H3 * rows::MW, 2 * tl - 4,
+                       lane);  // (fp32 output only: the host refuses out_f16 with V_D3_MAP)
     };
     auto cstep = [&](auto ic, const int g) {
       constexpr int I = decltype(ic)::value;  // g & 3
@@ -1210,10 +1223,13 @@ extern "C" int specenh_d3_stats(void* host, int bytes) {
 }
 #endif
 
-extern "C" int specenh_decoder3(int dtype, const void* x, int N, int H, int W, int C,
-                                const void* w1_gemm, const float* b1, int CO1, const void* wt_gemm,
-                                const float* bt, int CO2, const void* wo_gemm, const float* bo,
-                                int k, float* out, void* stream) {
+extern "C" int specenh_decoder3_ex(int dtype, const void* x, int N, int H, int W, int C,
+                                   const void* w1_gemm, const float* b1, int CO1,
+                                   const void* wt_gemm, const float* bt, int CO2,
+                                   const void* wo_gemm, const float* bo, int k, void* out,
+                                   int out_dtype, void* stream) {
+  if (out_dtype != SPECENH_DTYPE_F32 && out_dtype != SPECENH_DTYPE_F16)
+    return set_error(SPECENH_EUNSUPPORTED, "fused decoder: fp32 or fp16 output");
   if (N < 0 || H <= 0 || W <= 0) return set_error(SPECENH_EINVAL, "bad input shape");
   if (dtype != SPECENH_DTYPE_F16 && dtype != SPECENH_DTYPE_BF16)
     return set_error(SPECENH_EUNSUPPORTED, "fused decoder: fp16 / bf16 only");
@@ -1229,6 +1245,7 @@ extern "C" int specenh_decoder3(int dtype, const void* x, int N, int H, int W, i
   D3Args a{};
   a.x = x; a.w1 = w1_gemm; a.b1 = b1; a.wt = wt_gemm; a.bt = bt; a.wo = wo_gemm; a.bo = bo;
   a.out = out; a.N = N; a.H = H;
+  a.out_f16 = out_dtype == SPECENH_DTYPE_F16;
   hipStream_t st = (hipStream_t)stream;
   // (the kernels are named here, outside the lambda, so the device compilation instantiates
   // them)
@@ -1249,6 +1266,8 @@ extern "C" int specenh_decoder3(int dtype, const void* x, int N, int H, int W, i
   // the map ring)
   const unsigned grid = (unsigned)std::min<long long>(N, device_cus());
   const bool map = variant(V_D3_MAP) != 0, short_lead = variant(V_ROWS_SHORT_LEAD) != 0;
+  if (map && a.out_f16)
+    return set_error(SPECENH_EUNSUPPORTED, "fused decoder: the map consumer stores fp32 only");
   const dim3 gd(grid), bd(512);
   if (dtype == SPECENH_DTYPE_F16) {
     if (map)
@@ -1268,4 +1287,12 @@ extern "C" int specenh_decoder3(int dtype, const void* x, int N, int H, int W, i
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("decoder3: ") + hipGetErrorString(e));
   return SPECENH_OK;
+}
+
+extern "C" int specenh_decoder3(int dtype, const void* x, int N, int H, int W, int C,
+                                const void* w1_gemm, const float* b1, int CO1, const void* wt_gemm,
+                                const float* bt, int CO2, const void* wo_gemm, const float* bo,
+                                int k, float* out, void* stream) {
+  return specenh_decoder3_ex(dtype, x, N, H, W, C, w1_gemm, b1, CO1, wt_gemm, bt, CO2, wo_gemm, bo,
+                             k, out, SPECENH_DTYPE_F32, stream);
 }

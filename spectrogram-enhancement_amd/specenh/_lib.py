@@ -107,6 +107,10 @@ SIGNATURES = {
                                     _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p, _c.c_void_p,
                                     _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p,
                                     _c.c_void_p]),
+    "specenh_decoder3_ex": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                       _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p,
+                                       _c.c_void_p, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int,
+                                       _c.c_void_p, _c.c_int, _c.c_void_p]),
     "specenh_encoder2": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
                                     _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p, _c.c_void_p,
                                     _c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p]),

@@ -185,6 +185,7 @@ class AutoencoderEngine:
                          and _lib.get_variant("ENCODER_UNFUSED") == 0)
         self.t = 0  # Adam iterations
         self._bufs = {}
+        self.infer_out_dtype = torch.float32  # set_inference_output_dtype
         self._loss = torch.zeros(1, dtype=torch.float64, device=dev)
         # per-layer views into the flat buffers (the operators take tensors, not offsets)
         lp = self.w_lp if self.dt != F32 else self.w
@@ -234,6 +235,18 @@ class AutoencoderEngine:
         out.append((h, w, c))
         return out
 
+    def set_inference_output_dtype(self, dtype):
+        """Precision of forward(train=False)'s output: float32 (default, what Keras predict
+        returns) or float16 — BASELINE config 5's fp16 reconstructions (32,768 B per 128 x 128
+        shot), stored by the fused three-layer decoder (decoder3) itself."""
+        if dtype not in (torch.float32, torch.float16):
+            raise ValueError("inference output dtype must be torch.float32 or torch.float16")
+        if dtype != torch.float32 and not self.dec3:
+            raise NotImplementedError("fp16 inference output needs the fused three-layer decoder")
+        if dtype != self.infer_out_dtype:
+            self.infer_out_dtype = dtype
+            self._bufs = {k: v for k, v in self._bufs.items() if k[1]}  # drop inference buffers
+
     def _buffers(self, N, train):
         key = (N, train)
         b = self._bufs.get(key)
@@ -245,7 +258,7 @@ class AutoencoderEngine:
         for i in range(1, len(self.ops) + 1):
             H, W, C = shp[i]
             last = i == len(self.ops)
-            dtype = torch.float32 if (last and not train) else self.tdt
+            dtype = self.infer_out_dtype if (last and not train) else self.tdt
             tail_map = not train and ((self.tail and i == len(self.ops) - 1) or
                                       (self.dec3 and i == len(self.ops) - 2) or
                                       (self.enc2 and i == 2))  # maps kept in LDS

@@ -367,11 +367,11 @@ def _dec3_out(x, w1, b1, cout1, wt, bt, cout2, wo, bo, k, out):
     if any(t.dtype != torch.float32 for t in (b1, bt, bo)) or b1.numel() != cout1 or \
             bt.numel() != cout2 or bo.numel() != 1:
         raise ValueError("biases must be float32 [CO1], [CO2] and [1]")
-    if out.dtype != torch.float32 or out.numel() != N * 16 * H * W:
-        raise ValueError("out must be float32 [N, 4H, 4W(, 1)]")
-    _lib.check(_lib.lib().specenh_decoder3(
+    if out.dtype not in (torch.float32, torch.float16) or out.numel() != N * 16 * H * W:
+        raise ValueError("out must be float32 or float16 [N, 4H, 4W(, 1)]")
+    _lib.check(_lib.lib().specenh_decoder3_ex(
         _code(x), _vp(x), N, H, W, C, _vp(w1), _vp(b1), cout1, _vp(wt), _vp(bt), cout2, _vp(wo),
-        _vp(bo), k, _vp(out), _st(x)), "decoder3")
+        _vp(bo), k, _vp(out), _code(out), _st(x)), "decoder3")
 
 
 def _dec3(x, w1, b1, cout1, wt, bt, cout2, wo, bo, k):

@@ -172,3 +172,36 @@ def test_decoder3_lead_bitwise(gpu_device, hw, n, kernel_variant):
     assert "decoder3_kernel" in _lib.last_kernel_name()
     assert not torch.isnan(a).any()
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", ["float16", "mixed_bfloat16"])
+@pytest.mark.parametrize("hw,n", [((32, 32), 3), ((32, 32), 600), ((3, 32), 1000)])
+def test_decoder3_fp16_output(gpu_device, dtype, hw, n):
+    """set_inference_output_dtype(float16) (BASELINE config 5's fp16 reconstructions): the same
+    launch stores each sigmoid output rounded once to fp16, i.e. exactly the fp32 output cast
+    to fp16 (round to nearest even); the fp16 buffer is NaN-poisoned first."""
+    from specenh import _lib
+    eng, ops_, ws = _dec3_model(dtype, hw, seed=n + 21)
+    x = np.random.default_rng(n + 2).uniform(0, 1, (n,) + hw + (1,)).astype(np.float32)
+    xd = eng.to_compute(torch.from_numpy(x))
+    y32 = eng.forward(xd).clone()
+    eng.set_inference_output_dtype(torch.float16)
+    eng.forward(xd)
+    out = eng._buffers(n, False)["h"][len(ops_)]
+    assert out.dtype == torch.float16
+    out.fill_(float("nan"))
+    y16 = eng.forward(xd).clone()
+    torch.cuda.synchronize()
+    assert "decoder3_kernel" in _lib.last_kernel_name()
+    assert y16.dtype == torch.float16 and y16.shape == y32.shape
+    assert torch.equal(y16, y32.to(torch.float16))
+    eng.set_inference_output_dtype(torch.float32)
+    assert torch.equal(eng.forward(xd), y32)
+
+
+def test_fp16_output_needs_the_fused_decoder(gpu_device, kernel_variant):
+    kernel_variant("DECODER_UNFUSED", 1)
+    eng, _, _ = _dec3_model("float16", (8, 32), seed=1)
+    assert not eng.dec3
+    with pytest.raises(NotImplementedError, match="fused three-layer decoder"):
+        eng.set_inference_output_dtype(torch.float16)

@@ -1,5 +1,15 @@
-"""Time the conv-AE train step and inference forward (C4 shape: 128x128x1, 3-layer
-16/32/64 k5) on one GPU. Usage: python tools/ae_bench.py [--batch 128] [--dtype bf16]"""
+"""Time the conv-AE train step and inference forward on one GPU.
+
+    python tools/ae_bench.py [--model 3layer] [--batch 128] [--dtype bf16]
+
+Models (the reference's graphs, Keras layer order):
+  3layer        VAE/manual_scan_3layers.py:186-199, 128x128x1 (C4): conv 16/32/64 k5, pools,
+                convT 64/32/16 k5 s2, conv 1 k5 (the bench's model)
+  manual_scan   VAE/manual_scan.py:190-199 at (conv1, conv2, k) = (64, 32, 5), 256x128x1:
+                conv 64, pool, conv 32, pool, convT 32, convT 64, conv 1 (all k5)
+  hyper_k3/k5/k7  VAE/hyperparam_scan.py:153-161 (32/32 at kernel 3/5/7), 256x128x1
+  graphs        VAE/graphs.ipynb (the notebook's model = hyper_k3), 256x128x1
+FLOPs are counted from the layer list (2 x MACs, x3 for a training step)."""
 import argparse
 import json
 import os
@@ -13,25 +23,51 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
                                 "spectrogram-enhancement_amd"))
 from specenh import ae  # noqa: E402
 
-FLOP_FWD = 2 * 248.9e6  # per sample, SURVEY.md §8 A7 (sum of per-layer MACs x 2)
-
-
-def ops():
+def ops(model="3layer"):
     C, P = ae.ConvOp, ae.PoolOp
-    return [C("conv", 1, 16, 5, "relu"), P(), C("conv", 16, 32, 5, "relu"), P(),
-            C("conv", 32, 64, 5, "relu"), P(), C("convT", 64, 64, 5, "relu", stride=2),
-            C("convT", 64, 32, 5, "relu", stride=2), C("convT", 32, 16, 5, "relu", stride=2),
-            C("conv", 16, 1, 5, "sigmoid")]
+    if model == "3layer":
+        return [C("conv", 1, 16, 5, "relu"), P(), C("conv", 16, 32, 5, "relu"), P(),
+                C("conv", 32, 64, 5, "relu"), P(), C("convT", 64, 64, 5, "relu", stride=2),
+                C("convT", 64, 32, 5, "relu", stride=2), C("convT", 32, 16, 5, "relu", stride=2),
+                C("conv", 16, 1, 5, "sigmoid")], (128, 128, 1)
+    if model == "manual_scan":
+        c1, c2, k = 64, 32, 5
+    elif model in ("hyper_k3", "hyper_k5", "hyper_k7", "graphs"):
+        c1 = c2 = 32
+        k = 3 if model == "graphs" else int(model[-1])
+    else:
+        raise SystemExit(f"unknown model {model}")
+    return [C("conv", 1, c1, k, "relu"), P(), C("conv", c1, c2, k, "relu"), P(),
+            C("convT", c2, c2, k, "relu", stride=2), C("convT", c2, c1, k, "relu", stride=2),
+            C("conv", c1, 1, k, "sigmoid")], (256, 128, 1)
+
+
+def fwd_flops(layer_ops, shape):
+    h, w, _ = shape
+    f = 0
+    for op in layer_ops:
+        if isinstance(op, ae.PoolOp):
+            h, w = h // 2, w // 2
+            continue
+        if op.kind == "convT":  # MACs at the input resolution x stride^2 = output pixels x k^2 ci co / s^2
+            f += 2 * h * w * op.k * op.k * op.cin * op.cout
+            h, w = h * op.stride, w * op.stride
+        else:
+            f += 2 * h * w * op.k * op.k * op.cin * op.cout
+    return f
 
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="3layer")
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--infer-batch", type=int, default=1024)
     a = ap.parse_args()
-    eng = ae.AutoencoderEngine(ops(), (128, 128, 1), compute_dtype=a.dtype, device="cuda:0")
+    layer_ops, shape = ops(a.model)
+    FLOP_FWD = fwd_flops(layer_ops, shape)
+    eng = ae.AutoencoderEngine(layer_ops, shape, compute_dtype=a.dtype, device="cuda:0")
     rng = np.random.default_rng(0)
     ws = []
     for op in eng.ops:
@@ -40,8 +76,8 @@ def main():
             lim = np.sqrt(6.0 / (op.k * op.k * (op.cin + op.cout)))
             ws += [rng.uniform(-lim, lim, shape).astype(np.float32), np.zeros(op.cout, np.float32)]
     eng.set_keras_weights(ws)
-    x = eng.to_compute(torch.rand(a.batch, 128, 128, 1, device="cuda:0"))
-    y = eng.to_compute(torch.rand(a.batch, 128, 128, 1, device="cuda:0"))
+    x = eng.to_compute(torch.rand(a.batch, *shape, device="cuda:0"))
+    y = eng.to_compute(torch.rand(a.batch, *shape, device="cuda:0"))
     for _ in range(3):
         eng.train_step(x, y)
     torch.cuda.synchronize()
@@ -50,7 +86,7 @@ def main():
         eng.train_step(x, y)
     torch.cuda.synchronize()
     train_ms = (time.perf_counter() - t0) / a.steps * 1e3
-    xi = eng.to_compute(torch.rand(a.infer_batch, 128, 128, 1, device="cuda:0"))
+    xi = eng.to_compute(torch.rand(a.infer_batch, *shape, device="cuda:0"))
     for _ in range(2):
         eng.forward(xi)
     torch.cuda.synchronize()
@@ -59,12 +95,16 @@ def main():
         eng.forward(xi)
     torch.cuda.synchronize()
     inf_ms = (time.perf_counter() - t0) / a.steps * 1e3
-    res = {"dtype": a.dtype, "train_batch": a.batch, "train_ms": train_ms,
+    res = {"model": a.model, "input": shape, "fwd_gflop_per_sample": FLOP_FWD / 1e9,
+           "fused": {"enc2": eng.enc2, "dec3": eng.dec3, "tail": eng.tail,
+                     "conv_pool": sorted(eng.fused)},
+           "dtype": a.dtype, "train_batch": a.batch, "train_ms": train_ms,
            "train_samples_per_s": a.batch / train_ms * 1e3,
            "train_tflops": 3 * FLOP_FWD * a.batch / train_ms / 1e9,
            "infer_batch": a.infer_batch, "infer_ms": inf_ms,
            "infer_samples_per_s": a.infer_batch / inf_ms * 1e3,
-           "infer_tflops": FLOP_FWD * a.infer_batch / inf_ms / 1e9}
+           "infer_tflops": FLOP_FWD * a.infer_batch / inf_ms / 1e9,
+           "infer_frac_of_16bit_mfma_peak": FLOP_FWD * a.infer_batch / inf_ms / 1e9 / 2500.0}
     print(json.dumps(res))
 
 

@@ -1374,6 +1374,15 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
   // group addresses row q (pixel column + q, + 4 for the upper half) and elements 4p .. 4p+3
   const int g4 = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
   const int prow = g4 >> 1, pcol = 8 * (g4 & 1) + q;
+  // this wave's taps t = wave + 4 tt as patch offsets (elements), formed once; taps past the
+  // kernel repeat the last one (their MFMAs run, their sums are never stored)
+  int toff[C1 ? 1 : MAXT];
+#pragma unroll
+  for (int tt = 0; tt < (C1 ? 1 : MAXT); ++tt) {
+    const int t = min(wave + 4 * tt, ntap - 1);
+    const int jy = t / g.KW, jx = t - (t / g.KW) * g.KW;
+    toff[tt] = (jy * PW + jx) * PST;
+  }
 
   // ---- per-thread prefetch registers of one tile ----
   uint4 rd[NDV];
@@ -1517,26 +1526,31 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
         }
       }
     } else {
+      // Per pixel group: every fragment read is issued before the MFMAs that use it, and the
+      // MFMAs run unconditionally (a tap past the kernel reads a clamped, valid offset; its
+      // accumulator is never stored): round 4's loop read each tap's B fragment, waited
+      // lgkmcnt(0) and formed the next tap's offset with a run-time division, serialising
+      // ~15 SALU, an LDS round trip and two MFMAs per tap.
+#pragma unroll 2
       for (int pg = 0; pg < 8; ++pg) {
         const int r = 2 * pg + prow;
-        s16x8 af[NTW];
+        s16x8 af[NTW], bf[MAXT];
         const T* da = sD + (r * 16 + pcol) * DST + 4 * pp;
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
           const s16x4 lo = lds_tr16(da + 16 * j), hi = lds_tr16(da + 4 * DST + 16 * j);
           af[j] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         }
+        const T* pr = sP + (r * PW + pcol) * PST + 4 * pp;
 #pragma unroll
         for (int tt = 0; tt < MAXT; ++tt) {
-          const int t = wave + 4 * tt;
-          if (t >= ntap) break;  // wave-uniform
-          const int jy = t / g.KW, jx = t - (t / g.KW) * g.KW;
-          const T* pb = sP + ((r + jy) * PW + pcol + jx) * PST + 4 * pp;
-          const s16x4 lo = lds_tr16(pb), hi = lds_tr16(pb + 4 * PST);
-          const s16x8 bf = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-          for (int j = 0; j < NTW; ++j) acc[tt][j] = mfma_s16<T>(af[j], bf, acc[tt][j]);
+          const s16x4 lo = lds_tr16(pr + toff[tt]), hi = lds_tr16(pr + toff[tt] + 4 * PST);
+          bf[tt] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         }
+#pragma unroll
+        for (int tt = 0; tt < MAXT; ++tt)
+#pragma unroll
+          for (int j = 0; j < NTW; ++j) acc[tt][j] = mfma_s16<T>(af[j], bf[tt], acc[tt][j]);
         if (do_bias) {
 #pragma unroll
           for (int j = 0; j < NTW; ++j) bacc[j] = mfma_s16<T>(af[j], ones, bacc[j]);
@@ -1622,23 +1636,31 @@ __global__ __launch_bounds__(256) void wgrad_trp_kernel(WgradTrArgs a) {
   const T* __restrict__ dout = reinterpret_cast<const T*>(a.dout);
   const int CO = g0.CO, OHs = g0.OHs, OWs = g0.OWs;
 
-  // this wave's run of (phase, tap) blocks: u in [ub, ue) over the phases' taps in order
+  // this wave's run of (phase, tap) blocks: u in [ub, ue) over the phases' taps in order;
+  // blocks past the run repeat its last block (their MFMAs run, their sums are never
+  // stored). A run spans at most two phases (host-checked, wgrad_trp_runs_ok): blocks
+  // tt < split use phase pa's dOut fragment, the others phase pb's.
   int U = 0;
 #pragma unroll
   for (int p = 0; p < 4; ++p) U += a.g[p].KH * a.g[p].KW;
   const int ub = wave * U / 4, ue = (wave + 1) * U / 4;
-  int aoff[MAXT], boff[MAXT], tph[MAXT], ttap[MAXT];
+  int boff[MAXT], tph[MAXT], ttap[MAXT];
 #pragma unroll
   for (int tt = 0; tt < MAXT; ++tt) {
-    int u = ub + tt, p = 0;
+    int u = min(ub + tt, ue - 1), p = 0;
     while (p < 3 && u >= a.g[p].KH * a.g[p].KW) { u -= a.g[p].KH * a.g[p].KW; ++p; }
     const Geo& g = a.g[p];
     const int jy = u / max(g.KW, 1), jx = u - (u / max(g.KW, 1)) * g.KW;
     tph[tt] = p;
     ttap[tt] = u;
-    aoff[tt] = p * 256 * DST;
     boff[tt] = ((a.upt - g.pad_t + jy) * PW + a.upl - g.pad_l + jx) * PST;
   }
+  const int pa = tph[0], pb = tph[MAXT - 1];
+  int split = MAXT;
+#pragma unroll
+  for (int tt = MAXT - 1; tt >= 1; --tt)
+    if (tph[tt] != pa) split = tt;
+  const int aoffa = pa * 256 * DST, aoffb = pb * 256 * DST;
 
   f32x4 acc[MAXT];
 #pragma unroll
@@ -1710,20 +1732,24 @@ __global__ __launch_bounds__(256) void wgrad_trp_kernel(WgradTrArgs a) {
     stage();
     lds_sync();
     if (tile + 1 < t_end) fetch(tile + 1);
-#pragma unroll 1
+    // per pixel group: both dOut fragments and every B fragment read before the MFMAs, which
+    // then run back to back (round 4 waited lgkmcnt(0) before each one and branched around
+    // the run's end and phase changes, moving accumulators through VGPRs)
+#pragma unroll 2
     for (int pg = 0; pg < 8; ++pg) {
       const int r = 2 * pg + prow;
       const int pix = r * 16 + pcol, ppix = r * PW + pcol;
-      s16x8 af = afrag(sD + aoff[0] + pix * DST + 4 * pp);
+      const s16x8 a0 = afrag(sD + aoffa + pix * DST + 4 * pp);
+      const s16x8 a1 = afrag(sD + aoffb + pix * DST + 4 * pp);
+      s16x8 bf[MAXT];
 #pragma unroll
       for (int tt = 0; tt < MAXT; ++tt) {
-        if (ub + tt >= ue) break;  // wave-uniform
-        if (tt > 0 && tph[tt] != tph[tt - 1]) af = afrag(sD + aoff[tt] + pix * DST + 4 * pp);
-        const T* pb = sP + ppix * PST + boff[tt] + 4 * pp;
-        const s16x4 lo = lds_tr16(pb), hi = lds_tr16(pb + 4 * PST);
-        const s16x8 bf = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        acc[tt] = mfma_s16<T>(af, bf, acc[tt]);
+        const T* pb_ = sP + ppix * PST + boff[tt] + 4 * pp;
+        const s16x4 lo = lds_tr16(pb_), hi = lds_tr16(pb_ + 4 * PST);
+        bf[tt] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
+#pragma unroll
+      for (int tt = 0; tt < MAXT; ++tt) acc[tt] = mfma_s16<T>(tt < split ? a0 : a1, bf[tt], acc[tt]);
       if (do_bias) bacc = mfma_s16<T>(afrag(sD + wave * 256 * DST + pix * DST + 4 * pp), ones, bacc);
     }
   }
@@ -2546,6 +2572,16 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
       lo_x = std::min(lo_x, -g.pad_l);
       hi_x = std::max(hi_x, 15 - g.pad_l + g.KW - 1);
       U += g.KH * g.KW;
+    }
+    // each wave's run of (phase, tap) blocks (wgrad_trp_kernel) spans at most two phases
+    auto phase_of = [&](int u) {
+      int p = 0;
+      while (p < 3 && u >= w.g[p].KH * w.g[p].KW) { u -= w.g[p].KH * w.g[p].KW; ++p; }
+      return p;
+    };
+    for (int wv = 0; wv < 4 && ok && U > 0; ++wv) {
+      const int ub = wv * U / 4, ue = (wv + 1) * U / 4;
+      if (ue > ub && phase_of(ue - 1) - phase_of(ub) > 1) ok = false;
     }
     if (ok && hi_y - lo_y + 1 <= 20 && hi_x - lo_x + 1 <= 20 && U <= 28) {
       a.upt = upt;

@@ -38,6 +38,9 @@
 #define SPECENH_C1024_WAVES 4
 #define SPECENH_C1024_OCC 3
 #endif
+#ifndef SPECENH_C1024_PF
+#define SPECENH_C1024_PF 1
+#endif
 #ifndef SPECENH_STFT_PF_AFTER_WAIT
 #define SPECENH_STFT_PF_AFTER_WAIT 1
 #endif
@@ -105,7 +108,7 @@ template <> struct Cfg<64>   { static constexpr int G = 8,  WAVES = 8, OCC = 1, 
 template <> struct Cfg<128>  { static constexpr int G = 8,  WAVES = 8, OCC = 1, R1 = 16, R2 = 8,  R3 = 1, PF = 1; };
 template <> struct Cfg<256>  { static constexpr int G = 16, WAVES = 8, OCC = 1, R1 = 16, R2 = 16, R3 = 1, PF = 1; };
 template <> struct Cfg<512>  { static constexpr int G = 16, WAVES = 8, OCC = 1, R1 = 32, R2 = 16, R3 = 1, PF = 1; };
-template <> struct Cfg<1024> { static constexpr int G = 32, WAVES = SPECENH_C1024_WAVES, OCC = SPECENH_C1024_OCC, R1 = 32, R2 = 32, R3 = 1, PF = 1; };
+template <> struct Cfg<1024> { static constexpr int G = 32, WAVES = SPECENH_C1024_WAVES, OCC = SPECENH_C1024_OCC, R1 = 32, R2 = 32, R3 = 1, PF = SPECENH_C1024_PF; };
 template <> struct Cfg<2048> { static constexpr int G = 64, WAVES = 4, OCC = 1, R1 = 32, R2 = 8,  R3 = 8, PF = 1; };
 template <> struct Cfg<4096> { static constexpr int G = 64, WAVES = 2, OCC = 1, R1 = 32, R2 = 16, R3 = 8, PF = 0; };
 
@@ -1022,7 +1025,10 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
     }
     return;
   }
-  load_pair<N>(s0, make_rsrc(a.x + q * a.x_stride, xbytes), make_rsrc(a.x, 0), a.hop, fa, a.T, gl);
+  // C::PF = 0: no register prefetch; each task loads its own samples at its start (the
+  // other resident waves cover the latency)
+  if constexpr (C::PF)
+    load_pair<N>(s0, make_rsrc(a.x + q * a.x_stride, xbytes), make_rsrc(a.x, 0), a.hop, fa, a.T, gl);
   __syncthreads();
 
   // Per task: the tile's spectrum (next task's samples prefetched meanwhile), publish the
@@ -1038,7 +1044,10 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
     // NORMALIZE: the next task's samples are requested after the team wait, not inside
     // pair_spectrum: vmcnt is in order, so the wave polling the granules would otherwise
     // first wait for its whole prefetch to land while the workgroup idles at the barrier
-    constexpr bool pf_inside = !normalize || !SPECENH_STFT_PF_AFTER_WAIT;
+    constexpr bool pf_inside = C::PF && (!normalize || !SPECENH_STFT_PF_AFTER_WAIT);
+    if constexpr (!C::PF)
+      load_pair<N>(s0, make_rsrc(a.x + shot * a.x_stride, xbytes), make_rsrc(a.x, 0), a.hop, fa, a.T,
+                   gl);
     pair_spectrum<N>(a, s0, s0, s_tw, s_win, s_dc, buf, gl, dcb, xn, xn, fa, pf_inside, want_log, normalize,
                      pv, dmin, dmax);
     const __amdgpu_buffer_rsrc_t orr = make_rsrc(a.out + shot * plane, plane * 4);
@@ -1090,7 +1099,7 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
       }
     }
     lds_barrier();
-    if constexpr (!pf_inside) {
+    if constexpr (C::PF && !pf_inside) {
       __builtin_amdgcn_sched_barrier(0);
       load_pair<N>(s0, xn, xn, a.hop, (a.flags & SPECENH_STFT_DEV_NOLOAD) ? 0 : fa, a.T, gl);
       __builtin_amdgcn_sched_barrier(0);

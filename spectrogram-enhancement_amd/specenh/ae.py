@@ -336,6 +336,18 @@ class AutoencoderEngine:
         N = x.shape[0]
         if x.dtype != self.tdt or not x.is_contiguous() or tuple(x.shape[1:]) != self.input_shape:
             raise ValueError(f"forward expects a contiguous {self.tdt} [N, *{self.input_shape}]")
+        # one launch addresses at most 2^31 - 1 elements of a tensor: larger inference batches
+        # (e.g. the 64-channel manual_scan.py model at 256 x 128) run in consecutive slices
+        per = max(h * w * c for h, w, c in self.shapes())
+        cap = (2 ** 31 - 1) // per
+        if N > cap and not train and timing is None and kernels is None:
+            out = None
+            for s0 in range(0, N, cap):
+                y = self.forward(x[s0:s0 + cap])
+                if out is None:
+                    out = torch.empty((N,) + tuple(y.shape[1:]), dtype=y.dtype, device=y.device)
+                out[s0:s0 + y.shape[0]].copy_(y)
+            return out
         b = self._buffers(N, train)
         b["h"][0] = x
         if train:

@@ -63,18 +63,21 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--infer-batch", type=int, default=1024)
+    ap.add_argument("--infer-batch", type=int, default=None,
+                    help="default 1024 at 128 x 128, 512 at 256 x 128")
     a = ap.parse_args()
     layer_ops, shape = ops(a.model)
+    if a.infer_batch is None:
+        a.infer_batch = 1024 if shape[0] == 128 else 512
     FLOP_FWD = fwd_flops(layer_ops, shape)
     eng = ae.AutoencoderEngine(layer_ops, shape, compute_dtype=a.dtype, device="cuda:0")
     rng = np.random.default_rng(0)
     ws = []
     for op in eng.ops:
         if isinstance(op, ae.ConvOp):
-            shape = (op.k, op.k, op.cin, op.cout) if op.kind == "conv" else (op.k, op.k, op.cout, op.cin)
+            kshape = (op.k, op.k, op.cin, op.cout) if op.kind == "conv" else (op.k, op.k, op.cout, op.cin)
             lim = np.sqrt(6.0 / (op.k * op.k * (op.cin + op.cout)))
-            ws += [rng.uniform(-lim, lim, shape).astype(np.float32), np.zeros(op.cout, np.float32)]
+            ws += [rng.uniform(-lim, lim, kshape).astype(np.float32), np.zeros(op.cout, np.float32)]
     eng.set_keras_weights(ws)
     x = eng.to_compute(torch.rand(a.batch, *shape, device="cuda:0"))
     y = eng.to_compute(torch.rand(a.batch, *shape, device="cuda:0"))

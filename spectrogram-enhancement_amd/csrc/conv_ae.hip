@@ -1374,6 +1374,13 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
   // group addresses row q (pixel column + q, + 4 for the upper half) and elements 4p .. 4p+3
   const int g4 = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
   const int prow = g4 >> 1, pcol = 8 * (g4 & 1) + q;
+  // C1: the im2col taps t < 31 as offsets jy PW + jx into the staged patch (uniform)
+  int c1off[C1 ? 31 : 1];
+#pragma unroll
+  for (int t = 0; t < (C1 ? 31 : 1); ++t) {
+    const int tc = min(t, ntap - 1);
+    c1off[t] = (tc / g.KW) * PW + tc - (tc / g.KW) * g.KW;
+  }
   // this wave's taps t = wave + 4 tt as patch offsets (elements), formed once; taps past the
   // kernel repeat the last one (their MFMAs run, their sums are never stored)
   int toff[C1 ? 1 : MAXT];
@@ -1390,10 +1397,13 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
   uint4 rp[C1 ? 1 : NPV];
   T rp1[C1 ? NPV : 1];
   auto tile_org = [&](long long tile, int& n, int& oyt, int& oxt) {
-    n = (int)(tile / (nty * ntx));
-    const int trem = (int)(tile - (long long)n * nty * ntx);
-    oyt = (trem / ntx) * 16;
-    oxt = (trem - (trem / ntx) * ntx) * 16;
+    // 32-bit unsigned divisions (the host keeps N x tiles below 2^31): the 64-bit divide
+    // routine had cost ~200 SALU per tile
+    const unsigned tu = (unsigned)tile, per = (unsigned)(nty * ntx);
+    n = (int)(tu / per);
+    const unsigned trem = tu - (unsigned)n * per;
+    oyt = (int)(trem / (unsigned)ntx) * 16;
+    oxt = (int)(trem - (trem / (unsigned)ntx) * (unsigned)ntx) * 16;
   };
   auto fetch = [&](long long tile) {
     int n, oyt, oxt;
@@ -1468,7 +1478,9 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
       }
       lds_sync();
       // im2col row of this thread's pixel: taps (ky, kx) -> column ky*KW + kx; 31 = ones
-      const int r = tid >> 4, c = tid & 15;
+      // (tap offsets from c1off, formed once: a run-time division per tap and tile had made
+      // this kernel SALU-bound, 22 M SALU for 0.13 M MFMAs per C4 step)
+      const T* const srow = sIn + (tid >> 4) * PW + (tid & 15);
 #pragma unroll
       for (int t4 = 0; t4 < 8; ++t4) {
         uint32_t w[2];
@@ -1482,8 +1494,7 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
             if (t == 31) {
               b = (unsigned short)one;
             } else if (t < ntap) {
-              const int jy = t / g.KW, jx = t - (t / g.KW) * g.KW;
-              b = __builtin_bit_cast(unsigned short, sIn[(r + jy) * PW + c + jx]);
+              b = __builtin_bit_cast(unsigned short, srow[c1off[t]]);
             }
             pk |= (uint32_t)b << (16 * e2);
           }
@@ -1677,10 +1688,13 @@ __global__ __launch_bounds__(256) void wgrad_trp_kernel(WgradTrArgs a) {
   uint4 rd[8];  // 32 x 32 dOut pixels x 16 co: 2048 uint4
   uint4 rp[4];  // <= 20 x 20 patch pixels x 16 ci: 800 uint4
   auto tile_org = [&](long long tile, int& n, int& oyt, int& oxt) {
-    n = (int)(tile / (nty * ntx));
-    const int trem = (int)(tile - (long long)n * nty * ntx);
-    oyt = (trem / ntx) * 16;
-    oxt = (trem - (trem / ntx) * ntx) * 16;
+    // 32-bit unsigned divisions (the host keeps N x tiles below 2^31): the 64-bit divide
+    // routine had cost ~200 SALU per tile
+    const unsigned tu = (unsigned)tile, per = (unsigned)(nty * ntx);
+    n = (int)(tu / per);
+    const unsigned trem = tu - (unsigned)n * per;
+    oyt = (int)(trem / (unsigned)ntx) * 16;
+    oxt = (int)(trem - (trem / (unsigned)ntx) * (unsigned)ntx) * 16;
   };
   auto fetch = [&](long long tile) {
     int n, oyt, oxt;
@@ -1817,10 +1831,13 @@ __global__ __launch_bounds__(64) void wgrad_co1_kernel(WgradTrArgs a) {
   uint4 rp[NPV];
   uint2 rd;
   auto tile_org = [&](long long tile, int& n, int& oyt, int& oxt) {
-    n = (int)(tile / (nty * ntx));
-    const int trem = (int)(tile - (long long)n * nty * ntx);
-    oyt = (trem / ntx) * 16;
-    oxt = (trem - (trem / ntx) * ntx) * 16;
+    // 32-bit unsigned divisions (the host keeps N x tiles below 2^31): the 64-bit divide
+    // routine had cost ~200 SALU per tile
+    const unsigned tu = (unsigned)tile, per = (unsigned)(nty * ntx);
+    n = (int)(tu / per);
+    const unsigned trem = tu - (unsigned)n * per;
+    oyt = (int)(trem / (unsigned)ntx) * 16;
+    oxt = (int)(trem - (trem / (unsigned)ntx) * (unsigned)ntx) * 16;
   };
   auto fetch = [&](long long tile) {
     int n, oyt, oxt;
@@ -2065,19 +2082,19 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_vec_kernel(const T* __restri
 // Keras BCE after a sigmoid (graph mode): sigmoid_cross_entropy_with_logits; the grad of
 // the mean is (sigmoid(z) - t) / n. One fp64 atomic per workgroup.
 template <typename TT, typename TG>
-__global__ __launch_bounds__(512) void bce_logits_kernel(const float* __restrict__ z,
+__global__ __launch_bounds__(256) void bce_logits_kernel(const float* __restrict__ z,
                                                           const TT* __restrict__ t, long long n,
                                                           TG* __restrict__ grad,
                                                           double* __restrict__ loss) {
-  __shared__ double red[8];
+  __shared__ double red[4];
   double acc = 0.0;
   const float inv = 1.0f / (float)n;
   // BCE_U elements per thread per pass with all their loads issued first (a grid-stride loop
-  // of one element waited a full round trip per element: 22 us at C4's 2 M elements). The
-  // grid is at most 128 workgroups: every workgroup ends in one device-scope fp64 atomic on
-  // the same word, and those serialise at the memory side (~20 ns each: 1024 of them were
-  // 21 us of C4's 1.0 ms step, round 4)
-  constexpr int BCE_U = 32;
+  // of one element waited a full round trip per element: 22 us at C4's 2 M elements).
+  // log1p(e) for e = exp(-|z|) in (0, 1] by Goldberg's form u = 1 + e, log(u) e / (u - 1)
+  // (e when u rounds to 1), the sigmoid by the hardware reciprocal: the library log1pf and
+  // IEEE division were ~190 instructions per element (round 4: 21 us per C4 step).
+  constexpr int BCE_U = 8;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i0 = blockIdx.x * (long long)blockDim.x + threadIdx.x; i0 < n;
        i0 += BCE_U * stride) {
@@ -2088,21 +2105,26 @@ __global__ __launch_bounds__(512) void bce_logits_kernel(const float* __restrict
       zv[u] = i < n ? z[i] : 0.f;
       tv[u] = i < n ? to_f(t[i]) : 0.f;
     }
+    float part = 0.f;
 #pragma unroll
     for (int u = 0; u < BCE_U; ++u) {
       const long long i = i0 + u * stride;
-      if (i < n) {
-        const float zi = zv[u], ti = tv[u];
-        acc += (double)(fmaxf(zi, 0.f) - zi * ti + log1pf(__expf(-fabsf(zi))));
-        if (grad) grad[i] = from_f<TG>((1.f / (1.f + __expf(-zi)) - ti) * inv);
-      }
+      const float zi = zv[u], ti = tv[u];
+      const float e = __expf(-fabsf(zi));
+      const float w = 1.f + e;
+      const float l1p = w == 1.f ? e : __logf(w) * (e * __builtin_amdgcn_rcpf(w - 1.f));
+      const float li = fmaxf(zi, 0.f) - zi * ti + l1p;
+      part += i < n ? li : 0.f;
+      // sigmoid(z) = 1 / (1 + exp(-z)): exp(-z) = e for z >= 0, 1 / e otherwise
+      const float sg = zi >= 0.f ? __builtin_amdgcn_rcpf(w) : e * __builtin_amdgcn_rcpf(w);
+      if (grad && i < n) grad[i] = from_f<TG>((sg - ti) * inv);
     }
+    acc += (double)part;
   }
   for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0 && loss)
-    atomicAdd(loss, ((red[0] + red[1]) + (red[2] + red[3])) + ((red[4] + red[5]) + (red[6] + red[7])));
+  if (threadIdx.x == 0 && loss) atomicAdd(loss, (red[0] + red[1]) + (red[2] + red[3]));
 }
 
 template <typename T>
@@ -2794,9 +2816,9 @@ int specenh_bce_logits(const float* z, const void* target, int target_dtype, lon
                        void* grad, int grad_dtype, double* loss_sum, void* stream) {
   if (!z || !target || n <= 0) return set_error(SPECENH_EINVAL, "bce args");
   hipStream_t st = (hipStream_t)stream;
-  const unsigned gx = (unsigned)std::max<long long>(1, std::min<long long>((n + 512 * 32 - 1) / (512 * 32), 128));
+  const unsigned gx = std::min<unsigned>(grid1d(n), 1024);
 #define SPECENH_BCE(TT, TG)                                                                   \
-  SPECENH_LAUNCH((bce_logits_kernel<TT, TG>), dim3(gx), dim3(512), 0, st, z,             \
+  SPECENH_LAUNCH((bce_logits_kernel<TT, TG>), dim3(gx), dim3(256), 0, st, z,             \
                      (const TT*)target, n, (TG*)grad, loss_sum)
   if (target_dtype == 0 && grad_dtype == 0) SPECENH_BCE(float, float);
   else if (target_dtype == 0 && grad_dtype == 1) SPECENH_BCE(float, __bf16);

@@ -21,6 +21,8 @@ done
 for M in 3layer hyper_k3; do
   timeout -k 10 120 python tools/ae_bench.py --model $M --dtype float16 >> gpurun_out/ae_bench_$TAG.txt 2>&1 || exit 1
 done
+step "stft flags"
+timeout -k 10 200 python tools/stft_c2_flags.py > gpurun_out/stft_flags_$TAG.txt 2>&1 || exit 1
 step "rocprof c5"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_$TAG -o prof -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-stages --streams 1 > $R/gpurun_out/bench_prof_$TAG.json 2> $R/gpurun_out/bench_prof_$TAG.err || exit 1

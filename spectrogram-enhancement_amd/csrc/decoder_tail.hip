@@ -674,6 +674,9 @@ __device__ __forceinline__ int x2_off(int ps, int g) { return ps * d3::X2ST + 8 
 #ifndef SPECENH_D3_CPRIO
 #define SPECENH_D3_CPRIO 0  // measured +4 % (tools/lib_ab.sh, profiles/r04_d3_ab.txt)
 #endif
+#ifndef SPECENH_D3_READ_AHEAD
+#define SPECENH_D3_READ_AHEAD 1
+#endif
 #ifndef SPECENH_D3_BRANCHFREE
 #define SPECENH_D3_BRANCHFREE 1
 #endif
@@ -1005,11 +1008,27 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       // the scheduler can interleave their MFMA chains)
       f32x4 acc[4] = {bias, bias, bias, bias};
       int u0[4] = {0, 4, 10, 16};  // first tap register of each phase (4 / 6 / 6 / 9 taps)
+      // all nine B fragments first, then the 25 MFMAs: read in pairs just ahead of their
+      // MFMAs (the compiler's schedule), each pair's LDS latency was exposed
+#if SPECENH_D3_READ_AHEAD
+      uint4 bq[9];
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx)
+          bq[3 * (dy + 1) + dx + 1] =
+              *reinterpret_cast<const uint4*>(x2r + ((T8 + dy + 8) & 7) * X2ROW + xo[dx + 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
       for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
         for (int dx = -1; dx <= 1; ++dx) {
+#if SPECENH_D3_READ_AHEAD
+          const uint4 b = bq[3 * (dy + 1) + dx + 1];
+#else
           const uint4 b = *reinterpret_cast<const uint4*>(x2r + ((T8 + dy + 8) & 7) * X2ROW + xo[dx + 1]);
+#endif
 #pragma unroll
           for (int ph = 0; ph < 4; ++ph) {
             const int ky = ky_of(ph >> 1, dy), kx = ky_of(ph & 1, dx);

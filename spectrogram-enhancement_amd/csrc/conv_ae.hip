@@ -1926,9 +1926,10 @@ __global__ __launch_bounds__(64) void wgrad_co1_kernel(WgradTrArgs a) {
 
 // dst[e] += sum_{z < nz} part[z * n + e], always in the same order (bit-reproducible). One
 // launch carries two such sums (the weight and the bias gradient): blocks [0, nb0) do job 0.
-// A workgroup owns EW consecutive e (EW = 16, 4 or 1, fixed per job so that a small n still
-// spreads over enough workgroups) and ZL = 256 / EW z-lanes; lane zl sums z = zl, zl + ZL,
-// ... in order (8 loads in flight), then the lane sums meet in a fixed pairwise tree.
+// A 1024-thread workgroup owns 64 consecutive e (a wave's loads are one 256-byte run) and 16
+// z-lanes (its waves); lane zl sums z = zl, zl + 16, ... in order with 8 loads in flight, then
+// the 16 lane sums meet in a fixed pairwise tree. (Round 4 gave a workgroup 16 e x 16 z-lanes:
+// 64-byte runs per wave load and up to 16 serial round trips per lane, 8.7 us per launch.)
 struct SumJob {
   const float* part;
   float* dst;
@@ -1936,31 +1937,33 @@ struct SumJob {
   int nz, ew;
 };
 
-__global__ __launch_bounds__(256) void ordered_sum_kernel(SumJob j0, SumJob j1, unsigned nb0) {
-  __shared__ float red[256];
+constexpr int SUM_EW = 64, SUM_ZL = 16;
+
+__global__ __launch_bounds__(SUM_EW * SUM_ZL) void ordered_sum_kernel(SumJob j0, SumJob j1,
+                                                                      unsigned nb0) {
+  __shared__ float red[SUM_EW * SUM_ZL];
   const bool second = blockIdx.x >= nb0;
   const SumJob j = second ? j1 : j0;
   const long long blk = second ? blockIdx.x - nb0 : blockIdx.x;
-  const int EW = j.ew, ZL = 256 / EW;
-  const int el = threadIdx.x % EW, zl = threadIdx.x / EW;
-  const long long e = blk * EW + el;
+  const int el = threadIdx.x & (SUM_EW - 1), zl = threadIdx.x / SUM_EW;
+  const long long e = blk * SUM_EW + el;
   float t = 0.f;
   if (e < j.n) {
     const float* p = j.part + e;
     int z = zl;
-    for (; z + 7 * ZL < j.nz; z += 8 * ZL) {
+    for (; z + 7 * SUM_ZL < j.nz; z += 8 * SUM_ZL) {
       float v[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = p[(long long)(z + k * ZL) * j.n];
+      for (int k = 0; k < 8; ++k) v[k] = p[(long long)(z + k * SUM_ZL) * j.n];
 #pragma unroll
       for (int k = 0; k < 8; ++k) t += v[k];
     }
-    for (; z < j.nz; z += ZL) t += p[(long long)z * j.n];
+    for (; z < j.nz; z += SUM_ZL) t += p[(long long)z * j.n];
   }
   red[threadIdx.x] = t;
   __syncthreads();
-  for (int w = ZL / 2; w >= 1; w >>= 1) {
-    if (zl < w) red[threadIdx.x] += red[threadIdx.x + w * EW];
+  for (int w = SUM_ZL / 2; w >= 1; w >>= 1) {
+    if (zl < w) red[threadIdx.x] += red[threadIdx.x + w * SUM_EW];
     __syncthreads();
   }
   if (zl == 0 && e < j.n) j.dst[e] += red[threadIdx.x];
@@ -1968,11 +1971,9 @@ __global__ __launch_bounds__(256) void ordered_sum_kernel(SumJob j0, SumJob j1, 
 
 // the sums of one weight-gradient launch: dw over nz slices, db (if any) over nzb slices
 inline SumJob sum_job(const float* part, int nz, long long n, float* dst) {
-  SumJob j{part, dst, n, nz, 16};
-  if ((n + 15) / 16 < 256) j.ew = (n + 3) / 4 >= 128 ? 4 : 1;
-  return j;
+  return SumJob{part, dst, n, nz, SUM_EW};
 }
-inline unsigned sum_blocks(const SumJob& j) { return (unsigned)((j.n + j.ew - 1) / j.ew); }
+inline unsigned sum_blocks(const SumJob& j) { return (unsigned)((j.n + SUM_EW - 1) / SUM_EW); }
 inline void launch_ordered_sums(const float* part, int nz, long long n, float* dw, const float* bpart,
                                 int nzb, long long nb, float* db, hipStream_t st) {
   const SumJob j0 = sum_job(part, nz, n, dw);
@@ -1982,7 +1983,8 @@ inline void launch_ordered_sums(const float* part, int nz, long long n, float* d
     j1 = sum_job(bpart, nzb, nb, db);
     blocks += sum_blocks(j1);
   }
-  SPECENH_LAUNCH(ordered_sum_kernel, dim3(blocks), dim3(256), 0, st, j0, j1, sum_blocks(j0));
+  SPECENH_LAUNCH(ordered_sum_kernel, dim3(blocks), dim3(SUM_EW * SUM_ZL), 0, st, j0, j1,
+                 sum_blocks(j0));
 }
 
 // ------------------------------------------------------------------ elementwise
@@ -2102,11 +2104,14 @@ __global__ __launch_bounds__(256) void bce_logits_kernel(const float* __restrict
   for (long long i0 = blockIdx.x * (long long)blockDim.x + threadIdx.x; i0 < n;
        i0 += BCE_U * stride) {
     float zv[BCE_U], tv[BCE_U];
+    // unconditional loads from clamped indices (a guarded load is a branch per element, and
+    // the loads then went out one at a time); out-of-range values are masked below
 #pragma unroll
     for (int u = 0; u < BCE_U; ++u) {
       const long long i = i0 + u * stride;
-      zv[u] = i < n ? z[i] : 0.f;
-      tv[u] = i < n ? to_f(t[i]) : 0.f;
+      const long long ic = i < n ? i : n - 1;
+      zv[u] = z[ic];
+      tv[u] = to_f(t[ic]);
     }
     float part = 0.f;
 #pragma unroll

@@ -692,6 +692,181 @@ void convt_rows_pw_kernel(CRArgs a) {
   store_held();
 }
 
+// convt_rows_pg_kernel: convT1 with the four output phases split over two waves per 16-channel
+// block (8 waves, one workgroup per CU): wave group A runs phases (0,0) and (1,1) (4 + 9 taps),
+// group B phases (0,1) and (1,0) (6 + 6), so a wave holds 26 or 24 tap fragments (~100 VGPRs)
+// instead of 50 and has the registers to read all of a step's B fragments (18 / 16) before its
+// MFMAs: convt_rows_pw_kernel read them in pairs right before use, exposing an LDS round trip
+// per neighbourhood offset (PMC: MFMA busy 0.35). Each wave keeps its own input ring (LDS-DMA,
+// no barrier in the step loop), as convt_rows_pw_kernel.
+template <typename T, int LEAD>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+void convt_rows_pg_kernel(CRArgs a) {
+  static_assert(LEAD >= 1 && LEAD <= 4, "8-row ring: positions g .. g + 3 + LEAD live");
+  using C = TC<64, 16>;
+  constexpr int CO = 64, W = 16;
+  constexpr int WR = C::RING * C::ROWB;  // bytes per wave ring
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_pg[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = lane & 15, kg = lane >> 4;
+  const int nb = wv & 3;
+  unsigned char* const ring = lds_pg + wv * WR;
+  const int H = a.H, SPI = H + 1;
+  const int G = gridDim.x;
+  const int nimg = ((int)a.N - (int)blockIdx.x + G - 1) / G;
+  const int S = nimg * SPI;
+
+  for (int e = lane; e < WR / 16; e += 64) reinterpret_cast<uint4*>(ring)[e] = uint4{0u, 0u, 0u, 0u};
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // zero fill before the DMAs (other path)
+  const f32x4 bias = f32x4{a.b[16 * nb + 4 * kg], a.b[16 * nb + 4 * kg + 1],
+                           a.b[16 * nb + 4 * kg + 2], a.b[16 * nb + 4 * kg + 3]};
+  int xo[3];  // byte offset of pixel m + dx (stored + 1), group kg, in a ring row
+#pragma unroll
+  for (int dx = -1; dx <= 1; ++dx) {
+    const int ps = m + dx + 1;
+    xo[dx + 1] = ps * 128 + 16 * (kg ^ (ps & 7));
+  }
+  const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
+  int dsrc[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = 64 * h + lane;
+    const int ps = 1 + c / 8, gs = c & 7;
+    dsrc[h] = (ps - 1) * 64 + 8 * (gs ^ (ps & 7));
+  }
+  auto stage_at = [&](int p, int il, int r) -> int {
+    unsigned char* dst = ring + (p & 7) * C::ROWB + 128;
+    if (il < nimg && r >= 0) {
+      const long long n = (long long)blockIdx.x + (long long)il * G;
+      const T* src = X + ((n * H + r) * W) * 64;
+      lds_dma16(src + dsrc[0], dst);
+      lds_dma16(src + dsrc[1], dst + 1024);
+      return 2;
+    }
+    *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
+    *reinterpret_cast<uint4*>(dst + 1024 + 16 * lane) = uint4{0u, 0u, 0u, 0u};
+    return 0;
+  };
+  T* __restrict__ O = reinterpret_cast<T*>(a.out);
+  constexpr int OW = 2 * W;
+
+  // the wave group's program: phases PA, PB (compile time)
+  auto run = [&](auto pa_c, auto pb_c) {
+    constexpr int PA = decltype(pa_c)::value, PB = decltype(pb_c)::value;
+    constexpr int PHS[2] = {PA, PB};
+    // (dy, dx) offsets either phase uses, and the fragments: [phase slot][taps][K half]
+    constexpr int NF = 2 * (((PA >> 1) + 2) * ((PA & 1) + 2) + ((PB >> 1) + 2) * ((PB & 1) + 2));
+    uint4 wf[NF];
+    {
+      const T* __restrict__ Wg = reinterpret_cast<const T*>(a.w);
+      int u = 0;
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+          for (int dx = -1; dx <= 1; ++dx) {
+            const int ph = PHS[q];
+            if (!ttap(ph, dy, dx)) continue;
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh)
+              wf[u++] = *reinterpret_cast<const uint4*>(
+                  Wg + (((16 * nb + m) * 5 + tky(ph >> 1, dy)) * 5 + tky(ph & 1, dx)) * 64 +
+                  32 * kh + 8 * kg);
+          }
+    }
+    resident_loads_landed();
+#pragma unroll
+    for (int p = 0; p < 3 + LEAD; ++p) {
+      const int il = p / SPI;
+      stage_at(p, il, p - il * SPI - 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    uint2 pk[2];
+    long long po = -1;  // element offset of the held outputs' (2s, 2x) pixel, -1: none
+    int vmn = 0;        // this wave's vector-memory ops issued in the loop
+    int mk[LEAD + 1];   // vmn right after the DMAs of position g + 3 + i (-1: none in flight)
+#pragma unroll
+    for (int i = 0; i <= LEAD; ++i) mk[i] = -1;
+    auto store_held = [&]() {
+      if (po >= 0) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          gstore8(O + po + ((PHS[q] >> 1) * OW + (PHS[q] & 1)) * CO, pk[q]);
+        vmn += 2;
+      }
+    };
+    int il = 0, s = 0;
+    int ilp = (3 + LEAD) / SPI, sp = 3 + LEAD - ilp * SPI;
+    for (int g = 0; g < S; ++g) {
+      store_held();
+      po = -1;
+      const int nd = stage_at(g + 3 + LEAD, ilp, sp - 1);
+      vmn += nd;
+      mk[LEAD] = nd ? vmn : -1;
+      if (s < H) {
+        uint4 bq[9][2];
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy) {
+          const unsigned char* src = ring + ((g + 1 + dy) & 7) * C::ROWB;
+#pragma unroll
+          for (int dx = -1; dx <= 1; ++dx) {
+            if (!ttap(PA, dy, dx) && !ttap(PB, dy, dx)) continue;
+            bq[3 * (dy + 1) + dx + 1][0] = *reinterpret_cast<const uint4*>(src + xo[dx + 1]);
+            bq[3 * (dy + 1) + dx + 1][1] = *reinterpret_cast<const uint4*>(src + (xo[dx + 1] ^ 64));
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 acc[2] = {bias, bias};
+        int u0[2] = {0, NF / 2 - 0};
+        u0[1] = 2 * ((PA >> 1) + 2) * ((PA & 1) + 2);
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+          for (int dx = -1; dx <= 1; ++dx)
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+              if (ttap(PHS[q], dy, dx)) {
+                acc[q] = mfma<T>(wf[u0[q]], bq[3 * (dy + 1) + dx + 1][0], acc[q]);
+                acc[q] = mfma<T>(wf[u0[q] + 1], bq[3 * (dy + 1) + dx + 1][1], acc[q]);
+                u0[q] += 2;
+              }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) pk[q] = relu_pack4<T>(acc[q]);
+        const long long n = (long long)blockIdx.x + (long long)il * G;
+        po = ((n * 2 * H + 2 * s) * OW + 2 * m) * CO + 16 * nb + 4 * kg;
+      }
+      if (mk[0] >= 0) wait_vmcnt(vmn - mk[0]);
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < LEAD; ++i) mk[i] = mk[i + 1];
+      if (++s == SPI) { s = 0; ++il; }
+      if (++sp == SPI) { sp = 0; ++ilp; }
+    }
+    store_held();
+  };
+  if (wv < 4)
+    run(std::integral_constant<int, 0>{}, std::integral_constant<int, 3>{});
+  else
+    run(std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
+}
+
+template <typename T>
+hipError_t launch_convt_rows_pg(const CRArgs& a, hipStream_t st) {
+  using C = TC<64, 16>;
+  constexpr int LDS = 8 * C::RING * C::ROWB;
+  const void* k = reinterpret_cast<const void*>(&convt_rows_pg_kernel<T, 3>);
+  static bool attr[2] = {false, false};
+  if (!attr[__is_same(T, __bf16)]) {
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr[__is_same(T, __bf16)] = true;
+  }
+  const long long grid = std::min<long long>(a.N, (long long)device_cus());
+  SPECENH_LAUNCH((convt_rows_pg_kernel<T, 3>), dim3((unsigned)grid), dim3(512), LDS, st, a);
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_convt_rows_pw(const CRArgs& a, hipStream_t st) {
   using C = TC<64, 16>;
@@ -1266,7 +1441,9 @@ int convt_rows(int dtype, const void* x, int N, int H, int W, int CI, const void
   a.x = x; a.w = w; a.b = b; a.out = out; a.N = N; a.H = H;
   const bool f16 = dtype == SPECENH_DTYPE_F16;
   hipError_t e;
-  if (CO == 64 && W == 16 && variant(V_CONVT_SHARED_RING) == 0)
+  if (CO == 64 && W == 16 && variant(V_CONVT_SHARED_RING) == 0 && variant(V_CONVT_PW) == 0)
+    e = f16 ? launch_convt_rows_pg<_Float16>(a, st) : launch_convt_rows_pg<__bf16>(a, st);
+  else if (CO == 64 && W == 16 && variant(V_CONVT_SHARED_RING) == 0)
     e = f16 ? launch_convt_rows_pw<_Float16>(a, st) : launch_convt_rows_pw<__bf16>(a, st);
   else if (CO == 64 && W == 16)
     e = f16 ? launch_convt_rows<_Float16, 64, 16>(a, st) : launch_convt_rows<__bf16, 64, 16>(a, st);

@@ -41,6 +41,9 @@
 #ifndef SPECENH_C1024_PF
 #define SPECENH_C1024_PF 1
 #endif
+#ifndef SPECENH_STFT_WIDE_EMIT
+#define SPECENH_STFT_WIDE_EMIT 1
+#endif
 #ifndef SPECENH_STFT_PF_AFTER_WAIT
 #define SPECENH_STFT_PF_AFTER_WAIT 1
 #endif
@@ -636,6 +639,61 @@ __device__ __forceinline__ void tile_emit(const StftArgs& a, const float* s_tile
   }
 }
 
+// tile_emit for the swizzled 16-frame tile (G = 32, TF = 16: nperseg 1024) with 16-byte
+// stores: lane (row k, quad q) reads frames 4q .. 4q + 3 of row k as one ds_read_b128 and
+// writes them with one buffer_store_dwordx4 (dword-aligned: rows are T = 253 floats apart),
+// instead of four ds_read_b32 + four 4-byte stores. The tile's XOR swizzle moves frame f of
+// row k to f ^ s(k), s even: the quad lands at quad q ^ (s >> 2), its two pairs swapped when
+// s & 2. A quad with frames past T (the row's last member tile) goes out as dwords, the
+// invalid ones past the descriptor (dropped). Same arithmetic as tile_emit.
+template <int N>
+__device__ __forceinline__ void tile_emit4(const StftArgs& a, const float* s_tile, int tid,
+                                           __amdgpu_buffer_rsrc_t orr, int t0, float mn,
+                                           float inv, bool norm) {
+  using Lo = Layout<N>;
+  static_assert(Lo::TILE_SWZ && Lo::TF == 16, "16-frame swizzled tile");
+  const int tfv = min(Lo::TF, a.T - t0);
+  if (a.flags & SPECENH_STFT_DEV_NOSTORE) return;
+  constexpr int ROWS_PER_IT = Lo::THREADS / 4;
+  constexpr int ST = (Lo::NBINS + ROWS_PER_IT - 1) / ROWS_PER_IT;
+  const int q = tid & 3, k0 = tid >> 2;
+  const bool whole = 4 * q + 3 < tfv;
+  const int voff = (k0 * a.T + t0 + 4 * q) * 4;
+  const int sstep = ROWS_PER_IT * a.T * 4;
+#pragma unroll
+  for (int it = 0; it < ST; ++it) {
+    const int k = min(k0 + it * ROWS_PER_IT, Lo::NBINS - 1);  // rows past the tile: re-read
+    const int sw = tile_swz<N>(k);
+    const float4 r = *reinterpret_cast<const float4*>(s_tile + k * Lo::TS + 4 * (q ^ (sw >> 2)));
+    float v[4];
+    const bool swp = (sw & 2) != 0;
+    v[0] = swp ? r.z : r.x;
+    v[1] = swp ? r.w : r.y;
+    v[2] = swp ? r.x : r.z;
+    v[3] = swp ? r.y : r.w;
+    if (norm) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (v[j] - mn) * inv;
+    }
+    // rows k >= F_out fall past the descriptor (num_records = F_out T 4 bytes): dropped
+    const int row_ok = k0 + it * ROWS_PER_IT < Lo::NBINS;
+    const int off = row_ok ? voff : (1 << 30);
+    if (whole) {
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      __builtin_amdgcn_raw_buffer_store_b128(
+          u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                __float_as_uint(v[3])},
+          orr, off, it * sstep, 0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), orr,
+                                              4 * q + j < tfv ? off + 4 * j : (1 << 30),
+                                              it * sstep, 0);
+    }
+  }
+}
+
 // tile_write + tile_emit between workgroup LDS barriers: starts with one (every group is
 // done with its FFT buffer) unless the caller has just passed one, ends with one (the
 // tile = FFT buffers free for the next tile's FFTs).
@@ -1107,7 +1165,10 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_team_
     const float mn = s_red[2 * C::WAVES];
     const float inv = 1.0f / (s_red[2 * C::WAVES + 1] - mn);  // max == min -> NaN (0/0)
     const bool done = s_red[2 * C::WAVES + 2] != 0.f;
-    tile_emit<N>(a, s_tile, tid, orr, t0, mn, inv, done);
+    if constexpr (Lo::TILE_SWZ && Lo::TF == 16 && SPECENH_STFT_WIDE_EMIT)
+      tile_emit4<N>(a, s_tile, tid, orr, t0, mn, inv, done);
+    else
+      tile_emit<N>(a, s_tile, tid, orr, t0, mn, inv, done);
     lds_barrier();  // tile (= FFT buffers) free for the next task's FFTs
   }
 }

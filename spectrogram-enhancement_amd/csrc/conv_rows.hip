@@ -692,7 +692,9 @@ void convt_rows_pw_kernel(CRArgs a) {
   store_held();
 }
 
-// convt_rows_pg_kernel: convT1 with the four output phases split over two waves per 16-channel
+// convt_rows_pg_kernel (variant CONVT_PG; measured SLOWER than convt_rows_pw_kernel, 0.148 vs
+// 0.130 ms per 2048 shots, profiles/r05_convt1_pg_ab.txt: kept for the record of the trial):
+// convT1 with the four output phases split over two waves per 16-channel
 // block (8 waves, one workgroup per CU): wave group A runs phases (0,0) and (1,1) (4 + 9 taps),
 // group B phases (0,1) and (1,0) (6 + 6), so a wave holds 26 or 24 tap fragments (~100 VGPRs)
 // instead of 50 and has the registers to read all of a step's B fragments (18 / 16) before its
@@ -1441,7 +1443,7 @@ int convt_rows(int dtype, const void* x, int N, int H, int W, int CI, const void
   a.x = x; a.w = w; a.b = b; a.out = out; a.N = N; a.H = H;
   const bool f16 = dtype == SPECENH_DTYPE_F16;
   hipError_t e;
-  if (CO == 64 && W == 16 && variant(V_CONVT_SHARED_RING) == 0 && variant(V_CONVT_PW) == 0)
+  if (CO == 64 && W == 16 && variant(V_CONVT_SHARED_RING) == 0 && variant(V_CONVT_PG) != 0)
     e = f16 ? launch_convt_rows_pg<_Float16>(a, st) : launch_convt_rows_pg<__bf16>(a, st);
   else if (CO == 64 && W == 16 && variant(V_CONVT_SHARED_RING) == 0)
     e = f16 ? launch_convt_rows_pw<_Float16>(a, st) : launch_convt_rows_pw<__bf16>(a, st);

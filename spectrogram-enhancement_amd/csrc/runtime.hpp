@@ -39,7 +39,7 @@ enum Variant : int {
   V_ROWS_SHORT_LEAD,  // convT rows / decoder3 producer: the round-3 ring refill lead (1 / 0 steps, not 3)
   V_SVD_GRAM_F32,     // 128 < r <= 256 Gram on fp32 MFMA (round 3) instead of the fp16 hi/lo split
   V_SVD_RECON_BLOCKS, // SVD reconstruction one workgroup per row block (recon_mfma_kernel), not runs
-  V_CONVT_PW,         // convT1 row sweep: 4 waves x 50 resident taps (round 4), not the phase split
+  V_CONVT_PG,         // convT1 row sweep: phases split over 8 waves (round 5 trial, slower) instead of 4 x 50 taps
   V_COUNT
 };
 

@@ -44,6 +44,9 @@
 #ifndef SPECENH_STFT_WIDE_EMIT
 #define SPECENH_STFT_WIDE_EMIT 1
 #endif
+#ifndef SPECENH_STFT_STORE_AUX
+#define SPECENH_STFT_STORE_AUX 0  // cache-policy bits of the spectrogram stores
+#endif
 #ifndef SPECENH_STFT_PF_AFTER_WAIT
 #define SPECENH_STFT_PF_AFTER_WAIT 1
 #endif
@@ -635,7 +638,7 @@ __device__ __forceinline__ void tile_emit(const StftArgs& a, const float* s_tile
     for (int u = 0; u < GRP; ++u)
       if (g0 + u < ST && (g0 + u) * ROWS_PER_IT < Lo::NBINS)
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[u]), orr, voff, (g0 + u) * sstep,
-                                              0);
+                                              SPECENH_STFT_STORE_AUX);
   }
 }
 
@@ -683,13 +686,13 @@ __device__ __forceinline__ void tile_emit4(const StftArgs& a, const float* s_til
       __builtin_amdgcn_raw_buffer_store_b128(
           u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
                 __float_as_uint(v[3])},
-          orr, off, it * sstep, 0);
+          orr, off, it * sstep, SPECENH_STFT_STORE_AUX);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), orr,
                                               4 * q + j < tfv ? off + 4 * j : (1 << 30),
-                                              it * sstep, 0);
+                                              it * sstep, SPECENH_STFT_STORE_AUX);
     }
   }
 }

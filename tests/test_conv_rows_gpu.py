@@ -139,10 +139,10 @@ def test_convt_rows_matches_tile_kernel(gpu_device, kernel_variant, CO, W):
 
 @pytest.mark.parametrize("N,H", [(1, 5), (3, 1), (700, 16), (1100, 3)])
 def test_convt_rows_per_wave_ring_bitwise(gpu_device, kernel_variant, N, H):
-    """convT1 (CO 64 on 16-wide rows): the phase-split kernel (default: 8 waves, two phases
-    each, B fragments read ahead), the round-4 per-wave-ring kernel (CONVT_PW) and the
-    shared ring (CONVT_SHARED_RING): the same per-phase MFMA order, bitwise equal; several
-    images per persistent workgroup at N = 700 / 1100."""
+    """convT1 (CO 64 on 16-wide rows): the per-wave-ring kernel (default), the phase-split
+    trial (CONVT_PG: 8 waves, two phases each, B fragments read ahead) and the shared ring
+    (CONVT_SHARED_RING): the same per-phase MFMA order, bitwise equal; several images per
+    persistent workgroup at N = 700 / 1100."""
     rng = np.random.default_rng(17 + N + H)
     x = torch.tensor(rng.uniform(0, 1, (N, H, 16, 64)), dtype=torch.float16, device=gpu_device)
     w = torch.tensor(rng.standard_normal((64, 5, 5, 64)) * 0.03, dtype=torch.float16,
@@ -152,10 +152,10 @@ def test_convt_rows_per_wave_ring_bitwise(gpu_device, kernel_variant, N, H):
     b = torch.full_like(a, float("nan"))
     c = torch.full_like(a, float("nan"))
     _convt_run(x, w, bias, 64, a)
-    assert "convt_rows_pg_kernel" in _lib.last_kernel_name()
-    kernel_variant("CONVT_PW", 1)
-    _convt_run(x, w, bias, 64, c)
     assert "convt_rows_pw_kernel" in _lib.last_kernel_name()
+    kernel_variant("CONVT_PG", 1)
+    _convt_run(x, w, bias, 64, c)
+    assert "convt_rows_pg_kernel" in _lib.last_kernel_name()
     kernel_variant("CONVT_SHARED_RING", 1)
     _convt_run(x, w, bias, 64, b)
     torch.cuda.synchronize()

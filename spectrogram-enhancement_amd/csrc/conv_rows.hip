@@ -1106,6 +1106,9 @@ struct E2Args {
 };
 
 constexpr int E2R1 = 32;  // conv1 input ring rows (positions)
+#ifndef SPECENH_ENC2_STAGGER
+#define SPECENH_ENC2_STAGGER 1
+#endif
 
 // WPE: waves per SIMD the register budget is cut for (4: two workgroups per CU, 128 VGPRs;
 // 2: one workgroup, 256 VGPRs)
@@ -1306,10 +1309,10 @@ void enc2_rows_kernel(E2Args a) {
     // step s + 2 (positions 4s + 8 .. 4s + 15)
     const int nd = wv < 4 ? stage1_at(4 * s + 32 + wv, ilD, rD - 2) : 0;
     shift1(4 * s + 16);
-    produce(s + 2, ilB, qB);
     // this step's conv2 rows, unconditionally: past an image they are the zero rows the
     // conv1 stage stored (adding nothing)
     const int q = qC;
+    auto conv2_rows = [&]() {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int rs = (2 * s + j) & 7;
@@ -1339,6 +1342,20 @@ void enc2_rows_kernel(E2Args a) {
         if (kg < 2 || q != 0) bT = uint4{0u, 0u, 0u, 0u};
         acc[slot(1)] = mfma<T>(wf[10], bT, acc[slot(1)]);
       }
+    }
+    };
+    // The two waves of a SIMD (w, w + 4) run the same program and meet at one barrier per
+    // step; run in the same order, both would read conv1's LDS-heavy B fragments, then both
+    // issue conv2's MFMAs. Waves 4-7 take the two halves in the other order (they are
+    // independent: produce writes the ring slots of step s + 2, conv2 reads those of steps s,
+    // s + 1), so each SIMD pairs one wave's conv1 with the other's conv2 (MI355X_MICROARCH.md,
+    // two waves per SIMD, item 9: a stagger).
+    if (SPECENH_ENC2_STAGGER && wv >= 4) {
+      conv2_rows();
+      produce(s + 2, ilB, qB);
+    } else {
+      produce(s + 2, ilB, qB);
+      conv2_rows();
     }
     // the DMA of step s - 3 (copy-1 shifted at step s + 1) must have landed: wait for all
     // but this wave's vector-memory ops of steps s - 2 .. s (each step: its store, then its

@@ -1107,7 +1107,7 @@ struct E2Args {
 
 constexpr int E2R1 = 32;  // conv1 input ring rows (positions)
 #ifndef SPECENH_ENC2_STAGGER
-#define SPECENH_ENC2_STAGGER 1
+#define SPECENH_ENC2_STAGGER 0
 #endif
 
 // WPE: waves per SIMD the register budget is cut for (4: two workgroups per CU, 128 VGPRs;
@@ -1349,7 +1349,8 @@ void enc2_rows_kernel(E2Args a) {
     // issue conv2's MFMAs. Waves 4-7 take the two halves in the other order (they are
     // independent: produce writes the ring slots of step s + 2, conv2 reads those of steps s,
     // s + 1), so each SIMD pairs one wave's conv1 with the other's conv2 (MI355X_MICROARCH.md,
-    // two waves per SIMD, item 9: a stagger).
+    // two waves per SIMD, item 9: a stagger). Measured slower (0.337 vs 0.311 ms per 2048,
+    // profiles/r05_enc2_stagger_ab.txt; its VGPR spills rose 5 -> 20), so off by default.
     if (SPECENH_ENC2_STAGGER && wv >= 4) {
       conv2_rows();
       produce(s + 2, ilB, qB);

@@ -40,6 +40,7 @@ enum Variant : int {
   V_SVD_GRAM_F32,     // 128 < r <= 256 Gram on fp32 MFMA (round 3) instead of the fp16 hi/lo split
   V_SVD_RECON_BLOCKS, // SVD reconstruction one workgroup per row block (recon_mfma_kernel), not runs
   V_CONVT_PG,         // convT1 row sweep: phases split over 8 waves (round 5 trial, slower) instead of 4 x 50 taps
+  V_SVD_GZ_ROWS,      // subspace G Z one row per thread (round 4) instead of four
   V_COUNT
 };
 

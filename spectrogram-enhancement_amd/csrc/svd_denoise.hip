@@ -528,11 +528,15 @@ __device__ __forceinline__ float hash_unit(unsigned i, unsigned j) {
   return (float)(h & 0xFFFFFF) * (1.0f / 16777216.0f) - 0.5f;
 }
 
+#ifndef SPECENH_GZ_GB
+#define SPECENH_GZ_GB 8
+#endif
+
 // Y = G Z for symmetric G (global, r x r) and Z (LDS, r x P): Y[i][:] = sum_j G[j][i] Z[j][:].
 // One row i per thread; at each j the threads read row j of G coalesced and Z[j][:] is an
 // LDS broadcast.
 template <int P>
-__device__ void gemm_GZ(const float* G, int r, const float* sZ, float* sY) {
+__device__ __forceinline__ void gemm_GZ(const float* G, int r, const float* sZ, float* sY) {
   for (int i = threadIdx.x; i < r; i += SS_THREADS) {
     float acc[P];
 #pragma unroll
@@ -541,9 +545,10 @@ __device__ void gemm_GZ(const float* G, int r, const float* sZ, float* sY) {
     // trip), then the batch's FMAs in the same j order
     // G loads per batch: 8 for P <= 24 (C3 rank-16 5.05 -> 4.84 ms vs 16; 32: 6.2 ms, 64:
     // slower still — more rows in flight per thread congest L2 / the memory pipeline)
-    constexpr int GB = P <= 24 ? 8 : 16;
-    int j = 0;
-    for (; j + GB <= r; j += GB) {
+    constexpr int GB = P <= 24 ? SPECENH_GZ_GB : 16;
+    const int nb = r / GB;
+    for (int q = 0; q < nb; ++q) {
+      const int j = GB * q;
       float g[GB];
 #pragma unroll
       for (int u = 0; u < GB; ++u) g[u] = G[(long long)(j + u) * r + i];
@@ -560,7 +565,7 @@ __device__ void gemm_GZ(const float* G, int r, const float* sZ, float* sY) {
         }
       }
     }
-    for (; j < r; ++j) {
+    for (int j = nb * GB; j < r; ++j) {
       const float g = G[(long long)j * r + i];
       const float4* zj = reinterpret_cast<const float4*>(sZ + j * P);
 #pragma unroll
@@ -576,6 +581,91 @@ __device__ void gemm_GZ(const float* G, int r, const float* sZ, float* sY) {
 #pragma unroll
     for (int c4 = 0; c4 < P / 4; ++c4)
       yi[c4] = make_float4(acc[4 * c4], acc[4 * c4 + 1], acc[4 * c4 + 2], acc[4 * c4 + 3]);
+  }
+}
+
+// Y = G Z with FOUR rows per thread (r % 4 == 0, G 16-byte aligned): thread (quad q = lane,
+// wave w) takes rows 4q .. 4q + 3 of Y over the w-th quarter of the j range, so one
+// float4 load per lane moves a whole 1 KB row of G per wave instruction (gemm_GZ's dword
+// loads move 256 B) and each broadcast Z[j] read feeds 4 P FMAs instead of P. The four
+// quarter sums meet in sY in wave order (fixed: the result does not depend on timing).
+// C3 rank-16 5.11 -> 4.48 ms, default 3.40 -> 3.22 ms (profiles/r05_svd_ab_gzquad.txt);
+// SVD_GZ_ROWS=1 keeps one row per thread.
+template <int P>
+__device__ __forceinline__ void gemm_GZ4(const float* G, int r, const float* sZ, float* sY) {
+  constexpr int GB = 8;  // float4 loads in flight per batch
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int nq = r >> 2, jq = (r + 3) >> 2;
+  const int j0 = min(r, w * jq), j1 = min(r, j0 + jq);
+  const float4* __restrict__ G4 = reinterpret_cast<const float4*>(G);
+  for (int base = 0; base < nq; base += 64) {  // uniform trip count (barriers inside)
+    const int qd = base + lane;
+    const bool act = qd < nq;
+    const int qc = act ? qd : 0;  // inactive lanes load a valid row and discard it
+    float acc[4][P];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int c = 0; c < P; ++c) acc[k][c] = 0.f;
+    int j = j0;
+    for (; j + GB <= j1; j += GB) {
+      float4 g[GB];
+#pragma unroll
+      for (int u = 0; u < GB; ++u) g[u] = G4[(long long)(j + u) * nq + qc];
+#pragma unroll
+      for (int u = 0; u < GB; ++u) {
+        const float4* zj = reinterpret_cast<const float4*>(sZ + (j + u) * P);
+        const float gv[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
+#pragma unroll
+        for (int c4 = 0; c4 < P / 4; ++c4) {
+          const float4 z = zj[c4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            acc[k][4 * c4 + 0] = fmaf(gv[k], z.x, acc[k][4 * c4 + 0]);
+            acc[k][4 * c4 + 1] = fmaf(gv[k], z.y, acc[k][4 * c4 + 1]);
+            acc[k][4 * c4 + 2] = fmaf(gv[k], z.z, acc[k][4 * c4 + 2]);
+            acc[k][4 * c4 + 3] = fmaf(gv[k], z.w, acc[k][4 * c4 + 3]);
+          }
+        }
+      }
+    }
+    for (; j < j1; ++j) {
+      const float4 g = G4[(long long)j * nq + qc];
+      const float gv[4] = {g.x, g.y, g.z, g.w};
+      const float4* zj = reinterpret_cast<const float4*>(sZ + j * P);
+#pragma unroll
+      for (int c4 = 0; c4 < P / 4; ++c4) {
+        const float4 z = zj[c4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          acc[k][4 * c4 + 0] = fmaf(gv[k], z.x, acc[k][4 * c4 + 0]);
+          acc[k][4 * c4 + 1] = fmaf(gv[k], z.y, acc[k][4 * c4 + 1]);
+          acc[k][4 * c4 + 2] = fmaf(gv[k], z.z, acc[k][4 * c4 + 2]);
+          acc[k][4 * c4 + 3] = fmaf(gv[k], z.w, acc[k][4 * c4 + 3]);
+        }
+      }
+    }
+    // quarter sums into sY: wave 0 stores, waves 1, 2, 3 add in turn
+#pragma unroll
+    for (int s = 0; s < SS_THREADS / 64; ++s) {
+      if (w == s && act) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float4* yi = reinterpret_cast<float4*>(sY + (4 * qd + k) * P);
+#pragma unroll
+          for (int c4 = 0; c4 < P / 4; ++c4) {
+            float4 v = make_float4(acc[k][4 * c4], acc[k][4 * c4 + 1], acc[k][4 * c4 + 2],
+                                   acc[k][4 * c4 + 3]);
+            if (s > 0) {
+              const float4 o = yi[c4];
+              v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+            }
+            yi[c4] = v;
+          }
+        }
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -626,8 +716,9 @@ __device__ void gemm_GZ8(const float* G, int r, const float* sZ, float* sY, floa
     float acc[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) acc[c] = 0.f;
-    int j = j0;
-    for (; j + 16 <= j1; j += 16) {
+    const int nb = (j1 - j0) / 16;
+    for (int q = 0; q < nb; ++q) {
+      const int j = j0 + 16 * q;
       float g[16];
 #pragma unroll
       for (int u = 0; u < 16; ++u) g[u] = G[(long long)(j + u) * r + i];
@@ -641,7 +732,7 @@ __device__ void gemm_GZ8(const float* G, int r, const float* sZ, float* sY, floa
         acc[6] = fmaf(g[u], z1.z, acc[6]); acc[7] = fmaf(g[u], z1.w, acc[7]);
       }
     }
-    for (; j < j1; ++j) {
+    for (int j = j0 + 16 * nb; j < j1; ++j) {
       const float gj = G[(long long)j * r + i];
 #pragma unroll
       for (int c = 0; c < 8; ++c) acc[c] = fmaf(gj, sZ[j * 8 + c], acc[c]);
@@ -664,7 +755,7 @@ __device__ void gemm_GZ8(const float* G, int r, const float* sZ, float* sY, floa
 // (row (l >> 4) + 4 reg, col l & 15) of the tile. Ends with out visible to all threads.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 template <int P>
-__device__ void prodP(const float* sA, const float* sB, int r, double* out) {
+__device__ __forceinline__ void prodP(const float* sA, const float* sB, int r, double* out) {
   constexpr int NT = (P + 15) / 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m = lane & 15, kq = lane >> 4;
@@ -699,7 +790,7 @@ __device__ __forceinline__ double readlane_f64(double v, int src) {
 // S = Y^T Y, S = R^T R, Z = Y R^-1. fp64 keeps the Gram of Y (condition up to ~1e12
 // here) factorisable; callers run it twice (CholeskyQR2) for fp32-level orthogonality.
 template <int P>
-__device__ void cholqr(const float* sY, float* sZ, int r, double* sS, double* sRi) {
+__device__ __forceinline__ void cholqr(const float* sY, float* sZ, int r, double* sS, double* sRi) {
   const int tid = threadIdx.x;
   if constexpr (P == 8) {
     prod8(sY, sY, r, sS + 2 * P * P, sS);  // scratch [4][64] past sS, sRi (SsLayout)
@@ -753,16 +844,22 @@ __device__ void cholqr(const float* sY, float* sZ, int r, double* sS, double* sR
   if (tid < P) sRi[tid] = 1.0 / sS[tid * P + tid];
   __syncthreads();
   for (int i = tid; i < r; i += SS_THREADS) {
+    // Column by column (z_c from the finished z_0 .. z_{c-1}): each z_c is consumed by the
+    // next columns, so the FMAs stay in order. The pivot-row form (eliminate z_d from every
+    // later column) let the compiler sink each pivot's FMAs to the end and keep every R
+    // entry live: at P = 24 ~270 scratch spills per row and 512 registers per lane. R is
+    // the same for every row: the opaque zero offset, renewed per column, keeps its reads
+    // from being hoisted out of the row loop.
+    int opq = 0;
     double z[P];
 #pragma unroll
-    for (int c = 0; c < P; ++c) z[c] = sY[i * P + c];
+    for (int c = 0; c < P; ++c) {
+      asm volatile("" : "+v"(opq));
+      const double* rc = sS + c + opq;  // column c of R: rc[d * P]
+      double t = sY[i * P + c];
 #pragma unroll
-    for (int d = 0; d < P; ++d) {  // pivot d: z_d final, eliminate it from the later columns
-      z[d] *= sRi[d];
-      const double* rd = sS + d * P;
-#pragma unroll
-      for (int c = d + 1; c < P; ++c) z[c] = fma(-z[d], rd[c], z[c]);
-      __builtin_amdgcn_sched_barrier(0);  // (one pivot row of R in flight: no hoisted reads)
+      for (int d = 0; d < c; ++d) t = fma(-z[d], rc[d * P], t);
+      z[c] = t * sRi[c + opq];
     }
 #pragma unroll
     for (int c = 0; c < P; ++c) sZ[i * P + c] = (float)z[c];
@@ -774,12 +871,17 @@ __device__ void cholqr(const float* sY, float* sZ, int r, double* sS, double* sR
 // LDS, one wave: each round rotates P/2 disjoint (a, b) pairs at once; Q accumulates
 // the eigenvectors. Angles in fp64.
 template <int P>
-__device__ int jacobi(float* sH, float* sQ, float* sCS, int* sPair) {  // -> sweeps run
+__device__ __forceinline__ int jacobi(float* sH, float* sQ, float* sCS, int* sPair) {  // -> sweeps run
   const int lane = threadIdx.x;  // wave 0
   for (int idx = lane; idx < P * P; idx += 64) sQ[idx] = (idx / P == idx % P) ? 1.f : 0.f;
   wave_lds_sync();
   int sweep = 0;
   for (; sweep < 15; ++sweep) {
+    // The pairings of the unrolled rounds are the same every sweep: an opaque zero keeps
+    // the compiler from hoisting all (round, item) index sets out of the sweep loop, where
+    // they stayed live across the whole kernel and spilled (~270 VGPRs at P = 24)
+    int opq = 0;
+    asm volatile("" : "+v"(opq));
     double off = 0.0, diag = 0.0;
     for (int idx = lane; idx < P * P; idx += 64) {
       const double h = sH[idx];
@@ -794,7 +896,7 @@ __device__ int jacobi(float* sH, float* sQ, float* sCS, int* sPair) {  // -> swe
     if (off <= 1e-13 * diag) break;
     for (int round = 0; round < P - 1; ++round) {
       if (lane < P / 2) {  // tournament pairing: player 0 fixed, others rotate
-        auto player = [&](int k) { return k == 0 ? 0 : 1 + (k - 1 + round) % (P - 1); };
+        auto player = [&](int k) { return k == 0 ? 0 : 1 + (k - 1 + round + opq) % (P - 1); };
         int a = player(lane), b = player(P - 1 - lane);
         if (a > b) { const int t = a; a = b; b = t; }
         const double hab = sH[a * P + b];
@@ -824,7 +926,7 @@ __device__ int jacobi(float* sH, float* sQ, float* sCS, int* sPair) {  // -> swe
           a = sPair[2 * j];
           b = sPair[2 * j + 1];
         } else {
-          auto player = [&](int k) { return k == 0 ? 0 : 1 + (k - 1 + round) % (P - 1); };
+          auto player = [&](int k) { return k == 0 ? 0 : 1 + (k - 1 + round + opq) % (P - 1); };
           a = player(j);
           b = player(P - 1 - j);
           if (a > b) { const int t = a; a = b; b = t; }
@@ -893,11 +995,20 @@ struct SsLayout {
 // path (a cut with no spectral gap, e.g. inside a noise bulk, where subspace iteration does
 // not converge).
 template <int P>
-__global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, int r, int K,
+// Waves per SIMD the register budget is sized for (P = 16, 24: 256 VGPRs, 2 workgroups per CU)
+#ifndef SPECENH_SS_WPE
+#define SPECENH_SS_WPE 2
+#endif
+#ifndef SPECENH_SS8_WPE
+#define SPECENH_SS8_WPE 4  // (C3 default 3.22 -> 3.16 ms vs 2)
+#endif
+__global__ __launch_bounds__(SS_THREADS)
+__attribute__((amdgpu_waves_per_eu(P == 8 ? SPECENH_SS8_WPE : P <= 24 ? SPECENH_SS_WPE : 1)))
+void subspace_kernel(const float* G, int r, int K,
                                                               int iters, float* V,
                                                               float* theta, int cut2,
                                                               float tolv, int* flags, int seed,
-                                                              const int* only) {
+                                                              const int* only, int gz_quad) {
   __shared__ double sRed[4];
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* sS = reinterpret_cast<double*>(smem);            // P x P
@@ -929,8 +1040,10 @@ __global__ __launch_bounds__(SS_THREADS) void subspace_kernel(const float* G, in
   } while (0)
 #endif
 
+  // (gz_quad: the host checked r % 4 == 0 and a 16-byte aligned G, r^2 floats per matrix)
   auto GZ = [&](const float* z, float* y) {
-    if constexpr (P == 8) gemm_GZ8(Gb, r, z, y, sT);
+    if (P <= 24 && gz_quad) gemm_GZ4<P <= 24 ? P : 8>(Gb, r, z, y);
+    else if constexpr (P == 8) gemm_GZ8(Gb, r, z, y, sT);
     else gemm_GZ<P>(Gb, r, z, y);
   };
   if (only && !only[b]) return;  // (second pass: only the matrices the first one flagged)
@@ -2718,8 +2831,10 @@ hipError_t launch_subspace_t(const float* G, int r, int K, float* V, float* thet
   // 3 rounds when the subspace oversamples the wanted K by >= 8 columns, else 5
   // (a second pass over flagged matrices starts elsewhere and iterates 4x longer)
   const int iters = (P >= K + 8 ? 3 : 5) * (seed ? 4 : 1);
+  const int quad = P <= 24 && r % 4 == 0 && (reinterpret_cast<uintptr_t>(G) & 15) == 0 &&
+                   variant(V_SVD_GZ_ROWS) == 0;
   SPECENH_LAUNCH(subspace_kernel<P>, dim3((unsigned)batch), dim3(SS_THREADS), lds, st, G, r,
-                     K, iters, V, theta, cut2, 5e-6f, flags, seed, only);
+                     K, iters, V, theta, cut2, 5e-6f, flags, seed, only, quad);
   return hipGetLastError();
 }
 

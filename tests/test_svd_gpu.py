@@ -278,6 +278,40 @@ def test_gram_paths_agree(gpu_device, shape, kernel_variant):
         assert _rel(outs[0][b], truth) <= _rel(outs[2][b], truth) + 1e-6
 
 
+@pytest.mark.parametrize("shape,args", [((513, 256), (0, 16)), ((513, 256), ()),
+                                        ((300, 132), (0, 16)), ((201, 130), (0, 16)),
+                                        ((140, 301), ()), ((64, 48), (2, 30))])
+def test_subspace_gz_paths_agree(gpu_device, shape, args, kernel_variant):
+    """subspace_kernel's G Z with four rows per thread (default; r % 4 == 0, j range split
+    over the four waves and summed in wave order) and one row per thread (SVD_GZ_ROWS=1):
+    the same reconstruction to fp32 rounding, both on the oracle, and each bitwise
+    independent of the matrix's position in the batch. r = 130 takes the one-row path
+    either way; (64, 48) at (2, 30) runs the 40-wide subspace (one row per thread only)."""
+    import os
+    import sys
+
+    import torch
+
+    from specenh import svd
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import gapped_matrix
+
+    m, n = shape
+    A = np.stack([gapped_matrix(1200 + i, m, n, dtype=np.float32) for i in range(3)])
+    At = torch.as_tensor(np.concatenate([A, A[::-1]]), device=gpu_device)
+    outs = []
+    for rows in (0, 1):
+        kernel_variant("SVD_GZ_ROWS", rows)
+        o = svd.denoise_batch(At, *args)
+        assert torch.equal(o[:3], o[3:].flip(0)), rows  # position-independent
+        outs.append(o[:3].double().cpu().numpy())
+    for b in range(3):
+        truth = ref.denoiseSignal(A[b].astype(np.float64), *args)
+        for o in outs:
+            assert _rel(o[b], truth) <= TOL
+        assert _rel(outs[0][b], outs[1][b]) <= 1e-6
+
+
 @pytest.mark.parametrize("case", ["tiny", "huge", "late_rows", "zero_head", "col_range",
                                   "transposed_rows"])
 def test_split_gram_scale(gpu_device, case, kernel_variant):

@@ -184,6 +184,10 @@ class AutoencoderEngine:
                                                 self.input_shape[0], self.input_shape[1])
                          and _lib.get_variant("ENCODER_UNFUSED") == 0)
         self.t = 0  # Adam iterations
+        # backward: weight gradients on a second stream, off the input-gradient chain
+        # (SPECENH_WGRAD_SERIAL=1: one stream, the round-4 order)
+        self.wgrad_overlap = os.environ.get("SPECENH_WGRAD_SERIAL", "0") in ("", "0")
+        self._side = None
         self._bufs = {}
         self.infer_out_dtype = torch.float32  # set_inference_output_dtype
         self._loss = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -483,10 +487,24 @@ class AutoencoderEngine:
     def backward(self, on_layer_done=None):
         """Gradients of the last loss_and_grad() into self.g (overwritten).
         ``on_layer_done(i)`` (optional) is called once layer i's weight gradient is enqueued
-        (layers in reverse order): self.g[ops[i].off_w:] is then final on this stream."""
+        (layers in reverse order), with the stream that gradient was enqueued on current:
+        self.g[ops[i].off_w:] is final in that stream's order.
+
+        The input-gradient chain (dgrad, pool backward) stays on the current stream; each
+        layer's weight gradient (wgrad + its ordered partial sum) is enqueued on a second
+        stream as soon as the layer's output gradient exists, so the under-filled wgrad
+        launches of a 128-sample step run beside the chain instead of after each link. The
+        current stream waits for the second one before returning: the same kernels on the
+        same inputs, bitwise the serial result (tests/test_ae_gpu.py)."""
         N = self._last_train_N
         b = self._buffers(N, True)
         self.g.zero_()
+        main = torch.cuda.current_stream(self.device)
+        side = None
+        if self.wgrad_overlap:
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=self.device)
+            side = self._side
         n_ops = len(self.ops)
         for i in range(n_ops - 1, -1, -1):
             op = self.ops[i]
@@ -508,14 +526,24 @@ class AutoencoderEngine:
             _, IH, IW, C = hin.shape
             OH, OW = d_out.shape[1:3]
             s, pt, pl, dil = op.fwd_geom()
-            ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[i],
-                                 self._gbv[i], b["ws"])
-            if on_layer_done is not None:
-                on_layer_done(i)
+            if side is None:
+                ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[i],
+                                     self._gbv[i], b["ws"])
+                if on_layer_done is not None:
+                    on_layer_done(i)
+            else:
+                side.wait_stream(main)  # d_out (and the zeroed g) are ready
+                with torch.cuda.stream(side):
+                    ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[i],
+                                         self._gbv[i], b["ws"])
+                    if on_layer_done is not None:
+                        on_layer_done(i)
             if i == 0:
                 continue
             self._conv(i, d_out, b["d"][i], weights=self.w_d[i], geom=op.dgrad_geom(),
                        act=None, mask=relu_mask, bias=False, out_shape=(IH, IW), cout=op.cin)
+        if side is not None:
+            main.wait_stream(side)
 
     def adam(self, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7, grad_scale=1.0):
         """Keras Adam on the fp32 master weights; the low-precision copy and every layer's

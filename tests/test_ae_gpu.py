@@ -463,6 +463,34 @@ def test_backward_is_bitwise_deterministic(gpu_device):
     assert torch.equal(grads[0], grads[1])
 
 
+@pytest.mark.parametrize("dtype,hw,n", [("mixed_bfloat16", (128, 128), 128),
+                                        ("float16", (64, 64), 16), ("float32", (32, 32), 4)])
+def test_wgrad_side_stream_is_bitwise_serial(gpu_device, dtype, hw, n):
+    """backward() enqueues every weight gradient on a second stream beside the input-
+    gradient chain (default) or on the current stream (wgrad_overlap = False): after three
+    train steps (forward, BCE, backward, Adam) the gradients, weights and Adam moments of
+    both engines are bitwise equal, and the on_layer_done hook sees each layer once."""
+    ops = ref_model_ops()
+    rng = np.random.default_rng(17)
+    xs = [rng.uniform(0, 1, (n, *hw, 1)) for _ in range(3)]
+    ys = [rng.uniform(0, 1, (n, *hw, 1)) for _ in range(3)]
+    state = []
+    for overlap in (True, False):
+        eng, _ = make(ops, (*hw, 1), dtype=dtype, seed=41)
+        eng.wgrad_overlap = overlap
+        seen = []
+        for x, y in zip(xs, ys):
+            eng.forward(upload(eng, x), train=True)
+            eng.loss_and_grad(upload(eng, y))
+            eng.backward(on_layer_done=seen.append)
+            eng.adam()
+        torch.cuda.synchronize()
+        assert seen == [i for i in range(len(ops) - 1, -1, -1) if ops[i].__class__.__name__ == "ConvOp"] * 3
+        state.append([t.clone() for t in (eng.g, eng.w, eng.m, eng.v)])
+    for a, b in zip(*state):
+        assert torch.equal(a, b)
+
+
 def test_reference_model_fp16_relative(gpu_device):
     """C5 runs the autoencoder forward in fp16 (MFMA f16, fp32 accumulation): trained
     weights, C4-style inputs, out_rel / logit_rel within checks.TOL['float16']."""

@@ -867,6 +867,41 @@ __device__ __forceinline__ void cholqr(const float* sY, float* sZ, int r, double
   __syncthreads();
 }
 
+// fp64 1/x and 1/sqrt(x) from v_rcp_f64 / v_rsq_f64 and two Newton steps (full fp64
+// precision for finite x != 0 / x > 0): the IEEE division and sqrt sequences sat on the
+// critical path of every Jacobi round (the angle is computed once per pair, then rounded to
+// fp32 for the rotation).
+#ifndef SPECENH_SS_EXACT_ANGLE
+#define SPECENH_SS_EXACT_ANGLE 0
+#endif
+__device__ __forceinline__ double rcp64_2(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ double rsq64_2(double x) {
+  double r = __builtin_amdgcn_rsq(x);
+  r = fma(r * fma(-0.5 * x, r * r, 0.5), 1.0, r);      // r (1 + (1 - x r^2) / 2)
+  return fma(r * fma(-0.5 * x, r * r, 0.5), 1.0, r);
+}
+// rotation annihilating hab: tau = (hbb - haa) / (2 hab), t = sign(tau) / (|tau| +
+// sqrt(1 + tau^2)), c = 1 / sqrt(1 + t^2), s = t c (|hab| > 1e-37)
+__device__ __forceinline__ void jacobi_angle(double haa, double hbb, double hab, double& c,
+                                             double& s) {
+  if (SPECENH_SS_EXACT_ANGLE) {
+    const double tau = (hbb - haa) / (2.0 * hab);
+    const double tt = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+    c = 1.0 / sqrt(1.0 + tt * tt);
+    s = tt * c;
+    return;
+  }
+  const double tau = (hbb - haa) * rcp64_2(2.0 * hab);
+  const double u = fma(tau, tau, 1.0);
+  const double tt = copysign(rcp64_2(fabs(tau) + u * rsq64_2(u)), tau >= 0 ? 1.0 : -1.0);
+  c = rsq64_2(fma(tt, tt, 1.0));
+  s = tt * c;
+}
+
 // Parallel (round-robin / Brent-Luk) cyclic Jacobi on the symmetric P x P matrix H in
 // LDS, one wave: each round rotates P/2 disjoint (a, b) pairs at once; Q accumulates
 // the eigenvectors. Angles in fp64.
@@ -903,10 +938,7 @@ __device__ __forceinline__ int jacobi(float* sH, float* sQ, float* sCS, int* sPa
         double c = 1.0, s = 0.0;
         if (fabs(hab) > 1e-37) {
           const double haa = sH[a * P + a], hbb = sH[b * P + b];
-          const double tau = (hbb - haa) / (2.0 * hab);
-          const double tt = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
-          c = 1.0 / sqrt(1.0 + tt * tt);
-          s = tt * c;
+          jacobi_angle(haa, hbb, hab, c, s);
         }
         sCS[2 * lane] = (float)c;
         sCS[2 * lane + 1] = (float)s;

@@ -1008,6 +1008,98 @@ __device__ __forceinline__ int jacobi(float* sH, float* sQ, float* sCS, int* sPa
   return sweep;
 }
 
+// The same cyclic Jacobi with the lanes grouped by pair (default): L lanes per pair, lane
+// (pair j, sub) covering columns NC sub .. of rows (a, b) in the row pass and rows NC sub ..
+// of columns (a, b) in the column pass. Each lane computes its own pair's angle from the
+// reads of the row pass, so a round is two read -> write phases and two wave syncs; the
+// table form above (P / 2 angle lanes write (c, s) to LDS, sync, every lane reads them
+// back) adds a third dependent LDS round trip. The pair indices advance by one tournament
+// step per round in registers (no modulo per item and round).
+#ifndef SPECENH_SS_JACOBI_TABLE
+#define SPECENH_SS_JACOBI_TABLE 0
+#endif
+template <int P>
+__device__ __forceinline__ int jacobi_grouped(float* sH, float* sQ) {  // -> sweeps run
+  constexpr int NP = P / 2;                                   // pairs per round
+  constexpr int L = (128 / P) < P ? (128 / P) : P;            // lanes per pair
+  constexpr int NC = (P + L - 1) / L;                         // columns (rows) per lane
+  static_assert(L * NP <= 64, "lanes");
+  const int lane = threadIdx.x;  // wave 0
+  for (int idx = lane; idx < P * P; idx += 64) sQ[idx] = (idx / P == idx % P) ? 1.f : 0.f;
+  const int j = lane / L, sub = lane - j * L;
+  const bool live = j < NP;
+  const int k0 = NC * sub;
+  // tournament players of pair j: kA = j (player 0 never moves), kB = P - 1 - j; player
+  // k > 0 sits at 1 + (k - 1 + round) mod (P - 1)
+  const int kA = live ? j : 0, kB = live ? P - 1 - j : P - 1;
+  int ra0 = kA == 0 ? 0 : kA - 1, rb0 = kB - 1;  // round-0 offsets
+  wave_lds_sync();
+  int sweep = 0;
+  for (; sweep < 15; ++sweep) {
+    double off = 0.0, diag = 0.0;
+    for (int idx = lane; idx < P * P; idx += 64) {
+      const double h = sH[idx];
+      if (idx / P != idx % P) off += h * h; else diag += h * h;
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+      off += __shfl_xor(off, m);
+      diag += __shfl_xor(diag, m);
+    }
+    if (off <= 1e-13 * diag) break;  // (uniform; see jacobi)
+    int ra = ra0, rb = rb0;
+    for (int round = 0; round < P - 1; ++round) {
+      int a = kA == 0 ? 0 : 1 + ra, b = 1 + rb;
+      if (a > b) { const int t = a; a = b; b = t; }
+      // row pass: the pair's 2 x 2 entries and this lane's columns of rows a, b
+      const float haa = sH[a * P + a], hbb = sH[b * P + b], hab = sH[a * P + b];
+      float xa[NC], xb[NC];
+#pragma unroll
+      for (int u = 0; u < NC; ++u) {
+        const int k = min(k0 + u, P - 1);
+        xa[u] = sH[a * P + k];
+        xb[u] = sH[b * P + k];
+      }
+      double cd = 1.0, sd = 0.0;
+      if (fabs((double)hab) > 1e-37) jacobi_angle(haa, hbb, hab, cd, sd);
+      const float c = (float)cd, sn = (float)sd;
+      if (live) {
+#pragma unroll
+        for (int u = 0; u < NC; ++u)
+          if (k0 + u < P) {
+            sH[a * P + k0 + u] = c * xa[u] - sn * xb[u];
+            sH[b * P + k0 + u] = sn * xa[u] + c * xb[u];
+          }
+      }
+      wave_lds_sync();
+      // column pass: rows k0 .. of columns a, b of H and Q
+      float qa[NC], qb[NC];
+#pragma unroll
+      for (int u = 0; u < NC; ++u) {
+        const int k = min(k0 + u, P - 1);
+        xa[u] = sH[k * P + a];
+        xb[u] = sH[k * P + b];
+        qa[u] = sQ[k * P + a];
+        qb[u] = sQ[k * P + b];
+      }
+      if (live) {
+#pragma unroll
+        for (int u = 0; u < NC; ++u)
+          if (k0 + u < P) {
+            const int k = k0 + u;
+            sH[k * P + a] = c * xa[u] - sn * xb[u];
+            sH[k * P + b] = sn * xa[u] + c * xb[u];
+            sQ[k * P + a] = c * qa[u] - sn * qb[u];
+            sQ[k * P + b] = sn * qa[u] + c * qb[u];
+          }
+      }
+      wave_lds_sync();
+      ra = ra + 1 == P - 1 ? 0 : ra + 1;
+      rb = rb + 1 == P - 1 ? 0 : rb + 1;
+    }
+  }
+  return sweep;
+}
+
 // P = 8 adds the prod8 scratch ([4][64] doubles after sRi) and gemm_GZ8's sT (r x 8).
 template <int P>
 struct SsLayout {
@@ -1150,10 +1242,13 @@ void subspace_kernel(const float* G, int r, int K,
     __syncthreads();
     SS_MARK(3);
     if (tid < 64) {
+      const int sw = SPECENH_SS_JACOBI_TABLE ? jacobi<P>(sH, sQ, sCS, sPair)
+                                             : jacobi_grouped<P>(sH, sQ);
 #ifdef SPECENH_SS_STATS
-      sweeps +=
+      sweeps += sw;
+#else
+      (void)sw;
 #endif
-      jacobi<P>(sH, sQ, sCS, sPair);
       // Ritz values descending, ties in index order (a stable sort), as ranks: lane c counts
       // the values ahead of its own (thread 0's insertion sort was a serial chain of LDS
       // reads); NaN sorts last

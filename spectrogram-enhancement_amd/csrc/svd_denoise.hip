@@ -786,18 +786,50 @@ __device__ __forceinline__ double readlane_f64(double v, int src) {
   return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
+// fp64 1/x and 1/sqrt(x) from v_rcp_f64 / v_rsq_f64 and two Newton steps (full fp64
+// precision for finite x != 0 / x > 0): the IEEE division and sqrt sequences sat on the
+// critical path of every Jacobi round (the angle is computed once per pair, then rounded to
+// fp32 for the rotation).
+#ifndef SPECENH_SS_EXACT_ANGLE
+#define SPECENH_SS_EXACT_ANGLE 0
+#endif
+__device__ __forceinline__ double rcp64_2(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ double rsq64_2(double x) {
+  double r = __builtin_amdgcn_rsq(x);
+  r = fma(r * fma(-0.5 * x, r * r, 0.5), 1.0, r);      // r (1 + (1 - x r^2) / 2)
+  return fma(r * fma(-0.5 * x, r * r, 0.5), 1.0, r);
+}
 // Orthonormalise the columns of Y (r x P, LDS) into Z with CholeskyQR in fp64:
 // S = Y^T Y, S = R^T R, Z = Y R^-1. fp64 keeps the Gram of Y (condition up to ~1e12
 // here) factorisable; callers run it twice (CholeskyQR2) for fp32-level orthogonality.
 template <int P>
-__device__ __forceinline__ void cholqr(const float* sY, float* sZ, int r, double* sS, double* sRi) {
+__device__ __forceinline__ void cholqr(const float* sY, float* sZ, int r, double* sS, double* sRi,
+                                       long long* sub = nullptr) {
   const int tid = threadIdx.x;
+#ifdef SPECENH_SS_STATS  // sub-phase clocks: Gram, Cholesky, forward substitution
+  long long t_ = __builtin_amdgcn_s_memtime();
+#define CQ_MARK(q)                                              \
+  do {                                                          \
+    const long long n_ = __builtin_amdgcn_s_memtime();          \
+    if (sub) sub[q] += n_ - t_;                                 \
+    t_ = n_;                                                    \
+  } while (0)
+#else
+#define CQ_MARK(q) \
+  do {             \
+  } while (0)
+#endif
   if constexpr (P == 8) {
     prod8(sY, sY, r, sS + 2 * P * P, sS);  // scratch [4][64] past sS, sRi (SsLayout)
   } else {
     prodP<P>(sY, sY, r, sS);  // (full P x P; the factorisation reads the upper triangle)
   }
   __syncthreads();
+  CQ_MARK(0);
   if (tid < 64 && P > 24) {  // Cholesky S = R^T R (R upper, in place), one wave, in LDS
     for (int k = 0; k < P; ++k) {
       double d = sS[k * P + k];
@@ -823,8 +855,13 @@ __device__ __forceinline__ void cholqr(const float* sY, float* sZ, int r, double
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       double d = readlane_f64(col[k], k);
-      d = d > 0.0 ? sqrt(d) : 1e-300;  // rank-deficient: keep going, column ~ 0
-      col[k] = j == k ? d : col[k] / d;  // row k of R (lanes j > k; j < k hold zeros)
+      if (SPECENH_SS_EXACT_ANGLE) {
+        d = d > 0.0 ? sqrt(d) : 1e-300;  // rank-deficient: keep going, column ~ 0
+        col[k] = j == k ? d : col[k] / d;  // row k of R (lanes j > k; j < k hold zeros)
+      } else {  // the same from one v_rsq_f64 + Newton steps (the pivot's critical path)
+        const double ri = d > 0.0 ? rsq64_2(d) : 1e300;
+        col[k] = j == k ? (d > 0.0 ? d * ri : 1e-300) : col[k] * ri;
+      }
 #pragma unroll
       for (int i = k + 1; i < P; ++i) {  // trailing S[i][j] -= R[k][i] R[k][j], j >= i
         const double rki = readlane_f64(col[k], i);
@@ -843,6 +880,7 @@ __device__ __forceinline__ void cholqr(const float* sY, float* sZ, int r, double
   // multiplied by it (P^2 FMAs per row).
   if (tid < P) sRi[tid] = 1.0 / sS[tid * P + tid];
   __syncthreads();
+  CQ_MARK(1);
   for (int i = tid; i < r; i += SS_THREADS) {
     // Column by column (z_c from the finished z_0 .. z_{c-1}): each z_c is consumed by the
     // next columns, so the FMAs stay in order. The pivot-row form (eliminate z_d from every
@@ -865,25 +903,10 @@ __device__ __forceinline__ void cholqr(const float* sY, float* sZ, int r, double
     for (int c = 0; c < P; ++c) sZ[i * P + c] = (float)z[c];
   }
   __syncthreads();
+  CQ_MARK(2);
+#undef CQ_MARK
 }
 
-// fp64 1/x and 1/sqrt(x) from v_rcp_f64 / v_rsq_f64 and two Newton steps (full fp64
-// precision for finite x != 0 / x > 0): the IEEE division and sqrt sequences sat on the
-// critical path of every Jacobi round (the angle is computed once per pair, then rounded to
-// fp32 for the rotation).
-#ifndef SPECENH_SS_EXACT_ANGLE
-#define SPECENH_SS_EXACT_ANGLE 0
-#endif
-__device__ __forceinline__ double rcp64_2(double x) {
-  double r = __builtin_amdgcn_rcp(x);
-  r = fma(r, fma(-x, r, 1.0), r);
-  return fma(r, fma(-x, r, 1.0), r);
-}
-__device__ __forceinline__ double rsq64_2(double x) {
-  double r = __builtin_amdgcn_rsq(x);
-  r = fma(r * fma(-0.5 * x, r * r, 0.5), 1.0, r);      // r (1 + (1 - x r^2) / 2)
-  return fma(r * fma(-0.5 * x, r * r, 0.5), 1.0, r);
-}
 // rotation annihilating hab: tau = (hbb - haa) / (2 hab), t = sign(tau) / (|tau| +
 // sqrt(1 + tau^2)), c = 1 / sqrt(1 + t^2), s = t c (|hab| > 1e-37)
 __device__ __forceinline__ void jacobi_angle(double haa, double hbb, double hab, double& c,
@@ -1151,6 +1174,8 @@ void subspace_kernel(const float* G, int r, int K,
   const int tid = threadIdx.x;
 #ifdef SPECENH_SS_STATS  // development build (tools/ss_stats.py): shader clocks per phase
   long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
+  long long csub[3] = {0, 0, 0};
+#define CQ_SUB csub
   int sweeps = 0;
 #define SS_MARK(slot)                                    \
   do {                                                   \
@@ -1162,6 +1187,7 @@ void subspace_kernel(const float* G, int r, int K,
 #define SS_MARK(slot) \
   do {                \
   } while (0)
+#define CQ_SUB nullptr
 #endif
 
   // (gz_quad: the host checked r % 4 == 0 and a 16-byte aligned G, r^2 floats per matrix)
@@ -1204,15 +1230,15 @@ void subspace_kernel(const float* G, int r, int K,
         // Intermediate rounds only have to keep the block well conditioned (G Z
         // re-amplifies the dominant directions anyway): one CholeskyQR pass. The basis
         // that feeds the Rayleigh-Ritz step below gets the full CholeskyQR2.
-        cholqr<P>(sY, sZ, r, sS, sRi);  // Z = orth(Y) to ~cond(Y) * eps
+        cholqr<P>(sY, sZ, r, sS, sRi, CQ_SUB);  // Z = orth(Y) to ~cond(Y) * eps
         SS_MARK(1);
         GZ(sZ, sY);                     // Y = G Z
         __syncthreads();
         SS_MARK(2);
         continue;
       }
-      cholqr<P>(sY, sZ, r, sS, sRi);  // Z = orth(Y)
-      cholqr<P>(sZ, sY, r, sS, sRi);  // second pass into Y ...
+      cholqr<P>(sY, sZ, r, sS, sRi, CQ_SUB);  // Z = orth(Y)
+      cholqr<P>(sZ, sY, r, sS, sRi, CQ_SUB);  // second pass into Y ...
       SS_MARK(1);
       GZ(sY, sZ);                     // ... Z = G * orth(Y)
       __syncthreads();
@@ -1315,9 +1341,11 @@ void subspace_kernel(const float* G, int r, int K,
     long long* o = reinterpret_cast<long long*>(const_cast<float*>(Gb));
     for (int q = 0; q < 7; ++q) o[q] = tacc[q];
     o[7] = sweeps;
+    for (int q = 0; q < 3; ++q) o[8 + q] = csub[q];
   }
 #endif
 #undef SS_MARK
+#undef CQ_SUB
 }
 
 // Workgroup barrier that orders LDS only: waits for this wave's LDS operations, not for

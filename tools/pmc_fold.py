@@ -1,7 +1,7 @@
 """Fold the rocprofv3 --pmc passes of tools/pmc_refresh.sh into one JSON keyed by target,
-stage and exact kernel symbol (the file bench.py reads: profiles/pmc_r03.json).
+stage and exact kernel symbol (the file bench.py reads: profiles/pmc_r05.json).
 
-    python tools/pmc_fold.py gpurun_out/pmc profiles/pmc_r03.json
+    python tools/pmc_fold.py gpurun_out/pmc profiles/pmc_r05.json
 
 Each pass directory <target>_<pass> holds rocprofv3's counter_collection.csv and the
 manifest of tools/pmc_workload.py. The i-th dispatch whose kernel name contains "specenh"

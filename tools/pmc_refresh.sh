@@ -3,7 +3,7 @@
 # (tools/pmc_workload.py targets), one counter group per run, each under its own time limit.
 # Run from the repo root on the GPU box:
 #   bash tools/pmc_refresh.sh [targets...]      (default: c5 c2 csd c3 c4)
-# then fold here: python tools/pmc_fold.py gpurun_out/pmc profiles/pmc_r03.json
+# then fold here: python tools/pmc_fold.py gpurun_out/pmc profiles/pmc_r05.json
 R=$(pwd)
 OUT=$R/gpurun_out/pmc
 mkdir -p $OUT

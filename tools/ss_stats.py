@@ -28,9 +28,11 @@ for lo, hi in [(0, 16), (1, 256)]:
                                             ctypes.c_void_p(out.data_ptr()), 0,
                                             ctypes.c_void_p(ws.data_ptr()), None))
     torch.cuda.synchronize()
-    clk = ws[:B * n * n * 4].view(torch.int64).view(B, n * n // 2)[:, :8].double().cpu()
+    clk = ws[:B * n * n * 4].view(torch.int64).view(B, n * n // 2)[:, :11].double().cpu()
     tot = clk[:, :7].sum(1)
     print(f"[{lo}, {hi}): shader clocks per matrix (thread 0, mean over {B}): total "
           f"{tot.mean():.0f}, Jacobi sweeps mean {clk[:, 7].mean():.2f} max {clk[:, 7].max():.0f}")
     for q, nm in enumerate(names):
         print(f"  {nm:14s} {clk[:, q].mean():10.0f}  ({100 * clk[:, q].mean() / tot.mean():4.1f}%)")
+    for q, nm in zip(range(8, 11), ["  Gram Y^T Y", "  Cholesky", "  Z = Y R^-1"]):
+        print(f"  {nm:14s} {clk[:, q].mean():10.0f}  (of CholeskyQR, thread 0)")

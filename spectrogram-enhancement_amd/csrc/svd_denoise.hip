@@ -762,19 +762,89 @@ __device__ __forceinline__ void prodP(const float* sA, const float* sB, int r, d
   for (int t = wave; t < NT * NT; t += SS_THREADS / 64) {  // wave-uniform
     const int ta = t / NT, tb = t % NT;
     const int a = 16 * ta + m, c = 16 * tb + m;
-    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-    for (int i0 = 0; i0 < r; i0 += 4) {
+    // 16 rows per iteration into two accumulators, every read of an iteration (and, with
+    // the unroll, of the next) issued ahead of its MFMAs: the one-accumulator loop was a
+    // chain of r / 4 LDS reads -> convert -> MFMA round trips (~24 k clocks per Gram at
+    // r = 256, P = 24; SS_STATS build)
+    const bool va = a < P, vb = c < P;
+    const int ac = va ? a : 0, cc = vb ? c : 0;
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    int i0 = 0;
+    for (; i0 + 16 <= r; i0 += 16) {
+      double av[4], bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 4 * u + kq;
+        const float xa = sA[i * P + ac], xb = sB[i * P + cc];
+        av[u] = va ? (double)xa : 0.0;
+        bv[u] = vb ? (double)xb : 0.0;
+      }
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], bv[0], acc, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1], bv[1], acc1, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[2], bv[2], acc, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[3], bv[3], acc1, 0, 0, 0);
+    }
+    for (; i0 < r; i0 += 4) {
       const int i = i0 + kq;
-      const double av = (i < r && a < P) ? (double)sA[i * P + a] : 0.0;
-      const double bv = (i < r && c < P) ? (double)sB[i * P + c] : 0.0;
+      const double av = (i < r && va) ? (double)sA[i * P + ac] : 0.0;
+      const double bv = (i < r && vb) ? (double)sB[i * P + cc] : 0.0;
       acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
     }
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) acc[reg] += acc1[reg];
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
       const int row = 16 * ta + kq + 4 * reg, col = 16 * tb + m;
       if (row < P && col < P) out[row * P + col] = acc[reg];
     }
   }
+  __syncthreads();
+}
+
+// prod8 on the fp64 matrix cores: one 16 x 16 tile (the 8 x 8 block valid), the r rows
+// split over the four waves (16-row steps, two accumulators, as prodP), the four partial
+// 8 x 8 blocks summed in wave order through sPart[4][64]. prod8's butterflies were 64
+// cross-lane fp64 exchanges per call. Ends with out visible to all threads.
+#ifndef SPECENH_SS_PROD8_VALU
+#define SPECENH_SS_PROD8_VALU 0
+#endif
+__device__ __forceinline__ void prod8m(const float* sA, const float* sB, int r, double* sPart,
+                                       double* out) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m = lane & 15, kq = lane >> 4;
+  const bool v = m < 8;
+  const int mc = v ? m : 0;
+  const int rq = ((r + 15) / 16 + 3) / 4 * 16;  // rows per wave, a multiple of 16
+  const int i_lo = min(r, wave * rq), i_hi = min(r, i_lo + rq);
+  f64x4 acc = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+  int i0 = i_lo;
+  for (; i0 + 16 <= i_hi; i0 += 16) {
+    double av[4], bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + 4 * u + kq;
+      const float xa = sA[i * 8 + mc], xb = sB[i * 8 + mc];
+      av[u] = v ? (double)xa : 0.0;
+      bv[u] = v ? (double)xb : 0.0;
+    }
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], bv[0], acc, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1], bv[1], acc1, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[2], bv[2], acc, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[3], bv[3], acc1, 0, 0, 0);
+  }
+  for (; i0 < i_hi; i0 += 4) {
+    const int i = i0 + kq;
+    const double av = (i < i_hi && v) ? (double)sA[i * 8 + mc] : 0.0;
+    const double bv = (i < i_hi && v) ? (double)sB[i * 8 + mc] : 0.0;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) {
+    const int row = kq + 4 * reg;  // D row (a), column m (c)
+    if (row < 8 && v) sPart[wave * 64 + row * 8 + m] = acc[reg] + acc1[reg];
+  }
+  __syncthreads();
+  if (tid < 64) out[tid] = (sPart[tid] + sPart[64 + tid]) + (sPart[128 + tid] + sPart[192 + tid]);
   __syncthreads();
 }
 
@@ -824,7 +894,8 @@ __device__ __forceinline__ void cholqr(const float* sY, float* sZ, int r, double
   } while (0)
 #endif
   if constexpr (P == 8) {
-    prod8(sY, sY, r, sS + 2 * P * P, sS);  // scratch [4][64] past sS, sRi (SsLayout)
+    if (SPECENH_SS_PROD8_VALU) prod8(sY, sY, r, sS + 2 * P * P, sS);  // scratch [4][64] past sS, sRi
+    else prod8m(sY, sY, r, sS + 2 * P * P, sS);
   } else {
     prodP<P>(sY, sY, r, sS);  // (full P x P; the factorisation reads the upper triangle)
   }
@@ -1250,7 +1321,8 @@ void subspace_kernel(const float* G, int r, int K,
     }
     // Rayleigh-Ritz: H = Z^T (G Z) = Z^T Y
     if constexpr (P == 8) {
-      prod8(sZ, sY, r, sPart, sS);
+      if (SPECENH_SS_PROD8_VALU) prod8(sZ, sY, r, sPart, sS);
+      else prod8m(sZ, sY, r, sPart, sS);
       if (tid < 64) sH[tid] = (float)sS[tid];
     } else {
       prodP<P>(sZ, sY, r, sS);

@@ -2,7 +2,8 @@
 # Round-end measurement pass on the gpurun box: full GPU tests, the default bench, rocprof kernel
 # stats of the C5 chain (one stream), of the C4 train step and of the C3 SVD, the AE model
 # variants, and the PMC refresh of every target. Steps chained; the first failure ends the run.
-#   bash tools/gpu_final.sh TAG
+#   bash tools/gpu_final.sh TAG        (FINAL_PMC=0: skip the PMC passes, run them as a second
+#                                      call: bash tools/pmc_refresh.sh c5 c2 csd c3 c4)
 TAG=${1:-final}
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
@@ -27,7 +28,9 @@ echo "[final] rocprof c3"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/profc3_$TAG -o prof -- python3 $R/tools/svd_bench.py > $R/gpurun_out/c3prof_$TAG.log 2>&1 || exit 1
 mkdir -p $R/gpurun_out/profc3_$TAG && find /tmp/profc3_$TAG -name '*kernel_stats.csv' -exec cp {} $R/gpurun_out/profc3_$TAG/ \;
 cd $R
-echo "[final] pmc"
-rm -rf gpurun_out/pmc
-bash tools/pmc_refresh.sh c5 c2 csd c3 c4 || exit 1
+if [ "${FINAL_PMC:-1}" != 0 ]; then
+  echo "[final] pmc"
+  rm -rf gpurun_out/pmc
+  bash tools/pmc_refresh.sh c5 c2 csd c3 c4 || exit 1
+fi
 echo "[final] done"

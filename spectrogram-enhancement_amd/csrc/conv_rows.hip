@@ -1106,6 +1106,25 @@ struct E2Args {
 };
 
 constexpr int E2R1 = 32;  // conv1 input ring rows (positions)
+// Staged image rows: SPECENH_ENC2_COPIES element-shifted copies of C1CW words each. With 2
+// (copy c = the row shifted by c elements) a lane's 8-element B run starts on a word, so
+// it is read as two ds_read2_b32 (16 LDS cycles per fragment); with 4 (c = 0 .. 3) every
+// run starts on an even word and is read as two ds_read_b64 (8 cycles with their 2-way
+// conflicts: tools-free brute force over copy / row strides found no conflict-free even
+// layout). The conv1 B fragments are 8 of each step's 14 LDS reads per wave.
+#ifndef SPECENH_ENC2_COPIES
+#define SPECENH_ENC2_COPIES 4
+#endif
+constexpr int E2NC = SPECENH_ENC2_COPIES;
+// copy c at word E2CB(c) of a staged row. A half-wave's b64 reads cover copies (cb, cb + 2)
+// at words w .. w + 17 of one and w + 2 .. w + 19 of the other, for two ring rows: with
+// E2CB(cb) - E2CB(cb + 2) = 14 (mod 64) and a row stride of 32 (mod 64) those are 64
+// distinct banks (conflict-free; the plain 72-word stride was 2-way).
+__host__ __device__ constexpr int E2CB(int c) {
+  return E2NC == 4 ? (c == 0 ? 0 : c == 1 ? 72 : c == 2 ? 178 : 250) : c * C1CW;
+}
+constexpr int E2ROW = E2NC == 4 ? 352 : 2 * C1CW;  // words per staged row
+constexpr int E2RROWS = E2R1 + 2;                  // ring + two zero rows (parities)
 #ifndef SPECENH_ENC2_STAGGER
 #define SPECENH_ENC2_STAGGER 0
 #endif
@@ -1130,11 +1149,11 @@ void enc2_rows_kernel(E2Args a) {
   const int nimg = ((int)a.N - (int)blockIdx.x + G - 1) / G;
   const int S = nimg * SPI + 1;
 
-  for (int e = tid; e < (C::LDS + (E2R1 + 1) * C1ROW * 4) / 16; e += 512)
+  for (int e = tid; e < (C::LDS + E2RROWS * E2ROW * 4) / 16; e += 512)
     reinterpret_cast<uint4*>(lds)[e] = uint4{0u, 0u, 0u, 0u};
   // both layers' biases in LDS (read where used: as resident f32x4s they cost the 8 VGPRs
   // that made the 4-waves-per-SIMD build spill)
-  float* const btab = reinterpret_cast<float*>(lds + C::LDS + (E2R1 + 1) * C1ROW * 4);
+  float* const btab = reinterpret_cast<float*>(lds + C::LDS + E2RROWS * E2ROW * 4);
   if (tid < 16) btab[tid] = a.b1[tid];
   else if (tid < 48) btab[tid] = a.b2[tid - 16];
   auto bias2_ld = [&]() { return *reinterpret_cast<const f32x4*>(btab + 16 + 16 * nb + 4 * kg); };
@@ -1184,13 +1203,18 @@ void enc2_rows_kernel(E2Args a) {
   resident_loads_landed();
   const int w1x = wv & 3, jr = wv >> 2;  // conv1 pixel block, conv2 input row of the pair
   const int wbase = 16 * w1x + m + 3;
+  // 4 copies: the run of pooled pixel p = 16 w1x + m at column parity cb starts at element
+  // 2 p + cb + 6 of copy 0; copy c = that element mod 4 holds it at the even word w4
+  const int p1 = 16 * w1x + m;
+  const int c4hi = 2 * ((p1 + 3) & 1), w4 = p1 + 3 - ((p1 + 3) & 1);
+  const int cbase0 = E2CB(c4hi) + w4, cbase1 = E2CB(1 + c4hi) + w4;  // column parity 0 / 1
 
   // image-row stream: position pp = il (H1 + 4) + y + 2; waves 0-3 move positions pp + wv.
   // The loop keeps (image, row) of its positions and steps as scalar counters advanced per
   // step (a run-time division per use had cost ~25 SALU + a VALU reciprocal each).
   const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
   auto stage1_at = [&](int pos, int il, int y) -> int {  // position pos = il PPI + y + 2
-    uint32_t* dst = ring1 + (pos & (E2R1 - 1)) * C1ROW + 4;
+    uint32_t* dst = ring1 + (pos & (E2R1 - 1)) * E2ROW + 4;
     if (il < nimg && y >= 0 && y < H1) {
       const long long n = (long long)blockIdx.x + (long long)il * G;
       if (lane < 16) lds_dma16(X + (n * H1 + y) * C1W + 8 * lane, dst);
@@ -1205,23 +1229,42 @@ void enc2_rows_kernel(E2Args a) {
     const int il = pos / PPI;
     return stage1_at(pos, il, pos - il * PPI - 2);
   };
-  auto shift1 = [&](int pp) {  // copy 1 of positions pp .. pp + 3
-    if (tid < 4 * C1CW) {
-      const int j = tid / C1CW, i = tid - j * C1CW;
-      uint32_t* row = ring1 + ((pp + j) & (E2R1 - 1)) * C1ROW;
-      row[C1CW + i] = __builtin_amdgcn_alignbit(row[i + 1], row[i], 16);
+  auto shift1 = [&](int pp) {  // copies 1 .. E2NC - 1 of positions pp .. pp + 3
+    constexpr int NW = E2NC == 4 ? C1CW - 2 : C1CW;  // (copy 0 words read: i .. i + 2)
+    if (tid < 4 * NW) {
+      const int j = tid / NW, i = tid - j * NW;
+      uint32_t* row = ring1 + ((pp + j) & (E2R1 - 1)) * E2ROW;
+      const uint32_t r0 = row[i], r1 = row[i + 1];
+      row[E2CB(1) + i] = __builtin_amdgcn_alignbit(r1, r0, 16);
+      if constexpr (E2NC == 4) {
+        const uint32_t r2 = row[i + 2];
+        row[E2CB(2) + i] = r1;
+        row[E2CB(3) + i] = __builtin_amdgcn_alignbit(r2, r1, 16);
+      }
+    }
+  };
+  auto run_at = [&](const uint32_t* row, int cb) -> uint4 {  // row: staged row start
+    if constexpr (E2NC == 4) {
+      // volatile: two separate ds_read_b64 (2 LDS cycles each); the compiler otherwise pairs
+      // reads into ds_read2_b64, which costs 8
+      typedef __attribute__((address_space(3))) const volatile unsigned long long lds_u64;
+      const lds_u64* r = (const lds_u64*)(row + (cb ? cbase1 : cbase0));
+      const unsigned long long lo = r[0], hi = r[1];
+      return uint4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+    } else {
+      const uint32_t* r = row + cb * C1CW + wbase;
+      return uint4{r[0], r[1], r[2], r[3]};
     }
   };
   auto bfrag = [&](int pos, int cb) -> uint4 {
-    const uint32_t* row = ring1 + ((pos + kg) & (E2R1 - 1)) * C1ROW + cb * C1CW + wbase;
-    return uint4{row[0], row[1], row[2], row[3]};
+    return run_at(ring1 + ((pos + kg) & (E2R1 - 1)) * E2ROW, cb);
   };
   // B' (kernel row 4 only): lane group 0 reads row pos, groups 1-3 the zero row past the ring
   // (an address select instead of zeroing 4 data registers)
-  const uint32_t* const zrow = ring1 + E2R1 * C1ROW + wbase;
+  // (two zero rows: the one an odd number of rows from pos, so its banks miss lane group 0's)
   auto bfrag4 = [&](int pos, int cb) -> uint4 {
-    const uint32_t* row = kg == 0 ? ring1 + (pos & (E2R1 - 1)) * C1ROW + cb * C1CW + wbase : zrow;
-    return uint4{row[0], row[1], row[2], row[3]};
+    const uint32_t* zrow = ring1 + (E2NC == 4 ? E2R1 + 1 - (pos & 1) : E2R1) * E2ROW;
+    return run_at(kg == 0 ? ring1 + (pos & (E2R1 - 1)) * E2ROW : zrow, cb);
   };
   // conv2 input row 2 q2 + jr of conv2 step g2 (image g2 / SPI) into its ring slot: pooled
   // pixels 16 w1x + m, channels 4 kg .. 4 kg + 3 (zero rows outside the image)
@@ -1393,7 +1436,7 @@ void enc2_rows_kernel(E2Args a) {
   if (s + 1 < S) step(std::integral_constant<int, 1>{}, s + 1);
 }
 
-constexpr int E2LDS = RC<16, 32, 64>::LDS + (E2R1 + 1) * C1ROW * 4 + 48 * 4;
+constexpr int E2LDS = RC<16, 32, 64>::LDS + E2RROWS * E2ROW * 4 + 48 * 4;
 
 template <typename T, int WPE>
 hipError_t launch_enc2_wpe(const E2Args& a, hipStream_t st) {

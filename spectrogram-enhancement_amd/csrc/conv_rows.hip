@@ -185,9 +185,10 @@ void conv_rows_pool_kernel(CRArgs a) {
     ddst = 2 * C::PIX + (wv & 1) * 1024;
   }
   // rows of global step s: image (s / SPI) of this workgroup, rows 2q, 2q + 1 (q = s % SPI)
-  auto stage = [&](int s) -> bool {  // returns whether this wave issued an LDS-DMA
+  // rows of global step s = il SPI + q (the caller keeps (il, q) as scalar counters: a
+  // run-time division per use cost ~25 SALU and a VALU reciprocal, three per step)
+  auto stage_at = [&](int s, int il, int q) -> bool {  // whether this wave issued an LDS-DMA
     if (!dma_wave) return false;
-    const int il = s / SPI, q = s - il * SPI;
     const int r = 2 * q + (wv >> 1);
     unsigned char* dst = ring + ((2 * s + (wv >> 1)) & 7) * C::ROWB + ddst;
     if (s < S && il < nimg && r < H) {
@@ -198,6 +199,7 @@ void conv_rows_pool_kernel(CRArgs a) {
     *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
     return false;
   };
+  auto stage = [&](int s) { return stage_at(s, s / SPI, s - (s / SPI) * SPI); };  // (prologue)
   __syncthreads();  // ring zeroed
   stage(0);
   stage(1);
@@ -211,6 +213,11 @@ void conv_rows_pool_kernel(CRArgs a) {
   T* __restrict__ O = reinterpret_cast<T*>(a.out);
   const int PW = W / 2, PHh = H / 2;
 
+  // (image, step in image) of steps s - 2 (pool), s (conv), s + 3 (DMA), advanced per step
+  int ilA = -1, qA = SPI - 2, ilC = 0, qC = 0, ilS = 3 / SPI, qS = 3 - (3 / SPI) * SPI;
+  auto adv = [&](int& il, int& q) {
+    if (++q == SPI) { q = 0; ++il; }
+  };
   // step s with I = s % 3 compile-time (the accumulator ring: output row 2q + d -> slot
   // (2 I + d) mod 6)
   auto step = [&](auto ic, const int s) {
@@ -218,12 +225,11 @@ void conv_rows_pool_kernel(CRArgs a) {
     auto slot = [](int d) { return (2 * I + d + 12) % 6; };
     // (1) pair s - 2 (output rows 2q - 4, 2q - 3) is complete: pool, store, reset
     {
-      const int p = s - 2;
       f32x4& r0 = acc[slot(-4)];
       f32x4& r1 = acc[slot(-3)];
-      if (p >= 0) {
-        const int il = p / SPI, q = p - il * SPI;
-        if (il < nimg && q < PHh) {
+      {
+        const int il = ilA, q = qA;  // pair s - 2
+        if (il >= 0 && il < nimg && q < PHh) {
           float v[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[i] = fmaxf(max_pair(fmaxf(r0[i], r1[i])), 0.f);
@@ -238,9 +244,9 @@ void conv_rows_pool_kernel(CRArgs a) {
       r1 = bias;
     }
     // (2) rows of step s + 3 into the ring
-    const bool issued = stage(s + 3);
+    const bool issued = stage_at(s + 3, ilS, qS);
     // (3) this step's input rows
-    const int il = s / SPI, q = s - il * SPI;
+    const int il = ilC, q = qC;
     if (il < nimg && 2 * q < H) {
       // every B fragment of the step first (one LDS latency per step, not one per row or
       // tap column: sched_barrier keeps the compiler from sinking the reads to their MFMAs)
@@ -302,6 +308,9 @@ void conv_rows_pool_kernel(CRArgs a) {
     // older than its DMA and complete too
     if (issued) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    adv(ilA, qA);
+    adv(ilC, qC);
+    adv(ilS, qS);
     lds_barrier();
   };
   int s = 0;

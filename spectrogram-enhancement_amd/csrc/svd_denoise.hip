@@ -2423,9 +2423,9 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
 // fp64 Gram G = X^T X: 64x64 tile per workgroup (upper-triangle tiles, mirrored), 16 rows
 // of X per LDS stage, 4x4 outputs per thread. Products of fp32 inputs are exact in fp64.
 __device__ __forceinline__ void gram64_one(XView x, int K, int r, double* G, int nts,
-                                           long long b) {
+                                           long long b, int tile) {
   __shared__ double sa[16][65], sb[16][65];
-  int t = blockIdx.x, ti = 0;
+  int t = tile, ti = 0;
   while (t >= nts - ti) {
     t -= nts - ti;
     ++ti;
@@ -2489,7 +2489,7 @@ __global__ __launch_bounds__(256) void gram64_kernel(XView x, int K, int r, doub
                                                      const int* only, long long nmat) {
   for (long long b = blockIdx.y; b < nmat; b += gridDim.y) {
     if (only && !only[b]) continue;  // uniform: matrix not selected
-    gram64_one(x, K, r, G, nts, b);
+    gram64_one(x, K, r, G, nts, b, blockIdx.x);
     __syncthreads();  // (LDS reused by the next matrix)
   }
 }
@@ -2934,13 +2934,13 @@ template <typename TO>
 __device__ __forceinline__ void recon_eig_one(XView x, int Kr, int r, const double* Z,
                                               long long ld, const int* kinfo, TO* out,
                                               long long out_bstride, long long osk,
-                                              long long osi, long long b) {
+                                              long long osi, long long b, int kb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* sX = reinterpret_cast<float*>(smem);  // RB x (r + 1)
   float* sV = sX + RB * (r + 1);                // r x 33
   float* sY = sV + r * 33;                      // RB x 33
   const int kc = kinfo[2 * b], comp = kinfo[2 * b + 1];
-  const int k0 = blockIdx.x * RB, tid = threadIdx.x;
+  const int k0 = kb * RB, tid = threadIdx.x;
   const int rows = min(RB, Kr - k0);
   const float* X = x.base + b * x.batch_stride;
   if (x.si == 1) {
@@ -3002,7 +3002,7 @@ __global__ __launch_bounds__(256) void recon_eig_kernel(XView x, int Kr, int r, 
                                                         long long nmat) {
   for (long long b = blockIdx.y; b < nmat; b += gridDim.y) {
     if (only && !only[b]) continue;
-    recon_eig_one<TO>(x, Kr, r, Z, ld, kinfo, out, out_bstride, osk, osi, b);
+    recon_eig_one<TO>(x, Kr, r, Z, ld, kinfo, out, out_bstride, osk, osi, b, blockIdx.x);
     __syncthreads();
   }
 }
@@ -3182,6 +3182,42 @@ struct EigLayout {
 };
 EigLayout eig_layout(int r) { return EigLayout{r, (long long)(r / 2 + 2)}; }
 
+// The flagged-matrix fallback in ONE launch (`only` given, no optimal-rank step): a
+// workgroup takes a flagged matrix through the Gram tiles, the tridiagonalisation, the
+// eigenvectors and the reconstruction blocks in turn (device-scope fences between the
+// phases: each reads the previous one's global results). The four launches it replaces
+// cost ~4.8 us each even with nothing flagged (grids of 512-1536 workgroups that return at
+// once): ~39 us per 4096-shot C5 step.
+#ifndef SPECENH_EIG_MERGED
+#define SPECENH_EIG_MERGED 1
+#endif
+template <typename TO>
+__global__ __launch_bounds__(256) void eig_fallback_kernel(
+    XView x, int Kr, int r, double* G, int nts, double* dg, double* eg, double* taug, int lo,
+    int hi, double* Z, double* fac, long long ld, int* kinfo, TO* out, long long out_bstride,
+    long long osk, long long osi, const int* only, long long nmat) {
+  const int ntri = nts * (nts + 1) / 2, nkb = (Kr + RB - 1) / RB;
+  for (long long b = blockIdx.x; b < nmat; b += gridDim.x) {
+    if (!only[b]) continue;  // uniform
+    for (int t = 0; t < ntri; ++t) {
+      gram64_one(x, Kr, r, G, nts, b, t);
+      __syncthreads();
+    }
+    __threadfence();
+    __syncthreads();
+    tridiag_one(G, r, dg, eg, taug, b);
+    __threadfence();
+    __syncthreads();
+    eigvec_one(G, dg, eg, taug, r, lo, hi, nullptr, Z, fac, ld, kinfo, b);
+    __threadfence();
+    __syncthreads();
+    for (int kb = 0; kb < nkb; ++kb) {
+      recon_eig_one<TO>(x, Kr, r, Z, ld, kinfo, out, out_bstride, osk, osi, b, kb);
+      __syncthreads();
+    }
+  }
+}
+
 template <typename TO>
 hipError_t launch_recon_eig_t(XView xb, int Kr, int r, const double* Z, long long ld,
                               const int* kinfo, void* out, long long ob, long long osk,
@@ -3204,6 +3240,37 @@ hipError_t launch_recon_eig(int odt, XView xb, int Kr, int r, const double* Z, l
   if (odt == SPECENH_DTYPE_BF16)
     return launch_recon_eig_t<__bf16>(xb, Kr, r, Z, ld, kinfo, out, ob, osk, osi, nb, st, only);
   return launch_recon_eig_t<float>(xb, Kr, r, Z, ld, kinfo, out, ob, osk, osi, nb, st, only);
+}
+
+template <typename TO>
+hipError_t launch_eig_fallback_t(XView xb, int Kr, int r, double* G, int nts, double* dg,
+                                 double* eg, double* taug, int lo, int hi, double* Z,
+                                 double* fac, long long ld, int* kinfo, void* out, long long ob,
+                                 long long osk, long long osi, const int* only, long long nb,
+                                 unsigned gm, hipStream_t st) {
+  const size_t lds = (size_t)RB * (r + 1) * 4 + (size_t)r * 33 * 4 + (size_t)RB * 33 * 4;
+  hipError_t e = hipFuncSetAttribute((const void*)eig_fallback_kernel<TO>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  SPECENH_LAUNCH(eig_fallback_kernel<TO>, dim3(gm), dim3(256), lds, st, xb, Kr, r, G, nts, dg,
+                 eg, taug, lo, hi, Z, fac, ld, kinfo, reinterpret_cast<TO*>(out), ob, osk, osi,
+                 only, nb);
+  return hipGetLastError();
+}
+
+hipError_t launch_eig_fallback(int odt, XView xb, int Kr, int r, double* G, int nts, double* dg,
+                               double* eg, double* taug, int lo, int hi, double* Z, double* fac,
+                               long long ld, int* kinfo, void* out, long long ob, long long osk,
+                               long long osi, const int* only, long long nb, unsigned gm,
+                               hipStream_t st) {
+  if (odt == SPECENH_DTYPE_F16)
+    return launch_eig_fallback_t<_Float16>(xb, Kr, r, G, nts, dg, eg, taug, lo, hi, Z, fac, ld,
+                                           kinfo, out, ob, osk, osi, only, nb, gm, st);
+  if (odt == SPECENH_DTYPE_BF16)
+    return launch_eig_fallback_t<__bf16>(xb, Kr, r, G, nts, dg, eg, taug, lo, hi, Z, fac, ld,
+                                         kinfo, out, ob, osk, osi, only, nb, gm, st);
+  return launch_eig_fallback_t<float>(xb, Kr, r, G, nts, dg, eg, taug, lo, hi, Z, fac, ld, kinfo,
+                                      out, ob, osk, osi, only, nb, gm, st);
 }
 
 // The eigen path over the whole batch, chunk by chunk (stream-ordered, no host sync).
@@ -3252,6 +3319,14 @@ int eig_denoise(const float* A, long long batch, int m, int n, long long a_strid
     // fallback (on: the flagged few): a grid of at most two workgroups per CU looping over
     // the matrices instead of one per matrix (gram64_kernel's comment)
     const unsigned gm = on ? (unsigned)std::min<long long>(nb, 2LL * device_cus()) : (unsigned)nb;
+    if (on && opt_mode < 0 && SPECENH_EIG_MERGED && variant(V_EIG_SPLIT) == 0) {
+      const hipError_t e = launch_eig_fallback(odt, xv, Kr, r, G64, nts64, dd, ee, tau, lo, hi,
+                                               Z, fac, L.ld, kinfo,
+                                               static_cast<char*>(out) + (size_t)(b0 * ob) * osz,
+                                               ob, osk, osi, on, nb, gm, st);
+      if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("eigen fallback: ") + hipGetErrorString(e));
+      continue;
+    }
     SPECENH_LAUNCH(gram64_kernel, dim3(ntri64, gm), dim3(256), 0, st, xv, Kr, r, G64, nts64, on,
                    nb);
     SPECENH_LAUNCH(tridiag_kernel, dim3(gm), dim3(256), 0, st, G64, r, dd, ee, tau, on, nb);

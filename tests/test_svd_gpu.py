@@ -458,3 +458,35 @@ def test_fallback_loops_over_many_flagged(gpu_device, shape, args):
     for b in (0, 1, 299, 511, 512, 599):
         truth = ref.denoiseSignal(A[b].astype(np.float64), *args)
         assert _range_err(out[b], truth, A[b].astype(np.float64)) <= TOL, b
+
+
+@pytest.mark.parametrize("shape,args", [((64, 48), ()), ((128, 128), ()), ((300, 200), (0, 16)),
+                                        ((128, 128), (0, 16))])
+def test_merged_fallback_equals_four_launches(gpu_device, shape, args, kernel_variant):
+    """The flagged-matrix fp64 fallback as one launch (eig_fallback_kernel: Gram tiles,
+    tridiagonalisation, eigenvectors and reconstruction blocks per workgroup, default) and as
+    the four separate launches (EIG_SPLIT=1): the same kernels' arithmetic in the same order,
+    so bitwise equal outputs, on a batch where noise matrices are flagged between gapped ones
+    that are not."""
+    import os
+    import sys
+
+    import torch
+
+    from specenh import svd
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import gapped_matrix
+    rng = np.random.default_rng(23)
+    mats = [gapped_matrix(1500 + i, *shape, dtype=np.float32) if i % 3 else
+            rng.standard_normal(shape).astype(np.float32) for i in range(40)]
+    At = torch.as_tensor(np.stack(mats), device=gpu_device)
+    outs = []
+    for split in (0, 1):
+        kernel_variant("EIG_SPLIT", split)
+        outs.append(svd.denoise_batch(At, *args))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    for b in (0, 1, 3, 39):
+        truth = ref.denoiseSignal(mats[b].astype(np.float64), *args)
+        assert _range_err(outs[0][b].double().cpu().numpy(), truth,
+                          mats[b].astype(np.float64)) <= TOL, b

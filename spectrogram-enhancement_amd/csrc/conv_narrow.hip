@@ -475,6 +475,134 @@ int launch_co1(const NarrowArgs& a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 1 : set_error(SPECENH_EHIP, "conv_co1 launch");
 }
 
+// ---------------------------------------------------------------- CO == 1 on the MFMA
+// conv_co1m_kernel<T, NKS, K>: one output channel from C = 32 NKS input channels (the last
+// Conv2D of the reference's 64/32-channel variants, VAE/manual_scan.py:199,
+// hyperparam_scan.py:161) as D[kx][x'] = sum_(ky, ci) w[ky][kx][ci] in[y + ky - p][x'][ci]
+// on v_mfma_f32_16x16x32 (A = the weights, rows kx < K of 16; B = 16 input positions x'),
+// then out[y][x] = sum_kx D[kx][x + kx - p] through a per-wave LDS scratch. The 16 x 16 tile
+// keeps K of its 16 rows (5 / 16 at K = 5) where a 16-channel output tile keeps 1 / 16, and
+// the K taps of a kernel row cost one MFMA per 32 channels. A wave owns 16 output columns x R
+// output rows: each input row's B fragments (two tiles, x' = x0 - 8 .. x0 + 23) are loaded
+// once and feed the K output rows that use it.
+#ifndef SPECENH_CO1M_R
+#define SPECENH_CO1M_R 8
+#endif
+typedef _Float16 f16x8m __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8m __attribute__((ext_vector_type(8)));
+typedef float f32x4m __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ __forceinline__ f32x4m mfma16(const uint4& a, const uint4& b, f32x4m acc) {
+  if constexpr (__is_same(T, _Float16))
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8m, a),
+                                                  __builtin_bit_cast(f16x8m, b), acc, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8m, a),
+                                                   __builtin_bit_cast(bf16x8m, b), acc, 0, 0, 0);
+}
+
+template <typename T, int NKS, int K>
+__global__ __launch_bounds__(256) void conv_co1m_kernel(NarrowArgs a) {
+  constexpr int C = 32 * NKS, R = SPECENH_CO1M_R, P = K / 2, NIR = R + K - 1;
+  __shared__ __attribute__((aligned(16))) float scr[4][32][16];  // per wave: [x' - x0 + 8][kx]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int m = lane & 15, kg = lane >> 4;
+  const int nstrip = (a.OW + 15) / 16, ngrp = (nstrip + 3) / 4, nband = (a.OH + R - 1) / R;
+  int bid = blockIdx.x;
+  const int grp = bid % ngrp;
+  bid /= ngrp;
+  const int band = bid % nband, n = bid / nband;
+  const int strip = grp * 4 + wv;
+  if (strip >= nstrip) return;  // (whole wave: no barriers below)
+  const int x0 = 16 * strip, y0 = band * R;
+  const T* __restrict__ in = reinterpret_cast<const T*>(a.in) + (long long)n * a.IH * a.IW * C;
+  // weights: A fragment of (ky, k-step): row kx = m (< K), channels 32 ks + 8 kg .. + 7
+  uint4 wf[K][NKS];
+  {
+    const T* __restrict__ W = reinterpret_cast<const T*>(a.w);  // [1][K][K][C]
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+        wf[ky][ks] = m < K ? *reinterpret_cast<const uint4*>(W + ((ky * K + m) * C) + 32 * ks + 8 * kg)
+                           : uint4{0u, 0u, 0u, 0u};
+  }
+  f32x4m acc[R][2];
+#pragma unroll
+  for (int o = 0; o < R; ++o) acc[o][0] = acc[o][1] = f32x4m{0.f, 0.f, 0.f, 0.f};
+  // B fragments of input row iy: tile t, position x' = x0 - 8 + 16 t + m, channels of k-step
+  auto load_row = [&](int iy, uint4 (&b)[2][NKS]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int xp = x0 - 8 + 16 * t + m;
+      const bool ok = (unsigned)iy < (unsigned)a.IH && (unsigned)xp < (unsigned)a.IW;
+      const T* src = in + ((long long)(ok ? iy : 0) * a.IW + (ok ? xp : 0)) * C + 8 * kg;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const uint4 v = *reinterpret_cast<const uint4*>(src + 32 * ks);
+        b[t][ks] = ok ? v : uint4{0u, 0u, 0u, 0u};
+      }
+    }
+  };
+  uint4 bc[2][NKS], bn[2][NKS];
+  load_row(y0 - P, bc);
+#pragma unroll
+  for (int ir = 0; ir < NIR; ++ir) {
+    if (ir + 1 < NIR) load_row(y0 - P + ir + 1, bn);  // next row's loads behind these MFMAs
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+      const int o = ir - ky;  // output row y0 + o reads input row y0 + o + ky - P
+      if (o < 0 || o >= R) continue;  // compile-time
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) acc[o][t] = mfma16<T>(wf[ky][ks], bc[t][ks], acc[o][t]);
+    }
+    if (ir + 1 < NIR) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) bc[t][ks] = bn[t][ks];
+    }
+  }
+  // out[y][x0 + j] = sum_kx D[kx][x0 + j + kx - P]: lane (x' = m, rows kx = 4 kg + i) writes its
+  // four D values of each tile as one 16-byte run of scr[x'][kx]; lanes 0-15 sum the diagonal
+  const float bb = a.bias ? a.bias[0] : 0.f;
+  float (*sw)[16] = scr[wv];
+#pragma unroll
+  for (int o = 0; o < R; ++o) {
+    const int oy = y0 + o;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      *reinterpret_cast<float4*>(&sw[16 * t + m][4 * kg]) =
+          float4{acc[o][t][0], acc[o][t][1], acc[o][t][2], acc[o][t][3]};
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (LDS is in order per wave; this
+                                                          // also keeps the compiler's order)
+    float v = bb;
+#pragma unroll
+    for (int kx = 0; kx < K; ++kx) v += sw[m + kx - P + 8][kx];
+    const int ox = x0 + m;
+    if (lane < 16 && oy < a.OH && ox < a.OW) {
+      const long long oi = ((long long)n * a.OH + oy) * a.OW + ox;
+      if (a.logits) a.logits[oi] = v;
+      const float r = act_f(v, a.act);
+      if (a.out_f32) reinterpret_cast<float*>(a.out)[oi] = r;
+      else reinterpret_cast<T*>(a.out)[oi] = (T)r;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads before the next row's writes
+  }
+}
+
+template <typename T, int NKS, int K>
+int launch_co1m(const NarrowArgs& a, hipStream_t st) {
+  constexpr int R = SPECENH_CO1M_R;
+  const long long nstrip = (a.OW + 15) / 16, ngrp = (nstrip + 3) / 4;
+  const long long blocks = (long long)a.N * ((a.OH + R - 1) / R) * ngrp;
+  if (blocks > 0x7fffffffLL) return 0;
+  SPECENH_LAUNCH((conv_co1m_kernel<T, NKS, K>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? 1 : set_error(SPECENH_EHIP, "conv_co1m launch");
+}
+
 template <typename T, int K>
 int launch_c1(const NarrowArgs& a, bool pool, hipStream_t st) {
   const long long tiles = (long long)a.N * ((a.OH + C1_TILE - 1) / C1_TILE) *
@@ -498,6 +626,26 @@ int dispatch(const NarrowArgs& a, int K, bool pool, hipStream_t st) {
     }
   }
   if (a.CO == 1 && !pool) {
+    // C = 64, or 32 at K >= 5, "same" padding: the MFMA kernel (CO1_VALU=1 keeps
+    // conv_co1_kernel for 32). Per 512 x 256 x 128 launch: C 64 / K 5 1.85 ms (16-channel
+    // MFMA patch tile) -> 0.84, C 32 / K 7 1.15 (VALU) -> 0.57, C 32 / K 5 -> 0.39; C 32 / K 3
+    // stays on the VALU kernel (0.30 vs 0.35 ms).
+    const bool same = a.pad_t == K / 2 && a.pad_l == K / 2 && a.OH == a.IH && a.OW == a.IW;
+    if (same && (a.C == 64 || (a.C == 32 && K >= 5 && variant(V_CO1_VALU) == 0))) {
+      if (a.C == 64) {
+        switch (K) {
+          case 3: return launch_co1m<T, 2, 3>(a, st);
+          case 5: return launch_co1m<T, 2, 5>(a, st);
+          case 7: return launch_co1m<T, 2, 7>(a, st);
+          default: return 0;
+        }
+      }
+      switch (K) {
+        case 5: return launch_co1m<T, 1, 5>(a, st);
+        case 7: return launch_co1m<T, 1, 7>(a, st);
+        default: return 0;
+      }
+    }
     if (a.C == 16) {
       switch (K) {
         case 3: return launch_co1<T, 16, 3>(a, st);
@@ -520,7 +668,7 @@ int dispatch(const NarrowArgs& a, int K, bool pool, hipStream_t st) {
 
 }  // namespace
 
-// Narrow-channel direct convolution (C == 1, or CO == 1 with C in {16, 32}), bf16/f16,
+// Narrow-channel direct convolution (C == 1, or CO == 1 with C in {16, 32, 64}), bf16/f16,
 // stride 1, undilated, square odd kernel <= 7 (a ReLU mask only for C == 1 without pooling
 // or fp32 output). Returns 1 when launched, 0
 // when the shape is not covered (the caller takes the MFMA path), < 0 on error.

@@ -28,7 +28,7 @@ constexpr VariantName kVariants[V_COUNT] = {
     {"ENCODER_UNFUSED", 0},  {"STFT_NO_HOLD", 0},    {"D3_MAP", 0},
     {"ENC2_WPE2", 0},        {"CONVT_SHARED_RING", 0}, {"SVD_RECON_VALU", 0},
     {"ROWS_SHORT_LEAD", 0},  {"SVD_GRAM_F32", 0},
-    {"SVD_RECON_BLOCKS", 0}, {"CONVT_PG", 0}, {"SVD_GZ_ROWS", 0}, {"EIG_SPLIT", 0},
+    {"SVD_RECON_BLOCKS", 0}, {"CONVT_PG", 0}, {"SVD_GZ_ROWS", 0}, {"EIG_SPLIT", 0}, {"CO1_VALU", 0},
 };
 
 std::atomic<int> g_variant[V_COUNT];

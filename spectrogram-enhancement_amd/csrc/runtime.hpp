@@ -42,6 +42,7 @@ enum Variant : int {
   V_CONVT_PG,         // convT1 row sweep: phases split over 8 waves (round 5 trial, slower) instead of 4 x 50 taps
   V_SVD_GZ_ROWS,      // subspace G Z one row per thread (round 4) instead of four
   V_EIG_SPLIT,        // flagged-matrix fp64 fallback as four launches instead of one
+  V_CO1_VALU,         // one-output-channel conv on 32 channels: VALU dot2 kernel instead of MFMA
   V_COUNT
 };
 

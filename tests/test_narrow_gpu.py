@@ -82,6 +82,47 @@ def test_co1_bands(gpu_device, dtype, C, N, H, W):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("C,k", [(64, 5), (64, 3), (64, 7), (32, 5), (32, 7)])
+@pytest.mark.parametrize("N,H,W", [(4, 256, 128), (3, 37, 70), (2, 9, 17), (1, 1, 5)])
+@pytest.mark.parametrize("out", ["f32", "lowp_sigmoid", "logits"])
+def test_co1_mfma(gpu_device, kernel_variant, dtype, C, k, N, H, W, out):
+    """conv_co1m_kernel (one output channel from 32 / 64 channels on the MFMA, the last
+    Conv2D of manual_scan.py / hyperparam_scan.py): against float64 at ragged widths and
+    heights (partial 16-column strips, partial 8-row bands), fp32 or 16-bit sigmoid output,
+    and the fp32 logits of a training forward; for C = 32 also against the VALU kernel
+    (CO1_VALU=1)."""
+    rng = np.random.default_rng(C * 7 + k + N + H + W)
+    x = torch.tensor(rng.standard_normal((N, H, W, C)), dtype=dtype, device=gpu_device)
+    w = torch.tensor(rng.standard_normal((1, k, k, C)) * 0.1, dtype=dtype, device=gpu_device)
+    bias = torch.tensor([0.25], dtype=torch.float32, device=gpu_device)
+    ref, mag = _ref(x, w, bias, k)
+    tol = 1e-5 * (mag + 0.25) + 1e-30
+    act = 2 if out == "lowp_sigmoid" else 0  # SPECENH_ACT_SIGMOID
+    odt = dtype if out == "lowp_sigmoid" else torch.float32
+
+    def run():
+        y = torch.empty((N, H, W, 1), dtype=odt, device=gpu_device)
+        z = torch.full((N, H, W, 1), float("nan"), dtype=torch.float32, device=gpu_device) \
+            if out == "logits" else None
+        torch.ops.specenh.conv2d_out(x, w, bias, k, k, 1, 1, k // 2, k // 2, 1, H, W, act, None,
+                                     z, y, False, None)
+        return y, z
+
+    y, z = run()
+    if out == "lowp_sigmoid":
+        want = torch.sigmoid(ref)
+        assert torch.all((y.double().cpu() - want).abs() <= 2 ** -8 * want.abs() + tol)
+    else:
+        assert torch.all((y.double().cpu() - ref).abs() <= tol)
+    if out == "logits":
+        assert torch.all((z.double().cpu() - ref).abs() <= tol)
+    if C == 32:
+        kernel_variant("CO1_VALU", 1)
+        y2, _ = run()
+        assert torch.all((y2.double().cpu() - y.double().cpu()).abs() <= 2 * tol + (2 ** -8 if out == "lowp_sigmoid" else 0))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("C", [16, 8, 3])
 @pytest.mark.parametrize("masked", [False, True])
 def test_maxpool2_bwd_routes_to_argmax(gpu_device, dtype, C, masked):

@@ -508,8 +508,9 @@ void conv_patch_kernel(ConvArgs a) {
   // (CC = 64: 52 KB -> 3 workgroups per CU instead of 2)
   extern __shared__ __attribute__((aligned(16))) unsigned char sP_raw[];
   T* const sP = reinterpret_cast<T*>(sP_raw);
-  __shared__ int sTap[MAXPH][32];  // patch offset of tap t (elements), -1 past the last tap
-  __shared__ int sCol[MAXPH][32];  // weight column of tap t at ci = 0
+  constexpr int MAXTAP = 64;         // taps per phase (k <= 7: 49)
+  __shared__ int sTap[MAXPH][MAXTAP];  // patch offset of tap t (elements), -1 past the last tap
+  __shared__ int sCol[MAXPH][MAXTAP];  // weight column of tap t at ci = 0
 
   // the per-tile program; K5 workgroups run it persistently over tiles blockIdx.x,
   // + gridDim.x, ... with the weight rows staged once (first)
@@ -546,8 +547,8 @@ void conv_patch_kernel(ConvArgs a) {
   const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
   const T* __restrict__ W = reinterpret_cast<const T*>(a.w);
 
-  if (tid < 32 * (ph_hi - ph_lo)) {
-    const int p = ph_lo + (tid >> 5), t = tid & 31;
+  for (int e = tid; e < MAXTAP * (ph_hi - ph_lo); e += 256) {
+    const int p = ph_lo + e / MAXTAP, t = e % MAXTAP;
     const Geo& g = a.g[p];
     const int jy = t / g.KW, jx = t - (t / g.KW) * g.KW;
     const int dy = upt - g.pad_t, dx = upl - g.pad_l;  // this phase's shift in the patch
@@ -2458,13 +2459,19 @@ int patch_cc(const ConvArgs& a, int nph) {
   if (nph != 1 && nph != 4) return 0;
   for (int i = 0; i < nph; ++i) {
     const Geo& g = a.g[i];
-    if (g.stride != 1 || g.KH > 5 || g.KW > 5 || g.KH * g.KW > 32) return 0;
+    // (k <= 7: the 7 x 7 convs of hyperparam_scan.py:153-161 take the patch kernel too, a 22 x 22
+    // patch; round 4 stopped at 5 x 5 and sent them to the gather kernel, 2.5 ms per 512)
+    if (g.stride != 1 || g.KH > 7 || g.KW > 7 || g.KH * g.KW > 64) return 0;
   }
   const int C = a.g[0].C;
   if (C % 64 == 0) return 64;
   if (C % 32 == 0) return 32;
   if (C == 16) return 16;
-  if (C == 1) return 1;
+  if (C == 1) {  // one MFMA k-step holds all taps: at most 32 (k <= 5)
+    for (int i = 0; i < nph; ++i)
+      if (a.g[i].KH > 5 || a.g[i].KW > 5 || a.g[i].KH * a.g[i].KW > 32) return 0;
+    return 1;
+  }
   return 0;
 }
 

@@ -564,17 +564,23 @@ def test_reference_variants(gpu_device, name, dtype):
 
 
 @pytest.mark.parametrize("dtype", ["mixed_bfloat16", "float16"])
-def test_fused_conv_pool_is_bitwise_identical_to_unfused(gpu_device, dtype):
+@pytest.mark.parametrize("model", ["3layer", "2layer_32_k7"])
+def test_fused_conv_pool_is_bitwise_identical_to_unfused(gpu_device, dtype, model):
     """Conv2D + MaxPooling2D in one launch (pool taken in the conv's registers) gives the
-    same forward output and the same gradients as the two launches."""
-    ops = ref_model_ops()
-    fused, _ = make(ops, (64, 64, 1), dtype=dtype, seed=41)
-    plain, _ = make(ops, (64, 64, 1), dtype=dtype, seed=41)
-    assert fused.fused == {0, 2, 4}
+    same forward output and the same gradients as the two launches; 2layer_32_k7: the 7 x 7
+    convolution on the patch kernel (round 5; k <= 5 before), fused with its pool."""
+    if model == "3layer":
+        ops, hwc, want = ref_model_ops(), (64, 64, 1), {0, 2, 4}
+    else:
+        ops, _ = variant_ops(model)
+        hwc, want = (64, 48, 1), {2}
+    fused, _ = make(ops, hwc, dtype=dtype, seed=41)
+    plain, _ = make(ops, hwc, dtype=dtype, seed=41)
+    assert fused.fused == want
     plain.fused = set()
     rng = np.random.default_rng(11)
-    x = rng.uniform(0, 1, (6, 64, 64, 1)).astype(np.float32)
-    y = rng.uniform(0, 1, (6, 64, 64, 1)).astype(np.float32)
+    x = rng.uniform(0, 1, (6,) + hwc).astype(np.float32)
+    y = rng.uniform(0, 1, (6,) + hwc).astype(np.float32)
     outs, grads = [], []
     for eng in (fused, plain):
         outs.append(eng.forward(upload(eng, x)).clone())

@@ -146,8 +146,7 @@ class AutoencoderEngine:
         # (not when the pool is the model's output: that buffer is fp32 for inference)
         self.fused = {i for i, op in enumerate(self.ops[:-2])
                       if self.dt != F32 and isinstance(op, ConvOp) and op.kind == "conv"
-                      and isinstance(self.ops[i + 1], PoolOp)
-                      and (op.k <= 5 or (op.k <= 7 and op.cin != 1))
+                      and isinstance(self.ops[i + 1], PoolOp) and op.k <= 7
                       and (op.cin in (1, 16) or op.cin % 32 == 0)}
         # inference: the last Conv2DTranspose(relu) + Conv2D(1, sigmoid) as one launch
         # (csrc/decoder_tail.hip); its 16-channel map never reaches HBM

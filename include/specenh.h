@@ -63,6 +63,13 @@ long long specenh_launch_count(void);
  * specenh_launch_count) while it is among the thread's last 256 launches, else "". */
 const char* specenh_kernel_name_at(long long index);
 
+/* Make stream `waiter` wait for the work enqueued on stream `signaler` so far (both
+ * hipStream_t of the current device; no reference counterpart: the AE backward's fork and
+ * join of its weight-gradient stream). The event is recorded without the system-scope fence
+ * (hipEventDisableSystemFence) when `device_scope` is nonzero: both streams are on one
+ * device. Events come from a per-device ring (hipEventDisableTiming). */
+int specenh_stream_wait(void* waiter, void* signaler, int device_scope);
+
 /* Number of frames T = (length - nperseg) / (nperseg - noverlap) + 1 that
  * scipy.signal.spectrogram produces (no boundary padding), or a negative error. */
 long long specenh_stft_frames(long long length, int nperseg, int noverlap);
@@ -271,6 +278,17 @@ int specenh_convt_conv_out(int dtype, const void* x, int N, int H, int W, int C,
                            const void* wt_gemm, const float* bt, int CO, int kt,
                            const void* wo_gemm, const float* bo, int ko, float* out,
                            void* stream);
+
+/* Training form of specenh_convt_conv_out (Model.fit's forward through the same two layers,
+ * manual_scan_3layers.py:197-199, :213): the row-sweep launch also stores the ReLU'd CO-channel
+ * map (dtype [N][2H][2W][CO], rounded exactly as the unfused Conv2DTranspose stores it: the
+ * backward's ReLU mask and weight-gradient input), the fp32 logits [N][2H][2W] (the BCE input)
+ * and the sigmoid output in dtype [N][2H][2W]. W = 64 only (the reference model at 128 x 128),
+ * else SPECENH_EUNSUPPORTED (use the two specenh_conv2d launches). */
+int specenh_convt_conv_out_train(int dtype, const void* x, int N, int H, int W, int C,
+                                 const void* wt_gemm, const float* bt, int CO, int kt,
+                                 const void* wo_gemm, const float* bo, int ko, void* map,
+                                 float* logits, void* out, void* stream);
 
 /* The decoder's last THREE layers in one launch (VAE/manual_scan_3layers.py:196-199, the
  * inference path of predict :239):

@@ -328,7 +328,7 @@ int launch_conv_c1_mfma(int dtype, const void* in, int N, int IH, int IW, int C,
   if (KH != KW || KH > 8 || out_f32 || logits) return 0;
   // the masked full-resolution store (the C4 input gradient of the last conv) is faster on
   // the VALU kernel (tools/c1_bench.py: 630 vs 834 us per 2048 shots, fp16)
-  if (mask) return 0;
+  if (mask && variant(V_C1_MASK_MFMA) == 0) return 0;
   if (pool && ((OH & 1) || (OW & 1))) return 0;
   if ((IW & 1) || ((uintptr_t)in & 3)) return 0;  // staged as 32-bit words
   if ((long long)((OH + TILE - 1) / TILE) * ((OW + TILE - 1) / TILE) >= (1LL << 24) ||

@@ -393,7 +393,10 @@ struct RowsArgs {
   const float* bt;  // [CO]
   const void* wo;   // conv_out GEMM weights [KO][KO][CO]
   const float* bo;  // [1]
-  float* out;       // [N][2H][128]
+  float* out;       // [N][2H][128] (inference: sigmoid)
+  void* map;        // TRAIN: the ReLU'd map [N][2H][128][CO] (T)
+  float* logits;    // TRAIN: pre-sigmoid [N][2H][128]
+  void* out_t;      // TRAIN: sigmoid [N][2H][128] (T)
   int N, H, R, nb;  // R: output rows per band (even), nb: bands per image
 };
 
@@ -426,6 +429,7 @@ struct TailWave {
   float bo;
   uint4 wo[3];   // Conv2D(1) B fragments per map-row pair p: k = (dr, ci), n = 5 r + kx
   int mw[2];     // map write offset (elements, in a row) of this lane's pixel, px = 0, 1
+  int gw[2];     // the same in a plain [128][CO] HBM row (training: the stored map)
   int mrd[2];    // map read offset of this lane's A row (pair row dr = kg >> 1), block 0, 1
   int scw[2];    // scratch write offset, block 0, 1
   int scr;       // scratch read offset of this lane's output (r, x), kx = 0
@@ -461,6 +465,7 @@ struct TailWave {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       mw[i] = map_off(2 * (16 * w + m) + i, kg);
+      gw[i] = (2 * (16 * w + m) + i) * CO + 4 * kg;
       mrd[i] = (kg >> 1) * MROW + map_off(32 * w + 16 * i + m, 2 * (kg & 1));
       scw[i] = min(m, SCR - 1) * SCW + 4 + 32 * w + 16 * i + 4 * kg;
     }
@@ -470,10 +475,11 @@ struct TailWave {
 
   // Conv2DTranspose of one position row. xin: this lane's B-fragment address of input
   // row q - 1 (pixel 16 w + m - 1, group kg); xrow: elements between ring rows q+dy; xo(dx):
-  // offset of the dx-shifted pixel; -> map rows at mrow0 / mrow1 (rows 2q, 2q + 1).
-  template <typename RowOff, typename Xo>
+  // offset of the dx-shifted pixel; -> map rows at mrow0 / mrow1 (rows 2q, 2q + 1), and with
+  // GST to the HBM rows g01 / g01 + 128 CO (training; null: a row outside the band).
+  template <bool GST = false, typename RowOff, typename Xo>
   __device__ __forceinline__ void convt(const T* xin, RowOff xrow, Xo xo, T* mrow0,
-                                        T* mrow1) const {
+                                        T* mrow1, T* __restrict__ g01 = nullptr) const {
     f32x4 acc[4] = {bias, bias, bias, bias};
     int u0[4] = {0, 4, 10, 16};  // first tap register of each phase (4 / 6 / 6 / 9 taps)
 #pragma unroll
@@ -489,8 +495,12 @@ struct TailWave {
         }
       }
 #pragma unroll
-    for (int ph = 0; ph < 4; ++ph)
-      *reinterpret_cast<uint2*>(((ph >> 1) ? mrow1 : mrow0) + mw[ph & 1]) = relu_pack<T>(acc[ph]);
+    for (int ph = 0; ph < 4; ++ph) {
+      const uint2 v = relu_pack<T>(acc[ph]);
+      *reinterpret_cast<uint2*>(((ph >> 1) ? mrow1 : mrow0) + mw[ph & 1]) = v;
+      if constexpr (GST)
+        if (g01) *reinterpret_cast<uint2*>(g01 + (ph >> 1) * (rows::MW * CO) + gw[ph & 1]) = v;
+    }
   }
 
   __device__ __forceinline__ void zero_rows(T* mrow0, T* mrow1) const {
@@ -526,6 +536,17 @@ struct TailWave {
     for (int kx = 0; kx < KO; ++kx) s += scb[scr + kx * rows::SCW + kx];
     O[(long long)(y0 + (lane >> 5)) * rows::MW + ox] = __builtin_amdgcn_rcpf(1.f + __expf(-s));
   }
+
+  // training: the same sums -> fp32 logits and the sigmoid in T
+  __device__ __forceinline__ void conv_out_sums_train(const float* scb, float* __restrict__ L,
+                                                      T* __restrict__ Ot, int y0, int lane) const {
+    float s = bo;
+#pragma unroll
+    for (int kx = 0; kx < KO; ++kx) s += scb[scr + kx * rows::SCW + kx];
+    const long long o = (long long)(y0 + (lane >> 5)) * rows::MW + ox;
+    L[o] = s;
+    Ot[o] = (T)__builtin_amdgcn_rcpf(1.f + __expf(-s));
+  }
 };
 
 template <int I>
@@ -544,7 +565,7 @@ __device__ __forceinline__ float dpp_shift(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false));
 }
 
-template <typename T>
+template <typename T, bool TRAIN>
 __global__ __launch_bounds__(256, 2) void tail_rows_kernel(RowsArgs a) {
   using namespace rows;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -560,7 +581,10 @@ __global__ __launch_bounds__(256, 2) void tail_rows_kernel(RowsArgs a) {
   const int Y0 = band * a.R, Y1 = min(H2, Y0 + a.R);
   const int qa = max(0, Y0 / 2 - 1), qe = Y1 / 2;  // steps qa .. qe inclusive
   const T* __restrict__ X = reinterpret_cast<const T*>(a.x) + (long long)n * H * QW * CI;
-  float* __restrict__ O = a.out + (long long)n * H2 * MW;
+  float* __restrict__ O = TRAIN ? nullptr : a.out + (long long)n * H2 * MW;
+  float* __restrict__ L = TRAIN ? a.logits + (long long)n * H2 * MW : nullptr;
+  T* __restrict__ Ot = TRAIN ? reinterpret_cast<T*>(a.out_t) + (long long)n * H2 * MW : nullptr;
+  T* __restrict__ G = TRAIN ? reinterpret_cast<T*>(a.map) + (long long)n * H2 * MW * CO : nullptr;
 
   TailWave<T> tw;
   tw.load(a.wt, a.bt, a.wo, a.bo, w, lane);
@@ -593,10 +617,15 @@ __global__ __launch_bounds__(256, 2) void tail_rows_kernel(RowsArgs a) {
     const int q = qa + i;
     T* const m0 = mr + ((2 * I) & 7) * MROW;
     T* const m1 = mr + ((2 * I + 1) & 7) * MROW;
-    if (q < H)
-      tw.convt(xin, [](int dy) { return ((I + 1 + dy) & 3) * XROW; },
-               [](int dx) { return (dx + 1) * XST; }, m0, m1);
-    else  // below the image: the Conv2D(1) zero padding
+    if (q < H) {
+      if constexpr (TRAIN)  // map rows 2q, 2q + 1 to HBM when they are this band's
+        tw.template convt<true>(xin, [](int dy) { return ((I + 1 + dy) & 3) * XROW; },
+                                [](int dx) { return (dx + 1) * XST; }, m0, m1,
+                                2 * q >= Y0 && 2 * q < Y1 ? G + (long long)2 * q * MW * CO : nullptr);
+      else
+        tw.convt(xin, [](int dy) { return ((I + 1 + dy) & 3) * XROW; },
+                 [](int dx) { return (dx + 1) * XST; }, m0, m1);
+    } else  // below the image: the Conv2D(1) zero padding
       tw.zero_rows(m0, m1);
     const bool emit = 2 * q - 2 >= Y0;
     float* const scb = sc + (I & 1) * (SCR * SCW);
@@ -604,7 +633,10 @@ __global__ __launch_bounds__(256, 2) void tail_rows_kernel(RowsArgs a) {
       tw.conv_out_d([&](int j) { return mr + ((2 * I - 4 + j + 8) & 7) * MROW; }, scb, m);
     *reinterpret_cast<uint4*>(xst + ((I + 3) & 3) * XROW) = pre;  // input row q + 2
     lds_barrier();  // lgkmcnt only: the prefetch loads stay in flight across it
-    if (emit) tw.conv_out_sums(scb, O, 2 * q - 2, lane);
+    if (emit) {
+      if constexpr (TRAIN) tw.conv_out_sums_train(scb, L, Ot, 2 * q - 2, lane);
+      else tw.conv_out_sums(scb, O, 2 * q - 2, lane);
+    }
     pre = gload(q + 4);
   };
 
@@ -1173,6 +1205,51 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
 
 using namespace specenh;
 
+namespace {
+// the row sweep over bands of output rows per image: one band (no recomputed halo rows)
+// unless the batch leaves fewer than 2 workgroups per CU
+template <bool TRAIN>
+int launch_tail_rows(int dtype, RowsArgs& r, hipStream_t st) {
+  const int N = r.N, H = r.H;
+  int nb = 1;
+  while (nb < 8 && (long long)N * nb < 2ll * device_cus() && 2 * H / (2 * nb) >= 8) nb *= 2;
+  r.R = ((2 * H + nb - 1) / nb + 1) & ~1;
+  r.nb = (2 * H + r.R - 1) / r.R;
+  const long long grid = (long long)N * r.nb;
+  if (grid >= (1ll << 31)) return set_error(SPECENH_EINVAL, "too many workgroups");
+  if (dtype == SPECENH_DTYPE_F16)
+    SPECENH_LAUNCH((tail_rows_kernel<_Float16, TRAIN>), dim3((unsigned)grid), dim3(256), rows::LDS_BYTES, st, r);
+  else
+    SPECENH_LAUNCH((tail_rows_kernel<__bf16, TRAIN>), dim3((unsigned)grid), dim3(256), rows::LDS_BYTES, st, r);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("tail_rows: ") + hipGetErrorString(e));
+  return SPECENH_OK;
+}
+}  // namespace
+
+extern "C" int specenh_convt_conv_out_train(int dtype, const void* x, int N, int H, int W, int C,
+                                            const void* wt_gemm, const float* bt, int CO_, int kt,
+                                            const void* wo_gemm, const float* bo, int ko,
+                                            void* map, float* logits, void* out, void* stream) {
+  if (N < 0 || H <= 0 || W <= 0) return set_error(SPECENH_EINVAL, "bad input shape");
+  if (dtype != SPECENH_DTYPE_F16 && dtype != SPECENH_DTYPE_BF16)
+    return set_error(SPECENH_EUNSUPPORTED, "fused decoder tail: fp16 / bf16 only");
+  if (C != CI || CO_ != CO || kt != KT || ko != KO || W != rows::QW)
+    return set_error(SPECENH_EUNSUPPORTED,
+                     "fused decoder tail (training): Conv2DTranspose(16, 5) on 64-wide "
+                     "32-channel inputs + Conv2D(1, 5)");
+  if (N == 0) return SPECENH_OK;
+  if (!x || !wt_gemm || !bt || !wo_gemm || !bo || !map || !logits || !out)
+    return set_error(SPECENH_EINVAL, "null pointer");
+  if ((long long)N * H * W * C >= (1ll << 31) || (long long)N * 4 * H * W * CO >= (1ll << 31))
+    return set_error(SPECENH_EINVAL, "tensor too large (2^31 elements)");
+  RowsArgs r{};
+  r.x = x; r.wt = wt_gemm; r.bt = bt; r.wo = wo_gemm; r.bo = bo;
+  r.map = map; r.logits = logits; r.out_t = out;
+  r.N = N; r.H = H;
+  return launch_tail_rows<true>(dtype, r, (hipStream_t)stream);
+}
+
 extern "C" int specenh_convt_conv_out(int dtype, const void* x, int N, int H, int W, int C,
                                       const void* wt_gemm, const float* bt, int CO_, int kt,
                                       const void* wo_gemm, const float* bo, int ko, float* out,
@@ -1192,21 +1269,7 @@ extern "C" int specenh_convt_conv_out(int dtype, const void* x, int N, int H, in
     RowsArgs r{};
     r.x = x; r.wt = wt_gemm; r.bt = bt; r.wo = wo_gemm; r.bo = bo; r.out = out;
     r.N = N; r.H = H;
-    // bands of output rows per image: one band (no recomputed halo rows) unless the batch
-    // leaves fewer than 2 workgroups per CU
-    int nb = 1;
-    while (nb < 8 && (long long)N * nb < 2ll * device_cus() && 2 * H / (2 * nb) >= 8) nb *= 2;
-    r.R = ((2 * H + nb - 1) / nb + 1) & ~1;
-    r.nb = (2 * H + r.R - 1) / r.R;
-    const long long grid = (long long)N * r.nb;
-    if (grid >= (1ll << 31)) return set_error(SPECENH_EINVAL, "too many workgroups");
-    if (dtype == SPECENH_DTYPE_F16)
-      SPECENH_LAUNCH(tail_rows_kernel<_Float16>, dim3((unsigned)grid), dim3(256), rows::LDS_BYTES, st, r);
-    else
-      SPECENH_LAUNCH(tail_rows_kernel<__bf16>, dim3((unsigned)grid), dim3(256), rows::LDS_BYTES, st, r);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("tail_rows: ") + hipGetErrorString(e));
-    return SPECENH_OK;
+    return launch_tail_rows<false>(dtype, r, st);
   }
   if (!x || !wt_gemm || !bt || !wo_gemm || !bo || !out) return set_error(SPECENH_EINVAL, "null pointer");
   if ((long long)N * H * W * C >= (1ll << 31) || (long long)N * 4 * H * W >= (1ll << 31))

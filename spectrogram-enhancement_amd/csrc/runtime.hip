@@ -29,6 +29,7 @@ constexpr VariantName kVariants[V_COUNT] = {
     {"ENC2_WPE2", 0},        {"CONVT_SHARED_RING", 0}, {"SVD_RECON_VALU", 0},
     {"ROWS_SHORT_LEAD", 0},  {"SVD_GRAM_F32", 0},
     {"SVD_RECON_BLOCKS", 0}, {"CONVT_PG", 0}, {"SVD_GZ_ROWS", 0}, {"EIG_SPLIT", 0}, {"CO1_VALU", 0},
+    {"C1_MASK_MFMA", 0},
 };
 
 std::atomic<int> g_variant[V_COUNT];
@@ -105,6 +106,37 @@ const char* specenh_kernel_name_at(long long index) {
   if (index < 0 || index >= g_launches || index < g_launches - kRing) return "";
   const char* n = hipKernelNameRefByPtr(g_ring[index % kRing], nullptr);
   return n ? n : "";
+}
+
+int specenh_stream_wait(void* waiter, void* signaler, int device_scope) {
+  using namespace specenh;
+  constexpr int kEvents = 256;  // ring per device and fence kind: a reused event's earlier
+                                 // waits were enqueued (and bound) long before
+  static std::mutex mu;
+  static hipEvent_t ring[kMaxDevices][2][kEvents] = {};
+  static int next[kMaxDevices][2] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices)
+    return set_error(SPECENH_EHIP, "stream_wait: no current device");
+  const int kind = device_scope ? 1 : 0;
+  hipEvent_t ev;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    hipEvent_t& e = ring[dev][kind][next[dev][kind]];
+    next[dev][kind] = (next[dev][kind] + 1) % kEvents;
+    if (!e) {
+      const unsigned fl = hipEventDisableTiming | (device_scope ? hipEventDisableSystemFence : 0u);
+      if (hipEventCreateWithFlags(&e, fl) != hipSuccess) {
+        e = nullptr;
+        return set_error(SPECENH_EHIP, "stream_wait: hipEventCreateWithFlags");
+      }
+    }
+    ev = e;
+  }
+  if (hipEventRecord(ev, (hipStream_t)signaler) != hipSuccess ||
+      hipStreamWaitEvent((hipStream_t)waiter, ev, 0) != hipSuccess)
+    return set_error(SPECENH_EHIP, "stream_wait: record / wait");
+  return SPECENH_OK;
 }
 
 const char* specenh_last_kernel_name(void) {

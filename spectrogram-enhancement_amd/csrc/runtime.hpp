@@ -43,6 +43,7 @@ enum Variant : int {
   V_SVD_GZ_ROWS,      // subspace G Z one row per thread (round 4) instead of four
   V_EIG_SPLIT,        // flagged-matrix fp64 fallback as four launches instead of one
   V_CO1_VALU,         // one-output-channel conv on 32 channels: VALU dot2 kernel instead of MFMA
+  V_C1_MASK_MFMA,     // masked C = 1 conv (C4 input gradient of the last conv) on MFMA
   V_COUNT
 };
 

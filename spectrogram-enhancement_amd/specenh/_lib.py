@@ -56,6 +56,7 @@ SIGNATURES = {
     "specenh_last_kernel_name": (_c.c_char_p, []),
     "specenh_launch_count": (_c.c_longlong, []),
     "specenh_kernel_name_at": (_c.c_char_p, [_c.c_longlong]),
+    "specenh_stream_wait": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int]),
     "specenh_stft_frames": (_c.c_longlong, [_c.c_longlong, _c.c_int, _c.c_int]),
     "specenh_stft_plan_create": (_c.c_int, [_c.POINTER(_c.c_void_p), _c.c_int, _c.c_int,
                                             _c.POINTER(_c.c_double), _c.c_double, _c.c_int,
@@ -103,6 +104,11 @@ SIGNATURES = {
                                           _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int,
                                           _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p,
                                           _c.c_void_p]),
+    "specenh_convt_conv_out_train": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int,
+                                                _c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p,
+                                                _c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p,
+                                                _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                                _c.c_void_p]),
     "specenh_decoder3": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
                                     _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p, _c.c_void_p,
                                     _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p,
@@ -230,6 +236,13 @@ class variant:
     def __exit__(self, *exc):
         set_variant(self.name, self.old)
         return False
+
+
+def stream_wait(waiter, signaler, device_scope: bool = True) -> None:
+    """``waiter`` (torch.cuda.Stream) waits for the work enqueued on ``signaler`` so far, through
+    a library event recorded with a device-scope release (specenh_stream_wait)."""
+    check(lib().specenh_stream_wait(waiter.cuda_stream, signaler.cuda_stream,
+                                    1 if device_scope else 0), "stream_wait")
 
 
 def last_kernel_name() -> str:

@@ -159,6 +159,11 @@ class AutoencoderEngine:
                      and tail_supported(self.tdt, last2[0].cin, last2[0].cout, last2[0].k,
                                         last2[1].k)
                      and os.environ.get("SPECENH_NO_TAIL_FUSION", "0") in ("", "0"))
+        # training: the same two layers as one row-sweep launch that also stores the map (the
+        # backward's mask and weight-gradient input), the logits and the output
+        # (decoder_tail.hip tail_rows_kernel<T, true>), at 64-position-wide inputs
+        self.tail_train = (self.tail and self.shapes()[len(self.ops) - 2][1] == 64
+                           and os.environ.get("SPECENH_NO_TAIL_TRAIN", "0") in ("", "0"))
         # inference: the last THREE layers (Conv2DTranspose x2 + Conv2D(1)) as one launch
         # (csrc/decoder_tail.hip decoder3_kernel) when the shapes are the reference model's
         # at 128-wide inputs; both intermediate maps stay in LDS
@@ -188,6 +193,10 @@ class AutoencoderEngine:
         # (SPECENH_WGRAD_SERIAL=1: one stream, the round-4 order)
         self.wgrad_overlap = os.environ.get("SPECENH_WGRAD_SERIAL", "0") in ("", "0")
         self._side = None
+        # fork / join of the weight-gradient stream: "device" (library events with a
+        # device-scope release, the default), "system" (library events, system-scope
+        # fence), "torch" (torch.cuda.Stream.wait_stream)
+        self.fork_mode = os.environ.get("SPECENH_FORK", "device")
         self._bufs = {}
         self.infer_out_dtype = torch.float32  # set_inference_output_dtype
         self._loss = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -421,6 +430,17 @@ class AutoencoderEngine:
                 if kernels is not None:
                     kernels.append(_lib.last_kernel_name())
                 break
+            if self.tail_train and train and i == n_ops - 2:  # fused tail with stores, done
+                o2 = self.ops[i + 1]
+                ops.convt_conv_out_train_out(hin, self._wv[i], self._bv[i], op.cout, op.k,
+                                             self._wv[i + 1], self._bv[i + 1], o2.k, hout,
+                                             b["z"], b["h"][n_ops])
+                if timing is not None:
+                    ev[1].record(torch.cuda.current_stream(self.device))
+                    timing.append(ev)
+                if kernels is not None:
+                    kernels.append(_lib.last_kernel_name())
+                break
             if self.tail and not train and i == n_ops - 2:  # fused decoder tail, then done
                 o2 = self.ops[i + 1]
                 ops.convt_conv_out_out(hin, self._wv[i], self._bv[i], op.cout, op.k,
@@ -498,13 +518,15 @@ class AutoencoderEngine:
         same inputs, bitwise the serial result (tests/test_ae_gpu.py)."""
         N = self._last_train_N
         b = self._buffers(N, True)
-        self.g.zero_()
         main = torch.cuda.current_stream(self.device)
         side = None
         if self.wgrad_overlap:
             if self._side is None:
                 self._side = torch.cuda.Stream(device=self.device)
             side = self._side
+        else:
+            self.g.zero_()
+        zeroed = side is None
         n_ops = len(self.ops)
         for i in range(n_ops - 1, -1, -1):
             op = self.ops[i]
@@ -532,8 +554,11 @@ class AutoencoderEngine:
                 if on_layer_done is not None:
                     on_layer_done(i)
             else:
-                side.wait_stream(main)  # d_out (and the zeroed g) are ready
+                self._wait(side, main)  # d_out is ready
                 with torch.cuda.stream(side):
+                    if not zeroed:  # zeroed off the input-gradient chain
+                        self.g.zero_()
+                        zeroed = True
                     ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[i],
                                          self._gbv[i], b["ws"])
                     if on_layer_done is not None:
@@ -542,8 +567,16 @@ class AutoencoderEngine:
                 continue
             self._conv(i, d_out, b["d"][i], weights=self.w_d[i], geom=op.dgrad_geom(),
                        act=None, mask=relu_mask, bias=False, out_shape=(IH, IW), cout=op.cin)
+        if not zeroed:  # no convolution reported a gradient
+            self.g.zero_()
         if side is not None:
-            main.wait_stream(side)
+            self._wait(main, side)
+
+    def _wait(self, waiter, signaler):
+        if self.fork_mode == "torch":
+            waiter.wait_stream(signaler)
+        else:
+            _lib.stream_wait(waiter, signaler, device_scope=self.fork_mode != "system")
 
     def adam(self, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7, grad_scale=1.0):
         """Keras Adam on the fp32 master weights; the low-precision copy and every layer's

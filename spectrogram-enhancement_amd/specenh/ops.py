@@ -357,6 +357,33 @@ _op("convt_conv_out_out(Tensor x, Tensor wt, Tensor bt, int cout, int kt, Tensor
     "int ko, Tensor(a!) out) -> ()", _tail_out, lambda *a: None)
 
 
+def _tail_train_out(x, wt, bt, cout, kt, wo, bo, ko, map_out, logits, out):
+    _need(x, "x")
+    for t, n in ((map_out, "map_out"), (logits, "logits"), (out, "out")):
+        _need(t, n)
+    N, H, W, C = x.shape
+    if wt.dtype != x.dtype or wo.dtype != x.dtype or wt.numel() != cout * kt * kt * C or \
+            wo.numel() != ko * ko * cout:
+        raise ValueError("wt / wo must be the two layers' GEMM weights in x's dtype")
+    if bt.dtype != torch.float32 or bt.numel() != cout or bo.dtype != torch.float32 or \
+            bo.numel() != 1:
+        raise ValueError("biases must be float32 [CO] and [1]")
+    if tuple(map_out.shape) != (N, 2 * H, 2 * W, cout) or map_out.dtype != x.dtype:
+        raise ValueError("map_out must be [N, 2H, 2W, cout] in x's dtype")
+    if logits.dtype != torch.float32 or logits.numel() != N * 4 * H * W:
+        raise ValueError("logits must be float32 [N, 2H, 2W(, 1)]")
+    if out.dtype != x.dtype or out.numel() != N * 4 * H * W:
+        raise ValueError("out must be [N, 2H, 2W(, 1)] in x's dtype")
+    _lib.check(_lib.lib().specenh_convt_conv_out_train(
+        _code(x), _vp(x), N, H, W, C, _vp(wt), _vp(bt), cout, kt, _vp(wo), _vp(bo), ko,
+        _vp(map_out), _vp(logits), _vp(out), _st(x)), "convt_conv_out_train")
+
+
+_op("convt_conv_out_train_out(Tensor x, Tensor wt, Tensor bt, int cout, int kt, Tensor wo, "
+    "Tensor bo, int ko, Tensor(a!) map_out, Tensor(b!) logits, Tensor(c!) out) -> ()",
+    _tail_train_out, lambda *a: None)
+
+
 def _dec3_out(x, w1, b1, cout1, wt, bt, cout2, wo, bo, k, out):
     _need(x, "x")
     _need(out, "out")

@@ -594,6 +594,59 @@ def test_fused_conv_pool_is_bitwise_identical_to_unfused(gpu_device, dtype, mode
 
 
 @pytest.mark.parametrize("dtype", ["mixed_bfloat16", "float16"])
+@pytest.mark.parametrize("hwc,n", [((128, 128, 1), 6), ((256, 128, 1), 3), ((128, 128, 1), 130)])
+def test_training_tail_matches_two_launches(gpu_device, dtype, hwc, n):
+    """forward(train=True) runs Conv2DTranspose(16) + Conv2D(1) as ONE row-sweep launch that
+    also stores the 16-channel map, the fp32 logits and the sigmoid output (round 5,
+    decoder_tail.hip tail_rows_kernel<T, true>). Against the two launches (conv_patch +
+    conv_co1): the same products in another fp32 order, so the map is equal up to one
+    rounding step of T in a few elements, the logits agree to 1e-3 of their spread, the output
+    is the sigmoid of the logits rounded to T, and the gradients agree to 1e-2 (cosine 0.9999).
+    n = 130: bands of one image on several workgroups AND a partial last wave."""
+    ops = ref_model_ops()
+    fused, _ = make(ops, hwc, dtype=dtype, seed=43)
+    plain, _ = make(ops, hwc, dtype=dtype, seed=43)
+    assert fused.tail_train
+    plain.tail_train = False
+    ws, _, _ = trained_c4(1)
+    set_params(fused, ws)
+    set_params(plain, ws)
+    rng = np.random.default_rng(12)
+    x = rng.uniform(0, 1, (n,) + hwc).astype(np.float32)
+    y = rng.uniform(0, 1, (n,) + hwc).astype(np.float32)
+    res = []
+    for eng in (fused, plain):
+        out = eng.forward(upload(eng, x), train=True)
+        b = eng._buffers(n, True)
+        mp = b["h"][len(ops) - 1].float()
+        z = eng.last_logits().clone()
+        eng.loss_and_grad(upload(eng, y))
+        eng.backward()
+        res.append((mp, z, out.float().clone(), eng.g.clone()))
+    (m0, z0, o0, g0), (m1, z1, o1, g1) = res
+    ulp = 2.0 ** (-7 if dtype == "mixed_bfloat16" else -10)
+    dm = (m0 - m1).abs()
+    assert float((dm > 0).float().mean()) < 0.01
+    # one rounding step of T, or (sums that cancel to near zero, where the fp32 order
+    # matters more than T's step) 1e-4 of the map's range
+    bound = ulp * m1.abs() * 1.01 + 1e-4 * float(m1.abs().max())
+    j = int(torch.argmax(dm - bound))
+    print(f"map max diff {float(dm.max()):.3e} at worst {float(m0.flatten()[j]):.5e} vs "
+          f"{float(m1.flatten()[j]):.5e} (range {float(m1.abs().max()):.3e})")
+    assert bool((dm <= bound).all())
+    spread = float(z1.max() - z1.min())
+    assert spread > 1.0
+    print(f"map diff frac {float((dm > 0).float().mean()):.2e}, logit diff / spread "
+          f"{float((z0 - z1).abs().max()) / spread:.2e}")
+    assert float((z0 - z1).abs().max()) <= 1e-3 * spread
+    sig = torch.sigmoid(z0.double())
+    assert float((o0.double().reshape(sig.shape) - sig).abs().max()) <= 2 * ulp
+    cos = float(torch.dot(g0, g1) / (g0.norm() * g1.norm()))
+    assert cos >= 0.9999
+    assert float((g0 - g1).norm() / g1.norm()) <= 1e-2
+
+
+@pytest.mark.parametrize("dtype", ["mixed_bfloat16", "float16"])
 @pytest.mark.parametrize("hw", [(128, 128), (40, 56), (24, 8)])
 def test_convt_row_phase_pairs_bitwise_identical(gpu_device, dtype, hw, kernel_variant):
     """Conv2DTranspose forward in (tile, row-phase) workgroups with LDS-staged whole-row

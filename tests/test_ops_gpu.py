@@ -68,6 +68,12 @@ def _cases(dev):
         (ops.convt_conv_out, (xt, wt, bc16, 16, 5, wo, bo, 5)),
         (ops.convt_conv_out_out, (xt, wt, bc16, 16, 5, wo, bo, 5,
                                   torch.empty(2, 40, 24, 1, device=dev))),
+        (ops.convt_conv_out_train_out, (r(2, 4, 64, 32, dtype=torch.float16), wt, bc16, 16, 5, wo,
+                                        bo, 5, torch.empty(2, 8, 128, 16, device=dev,
+                                                           dtype=torch.float16),
+                                        torch.empty(2, 8, 128, 1, device=dev),
+                                        torch.empty(2, 8, 128, 1, device=dev,
+                                                    dtype=torch.float16))),
         (ops.decoder3, (x3, w3a, b3a, 32, wt, bc16, 16, wo, bo, 5)),
         (ops.decoder3_out, (x3, w3a, b3a, 32, wt, bc16, 16, wo, bo, 5,
                             torch.empty(2, 12, 128, 1, device=dev))),

@@ -8,7 +8,7 @@ import specenh  # noqa: F401  (registers the operators)
 
 OPS = ["stft_psd", "stft_psd_out", "csd", "svd_denoise", "svd_denoise_out", "svd_denoise_optimal",
        "conv2d", "conv2d_out", "conv2d_wgrad", "conv2d_wgrad_out", "convt_conv_out",
-       "convt_conv_out_out", "decoder3", "decoder3_out", "encoder2", "encoder2_out", "maxpool2",
+       "convt_conv_out_out", "convt_conv_out_train_out", "decoder3", "decoder3_out", "encoder2", "encoder2_out", "maxpool2",
        "maxpool2_out",
        "maxpool2_bwd", "maxpool2_bwd_out", "bce_logits", "bce_logits_out", "adam_step_", "adam_step_flip_",
        "weight_flip_transpose", "weight_flip_transpose_out", "cast", "cast_out", "label_filter",
@@ -20,7 +20,8 @@ CABI = {"specenh_stft_psd": "stft_psd_out", "specenh_stft_psd_f16": "stft_psd_ou
         "specenh_csd": "csd", "specenh_svd_denoise_ex": "svd_denoise_out",
         "specenh_svd_denoise_optimal": "svd_denoise_optimal_out", "specenh_conv2d": "conv2d_out",
         "specenh_conv2d_wgrad": "conv2d_wgrad_out",
-        "specenh_convt_conv_out": "convt_conv_out_out", "specenh_decoder3_ex": "decoder3_out",
+        "specenh_convt_conv_out": "convt_conv_out_out",
+        "specenh_convt_conv_out_train": "convt_conv_out_train_out", "specenh_decoder3_ex": "decoder3_out",
         "specenh_encoder2": "encoder2_out",
         "specenh_maxpool2_fwd": "maxpool2_out",
         "specenh_maxpool2_bwd": "maxpool2_bwd_out", "specenh_bce_logits": "bce_logits_out",
@@ -48,6 +49,7 @@ def test_every_compute_entry_point_has_an_operator():
                  "specenh_conv2d_wgrad_workspace_bytes", "specenh_filter_workspace_bytes",
                  "specenh_u8filter_workspace_bytes", "specenh_set_variant",
                  "specenh_get_variant", "specenh_last_kernel_name", "specenh_launch_count", "specenh_kernel_name_at",
+                 "specenh_stream_wait",
                  "specenh_svd_denoise",  # = specenh_svd_denoise_ex with an fp32 output
                  "specenh_decoder3"}  # = specenh_decoder3_ex with an fp32 output
     compute = [n for n in declared_functions() if n not in host_only]

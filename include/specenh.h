@@ -229,6 +229,18 @@ int specenh_conv2d_wgrad(int dtype, const void* in, int N, int IH, int IW, int C
                          const void* dout, int KH, int KW, int CO, int stride, int pad_t,
                          int pad_l, int in_dil, int OH, int OW, float* dw, float* dbias,
                          void* workspace, void* stream);
+/* specenh_conv2d_wgrad of a convolution followed by ReLU + MaxPooling2D((2,2)), given the
+ * POOL's output gradient dpool [N][OH/2][OW/2][CO] instead of dout: dout is what
+ * specenh_maxpool2_bwd(dpool, argmax, pooled) would write (the gradient routed to the argmax,
+ * zero where pooled <= 0; pooled may be NULL: no ReLU mask), formed while the tiles are staged
+ * (the model's first Conv2D in Model.fit, manual_scan_3layers.py:187-188: no full-resolution
+ * gradient is written). bf16 / f16, C = 1, stride 1, even OH / OW, CO % 8 == 0, else
+ * SPECENH_EUNSUPPORTED. Same workspace and accumulation as specenh_conv2d_wgrad. */
+int specenh_conv2d_wgrad_pooled(int dtype, const void* in, int N, int IH, int IW, int C,
+                                const void* dpool, const unsigned char* argmax, const void* pooled,
+                                int KH, int KW, int CO, int stride, int pad_t, int pad_l,
+                                int in_dil, int OH, int OW, float* dw, float* dbias,
+                                void* workspace, void* stream);
 /* MaxPooling2D((2,2), padding="same") on even H, W: out [N][H/2][W/2][C] + argmax (0..3). */
 int specenh_maxpool2_fwd(int dtype, const void* in, int N, int H, int W, int C, void* out,
                          unsigned char* argmax, void* stream);

@@ -1167,6 +1167,11 @@ struct WgradArgs {
   const void* dout;  // [N][OHs][OWs][CO]
   float* part;       // [Z][CO][Kf]
   float* bpart;      // [nphase][Z][CO] (bias) or null
+  // dOut given as the gradient of the following MaxPooling2D((2,2)) (specenh_conv2d_wgrad_pooled):
+  // dOut[y][x][c] = pd[y/2][x/2][c] where argmax pam == 2 (y&1) + (x&1) and pooled py > 0
+  const void* pd = nullptr;
+  const unsigned char* pam = nullptr;
+  const void* py = nullptr;  // or null: no ReLU mask
 };
 
 // Workgroup: 64 GEMM-K columns (blockIdx.x) x 16*NT channels (blockIdx.y) x one pixel
@@ -1302,6 +1307,9 @@ struct WgradTrArgs {
   float* part;       // [Z][CO][Kf]
   float* bpart;      // [nphase][Z][CO] or null
   int upt, upl, PH, PW;  // phase-shared launches (wgrad_trp_kernel): the union patch
+  const void* pd;        // C1 only: dOut from the pool's gradient (WgradArgs::pd), or null
+  const unsigned char* pam;
+  const void* py;
 };
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -1417,6 +1425,35 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
         const int oy = oyt + (pix >> 4), ox = oxt + (pix & 15);
         const int co = co0 + 8 * v;
         rd[u] = uint4{0u, 0u, 0u, 0u};
+        if constexpr (C1) {
+          if (a.pd) {  // routed from the pool's gradient: argmax select + ReLU mask, 8 channels
+            if (oy < g.OH && ox < g.OW && co < g.CO) {
+              const long long po = (((long long)n * (g.OH >> 1) + (oy >> 1)) * (g.OW >> 1) + (ox >> 1)) * g.CO + co;
+              const uint4 dv = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.pd) + po);
+              const uint2 am = *reinterpret_cast<const uint2*>(a.pam + po);
+              uint4 yv = uint4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};  // > 0
+              if (a.py) yv = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.py) + po);
+              const uint32_t sel = (uint32_t)(((oy & 1) << 1) | (ox & 1));
+              const uint32_t d4[4] = {dv.x, dv.y, dv.z, dv.w}, y4[4] = {yv.x, yv.y, yv.z, yv.w};
+              uint32_t o4[4];
+#pragma unroll
+              for (int h = 0; h < 4; ++h) {
+                const uint32_t amw = h < 2 ? am.x : am.y;
+                uint32_t r = 0u;
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                  const uint32_t y16 = (y4[h] >> (16 * b)) & 0xffffu;  // > 0: sign clear, nonzero
+                  const bool keep = ((amw >> (8 * (2 * (h & 1) + b))) & 0xffu) == sel &&
+                                    !(y16 & 0x8000u) && y16 != 0u;
+                  r |= keep ? (d4[h] & (0xffffu << (16 * b))) : 0u;
+                }
+                o4[h] = r;
+              }
+              rd[u] = uint4{o4[0], o4[1], o4[2], o4[3]};
+            }
+            continue;
+          }
+        }
         if (oy < g.OH && ox < g.OW && co < g.CO)
           rd[u] = *reinterpret_cast<const uint4*>(
               dout + (((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0) * g.CO + co);
@@ -2573,6 +2610,9 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
   a.dout = w.dout;
   a.part = w.part;
   a.bpart = w.bpart;
+  a.pd = w.pd;
+  a.pam = w.pam;
+  a.py = w.py;
   const int nt = std::min(4, (g0.CO + 15) / 16);
   const int ntw = nt >= 2 ? 2 : 1;
   a.ncog = (g0.CO + 16 * ntw - 1) / (16 * ntw);
@@ -2771,6 +2811,46 @@ int specenh_conv2d_wgrad(int dtype, const void* in, int N, int IH, int IW, int C
   if (dtype == SPECENH_DTYPE_F32) return launch_wgrad<float>(a, nph, dw, dbias, st);
   if (dtype == SPECENH_DTYPE_BF16) return launch_wgrad<__bf16>(a, nph, dw, dbias, st);
   return launch_wgrad<_Float16>(a, nph, dw, dbias, st);
+}
+
+int specenh_conv2d_wgrad_pooled(int dtype, const void* in, int N, int IH, int IW, int C,
+                                const void* dpool, const unsigned char* argmax, const void* pooled,
+                                int KH, int KW, int CO, int stride, int pad_t, int pad_l,
+                                int in_dil, int OH, int OW, float* dw, float* dbias,
+                                void* workspace, void* stream) {
+  if (int e = check_sizes(N, IH, IW, C, OH, OW, CO)) return e;
+  if (KH <= 0 || KW <= 0 || stride <= 0 || in_dil <= 0)
+    return set_error(SPECENH_EINVAL, "bad convolution geometry");
+  if (!in || !dpool || !argmax || !dw || !workspace) return set_error(SPECENH_EINVAL, "null pointer");
+  if (dtype != SPECENH_DTYPE_BF16 && dtype != SPECENH_DTYPE_F16)
+    return set_error(SPECENH_EUNSUPPORTED, "pooled wgrad: bf16 / f16");
+  if (C != 1 || stride != 1 || in_dil != 1 || (OH & 1) || (OW & 1) || (CO & 7) ||
+      ((uintptr_t)dpool & 15) || ((uintptr_t)argmax & 7) || ((uintptr_t)pooled & 15))
+    return set_error(SPECENH_EUNSUPPORTED,
+                     "pooled wgrad: one input channel, stride 1, even output, CO % 8 == 0");
+  WgradArgs a{};
+  int nph = 0;
+  if (int e = plan_phases(N, IH, IW, C, CO, KH, KW, stride, pad_t, pad_l, in_dil, OH, OW, a.g, &nph))
+    return e;
+  if (nph != 1 || a.g[0].oys != 1 || a.g[0].oxs != 1 || a.g[0].oy0 != 0 || a.g[0].ox0 != 0 ||
+      a.g[0].CO != CO || a.g[0].OHs != OH || a.g[0].OWs != OW)
+    return set_error(SPECENH_EUNSUPPORTED, "pooled wgrad: a plain stride-1 convolution");
+  const WgradPlan p = wgrad_plan(KH * KW * C, CO);
+  a.in = in;
+  a.dout = nullptr;
+  a.pd = dpool;
+  a.pam = argmax;
+  a.py = pooled;
+  a.part = (float*)workspace;
+  const size_t Zws = std::max<size_t>(p.Z, wgrad_tr_zmax(CO, (long long)KH * KW * C));
+  a.bpart = dbias ? a.part + Zws * CO * KH * KW * C : nullptr;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == SPECENH_DTYPE_BF16) {
+    if (!wgrad_tr_applies<__bf16>(a, nph)) return set_error(SPECENH_EUNSUPPORTED, "pooled wgrad: shape");
+    return launch_wgrad_tr<__bf16>(a, nph, dw, dbias, st);
+  }
+  if (!wgrad_tr_applies<_Float16>(a, nph)) return set_error(SPECENH_EUNSUPPORTED, "pooled wgrad: shape");
+  return launch_wgrad_tr<_Float16>(a, nph, dw, dbias, st);
 }
 
 int specenh_maxpool2_fwd(int dtype, const void* in, int N, int H, int W, int C, void* out,

@@ -188,6 +188,16 @@ class AutoencoderEngine:
                          and encoder2_supported(self.tdt, o1.cin, o1.cout, o2.cout, o1.k,
                                                 self.input_shape[0], self.input_shape[1])
                          and _lib.get_variant("ENCODER_UNFUSED") == 0)
+        # training: the first Conv2D's weight gradient straight from its pool's gradient
+        # (specenh_conv2d_wgrad_pooled: no full-resolution pool-backward output)
+        c0 = self.ops[0] if self.ops else None
+        self.wgrad_pooled = (self.dt != F32 and isinstance(c0, ConvOp) and c0.kind == "conv"
+                             and c0.cin == 1 and c0.cout % 8 == 0 and c0.stride == 1
+                             and c0.k <= 5 and c0.act in (None, "linear", "relu")
+                             and len(self.ops) > 1
+                             and isinstance(self.ops[1], PoolOp)
+                             and self.input_shape[0] % 2 == 0 and self.input_shape[1] % 2 == 0
+                             and os.environ.get("SPECENH_NO_WGRAD_POOLED", "0") in ("", "0"))
         self.t = 0  # Adam iterations
         # backward: weight gradients on a second stream, off the input-gradient chain
         # (SPECENH_WGRAD_SERIAL=1: one stream, the round-4 order)
@@ -293,6 +303,16 @@ class AutoencoderEngine:
                     ws = max(ws, int(self.L.specenh_conv2d_wgrad_workspace_bytes(
                         N, OH, OW, op.k, op.k, op.cin, op.cout)))
             b["ws"] = torch.empty(ws, dtype=torch.uint8, device=dev)
+            # the first convolution's weight gradient runs on the current stream beside the
+            # second stream's last ones (backward): a workspace of its own
+            first = next((i for i, op in enumerate(self.ops) if isinstance(op, ConvOp)), None)
+            ws0 = 16
+            if first is not None:
+                op = self.ops[first]
+                OH, OW, _ = shp[first + 1]
+                ws0 = max(ws0, int(self.L.specenh_conv2d_wgrad_workspace_bytes(
+                    N, OH, OW, op.k, op.k, op.cin, op.cout)))
+            b["ws0"] = torch.empty(ws0, dtype=torch.uint8, device=dev)
         if len(self._bufs) >= 4:  # e.g. full + partial batch for train and inference
             self._bufs.pop(next(iter(self._bufs)))
         self._bufs[key] = b
@@ -528,6 +548,12 @@ class AutoencoderEngine:
             self.g.zero_()
         zeroed = side is None
         n_ops = len(self.ops)
+        first = next((i for i, op in enumerate(self.ops) if isinstance(op, ConvOp)), -1)
+        # the first convolution's gradient slice g[:g0_end] (the layers' slices follow the op
+        # order; zero unless a second convolution exists: then the whole buffer is one slice)
+        second = next((i for i, op in enumerate(self.ops) if isinstance(op, ConvOp) and i > first),
+                      None)
+        g0_end = self.ops[second].off_w if second is not None else 0
         for i in range(n_ops - 1, -1, -1):
             op = self.ops[i]
             d_out = b["d"][i + 1]
@@ -536,8 +562,8 @@ class AutoencoderEngine:
             prev_relu = isinstance(prev, ConvOp) and prev.act == "relu"
             relu_mask = hin if prev_relu else None
             if isinstance(op, PoolOp):
-                if i == 0:
-                    continue  # nothing upstream needs the gradient
+                if i == 0 or (i == 1 and self.wgrad_pooled):
+                    continue  # nothing upstream needs it / conv 0's wgrad reads d[2] directly
                 _, H, W, C = d_out.shape
                 # ReLU mask of the pool's input at its argmax == (pooled output > 0)
                 ops.maxpool2_bwd_out(d_out, b["am"][i], b["h"][i + 1] if prev_relu else None,
@@ -549,18 +575,31 @@ class AutoencoderEngine:
             OH, OW = d_out.shape[1:3]
             s, pt, pl, dil = op.fwd_geom()
             if side is None:
-                ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[i],
-                                     self._gbv[i], b["ws"])
+                if i == 0:
+                    self._wgrad0(b, hin, d_out, op, s, pt, pl, dil, b["ws"])
+                else:
+                    ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[i],
+                                         self._gbv[i], b["ws"])
+                if on_layer_done is not None:
+                    on_layer_done(i)
+            elif i == first and zeroed:
+                # no input gradient follows: the current stream is idle, so this weight
+                # gradient runs there, beside the second stream's remaining ones
+                self.g[:g0_end].zero_()
+                self._wgrad0(b, hin, d_out, op, s, pt, pl, dil, b["ws0"])
                 if on_layer_done is not None:
                     on_layer_done(i)
             else:
                 self._wait(side, main)  # d_out is ready
                 with torch.cuda.stream(side):
-                    if not zeroed:  # zeroed off the input-gradient chain
-                        self.g.zero_()
+                    if not zeroed:  # zeroed off the input-gradient chain (but the first
+                        self.g[g0_end:].zero_()  # layer's slice: its wgrad runs on `main`)
                         zeroed = True
-                    ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[i],
-                                         self._gbv[i], b["ws"])
+                    if i == 0:
+                        self._wgrad0(b, hin, d_out, op, s, pt, pl, dil, b["ws"])
+                    else:
+                        ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil,
+                                             self._gwv[i], self._gbv[i], b["ws"])
                     if on_layer_done is not None:
                         on_layer_done(i)
             if i == 0:
@@ -571,6 +610,17 @@ class AutoencoderEngine:
             self.g.zero_()
         if side is not None:
             self._wait(main, side)
+
+    def _wgrad0(self, b, hin, d_out, op, s, pt, pl, dil, ws):
+        """Weight gradient of op 0: from its pool's gradient d[2] (argmax + ReLU mask of the
+        pooled output) when wgrad_pooled, else from d_out = d[1]."""
+        if self.wgrad_pooled:
+            ops.conv2d_wgrad_pooled_out(hin, b["d"][2], b["am"][1],
+                                        b["h"][2] if op.act == "relu" else None, op.k, op.k, s,
+                                        pt, pl, dil, self._gwv[0], self._gbv[0], ws)
+        else:
+            ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[0],
+                                 self._gbv[0], ws)
 
     def _wait(self, waiter, signaler):
         if self.fork_mode == "torch":

@@ -325,6 +325,37 @@ _op(f"conv2d_wgrad_out(Tensor x, Tensor dout, {_WG_ARGS}, Tensor(a!) dw, Tensor(
     "Tensor(c!) workspace) -> ()", _wgrad_out, lambda *a: None)
 
 
+def _wgrad_pooled_out(x, dpool, argmax, pooled, kh, kw, stride, pad_t, pad_l, in_dil, dw, dbias,
+                      workspace):
+    _need(x, "x")
+    _need(dpool, "dpool")
+    N, IH, IW, C = x.shape
+    _, PH, PW, CO = dpool.shape
+    OH, OW = 2 * PH, 2 * PW
+    if dpool.dtype != x.dtype or dpool.shape[0] != N:
+        raise ValueError("dpool must be [N, OH/2, OW/2, CO] in x's dtype")
+    if argmax.dtype != torch.uint8 or argmax.shape != dpool.shape:
+        raise ValueError("argmax must be uint8 like dpool")
+    if pooled is not None and (pooled.dtype != x.dtype or pooled.shape != dpool.shape):
+        raise ValueError("pooled must be like dpool")
+    if dw.dtype != torch.float32 or dw.numel() != CO * kh * kw * C or not dw.is_contiguous():
+        raise ValueError("dw must be contiguous float32 [CO][KH][KW][C]")
+    if dbias is not None and (dbias.dtype != torch.float32 or dbias.numel() != CO):
+        raise ValueError("dbias must be float32 [CO]")
+    need = int(_lib.lib().specenh_conv2d_wgrad_workspace_bytes(N, OH, OW, kh, kw, C, CO))
+    if workspace.numel() < need:
+        raise ValueError(f"workspace needs {need} bytes")
+    _lib.check(_lib.lib().specenh_conv2d_wgrad_pooled(
+        _code(x), _vp(x), N, IH, IW, C, _vp(dpool), _vp(argmax), _vp(pooled), kh, kw, CO, stride,
+        pad_t, pad_l, in_dil, OH, OW, _vp(dw), _vp(dbias), _vp(workspace), _st(x)),
+        "conv2d_wgrad_pooled")
+
+
+_op(f"conv2d_wgrad_pooled_out(Tensor x, Tensor dpool, Tensor argmax, Tensor? pooled, {_WG_ARGS}, "
+    "Tensor(a!) dw, Tensor(b!)? dbias, Tensor(c!) workspace) -> ()", _wgrad_pooled_out,
+    lambda *a: None)
+
+
 def _tail_out(x, wt, bt, cout, kt, wo, bo, ko, out):
     _need(x, "x")
     _need(out, "out")

@@ -195,6 +195,59 @@ def test_pool_backward_routes_to_argmax_with_relu_mask(gpu_device):
         assert normwise(a, b) <= TOL_GRAD
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("hw,co,k,relu", [((128, 128), 16, 5, True), ((20, 36), 8, 3, True),
+                                          ((34, 18), 24, 5, False)])
+def test_wgrad_pooled_equals_pool_backward_then_wgrad(gpu_device, dtype, hw, co, k, relu):
+    """specenh_conv2d_wgrad_pooled (the first Conv2D's weight gradient formed from its pool's
+    gradient, argmax and ReLU mask while the tiles are staged) is bitwise
+    specenh_maxpool2_bwd + specenh_conv2d_wgrad, incl. ragged tiles and no ReLU mask."""
+    from specenh.ops import ops, wgrad_workspace
+    dev = torch.device(gpu_device)
+    g = torch.Generator(device=dev).manual_seed(5)
+    N, (H, W) = 3, hw
+    x = torch.rand(N, H, W, 1, device=dev, generator=g).to(dtype)
+    conv = (torch.randn(N, H, W, co, device=dev, generator=g)).to(dtype)
+    pooled, am = ops.maxpool2(conv)
+    dpool = torch.randn(N, H // 2, W // 2, co, device=dev, generator=g).to(dtype)
+    ws = wgrad_workspace(x, conv, k, k)
+    p = (k - 1) // 2
+    res = []
+    for fused in (True, False):
+        dw = torch.zeros(co, k, k, 1, device=dev)
+        db = torch.zeros(co, device=dev)
+        if fused:
+            ops.conv2d_wgrad_pooled_out(x, dpool, am, pooled if relu else None, k, k, 1, p, p, 1,
+                                        dw, db, ws)
+        else:
+            d = torch.empty_like(conv)
+            ops.maxpool2_bwd_out(dpool, am, pooled if relu else None, d)
+            ops.conv2d_wgrad_out(x, d, k, k, 1, p, p, 1, dw, db, ws)
+        res.append((dw, db))
+    assert float(res[1][0].abs().max()) > 0
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+def test_engine_wgrad_pooled_is_bitwise(gpu_device):
+    """The engine's first-layer weight gradient through conv2d_wgrad_pooled (default) and
+    through the pool backward + wgrad (wgrad_pooled = False): bitwise equal gradients."""
+    ops_ = ref_model_ops()
+    rng = np.random.default_rng(21)
+    x = rng.uniform(0, 1, (8, 64, 64, 1))
+    y = rng.uniform(0, 1, (8, 64, 64, 1))
+    grads = []
+    for pooled in (True, False):
+        eng, _ = make(ops_, (64, 64, 1), dtype="mixed_bfloat16", seed=23)
+        assert eng.wgrad_pooled
+        eng.wgrad_pooled = pooled
+        eng.forward(upload(eng, x), train=True)
+        eng.loss_and_grad(upload(eng, y))
+        eng.backward()
+        grads.append(eng.g.clone())
+    assert float(grads[0].abs().max()) > 0
+    assert torch.equal(grads[0], grads[1])
+
+
 # ----------------------------------------------------------------------------- full model
 def test_reference_model_forward_fp32(gpu_device):
     ops = ref_model_ops()

@@ -30,6 +30,9 @@ def _cases(dev):
     w, gr, m, v = r(1000, lo=-1), r(1000, lo=-1), r(1000, lo=-1), r(1000)
     F64 = r(2, 32, 40, dtype=torch.float64)
     xt = r(2, 20, 12, 32, dtype=torch.float16)
+    xb1 = r(2, 8, 8, 1, dtype=torch.bfloat16)
+    pooled_b, am_b = r(2, 4, 4, 8, dtype=torch.bfloat16), torch.zeros(2, 4, 4, 8, dtype=torch.uint8,
+                                                                     device=dev)
     wt, bc16 = r(16 * 25 * 32, dtype=torch.float16, lo=-0.1, hi=0.1), r(16, lo=-0.1, hi=0.1)
     wo, bo = r(25 * 16, dtype=torch.float16, lo=-0.2, hi=0.2), r(1)
     Sp = r(1, 256, 3845)
@@ -65,6 +68,10 @@ def _cases(dev):
         (ops.conv2d_wgrad_out, (xc, dout, 3, 3, 1, 1, 1, 1, torch.zeros(8, 3, 3, 4, device=dev),
                                 torch.zeros(8, device=dev),
                                 torch.empty(1 << 20, dtype=torch.uint8, device=dev))),
+        (ops.conv2d_wgrad_pooled_out, (xb1, pooled_b, am_b, pooled_b, 3, 3, 1, 1, 1, 1,
+                                       torch.zeros(8, 3, 3, 1, device=dev),
+                                       torch.zeros(8, device=dev),
+                                       torch.empty(1 << 20, dtype=torch.uint8, device=dev))),
         (ops.convt_conv_out, (xt, wt, bc16, 16, 5, wo, bo, 5)),
         (ops.convt_conv_out_out, (xt, wt, bc16, 16, 5, wo, bo, 5,
                                   torch.empty(2, 40, 24, 1, device=dev))),

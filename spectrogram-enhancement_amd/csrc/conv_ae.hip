@@ -1302,6 +1302,7 @@ struct WgradTrArgs {
   Geo g[MAXPH];
   int Z;     // tile runs per phase (blockIdx.x)
   int ncog;  // co groups of 16 * NTW (blockIdx.y = chunk * ncog + cog)
+  int ntg;   // wgrad_tr_kernel: groups of 28 taps (blockIdx.z = phase * ntg + group; k 7: 2)
   const void* in;
   const void* dout;  // [N][OHs][OWs][CO]
   float* part;       // [Z][CO][Kf]
@@ -1343,13 +1344,13 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
   constexpr int DST = COT + 8;       // dOut tile row stride (elements; 16-B multiple, 2-way max)
   constexpr int PST = C1 ? 40 : CH + 8;  // B rows: im2col taps (C1) or patch pixel channels
   constexpr int MAXT = C1 ? 1 : 7;   // taps (k-blocks) per wave
-  constexpr int PROWS = C1 ? 256 : 400;
+  constexpr int PROWS = C1 ? 256 : 484;  // the 22 x 22 patch of a 7 x 7 kernel
   constexpr int NDV = COT / 8;       // dOut uint4 per thread (256 pixels x COT channels)
   constexpr int NPV = C1 ? 2 : 4;    // patch elements (C1: T) / uint4 per thread
   __shared__ __attribute__((aligned(16))) T sD[256 * DST];
   __shared__ __attribute__((aligned(16))) T sP[PROWS * PST];
   __shared__ __attribute__((aligned(16))) T sIn[C1 ? 20 * 20 : 8];
-  const int ph = blockIdx.z;
+  const int ph = blockIdx.z / a.ntg, tb = 28 * (blockIdx.z - ph * a.ntg);  // first tap
   const Geo& g = a.g[ph];
   const int chunk = blockIdx.y / a.ncog, cog = blockIdx.y - (blockIdx.y / a.ncog) * a.ncog;
   const int c0 = chunk * CH, co0 = cog * COT;
@@ -1372,7 +1373,7 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
   f32x4 bacc[NTW];
 #pragma unroll
   for (int j = 0; j < NTW; ++j) bacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool do_bias = !C1 && a.bpart && chunk == 0 && wave == 0;
+  const bool do_bias = !C1 && a.bpart && chunk == 0 && wave == 0 && tb == 0;
   s16x8 ones;
   const short one = __builtin_bit_cast(short, from_f<T>(1.f));
 #pragma unroll
@@ -1395,7 +1396,7 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
   int toff[C1 ? 1 : MAXT];
 #pragma unroll
   for (int tt = 0; tt < (C1 ? 1 : MAXT); ++tt) {
-    const int t = min(wave + 4 * tt, ntap - 1);
+    const int t = min(tb + wave + 4 * tt, ntap - 1);
     const int jy = t / g.KW, jx = t - (t / g.KW) * g.KW;
     toff[tt] = (jy * PW + jx) * PST;
   }
@@ -1638,7 +1639,7 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
   const int ci = c0 + (lane & 15);
 #pragma unroll
   for (int tt = 0; tt < MAXT; ++tt) {
-    const int t = wave + 4 * tt;
+    const int t = tb + wave + 4 * tt;
     if (t >= ntap) break;
     const int col = wcol(g, t, ci);
 #pragma unroll
@@ -2593,9 +2594,10 @@ bool wgrad_tr_applies(const WgradArgs& a, int nph) {
   if ((variant(V_WGRAD_GENERIC) != 0)) return false;
   for (int i = 0; i < nph; ++i) {
     const Geo& g = a.g[i];
-    if ((g.C % 16 != 0 && g.C != 1) || g.stride != 1 || g.KH * g.KW > 28 || g.KH > 5 || g.KW > 5)
+    if ((g.C % 16 != 0 && g.C != 1) || g.stride != 1 || g.KH > 7 || g.KW > 7)
       return false;
-    if (g.C == 1 && g.KH * g.KW > 31) return false;  // im2col columns 0..30 (+ the ones column)
+    if (g.C == 1 && (g.KH * g.KW > 31 || g.KH > 5 || g.KW > 5))
+      return false;  // im2col columns 0..30 (+ the ones column)
   }
   return true;
 }
@@ -2616,13 +2618,15 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
   const int nt = std::min(4, (g0.CO + 15) / 16);
   const int ntw = nt >= 2 ? 2 : 1;
   a.ncog = (g0.CO + 16 * ntw - 1) / (16 * ntw);
+  a.ntg = 1;
+  for (int i = 0; i < nph; ++i) a.ntg = std::max(a.ntg, (w.g[i].KH * w.g[i].KW + 27) / 28);
   const bool c1 = g0.C == 1;
   const int nchunk = c1 ? 1 : g0.C / 16;
   long long tiles = 1;
   for (int i = 0; i < nph; ++i)
     tiles = std::max(tiles, (long long)w.g[i].N * ((w.g[i].OH + 15) / 16) * ((w.g[i].OW + 15) / 16));
   // ~4096 workgroups, at least 4 tiles each
-  long long z = 4096 / std::max(1LL, (long long)nchunk * a.ncog * nph);
+  long long z = 4096 / std::max(1LL, (long long)nchunk * a.ncog * nph * a.ntg);
   z = std::min<long long>(z, std::max(1LL, tiles / 4));
   a.Z = (int)std::max(1LL, std::min<long long>(z, wgrad_tr_zmax(g0.CO, g0.Kf)));
   // one output channel over 16 input channels: jy-shifted input x jx-shifted dOut
@@ -2634,7 +2638,7 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
     return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
   }
   // Conv2DTranspose stride 2: all four phases per workgroup over one union patch
-  if (!c1 && nph == 4 && g0.CO % 16 == 0 && !(variant(V_WGRAD_PERPHASE) != 0)) {
+  if (!c1 && nph == 4 && g0.CO % 16 == 0 && a.ntg == 1 && !(variant(V_WGRAD_PERPHASE) != 0)) {
     bool ok = true;
     int upt = -1 << 20, upl = -1 << 20, lo_y = 1 << 20, hi_y = -(1 << 20), lo_x = 1 << 20,
         hi_x = -(1 << 20), U = 0;
@@ -2675,7 +2679,7 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
       return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
     }
   }
-  const dim3 grid((unsigned)a.Z, (unsigned)(nchunk * a.ncog), (unsigned)nph);
+  const dim3 grid((unsigned)a.Z, (unsigned)(nchunk * a.ncog), (unsigned)(nph * a.ntg));
   if (c1) {
     if (ntw == 1) SPECENH_LAUNCH((wgrad_tr_kernel<T, 1, true>), grid, dim3(256), 0, st, a);
     else SPECENH_LAUNCH((wgrad_tr_kernel<T, 2, true>), grid, dim3(256), 0, st, a);

@@ -25,7 +25,10 @@ CASES = [("conv", 16, 32, 5, 20, 18, 3), ("conv", 32, 64, 5, 16, 16, 2),
          ("convT", 64, 64, 5, 8, 8, 2), ("convT", 64, 32, 5, 10, 6, 3),
          ("convT", 32, 16, 5, 12, 12, 2), ("conv", 64, 48, 5, 17, 17, 1),
          ("conv", 1, 16, 5, 33, 18, 2), ("conv", 1, 32, 3, 16, 16, 1),
-         ("conv", 16, 1, 5, 37, 29, 3), ("conv", 16, 1, 3, 16, 40, 1)]
+         ("conv", 16, 1, 5, 37, 29, 3), ("conv", 16, 1, 3, 16, 40, 1),
+         # 7 x 7 (hyperparam_scan.py:153-161; round 5: two 28-tap groups per workgroup row)
+         ("conv", 32, 32, 7, 23, 19, 2), ("conv", 32, 1, 7, 21, 30, 2),
+         ("convT", 32, 32, 7, 9, 7, 2), ("conv", 16, 24, 7, 16, 16, 1), ("conv", 1, 32, 7, 20, 14, 2)]
 
 
 def _reference(x, dz, op):

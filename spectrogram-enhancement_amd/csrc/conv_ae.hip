@@ -2324,7 +2324,8 @@ size_t patch_lds_bytes(const ConvArgs& a, int nph, int NT, bool pair) {
 // blocks over more workgroups (each re-stages the patch, an L2 hit)
 inline int patch_nt(int CO, unsigned tiles) {
   int nt = std::min(4, (CO + 15) / 16);
-  while (nt > 1 && (unsigned long long)tiles * ((CO + 16 * nt - 1) / (16 * nt)) < 512) nt = (nt + 1) / 2;
+  const unsigned long long want = (unsigned long long)std::max(1, variant(V_PATCH_MIN_WG));
+  while (nt > 1 && (unsigned long long)tiles * ((CO + 16 * nt - 1) / (16 * nt)) < want) nt = (nt + 1) / 2;
   return nt;
 }
 
@@ -2470,12 +2471,16 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "conv launch");
 }
 
-// stride-2 conv (Conv2DTranspose input gradient) over de-interleaved 16-channel patches
+// stride-2 conv (Conv2DTranspose input gradient) over de-interleaved 16-channel patches. At
+// least 2 N tiles per workgroup (SPECENH_S2_MIN_NT, default 2): with C > 16 every N tile
+// re-stages all channel chunks, and the C4 step's 16 x 16 convT1 gradient (128 tiles) ran 512
+// one-tile workgroups: 0.737 -> 0.716 ms per step with 2 (profiles/r05_c4_s2_nt_ab.txt)
 template <typename T>
 int launch_patch_s2(const ConvArgs& a, hipStream_t st) {
   const Geo& g = a.g[0];
   const unsigned tiles = (unsigned)(g.N * ((g.OH + 15) / 16) * ((g.OW + 15) / 16));
-  const int nt = patch_nt(g.CO, tiles);
+  const int nt = std::min(std::max(patch_nt(g.CO, tiles), variant(V_S2_MIN_NT)),
+                          std::min(4, (g.CO + 15) / 16));
   const int sph = (30 + g.KH + 1) / 2, spw = (30 + g.KW + 1) / 2;
   const size_t lds = ((size_t)4 * sph * spw * Patch<16>::PST * sizeof(T) + 15) / 16 * 16;
   const dim3 grid(tiles, (unsigned)((g.CO + 16 * nt - 1) / (16 * nt)), 1);

@@ -44,6 +44,8 @@ enum Variant : int {
   V_EIG_SPLIT,        // flagged-matrix fp64 fallback as four launches instead of one
   V_CO1_VALU,         // one-output-channel conv on 32 channels: VALU dot2 kernel instead of MFMA
   V_C1_MASK_MFMA,     // masked C = 1 conv (C4 input gradient of the last conv) on MFMA
+  V_S2_MIN_NT,        // stride-2 input-gradient patch kernel: at least this many 16-channel N tiles
+  V_PATCH_MIN_WG,     // patch kernels: fewer output-channel tiles per workgroup until this many workgroups
   V_COUNT
 };
 

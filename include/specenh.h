@@ -235,7 +235,8 @@ int specenh_conv2d_wgrad(int dtype, const void* in, int N, int IH, int IW, int C
  * zero where pooled <= 0; pooled may be NULL: no ReLU mask), formed while the tiles are staged
  * (the model's first Conv2D in Model.fit, manual_scan_3layers.py:187-188: no full-resolution
  * gradient is written). bf16 / f16, C = 1, stride 1, even OH / OW, CO % 8 == 0, else
- * SPECENH_EUNSUPPORTED. Same workspace and accumulation as specenh_conv2d_wgrad. */
+ * SPECENH_EUNSUPPORTED. Same workspace as specenh_conv2d_wgrad, but dw and dbias are
+ * OVERWRITTEN with the gradient (not accumulated: no zeroing launch before it). */
 int specenh_conv2d_wgrad_pooled(int dtype, const void* in, int N, int IH, int IW, int C,
                                 const void* dpool, const unsigned char* argmax, const void* pooled,
                                 int KH, int KW, int CO, int stride, int pad_t, int pad_l,

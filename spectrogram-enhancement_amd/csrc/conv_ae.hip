@@ -1172,6 +1172,7 @@ struct WgradArgs {
   const void* pd = nullptr;
   const unsigned char* pam = nullptr;
   const void* py = nullptr;  // or null: no ReLU mask
+  bool overwrite = false;    // dw / dbias = the gradient (specenh_conv2d_wgrad_pooled)
 };
 
 // Workgroup: 64 GEMM-K columns (blockIdx.x) x 16*NT channels (blockIdx.y) x one pixel
@@ -1974,6 +1975,7 @@ struct SumJob {
   float* dst;
   long long n;
   int nz, ew;
+  int overwrite;  // dst = sum instead of dst += sum
 };
 
 constexpr int SUM_EW = 64, SUM_ZL = 16;
@@ -2005,21 +2007,22 @@ __global__ __launch_bounds__(SUM_EW * SUM_ZL) void ordered_sum_kernel(SumJob j0,
     if (zl < w) red[threadIdx.x] += red[threadIdx.x + w * SUM_EW];
     __syncthreads();
   }
-  if (zl == 0 && e < j.n) j.dst[e] += red[threadIdx.x];
+  if (zl == 0 && e < j.n) j.dst[e] = j.overwrite ? red[threadIdx.x] : j.dst[e] + red[threadIdx.x];
 }
 
 // the sums of one weight-gradient launch: dw over nz slices, db (if any) over nzb slices
-inline SumJob sum_job(const float* part, int nz, long long n, float* dst) {
-  return SumJob{part, dst, n, nz, SUM_EW};
+inline SumJob sum_job(const float* part, int nz, long long n, float* dst, bool overwrite) {
+  return SumJob{part, dst, n, nz, SUM_EW, overwrite ? 1 : 0};
 }
 inline unsigned sum_blocks(const SumJob& j) { return (unsigned)((j.n + SUM_EW - 1) / SUM_EW); }
 inline void launch_ordered_sums(const float* part, int nz, long long n, float* dw, const float* bpart,
-                                int nzb, long long nb, float* db, hipStream_t st) {
-  const SumJob j0 = sum_job(part, nz, n, dw);
+                                int nzb, long long nb, float* db, hipStream_t st,
+                                bool overwrite = false) {
+  const SumJob j0 = sum_job(part, nz, n, dw, overwrite);
   SumJob j1{};
   unsigned blocks = sum_blocks(j0);
   if (db) {
-    j1 = sum_job(bpart, nzb, nb, db);
+    j1 = sum_job(bpart, nzb, nb, db, overwrite);
     blocks += sum_blocks(j1);
   }
   SPECENH_LAUNCH(ordered_sum_kernel, dim3(blocks), dim3(SUM_EW * SUM_ZL), 0, st, j0, j1,
@@ -2631,13 +2634,14 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
   for (int i = 0; i < nph; ++i)
     tiles = std::max(tiles, (long long)w.g[i].N * ((w.g[i].OH + 15) / 16) * ((w.g[i].OW + 15) / 16));
   // ~4096 workgroups, at least 4 tiles each
-  long long z = 4096 / std::max(1LL, (long long)nchunk * a.ncog * nph * a.ntg);
+  const long long wg_target = std::max(1, variant(V_WGRAD_WG));
+  long long z = wg_target / std::max(1LL, (long long)nchunk * a.ncog * nph * a.ntg);
   z = std::min<long long>(z, std::max(1LL, tiles / 4));
   a.Z = (int)std::max(1LL, std::min<long long>(z, wgrad_tr_zmax(g0.CO, g0.Kf)));
   // one output channel over 16 input channels: jy-shifted input x jx-shifted dOut
   if (nph == 1 && g0.CO == 1 && g0.C == 16 && g0.KH <= 5 && g0.KW <= 5 &&
       !(variant(V_WGRAD_NO_CO1) != 0)) {
-    a.Z = (int)std::max(1LL, std::min<long long>({tiles / 2, (long long)wgrad_tr_zmax(1, g0.Kf), 4096LL}));
+    a.Z = (int)std::max(1LL, std::min<long long>({tiles / 2, (long long)wgrad_tr_zmax(1, g0.Kf), wg_target}));
     SPECENH_LAUNCH(wgrad_co1_kernel<T>, dim3((unsigned)a.Z), dim3(64), 0, st, a);
     launch_ordered_sums(a.part, a.Z, g0.Kf, dw, a.bpart, a.Z, 1, db, st);
     return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
@@ -2675,7 +2679,7 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
       a.PH = hi_y - lo_y + 1;
       a.PW = hi_x - lo_x + 1;
       a.ncog = g0.CO / 16;
-      long long zp = 4096 / std::max(1LL, (long long)nchunk * a.ncog);
+      long long zp = wg_target / std::max(1LL, (long long)nchunk * a.ncog);
       zp = std::min<long long>(zp, std::max(1LL, tiles / 4));
       a.Z = (int)std::max(1LL, std::min<long long>(zp, wgrad_tr_zmax(g0.CO, g0.Kf)));
       SPECENH_LAUNCH(wgrad_trp_kernel<T>, dim3((unsigned)a.Z, (unsigned)(nchunk * a.ncog)), dim3(256), 0,
@@ -2692,7 +2696,8 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
     if (ntw == 1) SPECENH_LAUNCH((wgrad_tr_kernel<T, 1, false>), grid, dim3(256), 0, st, a);
     else SPECENH_LAUNCH((wgrad_tr_kernel<T, 2, false>), grid, dim3(256), 0, st, a);
   }
-  launch_ordered_sums(a.part, a.Z, (long long)g0.CO * g0.Kf, dw, a.bpart, nph * a.Z, g0.CO, db, st);
+  launch_ordered_sums(a.part, a.Z, (long long)g0.CO * g0.Kf, dw, a.bpart, nph * a.Z, g0.CO, db, st,
+                      w.overwrite);
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
 }
 
@@ -2850,6 +2855,7 @@ int specenh_conv2d_wgrad_pooled(int dtype, const void* in, int N, int IH, int IW
   a.pd = dpool;
   a.pam = argmax;
   a.py = pooled;
+  a.overwrite = true;
   a.part = (float*)workspace;
   const size_t Zws = std::max<size_t>(p.Z, wgrad_tr_zmax(CO, (long long)KH * KW * C));
   a.bpart = dbias ? a.part + Zws * CO * KH * KW * C : nullptr;

@@ -585,7 +585,8 @@ class AutoencoderEngine:
             elif i == first and zeroed:
                 # no input gradient follows: the current stream is idle, so this weight
                 # gradient runs there, beside the second stream's remaining ones
-                self.g[:g0_end].zero_()
+                if not self.wgrad_pooled:  # (the pooled form overwrites its slice)
+                    self.g[:g0_end].zero_()
                 self._wgrad0(b, hin, d_out, op, s, pt, pl, dil, b["ws0"])
                 if on_layer_done is not None:
                     on_layer_done(i)

@@ -200,8 +200,9 @@ def test_pool_backward_routes_to_argmax_with_relu_mask(gpu_device):
                                           ((34, 18), 24, 5, False)])
 def test_wgrad_pooled_equals_pool_backward_then_wgrad(gpu_device, dtype, hw, co, k, relu):
     """specenh_conv2d_wgrad_pooled (the first Conv2D's weight gradient formed from its pool's
-    gradient, argmax and ReLU mask while the tiles are staged) is bitwise
-    specenh_maxpool2_bwd + specenh_conv2d_wgrad, incl. ragged tiles and no ReLU mask."""
+    gradient, argmax and ReLU mask while the tiles are staged; it overwrites dw / dbias) is
+    bitwise specenh_maxpool2_bwd + specenh_conv2d_wgrad into zeroed buffers, incl. ragged
+    tiles and no ReLU mask."""
     from specenh.ops import ops, wgrad_workspace
     dev = torch.device(gpu_device)
     g = torch.Generator(device=dev).manual_seed(5)
@@ -214,8 +215,9 @@ def test_wgrad_pooled_equals_pool_backward_then_wgrad(gpu_device, dtype, hw, co,
     p = (k - 1) // 2
     res = []
     for fused in (True, False):
-        dw = torch.zeros(co, k, k, 1, device=dev)
-        db = torch.zeros(co, device=dev)
+        # the pooled form OVERWRITES dw / dbias (no zeroing launch before it)
+        dw = torch.full((co, k, k, 1), 7.0 if fused else 0.0, device=dev)
+        db = torch.full((co,), -3.0 if fused else 0.0, device=dev)
         if fused:
             ops.conv2d_wgrad_pooled_out(x, dpool, am, pooled if relu else None, k, k, 1, p, p, 1,
                                         dw, db, ws)

@@ -1338,12 +1338,22 @@ __device__ __forceinline__ f32x4 mfma_s16(s16x8 a, s16x8 b, f32x4 acc) {
 // gradient); waves w take k-block w & 1 over pixel groups of parity w >> 1 and pairs of waves
 // are summed in a fixed order at the end. The next tile's global data is prefetched into
 // registers while the current tile computes.
+#ifndef SPECENH_WGRAD_SWZ
+#define SPECENH_WGRAD_SWZ 1
+#endif
 template <typename T, int NTW, bool C1>
 __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
   constexpr int CH = 16;             // input channels per workgroup: one k-block per tap
   constexpr int COT = 16 * NTW;      // output channels per workgroup
-  constexpr int DST = COT + 8;       // dOut tile row stride (elements; 16-B multiple, 2-way max)
-  constexpr int PST = C1 ? 40 : CH + 8;  // B rows: im2col taps (C1) or patch pixel channels
+  // SWZ (round 5): a half-wave's transposed reads cover 8 CONSECUTIVE pixels (K element k of
+  // lane group g4: pixel 4 (g4 & 1) + (k & 3) + 8 (k >> 2) of its tile row; round 4 read
+  // columns 0-3 and 8-11 together) from unpadded 32-byte pixel rows: 256 B = all 64 banks,
+  // whatever the tap offset; 64-byte dOut rows (32 channels) swap their two 32-byte chunks on
+  // pixel bit 2. PMC had SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.50 with padded rows.
+  constexpr bool SWZ = SPECENH_WGRAD_SWZ != 0;
+  constexpr int DST = SWZ ? COT : COT + 8;  // dOut tile row stride (elements)
+  constexpr int PST = C1 ? 40 : (SWZ ? CH : CH + 8);  // B rows: im2col taps (C1) or patch pixel channels
+  constexpr int HI = SWZ ? 8 : 4;           // pixel step of a fragment's second 4 K elements
   constexpr int MAXT = C1 ? 1 : 7;   // taps (k-blocks) per wave
   constexpr int PROWS = C1 ? 256 : 484;  // the 22 x 22 patch of a 7 x 7 kernel
   constexpr int NDV = COT / 8;       // dOut uint4 per thread (256 pixels x COT channels)
@@ -1384,7 +1394,9 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
   // (row 2 pg + (g4 >> 1), columns 8 (g4 & 1) .. + 7) of pixel group pg; lane 4q + p of the
   // group addresses row q (pixel column + q, + 4 for the upper half) and elements 4p .. 4p+3
   const int g4 = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-  const int prow = g4 >> 1, pcol = 8 * (g4 & 1) + q;
+  const int prow = g4 >> 1, pcol = (SWZ ? 4 : 8) * (g4 & 1) + q;
+  // dOut chunk slot of 16-channel chunk j at pixel P (element offset 16 dch(P, j))
+  auto dch = [](int P, int j) { return (SWZ && COT == 32) ? (j ^ ((P >> 2) & 1)) : j; };
   // C1: the im2col taps t < 31 as offsets jy PW + jx into the staged patch (uniform)
   int c1off[C1 ? 31 : 1];
 #pragma unroll
@@ -1491,13 +1503,14 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
       for (int u = 0; u < NDV; ++u) {
         const int e = tid + 256 * u;
         const int pix = e / NDV, v = e - (e / NDV) * NDV;
-        *reinterpret_cast<uint4*>(sD + pix * DST + 8 * v) = rd[u];
+        *reinterpret_cast<uint4*>(sD + pix * DST + 16 * dch(pix, v >> 1) + 8 * (v & 1)) = rd[u];
       }
     } else if (co_one) {
       const uint32_t w0 = __builtin_bit_cast(unsigned short, rd1);
 #pragma unroll
       for (int v = 0; v < COT / 8; ++v)
-        *reinterpret_cast<uint4*>(sD + tid * DST + 8 * v) = uint4{v == 0 ? w0 : 0u, 0u, 0u, 0u};
+        *reinterpret_cast<uint4*>(sD + tid * DST + 16 * dch(tid, v >> 1) + 8 * (v & 1)) =
+            uint4{v == 0 ? w0 : 0u, 0u, 0u, 0u};
     } else {  // other narrow CO: element-wise, not prefetched
       int n, oyt, oxt;
       tile_org(tile, n, oyt, oxt);
@@ -1507,7 +1520,7 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
         T val = from_f<T>(0.f);
         if (oy < g.OH && ox < g.OW && co0 + c < g.CO)
           val = dout[(((long long)n * g.OHs + oy * g.oys + g.oy0) * g.OWs + ox * g.oxs + g.ox0) * g.CO + co0 + c];
-        sD[pix * DST + c] = val;
+        sD[pix * DST + 16 * dch(pix, c >> 4) + (c & 15)] = val;
       }
     }
     if constexpr (C1) {
@@ -1567,11 +1580,12 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
         const int r = 2 * pg + prow;
         const T* da = sD + (r * 16 + pcol) * DST + 4 * pp;
         const T* pb = sP + (r * 16 + pcol) * PST + 16 * kb + 4 * pp;
-        const s16x4 blo = lds_tr16(pb), bhi = lds_tr16(pb + 4 * PST);
+        const s16x4 blo = lds_tr16(pb), bhi = lds_tr16(pb + HI * PST);
         const s16x8 bf = s16x8{blo[0], blo[1], blo[2], blo[3], bhi[0], bhi[1], bhi[2], bhi[3]};
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
-          const s16x4 lo = lds_tr16(da + 16 * j), hi = lds_tr16(da + 4 * DST + 16 * j);
+          const int jc = 16 * dch(pcol, j);
+          const s16x4 lo = lds_tr16(da + jc), hi = lds_tr16(da + HI * DST + jc);
           const s16x8 af = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           acc[0][j] = mfma_s16<T>(af, bf, acc[0][j]);
         }
@@ -1589,13 +1603,14 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
         const T* da = sD + (r * 16 + pcol) * DST + 4 * pp;
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
-          const s16x4 lo = lds_tr16(da + 16 * j), hi = lds_tr16(da + 4 * DST + 16 * j);
+          const int jc = 16 * dch(pcol, j);
+          const s16x4 lo = lds_tr16(da + jc), hi = lds_tr16(da + HI * DST + jc);
           af[j] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         }
         const T* pr = sP + (r * PW + pcol) * PST + 4 * pp;
 #pragma unroll
         for (int tt = 0; tt < MAXT; ++tt) {
-          const s16x4 lo = lds_tr16(pr + toff[tt]), hi = lds_tr16(pr + toff[tt] + 4 * PST);
+          const s16x4 lo = lds_tr16(pr + toff[tt]), hi = lds_tr16(pr + toff[tt] + HI * PST);
           bf[tt] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         }
 #pragma unroll

@@ -2651,7 +2651,7 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
   // ~4096 workgroups, at least 4 tiles each
   const long long wg_target = std::max(1, variant(V_WGRAD_WG));
   long long z = wg_target / std::max(1LL, (long long)nchunk * a.ncog * nph * a.ntg);
-  z = std::min<long long>(z, std::max(1LL, tiles / 4));
+  z = std::min<long long>(z, std::max(1LL, tiles / (c1 ? std::max(1, variant(V_WGRAD_C1_TILES)) : 4)));
   a.Z = (int)std::max(1LL, std::min<long long>(z, wgrad_tr_zmax(g0.CO, g0.Kf)));
   // one output channel over 16 input channels: jy-shifted input x jx-shifted dOut
   if (nph == 1 && g0.CO == 1 && g0.C == 16 && g0.KH <= 5 && g0.KW <= 5 &&

@@ -47,6 +47,7 @@ enum Variant : int {
   V_S2_MIN_NT,        // stride-2 input-gradient patch kernel: at least this many 16-channel N tiles
   V_PATCH_MIN_WG,     // patch kernels: fewer output-channel tiles per workgroup until this many workgroups
   V_WGRAD_WG,         // weight-gradient MFMA kernels: workgroups per launch aimed at (tile runs)
+  V_WGRAD_C1_TILES,   // one-input-channel weight gradient: at least this many tiles per workgroup
   V_COUNT
 };
 

@@ -33,6 +33,11 @@ extern "C" {
 #define SPECENH_STFT_LOG 1          /* natural log(P + eps)                  pipeline_data.py:33 */
 #define SPECENH_STFT_NORMALIZE 2    /* per-spectrogram min-max (implies LOG) pipeline_data.py:34 */
 #define SPECENH_STFT_DROP_NYQUIST 4 /* drop the last frequency row         pipeline_data.py:35 */
+/* One real frame per complex FFT instead of two (no reference counterpart: an accuracy
+ * mode). The two-for-one FFT gives a bin at a spectral null the partner frame's fp32
+ * rounding; EXACT keeps the reference's 1e-5 on such bins for twice the FFT work. The
+ * numpy-compat entries (specgr, specgr_array) set it; the throughput paths do not. */
+#define SPECENH_STFT_EXACT 8
 
 /* detrend / scaling codes (the 'detrend' and 'scaling' keys of spec_params,
  * pipeline_data.py:77-84). */

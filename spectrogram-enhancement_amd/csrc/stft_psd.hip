@@ -785,7 +785,15 @@ __device__ __forceinline__ double dc_lane_base(const StftArgs& a, int gl) {
 // per XCD (4 MB) do not stay in its 4 MB L2. Same arithmetic ((v - mn) * inv); the two
 // instantiations' FFT code is scheduled differently, so values agree to an ulp or so of the
 // log2 PSD (<= 1e-6 on [0, 1], measured; N = 512 bitwise), not bit for bit.
-template <int N, bool XH = false, int HOLD = 0>
+//
+// EXACT (SPECENH_STFT_EXACT, the numpy-compat entries specgr / specgr_array): one real frame
+// per complex FFT, its partner the zero frame (the loads go through a zero-length buffer
+// descriptor, which returns 0). A lane group runs its tile's two frames as two FFTs, so the
+// tile layout, the normalising sweep and the stores are unchanged. The two-for-one
+// separation hands bin k of frame a the partner frame's fp32 rounding at the same bin, which
+// at a spectral null of frame a is relatively large (tools/stft_pair_error.py: ln-PSD error
+// 1.5e-4 paired, 3.7e-5 against a zero partner). Twice the FFT work: not a throughput path.
+template <int N, bool XH = false, int HOLD = 0, bool EXACT = false>
 __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_kernel(
     StftArgs a) {
   using C = Cfg<N>;
@@ -823,10 +831,38 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
 
   const __amdgpu_buffer_rsrc_t orr = make_rsrc(o_shot, (long long)a.F_out * a.T * 4);
   PairSamples<N> s0;
-  if constexpr (C::PF) load_pair<N, XH>(s0, xr, xr, a.hop, 2 * fi, a.T, gl);
+  const __amdgpu_buffer_rsrc_t zr = make_rsrc(a.x, 0);  // EXACT: the zero partner frame
+  if constexpr (EXACT) {
+    if constexpr (C::PF) load_pair<N, XH, true>(s0, xr, zr, a.hop, 2 * fi, a.T, gl);
+  } else if constexpr (C::PF) {
+    load_pair<N, XH>(s0, xr, xr, a.hop, 2 * fi, a.T, gl);
+  }
   __syncthreads();
 
-  if constexpr (HOLD > 0) {  // (host-checked: NORMALIZE, ntiles == HOLD)
+  if constexpr (EXACT) {
+    static_assert(HOLD == 0, "exact mode runs the sweep schedule");
+    for (int tile = 0; tile < ntiles; ++tile) {
+      const int t0 = tile * Lo::TF;
+      const int fa = t0 + 2 * fi;  // frames fa, fa + 1: one FFT each
+      f2v pv[IB], pw[IB];
+      float dmn = INFINITY, dmx = -INFINITY;  // (the zero frame's values: unused)
+      if constexpr (!C::PF) load_pair<N, XH, true>(s0, xr, zr, a.hop, fa, a.T, gl);
+      pair_spectrum<N, XH, true>(a, s0, s0, s_tw, s_win, s_dc, buf, gl, dcb, xr, zr, fa + 1,
+                                 C::PF != 0, want_log, log2_out, pv, dmn, dmx);
+      if constexpr (!C::PF) load_pair<N, XH, true>(s0, xr, zr, a.hop, fa + 1, a.T, gl);
+      // the second FFT re-uses the lane group's buffer: its first exchange writes only after
+      // the group's own reads of the first (wave-local, ordered by wave_lds_sync)
+      pair_spectrum<N, XH, true>(a, s0, s0, s_tw, s_win, s_dc, buf, gl, dcb, xr, zr,
+                                 fa + Lo::TF, C::PF != 0, want_log, log2_out, pw, dmn, dmx);
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        pv[i].y = pw[i].x;
+        lmin = fminf(lmin, fminf(pv[i].x, pv[i].y));
+        lmax = fmaxf(lmax, fmaxf(pv[i].x, pv[i].y));
+      }
+      tile_store<N>(a, s_tile, pv, gl, fi, tid, orr, t0, 0.f, 1.f, false);
+    }
+  } else if constexpr (HOLD > 0) {  // (host-checked: NORMALIZE, ntiles == HOLD)
     f2v pv[HOLD][IB];
 #pragma unroll
     for (int tile = 0; tile < HOLD; ++tile) {
@@ -859,14 +895,16 @@ __global__ __launch_bounds__(Layout<N>::THREADS, Layout<N>::WPE) void stft_psd_k
                     tile > 0);
     return;
   }
-  for (int tile = 0; tile < ntiles; ++tile) {
-    const int t0 = tile * Lo::TF;
-    const int fa = t0 + 2 * fi;  // tail frames are clamped duplicates (load_pair)
-    if constexpr (!C::PF) load_pair<N, XH>(s0, xr, xr, a.hop, fa, a.T, gl);
-    f2v pv[IB];
-    pair_spectrum<N, XH>(a, s0, s0, s_tw, s_win, s_dc, buf, gl, dcb, xr, xr, fa + Lo::TF, C::PF != 0,
-                         want_log, log2_out, pv, lmin, lmax);
-    tile_store<N>(a, s_tile, pv, gl, fi, tid, orr, t0, 0.f, 1.f, false);
+  if constexpr (!EXACT) {
+    for (int tile = 0; tile < ntiles; ++tile) {
+      const int t0 = tile * Lo::TF;
+      const int fa = t0 + 2 * fi;  // tail frames are clamped duplicates (load_pair)
+      if constexpr (!C::PF) load_pair<N, XH>(s0, xr, xr, a.hop, fa, a.T, gl);
+      f2v pv[IB];
+      pair_spectrum<N, XH>(a, s0, s0, s_tw, s_win, s_dc, buf, gl, dcb, xr, xr, fa + Lo::TF,
+                           C::PF != 0, want_log, log2_out, pv, lmin, lmax);
+      tile_store<N>(a, s_tile, pv, gl, fi, tid, orr, t0, 0.f, 1.f, false);
+    }
   }
 
   if (a.flags & SPECENH_STFT_NORMALIZE) {
@@ -914,12 +952,20 @@ hipError_t launch_stft(const StftArgs& a, long long batch, hipStream_t stream) {
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)stft_psd_kernel<N, XH>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, Lo::BYTES);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)stft_psd_kernel<N, XH, 0, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, Lo::BYTES);
     if constexpr (N <= 512)
       for (const void* k : {(const void*)stft_psd_kernel<N, XH, 1>, (const void*)stft_psd_kernel<N, XH, 2>})
         if (e == hipSuccess)
           e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, Lo::BYTES);
     if (e != hipSuccess) return e;
     attr_set = true;
+  }
+  if (a.flags & SPECENH_STFT_EXACT) {
+    SPECENH_LAUNCH((stft_psd_kernel<N, XH, 0, true>), dim3((unsigned)batch), dim3(Lo::THREADS),
+                   Lo::BYTES, stream, a);
+    return hipGetLastError();
   }
   // held tiles: normalised spectrograms of one or two tiles (larger N hold more bins per
   // lane: the second tile's values would spill)
@@ -1468,7 +1514,9 @@ int specenh_stft_psd(const specenh_stft_plan* plan, const float* x, long long ba
   // (measured). Without NORMALIZE it needs no workspace.
   const bool team = (F_out * T * 4 >= (256ll << 10)) || (flags & STFT_DEV_FORCETEAM);
   const bool norm = (flags & SPECENH_STFT_NORMALIZE) != 0;
-  if ((workspace || !norm) && !(flags & STFT_DEV_NOTEAM) && team && batch <= (1ll << 30)) {
+  // EXACT: one frame per FFT on the sweep schedule (launch_stft)
+  if ((workspace || !norm) && !(flags & (STFT_DEV_NOTEAM | SPECENH_STFT_EXACT)) && team &&
+      batch <= (1ll << 30)) {
     bool launched = false;
     hipError_t e = hipSuccess;
     switch (N) {

@@ -34,6 +34,7 @@ SVD_COMPUTE = 1
 STFT_LOG = 1
 STFT_NORMALIZE = 2
 STFT_DROP_NYQUIST = 4
+STFT_EXACT = 8  # one frame per FFT (include/specenh.h SPECENH_STFT_EXACT)
 
 DETREND = {False: 0, None: 0, "constant": 1, "c": 1, "linear": 2, "l": 2}
 SCALING = {"density": 0, "spectrum": 1}

@@ -45,24 +45,27 @@ def _params(spec_params):
 
 
 def specgr_batch(x: torch.Tensor, spec_params: dict, cut_shot: float | None = None,
-                 out: torch.Tensor | None = None) -> torch.Tensor:
+                 out: torch.Tensor | None = None, exact: bool = False) -> torch.Tensor:
     """Batched specgr on device tensors: ``x[B, L]`` -> ``Sxx[B, nperseg//2, T]`` fp32.
 
     Normalisation is per spectrogram (pipeline_data.py:34 applied to each row of x).
+    ``exact=True`` runs one frame per FFT (the numpy entries below use it): the default
+    two-for-one FFT hands a bin at a spectral null the partner frame's fp32 rounding, which
+    on the reference's 1M-sample production shots reaches 1.02e-5.
     """
     p = _params(spec_params)
     if cut_shot is not None:
         x = x[..., : np.int_(cut_shot * p["fs"])]
     return _stft.stft_psd(x, p["nperseg"], p["noverlap"], p["window"], p["fs"], p["scaling"],
                           p["detrend"], p["eps"], log=True, normalize=True, drop_nyquist=True,
-                          out=out)
+                          out=out, exact=exact)
 
 
 def specgr_array(sig_in, spec_params: dict):
     """specgr on an in-memory 1-D signal: returns (Sxx float64, f, t) like the reference."""
     p = _params(spec_params)
     x = torch.as_tensor(np.ascontiguousarray(sig_in), dtype=torch.float32, device=_device())
-    S = specgr_batch(x.unsqueeze(0), spec_params)[0]
+    S = specgr_batch(x.unsqueeze(0), spec_params, exact=True)[0]
     f = _stft.frequencies(p["nperseg"], p["fs"])[:-1]
     t = _stft.times(x.shape[-1], p["nperseg"], p["noverlap"], p["fs"])
     return S.double().cpu().numpy(), f, t

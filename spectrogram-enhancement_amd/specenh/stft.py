@@ -200,13 +200,15 @@ def _check_input(x: torch.Tensor) -> torch.Tensor:
 def stft_psd(x: torch.Tensor, nperseg: int, noverlap: int, window="hann", fs: float = 1.0,
              scaling="density", detrend="linear", eps: float = 1e-11, log: bool = False,
              normalize: bool = False, drop_nyquist: bool = False,
-             out: torch.Tensor | None = None) -> torch.Tensor:
+             out: torch.Tensor | None = None, exact: bool = False) -> torch.Tensor:
     """Batched spectrogram of ``x[B, L]`` (fp32 or fp16 samples, on a ROCm device) ->
     ``[B, F, T]`` fp32 (fp16 samples are widened on load; the arithmetic is fp32).
 
     ``F = nperseg//2 + 1`` (``nperseg//2`` with ``drop_nyquist``),
     ``T = (L - nperseg)//(nperseg - noverlap) + 1``.
     ``normalize`` implies ``log`` (the specgr chain of pipeline_data.py:33-35).
+    ``exact``: one real frame per complex FFT instead of two (SPECENH_STFT_EXACT; twice the
+    FFT work): keeps bins at spectral nulls free of the partner frame's rounding.
     """
     from .ops import ops, window_key
     squeeze = x.dim() == 1
@@ -217,7 +219,8 @@ def stft_psd(x: torch.Tensor, nperseg: int, noverlap: int, window="hann", fs: fl
     T = frame_count(x.shape[1], nperseg, noverlap)
     F = nperseg // 2 + (0 if drop_nyquist else 1)
     flags = ((_lib.STFT_LOG if log else 0) | (_lib.STFT_NORMALIZE if normalize else 0)
-             | (_lib.STFT_DROP_NYQUIST if drop_nyquist else 0))
+             | (_lib.STFT_DROP_NYQUIST if drop_nyquist else 0)
+             | (_lib.STFT_EXACT if exact else 0))
     if out is None:
         out = torch.empty((x.shape[0], F, T), dtype=torch.float32, device=x.device)
     elif out.shape != (x.shape[0], F, T) or out.dtype != torch.float32 or not out.is_contiguous():

@@ -8,16 +8,14 @@ dropped. The notebook's loop (``denoising_by_svd.ipynb:250-263``) then calls
 
 Tolerances (the contract of tests/test_stft_gpu.py and tests/test_svd_gpu.py):
   * specgr: f / t bit-exact; normalised log output vs the fp64 truth (fp32 samples on both
-    sides). EXPLICIT EXCEPTION to SURVEY §8(d)'s 1e-5 max: on these 1M-value
-    production spectrograms the bound is max <= 2e-5 and 99.99th percentile <= 2e-6, AND
-    both no larger than scipy's own fp32 spectrogram of the same samples (the reference's
-    path when a shot is stored as float32: scipy computes in the input's precision). Measured
-    on MI355X: max 4.3e-6 / 1.02e-5 / 4.8e-6 for the three channels, p99.99 1.2e-6 .. 1.3e-6
-    (tools/diag_prodshot.py); scipy fp32: max 2.9e-5 / 6.7e-5 / 3.0e-5, p99.99 2.5e-6 ..
-    8.0e-6. The 1e-5 case is one bin at a spectral null (PSD 1e-6 of its neighbours): the
-    two-for-one FFT (two real frames in one complex FFT) leaks the partner frame's fp32
-    rounding at the same bin into it. tools/stft_pair_error.py emulates the kernel's fp32
-    arithmetic: ln-PSD error 3.4e-5 at that bin with one frame per FFT, 1.5e-4 paired;
+    sides): max |delta| <= 1e-5, and both the max and the 99.99th percentile no
+    larger than scipy's own fp32 spectrogram of the same samples. The numpy entries run the
+    exact mode (one real frame per complex FFT, SPECENH_STFT_EXACT): the default two-for-one
+    FFT leaks the partner frame's fp32 rounding into a bin at a spectral null (PSD 1e-6 of its
+    neighbours), which reached 1.02e-5 on channel 2 (round 5; tools/stft_pair_error.py
+    emulates the kernel's fp32 arithmetic: ln-PSD error 1.5e-4 paired, 3.7e-5 against a zero
+    partner at that bin). The paired throughput path is checked on the same shots at the
+    round-5 bound (2e-5) so that a regression there still shows.
     * denoiseSignal: ||GPU - ref||_F / ||ref||_F <= 1e-5 where the kept range has a spectral
     gap (default [1, r): sigma_1 / sigma_2 ~ 60 on these spectrograms; use_optimal).
     The (0, 16) cut of a log spectrogram of chirps + noise has NO gap (sigma_16 / sigma_17 =
@@ -41,17 +39,19 @@ FS = 500000
 SPEC = {"nperseg": 512, "noverlap": 256, "fs": FS, "window": "hamm", "scaling": "density",
         "detrend": "linear", "eps": 1e-11}          # pipeline_data.py:77-84
 L_SHOT = 2 * FS                                     # cut_shot = 2 (pipeline_data.py:28)
-TOL_NORM = 2e-5      # max |GPU - truth| on a 1M-value spectrogram (module docstring)
+TOL_NORM = 1e-5      # max |GPU - truth| on a 1M-value spectrogram, exact mode (docstring)
 TOL_NORM_P = 2e-6    # its 99.99th percentile (both also <= scipy fp32's, _check_specgr)
+TOL_NORM_PAIRED = 2e-5  # the two-for-one throughput path (specgr_batch default)
 TOL_SVD = 1e-5
 
 
-def _check_specgr(S, St, S32):
+def _check_specgr(S, St, S32, tol=TOL_NORM):
     """GPU S vs the fp64 truth St, next to scipy's fp32 spectrogram S32 of the same samples."""
     e = np.abs(S - St)
     e32 = np.abs(S32 - St)
     q, q32 = np.quantile(e, 0.9999), np.quantile(e32, 0.9999)
-    assert e.max() <= TOL_NORM, e.max()
+    print(f"max {e.max():.3e} p99.99 {q:.3e} (scipy fp32 {e32.max():.3e} / {q32:.3e})")
+    assert e.max() <= tol, e.max()
     assert q <= TOL_NORM_P, q
     assert e.max() <= e32.max(), ("worse than scipy fp32", e.max(), e32.max())
     assert q <= q32, ("p99.99 worse than scipy fp32", q, q32)
@@ -111,16 +111,20 @@ def test_specgr_bes_variant_production_shot(shots, truth, tmp_path, gpu_device):
 
 
 def test_specgr_batch_production_shots(shots, truth, gpu_device):
-    """The same three channels in one launch, cut on the device (specgr_batch cut_shot)."""
+    """The same three channels in one launch, cut on the device (specgr_batch cut_shot), in
+    the exact mode at 1e-5 and on the paired throughput path at its own bound."""
     import torch
 
     from specenh import pipeline_data
 
     x = torch.as_tensor(shots, device=gpu_device)
-    S = pipeline_data.specgr_batch(x, SPEC, cut_shot=2).double().cpu().numpy()
+    S = pipeline_data.specgr_batch(x, SPEC, cut_shot=2, exact=True).double().cpu().numpy()
     assert S.shape == (3, 256, 3905)
     for c in range(3):
         _check_specgr(S[c], truth[c][0], truth[c][3])
+    S = pipeline_data.specgr_batch(x, SPEC, cut_shot=2).double().cpu().numpy()
+    for c in range(3):
+        _check_specgr(S[c], truth[c][0], truth[c][3], tol=TOL_NORM_PAIRED)
 
 
 @pytest.fixture(scope="module")

@@ -44,17 +44,22 @@ def test_specgr_vs_golden_and_oracle(case, gpu_device):
     # fp32 fixtures were computed by scipy in fp32 (DC-row detrend error ~1e-4, see
     # tests/test_oracle_golden.py); fp64 fixtures differ from ours only by the input cast
     assert gerr <= (TOL_NORM * 3 if g["Sxx"].dtype == np.float64 else 1e-4), gerr
+    # specgr_array runs the exact mode (one frame per FFT); the paired throughput path of
+    # specgr_batch is held to the same bound on every golden case
+    Sp = pipeline_data.specgr_batch(_gpu(x, gpu_device)[None], p)[0].double().cpu().numpy()
+    assert np.abs(Sp - truth).max() <= TOL_NORM
 
 
+@pytest.mark.parametrize("exact", [False, True])
 @pytest.mark.parametrize("case", [c for c in stft_cases() if c != "bes_variant"])
-def test_raw_psd_vs_oracle(case, gpu_device):
+def test_raw_psd_vs_oracle(case, exact, gpu_device):
     from specenh import stft
 
     g = load_golden(f"stft_{case}")
     x = golden_signal(g).astype(np.float32)
     p = golden_params(g)
     P = stft.stft_psd(_gpu(x, gpu_device), p["nperseg"], p["noverlap"], p["window"], p["fs"],
-                      p["scaling"], p["detrend"], p["eps"]).double().cpu().numpy()
+                      p["scaling"], p["detrend"], p["eps"], exact=exact).double().cpu().numpy()
     _, _, truth = ref.spectrogram_psd(x.astype(np.float64), fs=p["fs"], window=p["window"],
                                       nperseg=p["nperseg"], noverlap=p["noverlap"],
                                       detrend=p["detrend"], scaling=p["scaling"])
@@ -66,8 +71,10 @@ def test_raw_psd_vs_oracle(case, gpu_device):
 @pytest.mark.parametrize("nperseg,noverlap,window", [
     (64, 48, "hann"), (128, 64, "hamm"), (256, 128, "hann"), (512, 256, "hamm"),
     (1024, 768, "hamm"), (2048, 1536, "hann"), (4096, 3072, "hamm")])
-def test_batched_random_shots(nperseg, noverlap, window, gpu_device):
-    """Several seeded shots per launch, every spectrogram normalised independently."""
+@pytest.mark.parametrize("exact", [False, True])
+def test_batched_random_shots(nperseg, noverlap, window, exact, gpu_device):
+    """Several seeded shots per launch, every spectrogram normalised independently; paired
+    and exact (one frame per FFT, SPECENH_STFT_EXACT) schedules."""
     from specenh import pipeline_data
     from specenh.synthetic import plasma_chirps
 
@@ -75,7 +82,7 @@ def test_batched_random_shots(nperseg, noverlap, window, gpu_device):
     x = plasma_chirps(5, L, seed0=1000 + nperseg, dtype=np.float32)
     p = {"nperseg": nperseg, "noverlap": noverlap, "fs": 500000, "window": window,
          "scaling": "density", "detrend": "linear", "eps": 1e-11}
-    S = pipeline_data.specgr_batch(_gpu(x, gpu_device), p).double().cpu().numpy()
+    S = pipeline_data.specgr_batch(_gpu(x, gpu_device), p, exact=exact).double().cpu().numpy()
     truth, _, _ = ref.specgr_arrays(x.astype(np.float64), p)
     assert S.shape == truth.shape
     assert np.abs(S - truth).max() <= TOL_NORM

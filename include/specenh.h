@@ -69,8 +69,9 @@ long long specenh_launch_count(void);
 const char* specenh_kernel_name_at(long long index);
 
 /* Make stream `waiter` wait for the work enqueued on stream `signaler` so far (both
- * hipStream_t of the current device; no reference counterpart: the AE backward's fork and
- * join of its weight-gradient stream). The event is recorded without the system-scope fence
+ * hipStream_t of one device, not necessarily the current one: the event lives on the
+ * signaler's device; no reference counterpart: the AE backward's fork and join of its
+ * weight-gradient stream). The event is recorded without the system-scope fence
  * (hipEventDisableSystemFence) when `device_scope` is nonzero: both streams are on one
  * device. Events come from a per-device ring (hipEventDisableTiming). */
 int specenh_stream_wait(void* waiter, void* signaler, int device_scope);
@@ -299,8 +300,11 @@ int specenh_convt_conv_out(int dtype, const void* x, int N, int H, int W, int C,
 
 /* Training form of specenh_convt_conv_out (Model.fit's forward through the same two layers,
  * manual_scan_3layers.py:197-199, :213): the row-sweep launch also stores the ReLU'd CO-channel
- * map (dtype [N][2H][2W][CO], rounded exactly as the unfused Conv2DTranspose stores it: the
- * backward's ReLU mask and weight-gradient input), the fp32 logits [N][2H][2W] (the BCE input)
+ * map (dtype [N][2H][2W][CO]: the backward's ReLU mask and weight-gradient input; the same
+ * products as the unfused Conv2DTranspose summed in a different fp32 order, so a few elements
+ * can differ from its store by one rounding step of dtype, and training is not bitwise the
+ * unfused path's: SPECENH_NO_TAIL_TRAIN=1 selects the two launches when bitwise parity with
+ * them is needed), the fp32 logits [N][2H][2W] (the BCE input)
  * and the sigmoid output in dtype [N][2H][2W]. W = 64 only (the reference model at 128 x 128),
  * else SPECENH_EUNSUPPORTED (use the two specenh_conv2d launches). */
 int specenh_convt_conv_out_train(int dtype, const void* x, int N, int H, int W, int C,

@@ -115,9 +115,12 @@ int specenh_stream_wait(void* waiter, void* signaler, int device_scope) {
   static std::mutex mu;
   static hipEvent_t ring[kMaxDevices][2][kEvents] = {};
   static int next[kMaxDevices][2] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices)
-    return set_error(SPECENH_EHIP, "stream_wait: no current device");
+  // The ring and the event belong to the signaler's device, not the thread's current one
+  // (an engine on cuda:1 may run while the current device is 0).
+  int dev = 0, cur = 0;
+  if (hipStreamGetDevice((hipStream_t)signaler, &dev) != hipSuccess || dev < 0 ||
+      dev >= kMaxDevices || hipGetDevice(&cur) != hipSuccess)
+    return set_error(SPECENH_EHIP, "stream_wait: no device for the signaler stream");
   const int kind = device_scope ? 1 : 0;
   hipEvent_t ev;
   {
@@ -126,7 +129,13 @@ int specenh_stream_wait(void* waiter, void* signaler, int device_scope) {
     next[dev][kind] = (next[dev][kind] + 1) % kEvents;
     if (!e) {
       const unsigned fl = hipEventDisableTiming | (device_scope ? hipEventDisableSystemFence : 0u);
-      if (hipEventCreateWithFlags(&e, fl) != hipSuccess) {
+      // events are created on the current device: switch to the signaler's for the creation
+      const bool sw = cur != dev;
+      if (sw && hipSetDevice(dev) != hipSuccess)
+        return set_error(SPECENH_EHIP, "stream_wait: hipSetDevice");
+      const hipError_t ce = hipEventCreateWithFlags(&e, fl);
+      if (sw) (void)hipSetDevice(cur);
+      if (ce != hipSuccess) {
         e = nullptr;
         return set_error(SPECENH_EHIP, "stream_wait: hipEventCreateWithFlags");
       }

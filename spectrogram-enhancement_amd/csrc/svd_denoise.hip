@@ -3319,7 +3319,12 @@ int eig_denoise(const float* A, long long batch, int m, int n, long long a_strid
     // fallback (on: the flagged few): a grid of at most two workgroups per CU looping over
     // the matrices instead of one per matrix (gram64_kernel's comment)
     const unsigned gm = on ? (unsigned)std::min<long long>(nb, 2LL * device_cus()) : (unsigned)nb;
-    if (on && opt_mode < 0 && SPECENH_EIG_MERGED && variant(V_EIG_SPLIT) == 0) {
+    // The merged one-workgroup-per-matrix fallback was A/B'd at C5's size (128 x 128, a few
+    // flagged matrices); a large matrix (C3: 513 x 256) puts its whole Gram, tridiagonal
+    // solve and reconstruction on one workgroup per CU, which loses to the split launches'
+    // tile-parallel grids once many matrices are flagged. Merged only while r * Kr is small.
+    const bool merged_fits = (long long)r * Kr <= 128LL * 128;
+    if (on && opt_mode < 0 && merged_fits && SPECENH_EIG_MERGED && variant(V_EIG_SPLIT) == 0) {
       const hipError_t e = launch_eig_fallback(odt, xv, Kr, r, G64, nts64, dd, ee, tau, lo, hi,
                                                Z, fac, L.ld, kinfo,
                                                static_cast<char*>(out) + (size_t)(b0 * ob) * osz,

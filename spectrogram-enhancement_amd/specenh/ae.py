@@ -361,11 +361,14 @@ class AutoencoderEngine:
 
     def forward(self, x, train=False, timing=None, kernels=None):
         """x: device [N, H, W, C] in the compute dtype. Returns the output buffer
-        (fp32 for inference, compute dtype for training; reused between calls).
+        (fp32 for inference, compute dtype for training; reused between calls), except for
+        an inference batch above the int32 element cap of one launch: that batch runs in
+        consecutive slices and the result is a newly allocated tensor.
         ``timing``: optional list; a (start, end) pair of torch.cuda.Event recorded on the
         launch stream is appended around every convolution launch. ``kernels``: optional
         list; the symbol of each such launch's kernel is appended (the key of its PMC
-        record, tools/pmc_fold.py)."""
+        record, tools/pmc_fold.py). Neither can be given with a batch above the cap (one
+        launch per layer is what they describe): ValueError."""
         N = x.shape[0]
         if x.dtype != self.tdt or not x.is_contiguous() or tuple(x.shape[1:]) != self.input_shape:
             raise ValueError(f"forward expects a contiguous {self.tdt} [N, *{self.input_shape}]")
@@ -373,7 +376,11 @@ class AutoencoderEngine:
         # (e.g. the 64-channel manual_scan.py model at 256 x 128) run in consecutive slices
         per = max(h * w * c for h, w, c in self.shapes())
         cap = (2 ** 31 - 1) // per
-        if N > cap and not train and timing is None and kernels is None:
+        if N > cap and (timing is not None or kernels is not None):
+            raise ValueError(f"batch {N} exceeds one launch's int32 element cap ({cap} samples "
+                             f"of this model): it cannot be timed or profiled as one launch "
+                             f"per layer; pass at most {cap} samples")
+        if N > cap and not train:
             out = None
             for s0 in range(0, N, cap):
                 y = self.forward(x[s0:s0 + cap])

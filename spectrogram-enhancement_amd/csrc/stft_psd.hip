@@ -50,6 +50,9 @@
 #ifndef SPECENH_STFT_PF_AFTER_WAIT
 #define SPECENH_STFT_PF_AFTER_WAIT 1
 #endif
+#ifndef SPECENH_STFT_BUFPAD
+#define SPECENH_STFT_BUFPAD 1  // bank offset between the FFT buffers of one 32-lane half
+#endif
 #ifndef SPECENH_STFT_PF_EARLY
 #define SPECENH_STFT_PF_EARLY 0
 #endif
@@ -150,8 +153,13 @@ struct Layout {
   static constexpr int TS = TILE_SWZ ? TF : TF + 1;
   static constexpr int NBINS = N / 2 + 1;
   static constexpr int IB = (NBINS + G - 1) / G;     // bins per lane in the epilogue
-  // per-FFT exchange buffer: N padded FLOATS (real and imaginary parts take turns)
-  static constexpr int BUF = N + N / 32;
+  // per-FFT exchange buffer: N padded FLOATS (real and imaginary parts take turns), plus a
+  // bank offset between the FFTs that share a 32-lane half (G = 8, 16): at BUF = N + N/32 the
+  // neighbouring FFTs' contiguous 16-element reads overlapped on 8 banks (2-way conflicts in
+  // every exchange read); the extra 4 / 8 floats put them on disjoint banks (tools/lds_banks.py:
+  // N = 256 exchange reads 284 -> 160 LDS cycles per FFT pass pair, writes unchanged)
+  static constexpr int BUF =
+      N + N / 32 + (SPECENH_STFT_BUFPAD ? (G == 16 ? 8 : (G == 8 ? 4 : 0)) : 0);
   static constexpr int BUF_BYTES = FFTS * BUF * 4;
   static constexpr int TILE_BYTES = NBINS * TS * 4;  // aliases the FFT buffers
   static constexpr int TWN = TwOff<N>::TOTAL;

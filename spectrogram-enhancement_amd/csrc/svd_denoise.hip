@@ -1862,12 +1862,37 @@ __global__ __launch_bounds__(256, 2) void recon_stream_kernel(
 // subspace kernel: sqrt(theta_1) ||G v - theta_1 v|| <= tolv (theta_1 - theta_2) ||X||_F
 // with G v = Y q_1. A matrix that fails it after TOP1_MAX_ROUNDS is flagged for the fp64
 // eigen path (its output is overwritten there).
+#ifndef SPECENH_TOP1_SWZ
+#define SPECENH_TOP1_SWZ 1  // round 6: bank-conflict-free LDS layouts (tools/lds_banks.py)
+#endif
 namespace top1 {
 constexpr int N = 128;              // X tile (rows k, columns i), zero-padded
 constexpr int LD = N + 4;           // LDS row pitch in words: conflict-free row walks
 constexpr int MAX_ROUNDS = 24;
-// X | Zt (4 x N, basis transposed) | U (N x 4) | part (4 waves x N x 4) | reduction scratch
-constexpr size_t LDS_BYTES = (size_t)N * LD * 4 + 4 * N * 4 + N * 4 * 4 + 4 * N * 4 * 4 + 64 * 8;
+// Zt row pitch and element offset. With SPECENH_TOP1_SWZ 4 pad words follow every 64
+// columns, so the X Z phase's basis reads of chunks c and c + 16 (one ds_read_b128 lane
+// group) land 4 banks apart instead of on the same 4 banks.
+constexpr int ZP = SPECENH_TOP1_SWZ ? N + 8 : N;
+__host__ __device__ constexpr int zt(int p, int k) {
+  return p * ZP + k + (SPECENH_TOP1_SWZ ? 4 * (k >> 6) : 0);
+}
+// The per-wave partial sums of Y = X^T U: row i at slot pos(i). The writers (lane (cc, h):
+// rows 4 cc + 2 h + {0, 1}, two ds_write_b128) were 4-way conflicted at slot = i; the XOR of
+// bits 3-5 into bits 0-2 keeps every 8-lane write group on 8 distinct 16-byte slots and stays
+// inside the row's 8-row block (the same wave's range for the reduction's readers).
+__device__ __forceinline__ int ppos(int i) { return SPECENH_TOP1_SWZ ? i ^ ((i >> 3) & 7) : i; }
+// X Z phase: the float4 column chunk of lane column group g (0..7) in k-step j (0..3). Each
+// ds_read_b128 lane group holds g in {0..3} or {4..7} with 4 rows kb each; the chunks of
+// g = 0, 1 share a 16-bank quarter, g = 2, 3 the opposite one, all four the same chunk
+// residue mod 4: 64 distinct banks per group (the old mapping 8 (g & 1) + (g >> 1) + ... put
+// two addresses on one bank in every group).
+__device__ __forceinline__ int xz_chunk(int g, int j) {
+  if (SPECENH_TOP1_SWZ)
+    return 2 * (j >> 1) + (g >> 2) + 4 * ((j & 1) + 2 * ((g >> 1) & 1)) + 16 * (g & 1);
+  return 8 * (g & 1) + (g >> 1) + 16 * (j & 1) + 4 * (j >> 1);
+}
+// X | Zt (4 x ZP, basis transposed) | U (N x 4) | part (4 waves x N x 4) | reduction scratch
+constexpr size_t LDS_BYTES = (size_t)N * LD * 4 + 4 * ZP * 4 + N * 4 * 4 + 4 * N * 4 * 4 + 64 * 8;
 
 
 // 1/sqrt(d) for d > 0: v_rsq_f64 plus one Newton step (the factors below only need to be
@@ -1999,8 +2024,11 @@ __device__ __forceinline__ void bsum128(double (&v)[NV], double* sR) {
 
 // Gram entries of the 128-row blocks, fp64: value j < NV is sum_i A[i][a] A[i][b] for the
 // pair n = j % 10 of the upper triangle of block j / 10 (0: Y, 1: Z, 2: U). Thread
-// (j, chunk c) sums 16 rows, the 8 chunks meet through DPP inside each 8-lane group; every
-// thread returns all NV sums. Y and U are row-major N x 4, Z transposed (4 x N).
+// (j, c) sums 16 rows, the 8 partial sums meet through DPP inside each 8-lane group; every
+// thread returns all NV sums. Y and U are row-major N x 4, Z transposed (4 x ZP). With
+// SPECENH_TOP1_SWZ thread c takes rows 8 i + c (the 8 lanes of one j on 8 banks); the
+// contiguous 16-row chunks (rows 16 c + i) put them on ONE bank of the row-major blocks
+// (8-way: 1,936 of 2,192 LDS cycles of a check round, tools/lds_banks.py).
 template <int NV>
 __device__ __forceinline__ void gram_sums(const float* sY, const float* sZt, const float* sU,
                                           double* sRed) {
@@ -2010,12 +2038,13 @@ __device__ __forceinline__ void gram_sums(const float* sY, const float* sZt, con
     const int n = j % 10, src = j / 10;
     const int a = (int)((0x3221110000ULL >> (4 * n)) & 15);
     const int b = (int)((0x3323213210ULL >> (4 * n)) & 15);
-    const float* base = src == 0 ? sY : (src == 1 ? sZt : sU);
-    const int rs = src == 1 ? 1 : 4;
-    const float* pa = base + (src == 1 ? a * N : a) + 16 * c * rs;
-    const float* pb = base + (src == 1 ? b * N : b) + 16 * c * rs;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) s = fma((double)pa[i * rs], (double)pb[i * rs], s);
+    for (int i = 0; i < 16; ++i) {
+      const int row = SPECENH_TOP1_SWZ ? 8 * i + c : 16 * c + i;
+      const float va = src == 0 ? sY[4 * row + a] : (src == 1 ? sZt[zt(a, row)] : sU[4 * row + a]);
+      const float vb = src == 0 ? sY[4 * row + b] : (src == 1 ? sZt[zt(b, row)] : sU[4 * row + b]);
+      s = fma((double)va, (double)vb, s);
+    }
   }
   s += dpp64<0xB1>(s);   // quad_perm [1, 0, 3, 2]
   s += dpp64<0x4E>(s);   // quad_perm [2, 3, 0, 1]
@@ -2058,8 +2087,8 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
 #endif
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* sX = reinterpret_cast<float*>(smem);  // N x LD
-  float* sZt = sX + N * LD;                     // 4 x N
-  float* sU = sZt + 4 * N;                      // N x 4
+  float* sZt = sX + N * LD;                     // 4 x ZP
+  float* sU = sZt + 4 * ZP;                     // N x 4
   float* sP = sU + 4 * N;                       // 4 x N x 4
   double* sR = reinterpret_cast<double*>(sP + 16 * N);  // 64
   double* vd = reinterpret_cast<double*>(sP);  // N: final v (fp64), after the iteration
@@ -2112,7 +2141,7 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
 #pragma unroll
     for (int p = 0; p < 4; ++p)  // column 0 all ones (close to v1 for the non-negative
                                    // log spectrograms), the others pseudo-random
-      sZt[p * N + tid] = tid < r ? (p == 0 ? 1.f : hash_unit(tid, p)) : 0.f;
+      sZt[zt(p, tid)] = tid < r ? (p == 0 ? 1.f : hash_unit(tid, p)) : 0.f;
   lds_sync();
   const double tr = (sR[32] + sR[33]) + (sR[34] + sR[35]);
   T1_MARK(0);
@@ -2131,10 +2160,10 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
       for (int q = 0; q < 16; ++q) a[q] = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int c = 8 * (g & 1) + (g >> 1) + 16 * (j & 1) + 4 * (j >> 1);
+        const int c = xz_chunk(g, j);
         float4 zv[4];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) zv[p] = *reinterpret_cast<const float4*>(sZt + p * N + 4 * c);
+        for (int p = 0; p < 4; ++p) zv[p] = *reinterpret_cast<const float4*>(sZt + zt(p, 4 * c));
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const float4 xv = *reinterpret_cast<const float4*>(sX + (kb + 32 * m) * LD + 4 * c);
@@ -2196,16 +2225,17 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
         const float keep = h ? a[8 + q] : a[q], send = h ? a[q] : a[8 + q];
         a8[q] = keep + __shfl_xor(send, 32);
       }
-      float* dst = sP + w * 4 * N + 4 * (4 * cc + 2 * h);
-      *reinterpret_cast<float4*>(dst) = make_float4(a8[0], a8[1], a8[2], a8[3]);
-      *reinterpret_cast<float4*>(dst + 4) = make_float4(a8[4], a8[5], a8[6], a8[7]);
+      float* dst = sP + w * 4 * N;
+      *reinterpret_cast<float4*>(dst + 4 * ppos(4 * cc + 2 * h)) = make_float4(a8[0], a8[1], a8[2], a8[3]);
+      *reinterpret_cast<float4*>(dst + 4 * ppos(4 * cc + 2 * h + 1)) = make_float4(a8[4], a8[5], a8[6], a8[7]);
     }
     lds_sync();
     if (tid < N) {
-      float4 s = *reinterpret_cast<const float4*>(sP + 4 * tid);
+      const int pt = ppos(tid);
+      float4 s = *reinterpret_cast<const float4*>(sP + 4 * pt);
 #pragma unroll
       for (int ww = 1; ww < 4; ++ww) {
-        const float4 o = *reinterpret_cast<const float4*>(sP + ww * 4 * N + 4 * tid);
+        const float4 o = *reinterpret_cast<const float4*>(sP + ww * 4 * N + 4 * pt);
         s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
       }
       y[0] = s.x; y[1] = s.y; y[2] = s.z; y[3] = s.w;
@@ -2213,7 +2243,7 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
       const float4 u4 = *reinterpret_cast<const float4*>(sU + 4 * tid);
       uk[0] = u4.x; uk[1] = u4.y; uk[2] = u4.z; uk[3] = u4.w;
 #pragma unroll
-      for (int p = 0; p < 4; ++p) z[p] = sZt[p * N + tid];
+      for (int p = 0; p < 4; ++p) z[p] = sZt[zt(p, tid)];
     } else {
 #pragma unroll
       for (int p = 0; p < 4; ++p) y[p] = z[p] = uk[p] = 0.f;
@@ -2324,7 +2354,7 @@ __global__ __launch_bounds__(256, 2) void top1_kernel(XView x, int Kr, int r, fl
       for (int p = 0; p < 4; ++p) yd[p] = y[p];
       solve_row(L, ri, yd, zd);
 #pragma unroll
-      for (int p = 0; p < 4; ++p) sZt[p * N + tid] = (float)zd[p];
+      for (int p = 0; p < 4; ++p) sZt[zt(p, tid)] = (float)zd[p];
     }
     lds_sync();
     T1_MARK(3);

@@ -291,7 +291,10 @@ int specenh_cast(int src_dtype, const void* src, int dst_dtype, void* dst, long 
  * with wt_gemm / bt and wo_gemm / bo the two layers' specenh_conv2d weights (GEMM layout,
  * dtype) and fp32 biases (device pointers). The CO-channel map between the layers stays
  * in LDS; it is rounded to dtype after the ReLU exactly as the two-launch path stores it.
- * dtype BF16 / F16; C = 32, CO = 16, kt = ko = 5 (the reference model), otherwise
+ * dtype BF16 / F16; C = 32 with CO = 16, kt = ko = 5 (the reference model,
+ * manual_scan_3layers.py:197-199), or, on W = 64 inputs, CO = 32, kt = ko in {3, 5, 7} (the
+ * 32/32 models of hyperparam_scan.py:160-162 at their 256 x 128 inputs) or CO = 64,
+ * kt = ko in {3, 5} (manual_scan.py:198-199); otherwise
  * SPECENH_EUNSUPPORTED (use the two specenh_conv2d launches). */
 int specenh_convt_conv_out(int dtype, const void* x, int N, int H, int W, int C,
                            const void* wt_gemm, const float* bt, int CO, int kt,

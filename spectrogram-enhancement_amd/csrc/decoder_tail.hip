@@ -1250,6 +1250,14 @@ extern "C" int specenh_convt_conv_out_train(int dtype, const void* x, int N, int
   return launch_tail_rows<true>(dtype, r, (hipStream_t)stream);
 }
 
+namespace specenh {
+// tail_rows_g.hip: the reference's other autoencoders' tails (CO = 32, k = 3 / 5 / 7)
+bool tail_rows_general_supported(int C, int CO, int kt, int ko, int W);
+int tail_rows_general(int dtype, const void* x, int N, int H, int W, int C, const void* wt,
+                      const float* bt, int CO, int kt, const void* wo, const float* bo, int ko,
+                      float* out, hipStream_t st, bool* launched);
+}  // namespace specenh
+
 extern "C" int specenh_convt_conv_out(int dtype, const void* x, int N, int H, int W, int C,
                                       const void* wt_gemm, const float* bt, int CO_, int kt,
                                       const void* wo_gemm, const float* bo, int ko, float* out,
@@ -1257,11 +1265,19 @@ extern "C" int specenh_convt_conv_out(int dtype, const void* x, int N, int H, in
   if (N < 0 || H <= 0 || W <= 0) return set_error(SPECENH_EINVAL, "bad input shape");
   if (dtype != SPECENH_DTYPE_F16 && dtype != SPECENH_DTYPE_BF16)
     return set_error(SPECENH_EUNSUPPORTED, "fused decoder tail: fp16 / bf16 only");
+  hipStream_t st = (hipStream_t)stream;
+  if (tail_rows_general_supported(C, CO_, kt, ko, W)) {
+    if (N == 0) return SPECENH_OK;
+    bool launched = false;
+    const int rc = tail_rows_general(dtype, x, N, H, W, C, wt_gemm, bt, CO_, kt, wo_gemm, bo, ko,
+                                     out, st, &launched);
+    if (rc != SPECENH_OK || launched) return rc;
+  }
   if (C != CI || CO_ != CO || kt != KT || ko != KO)
     return set_error(SPECENH_EUNSUPPORTED,
-                     "fused decoder tail: Conv2DTranspose(16, 5) on 32 channels + Conv2D(1, 5)");
+                     "fused decoder tail: Conv2DTranspose(16, 5) on 32 channels + Conv2D(1, 5), "
+                     "or Conv2DTranspose(32, k) + Conv2D(1, k), k = 3 / 5 / 7, on 64-wide inputs");
   if (N == 0) return SPECENH_OK;
-  hipStream_t st = (hipStream_t)stream;
   if (W == rows::QW && variant(V_TAIL_TILES) == 0) {  // the row-sweep kernel
     if (!x || !wt_gemm || !bt || !wo_gemm || !bo || !out) return set_error(SPECENH_EINVAL, "null pointer");
     if ((long long)N * H * W * C >= (1ll << 31) || (long long)N * 4 * H * W >= (1ll << 31))

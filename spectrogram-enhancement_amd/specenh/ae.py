@@ -157,12 +157,14 @@ class AutoencoderEngine:
                      and last2[1].cout == 1 and last2[1].act == "sigmoid"
                      and last2[1].padding == "same"
                      and tail_supported(self.tdt, last2[0].cin, last2[0].cout, last2[0].k,
-                                        last2[1].k)
+                                        last2[1].k, self.shapes()[len(self.ops) - 2][1])
                      and os.environ.get("SPECENH_NO_TAIL_FUSION", "0") in ("", "0"))
         # training: the same two layers as one row-sweep launch that also stores the map (the
         # backward's mask and weight-gradient input), the logits and the output
         # (decoder_tail.hip tail_rows_kernel<T, true>), at 64-position-wide inputs
         self.tail_train = (self.tail and self.shapes()[len(self.ops) - 2][1] == 64
+                           and (last2[0].cin, last2[0].cout, last2[0].k, last2[1].k)
+                           == (32, 16, 5, 5)
                            and os.environ.get("SPECENH_NO_TAIL_TRAIN", "0") in ("", "0"))
         # inference: the last THREE layers (Conv2DTranspose x2 + Conv2D(1)) as one launch
         # (csrc/decoder_tail.hip decoder3_kernel) when the shapes are the reference model's

@@ -495,9 +495,18 @@ def decoder3_supported(dtype: torch.dtype, cin: int, cout1: int, cout2: int, k: 
         (64, 32, 16, 5, 32)
 
 
-def tail_supported(dtype: torch.dtype, cin: int, cout: int, kt: int, ko: int) -> bool:
-    """specenh_convt_conv_out's configurations (the reference model's last two layers)."""
-    return dtype in (torch.float16, torch.bfloat16) and (cin, cout, kt, ko) == (32, 16, 5, 5)
+def tail_supported(dtype: torch.dtype, cin: int, cout: int, kt: int, ko: int,
+                   w_in: int | None = None) -> bool:
+    """specenh_convt_conv_out's configurations: the reference model's last two layers
+    (32 -> 16, k 5, any width), and the 32 -> 32 tails of the hyperparameter-scan models
+    (k = 3 / 5 / 7) and manual_scan.py's 32 -> 64 (k = 3 / 5) on 64-position-wide inputs
+    (csrc/tail_rows_g.hip)."""
+    if dtype not in (torch.float16, torch.bfloat16):
+        return False
+    if (cin, cout, kt, ko) == (32, 16, 5, 5):
+        return True
+    return w_in == 64 and cin == 32 and kt == ko and ((cout == 32 and kt in (3, 5, 7)) or
+                                                       (cout == 64 and kt in (3, 5)))
 
 
 # ---------------------------------------------------------------- pooling, loss, optimizer

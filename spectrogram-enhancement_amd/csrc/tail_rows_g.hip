@@ -34,8 +34,13 @@
 #include <mutex>
 #include <string>
 
+#include "lds_dma.hpp"
 #include "specenh.h"
 #include "runtime.hpp"
+
+#ifndef SPECENH_TAILG_PYSPLIT
+#define SPECENH_TAILG_PYSPLIT 0
+#endif
 
 namespace specenh {
 int set_error(int code, const std::string& msg);  // stft_psd.hip
@@ -139,9 +144,16 @@ struct TG {
   static constexpr int HO = KO / 2;
   static constexpr int L = (HO + 1) / 2;  // output pair Y = 2q - 2L: map rows Y - HO .. Y + 1 + HO <= 2q + 1
   static constexpr int P = HO + 1;        // map-row pairs of one output pair
-  static constexpr int NEED_X = NDY + 1;  // input rows live in a step (+ the one staged)
+  // input staging: LDS-DMA two rows ahead when the tap fragments leave no registers for a
+  // prefetch (CO = 64, k = 5: 36 instead of 46 spilled VGPRs; the others ran 4-13 % slower
+  // with it, profiles/r06_ae_layers_variants_b.txt), else a register prefetch two rows ahead
+  // stored one row ahead
+  static constexpr bool DMA = CO == 64 && NTAP * CPW > 40;
+  static constexpr int NEED_X = NDY + (DMA ? 2 : 1);  // input rows live in a step
   static constexpr int NEED_M = 2 * L + HO + 2;  // map rows live in a step
-  static constexpr int XST = 48;                 // input pixel stride (elements): 96 B
+  // input pixel stride: dense 64 B with swizzled groups (DMA: lane-linear rows), else 96 B
+  // (conflict-free unswizzled reads, the dx shifts then immediates)
+  static constexpr int XST = DMA ? CI : 48;
   static constexpr int XROW = (QW + NDY - 1) * XST;
   static constexpr int MROW = MW * CO;
   static constexpr int NSC = 2 * KO;  // scratch rows n = KO r + kx
@@ -150,6 +162,7 @@ struct TG {
   // Conv2D(1) weight fragments: in registers unless the tap fragments leave no room
   static constexpr bool WO_LDS = NTAP * CPW * 4 + P * CPW * 4 > 200;
   static constexpr int WO_BYTES = WO_LDS ? NCB * P * 64 * 16 : 0;
+  static constexpr int BIAS_BYTES = CO * 4;
   // ring sizes and the unroll period: input ring NXR (| UU), map ring NMR (| 2 UU), within LDS
   struct Plan {
     int nx, nm, u;
@@ -159,10 +172,10 @@ struct TG {
     long best_lds = 1L << 40;
     for (int nx = NEED_X; nx <= NEED_X + 4; ++nx)
       for (int nm2 = (NEED_M + 1) / 2; nm2 <= (NEED_M + 1) / 2 + 4; ++nm2) {
-        const long lds = (long)nx * XROW * 2 + 2L * nm2 * MROW * 2 + SC_BYTES + WO_BYTES;
+        const long lds = (long)nx * XROW * 2 + 2L * nm2 * MROW * 2 + SC_BYTES + WO_BYTES + BIAS_BYTES;
         if (lds > 160L * 1024) continue;
         int u = lcm_c(nx, nm2);
-        if (u % 2) u *= 2;  // even: the two prefetch register sets alternate with q
+        if (!DMA && u % 2) u *= 2;  // even: the two prefetch register sets alternate with q
         if (u < best.u || (u == best.u && lds < best_lds)) {
           best = Plan{nx, 2 * nm2, u};
           best_lds = lds;
@@ -174,13 +187,24 @@ struct TG {
   static constexpr int LDS_X = NXR * XROW * 2, LDS_M = NMR * MROW * 2;
   static constexpr int OFF_SC = LDS_X + LDS_M;
   static constexpr int OFF_WO = OFF_SC + SC_BYTES;
-  static constexpr int LDS_BYTES = OFF_WO + WO_BYTES;
+  static constexpr int OFF_BIAS = OFF_WO + WO_BYTES;
+  static constexpr int LDS_BYTES = OFF_BIAS + BIAS_BYTES;
   static_assert(NXR > 0 && UU <= 12, "no ring plan fits the LDS");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
   static_assert(CO % 16 == 0 && NCB % CPW == 0, "channel blocks");
   static_assert(2 * KO <= 16, "Conv2D(1) N columns (r, kx)");
   static constexpr int SWM = CO / 8 - 1;
+  static constexpr bool PYSPLIT = SPECENH_TAILG_PYSPLIT ? NTAP * CPW * 4 > 150 : DMA;
 };
+
+// input ring pixel P (stored x - DY0), 8-channel group g (16 B): g XOR ((P >> 1) & 3), so the
+// B-fragment reads (16 consecutive pixels, one group) are conflict-free at any pixel offset
+// (tools/lds_banks.py); the rows arrive by LDS-DMA (lane-linear) with the swizzle applied on
+// the source side
+template <bool DMA>
+__device__ __forceinline__ int xoff(int P, int g) {
+  return DMA ? P * 32 + 8 * (g ^ ((P >> 1) & 3)) : P * 48 + 8 * g;
+}
 
 // map pixel col, 4-channel group g (8 B): g XOR 2 ((col >> 1) & (CO/8 - 1)) keeps the 16-byte
 // pairs (2k, 2k + 1) the Conv2D(1) A reads take together and spreads both the epilogue's
@@ -212,6 +236,7 @@ __global__ __launch_bounds__((TG<CO, KT, KO>::THREADS)) void tailg_kernel(TGArgs
   T* const mr = reinterpret_cast<T*>(lds + C::LDS_X);
   float* const sc = reinterpret_cast<float*>(lds + C::OFF_SC);
   uint4* const wol = reinterpret_cast<uint4*>(lds + C::OFF_WO);
+  float* const sbias = reinterpret_cast<float*>(lds + C::OFF_BIAS);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -224,7 +249,6 @@ __global__ __launch_bounds__((TG<CO, KT, KO>::THREADS)) void tailg_kernel(TGArgs
 
   // ---- resident fragments ----
   uint4 wt[CPW][NTAP];
-  f32x4 bias[CPW];
   {
     const T* __restrict__ Wt = reinterpret_cast<const T*>(a.wt);
 #pragma unroll
@@ -239,8 +263,6 @@ __global__ __launch_bounds__((TG<CO, KT, KO>::THREADS)) void tailg_kernel(TGArgs
             if (C::tap(ph, dy, dx))
               wt[cb][C::tap_index(ph, dy, dx)] = *reinterpret_cast<const uint4*>(
                   Wt + ((co * KT + C::ky_of(ph >> 1, dy)) * KT + C::ky_of(ph & 1, dx)) * CI + 8 * kg);
-      const int c4 = 16 * (cg * CPW + cb) + 4 * kg;
-      bias[cb] = f32x4{a.bt[c4], a.bt[c4 + 1], a.bt[c4 + 2], a.bt[c4 + 3]};
     }
   }
   // Conv2D(1) B fragment of map-row pair p, channel block cbabs: n = m = KO r + kx,
@@ -267,72 +289,118 @@ __global__ __launch_bounds__((TG<CO, KT, KO>::THREADS)) void tailg_kernel(TGArgs
   if constexpr (C::WO_LDS) {  // [cbabs][p][lane] fragments, written after the zeroing
     for (int f = wv; f < C::NCB * P; f += C::NW) wol[f * 64 + lane] = wo_frag(f % P, f / P);
   }
+  for (int c = tid; c < CO; c += C::THREADS) sbias[c] = a.bt[c];
   // the launch-resident loads have landed (otherwise their wait sits inside the step loop and
-  // drains the prefetch every step)
+  // drains the ring's LDS-DMAs every step)
   __builtin_amdgcn_s_waitcnt(0x0F70);
 
-  // input staging: threads 0-255 move one row (64 pixels x 64 B) as 16 B each
-  const bool stager = tid < 256;
-  const int spix = (tid >> 2) & 63, scg = tid & 3;
-  const int xso = (spix - DY0) * C::XST + 8 * scg;
+  // input staging, waves 0-3: one row (64 pixels x 64 B) as one 1-KB LDS-DMA per wave (DMA:
+  // lane i -> pixel 16 wv + i / 4, stored group i & 3, source group swizzled), or as 16 B per
+  // thread from the register prefetch; rows outside the image are zero rows. stage() returns
+  // whether this wave issued a DMA (its vector-memory ledger).
+  const bool stager = wv < 4;
+  const int sx = C::DMA ? 16 * wv + (lane >> 2) : tid >> 2;  // (stager threads: tid < 256)
+  const int sP = sx - DY0;
+  const int sg = C::DMA ? (lane & 3) ^ ((sP >> 1) & 3) : (tid & 3);
+  const int xso = C::DMA ? 0 : xoff<false>(sP, sg);  // register staging: this thread's 16 B
+  auto stage = [&](int row, int slot) -> int {
+    T* dst = xr + slot * C::XROW + (16 * wv - DY0) * C::XST;  // wave-uniform, 16-B aligned
+    if (row >= 0 && row < H) {
+      lds_dma16(X + ((long long)row * C::QW + sx) * CI + 8 * sg, dst);
+      return 1;
+    }
+    *reinterpret_cast<uint4*>(dst + 8 * lane) = uint4{0u, 0u, 0u, 0u};
+    return 0;
+  };
   auto gload = [&](int row) -> uint4 {
     const int rr = min(max(row, 0), H - 1);
-    uint4 v = *reinterpret_cast<const uint4*>(X + ((long long)rr * C::QW + spix) * CI + 8 * scg);
+    uint4 v = *reinterpret_cast<const uint4*>(X + ((long long)rr * C::QW + sx) * CI + 8 * sg);
     if (row < 0 || row >= H) v = uint4{0u, 0u, 0u, 0u};
     return v;
   };
+  uint4 pre[C::DMA ? 1 : 2];
   if (stager) {
+    if constexpr (C::DMA) {
 #pragma unroll
-    for (int row = 0; row <= DY1; ++row)
-      if (row < H) *reinterpret_cast<uint4*>(xr + pmod(row, NXR) * C::XROW + xso) = gload(row);
+      for (int row = 0; row <= DY1 + 1; ++row) stage(row, pmod(row, NXR));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+#pragma unroll
+      for (int row = 0; row <= DY1; ++row)
+        *reinterpret_cast<uint4*>(xr + pmod(row, NXR) * C::XROW + xso) = gload(row);
+      pre[0] = gload(DY1 + 1);
+      pre[1] = gload(DY1 + 2);
+    }
   }
-  uint4 pre[2];
-  pre[0] = stager ? gload(DY1 + 1) : uint4{0u, 0u, 0u, 0u};
-  pre[1] = stager ? gload(DY1 + 2) : uint4{0u, 0u, 0u, 0u};
   lds_barrier();
 
-  // this lane's B-fragment offset (pixel 16 w + m, group kg) in an input ring row
-  const int xb = (16 * w + m - DY0) * C::XST + 8 * kg;
+  // this lane's B-fragment offsets (pixel 16 w + m + dx, group kg) in an input ring row
+  int xo[C::DMA ? C::NDY : 1];
+  if constexpr (C::DMA) {
+#pragma unroll
+    for (int dx = DY0; dx <= DY1; ++dx) xo[dx - DY0] = xoff<true>(16 * w + m + dx - DY0, kg);
+  } else {
+    xo[0] = xoff<false>(16 * w + m - DY0, kg);  // + dx * XST: an immediate
+  }
   // scratch: D of column block b at [cg][buf][n = m][4 + 16 b + 4 kg]; sums of waves 0-3
   const int ox = 32 * w + (lane & 31), orow = lane >> 5;
   const int NS = H + C::L;  // steps: output pairs Y = 0 .. 2H - 2
+  int st_prev = 0;          // this wave's output stores of the previous step (vmcnt ledger)
 
   auto step = [&](auto ic, const int q) {
     constexpr int I = decltype(ic)::value;
     if (q >= NS) return;  // uniform
+    // input row q + DY1 + 2 into its ring slot (needed from step q + 2 on; the slot held row
+    // q + DY1 + 2 - NXR < q + DY0: no step still running reads it)
+    int nd = 0;
+    if constexpr (C::DMA) nd = stager ? stage(q + DY1 + 2, pmod(I + DY1 + 2, NXR)) : 0;
     // ---- a. Conv2DTranspose of input row q -> map rows 2q, 2q + 1 ----
     T* const m0 = mr + pmod(2 * I, NMR) * C::MROW;
     T* const m1 = mr + pmod(2 * I + 1, NMR) * C::MROW;
     if (q < H) {
-      f32x4 acc[CPW][4];
+      // output row phases py = 0, 1 together (one B read per neighbourhood offset feeds all
+      // four phases), or one after the other when the taps leave no room for all 4 CPW
+      // accumulators (C::PYSPLIT: half the accumulators, the B fragments read twice)
 #pragma unroll
-      for (int cb = 0; cb < CPW; ++cb)
+      for (int half = 0; half < (C::PYSPLIT ? 2 : 1); ++half) {
+        constexpr int NPH = C::PYSPLIT ? 2 : 4;
+        const int ph0 = C::PYSPLIT ? 2 * half : 0;
+        f32x4 acc[CPW][NPH];
 #pragma unroll
-        for (int ph = 0; ph < 4; ++ph) acc[cb][ph] = bias[cb];
+        for (int cb = 0; cb < CPW; ++cb)
 #pragma unroll
-      for (int dy = DY0; dy <= DY1; ++dy) {
-        const T* src = xr + pmod(I + dy, NXR) * C::XROW + xb;
+          for (int j = 0; j < NPH; ++j)
+            acc[cb][j] = *reinterpret_cast<const f32x4*>(sbias + 16 * (cg * CPW + cb) + 4 * kg);
 #pragma unroll
-        for (int dx = DY0; dx <= DY1; ++dx) {
-          if (!C::any_tap(dy, dx)) continue;
-          const uint4 b = *reinterpret_cast<const uint4*>(src + dx * C::XST);
+        for (int dy = DY0; dy <= DY1; ++dy) {
+          const T* src = xr + pmod(I + dy, NXR) * C::XROW;
 #pragma unroll
-          for (int ph = 0; ph < 4; ++ph) {
-            if (!C::tap(ph, dy, dx)) continue;
+          for (int dx = DY0; dx <= DY1; ++dx) {
+            bool any = false;
 #pragma unroll
-            for (int cb = 0; cb < CPW; ++cb)
-              acc[cb][ph] = mfma<T>(wt[cb][C::tap_index(ph, dy, dx)], b, acc[cb][ph]);
+            for (int j = 0; j < NPH; ++j) any = any || C::tap(ph0 + j, dy, dx);
+            if (!any) continue;
+            const uint4 b = *reinterpret_cast<const uint4*>(
+                src + (C::DMA ? xo[C::DMA ? dx - DY0 : 0] : xo[0] + dx * C::XST));
+#pragma unroll
+            for (int j = 0; j < NPH; ++j) {
+              if (!C::tap(ph0 + j, dy, dx)) continue;
+#pragma unroll
+              for (int cb = 0; cb < CPW; ++cb)
+                acc[cb][j] = mfma<T>(wt[cb][C::tap_index(ph0 + j, dy, dx)], b, acc[cb][j]);
+            }
           }
         }
+#pragma unroll
+        for (int cb = 0; cb < CPW; ++cb)
+#pragma unroll
+          for (int j = 0; j < NPH; ++j) {
+            const int ph = ph0 + j;
+            const int col = 2 * (16 * w + m) + (ph & 1);
+            *reinterpret_cast<uint2*>(((ph >> 1) ? m1 : m0) +
+                                      moff<CO>(col, 4 * (cg * CPW + cb) + kg)) = relu_pack<T>(acc[cb][j]);
+          }
       }
-#pragma unroll
-      for (int cb = 0; cb < CPW; ++cb)
-#pragma unroll
-        for (int ph = 0; ph < 4; ++ph) {
-          const int col = 2 * (16 * w + m) + (ph & 1);
-          *reinterpret_cast<uint2*>(((ph >> 1) ? m1 : m0) +
-                                    moff<CO>(col, 4 * (cg * CPW + cb) + kg)) = relu_pack<T>(acc[cb][ph]);
-        }
     } else {  // below the image: the Conv2D(1) zero padding
 #pragma unroll
       for (int cb = 0; cb < CPW; ++cb)
@@ -372,8 +440,14 @@ __global__ __launch_bounds__((TG<CO, KT, KO>::THREADS)) void tailg_kernel(TGArgs
           *reinterpret_cast<f32x4*>(scb + m * C::SCW + 4 + 32 * w + 16 * blk + 4 * kg) = d;
       }
     }
-    // ---- c. input row q + DY1 + 1 into its ring slot ----
-    if (stager) *reinterpret_cast<uint4*>(xr + pmod(I + DY1 + 1, NXR) * C::XROW + xso) = pre[I & 1];
+    // ---- c. the DMA of step q - 1 (row q + DY1 + 1, read from step q + 1 on) has landed: wait
+    // for all but this wave's younger vector-memory ops (the previous step's store, this step's
+    // DMA) ----
+    if constexpr (C::DMA) {
+      if (stager) wait_vmcnt(st_prev + nd);
+    } else if (stager) {  // input row q + DY1 + 1 (loaded two steps ago) into its ring slot
+      *reinterpret_cast<uint4*>(xr + pmod(I + DY1 + 1, NXR) * C::XROW + xso) = pre[I & 1];
+    }
     lds_barrier();
     // ---- d. diagonal sums over the channel groups' partials, sigmoid, stores ----
     if (emit && wv < 4) {
@@ -386,7 +460,8 @@ __global__ __launch_bounds__((TG<CO, KT, KO>::THREADS)) void tailg_kernel(TGArgs
       }
       O[(long long)(Y + orow) * C::MW + ox] = __builtin_amdgcn_rcpf(1.f + __expf(-s));
     }
-    if (stager) pre[I & 1] = gload(q + DY1 + 3);
+    if constexpr (C::DMA) st_prev = emit && wv < 4 ? 1 : 0;
+    else if (stager) pre[I & 1] = gload(q + DY1 + 3);
   };
 
   for (int q0 = 0; q0 < NS; q0 += UU) {

@@ -1,14 +1,9 @@
-# round-6 GPU session: general decoder tail (tests + variant measurements)
+# round-6 GPU session: general decoder tail (DMA staging) tests + variant layer times
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-bash tools/gpu.sh s4 tests:tests/test_tail_general_gpu.py,tests/test_decoder_tail_gpu.py || exit 1
-bash tools/gpu.sh s4v "tests:tests/test_ae_gpu.py::test_reference_variants" || exit 1
+bash tools/gpu.sh s6 tests:tests/test_tail_general_gpu.py || exit 1
 for M in hyper_k3 hyper_k5 hyper_k7 manual_scan; do
-  timeout -k 10 200 python tools/ae_layers.py --model $M > gpurun_out/s4_layers_$M.txt 2>&1 || { tail -5 gpurun_out/s4_layers_$M.txt; exit 1; }
-  grep -v amdgpu.ids gpurun_out/s4_layers_$M.txt | python -c "import sys,json; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d['model'], d['total_ms'], [(l['kernel'][:40], l['ms']) for l in d['launches']])"
-done
-for M in hyper_k3 hyper_k5 hyper_k7 manual_scan; do
-  timeout -k 10 300 python tools/ae_bench.py --model $M --dtype fp16 > gpurun_out/s4_bench_$M.txt 2>&1 || { tail -5 gpurun_out/s4_bench_$M.txt; exit 1; }
-  grep -v amdgpu.ids gpurun_out/s4_bench_$M.txt | tail -1
+  timeout -k 10 200 python tools/ae_layers.py --model $M > gpurun_out/s6_layers_$M.txt 2>&1 || { tail -5 gpurun_out/s6_layers_$M.txt; exit 1; }
+  grep -v amdgpu.ids gpurun_out/s6_layers_$M.txt | python -c "import sys,json; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d['model'], d['total_ms'], [(l['kernel'][:40], l['ms']) for l in d['launches']])"
 done

@@ -2539,7 +2539,7 @@ int patch_cc(const ConvArgs& a, int nph) {
 // conv_rows.hip: inference Conv2D(5, relu, same) + MaxPooling2D(2) and Conv2DTranspose(5,
 // s2, relu, same) on 64 channels as row sweeps
 int conv_rows_pool(int dtype, const void* x, int N, int H, int W, int CI, const void* w,
-                   const float* b, int CO, void* out, hipStream_t st, bool* launched);
+                   const float* b, int CO, int K, void* out, hipStream_t st, bool* launched);
 int convt_rows(int dtype, const void* x, int N, int H, int W, int CI, const void* w,
                const float* b, int CO, void* out, hipStream_t st, bool* launched);
 int conv1_rows_pool(int dtype, const void* x, int N, int H, int W, const void* w,
@@ -2550,14 +2550,15 @@ int launch_fwd(const ConvArgs& a, int nph, hipStream_t st) {
   if constexpr (!__is_same(T, float)) {
     const Geo& g = a.g[0];
     if (nph == 1 && a.pool && !a.argmax && !a.mask && !a.logits && !a.out_f32 && a.act == 1 &&
-        a.bias && g.stride == 1 && g.KH == 5 && g.KW == 5 && g.pad_t == 2 && g.pad_l == 2 &&
+        a.bias && g.stride == 1 && (g.KH == 5 || g.KH == 3) && g.KW == g.KH &&
+        g.pad_t == g.KH / 2 && g.pad_l == g.KH / 2 &&
         g.OH == g.IH && g.OW == g.IW && g.ky0 == 0 && g.kx0 == 0 && g.kstep == 1 &&
-        g.KWf == 5 && g.Kf == 25 * g.C && g.oys == 1 && g.oxs == 1 && g.oy0 == 0 &&
+        g.KWf == g.KH && g.Kf == g.KH * g.KH * g.C && g.oys == 1 && g.oxs == 1 && g.oy0 == 0 &&
         g.ox0 == 0) {
       bool launched = false;
       const int rc = conv_rows_pool(__is_same(T, _Float16) ? SPECENH_DTYPE_F16 : SPECENH_DTYPE_BF16,
-                                    a.in, g.N, g.IH, g.IW, g.C, a.w, a.bias, g.CO, a.out, st,
-                                    &launched);
+                                    a.in, g.N, g.IH, g.IW, g.C, a.w, a.bias, g.CO, g.KH, a.out,
+                                    st, &launched);
       if (rc != SPECENH_OK || launched) return rc;
     }
     if (!(variant(V_CONV_NO_PATCH) != 0)) {

@@ -81,7 +81,7 @@ __device__ __forceinline__ float max_pair(float v) {
   return fmaxf(v, o);
 }
 
-template <int CIN, int COUT, int W>
+template <int CIN, int COUT, int W, int K = 5>
 struct RC {
   static constexpr int NWIN = W / 16;                 // 16-column windows
   static constexpr int NNB = COUT / 16;               // 16-channel blocks
@@ -91,13 +91,15 @@ struct RC {
   static constexpr int ROWB = (W + 4) * PIX;          // ring row: 2 zero pixels each side
   static constexpr int RING = 8;                      // rows (4 steps)
   static constexpr int LDS = RING * ROWB;
-  static constexpr int NW = CIN == 16 ? 13 : 25;      // resident weight fragments
+  static constexpr int NW = CIN == 16 ? 13 : K * K;   // resident weight fragments
+  static_assert(K == 5 || (CIN == 32 && (K == 3 || K == 5)), "kernel size");
   static constexpr int CPP = CIN / 8;                 // 16-byte groups per pixel
   static constexpr int CHUNKS = W * CPP;              // 16-byte chunks per row
-  static constexpr int DMA_WAVES = 2 * CHUNKS / 64;   // waves moving a step's two rows
+  static constexpr int WPR = CHUNKS / 64;             // waves moving one row (1 KB each)
+  static constexpr int DMA_WAVES = 2 * WPR;           // waves moving a step's two rows
   static_assert(WAVES == 8 && CHUNKS % 64 == 0 && DMA_WAVES <= WAVES, "shape");
-  // waves per SIMD the register budget is sized for (CIN = 32 holds 25 fragments)
-  static constexpr int WPE = CIN == 16 ? 4 : 2;
+  // waves per SIMD the register budget is sized for (CIN = 32 holds K^2 fragments)
+  static constexpr int WPE = CIN == 16 || K == 3 ? 4 : 2;
 };
 
 struct CRArgs {
@@ -108,11 +110,14 @@ struct CRArgs {
   int N, H;
 };
 
-template <typename T, int CIN, int COUT, int W>
-__global__ __launch_bounds__((RC<CIN, COUT, W>::THREADS))
-__attribute__((amdgpu_waves_per_eu(RC<CIN, COUT, W>::WPE)))
+// K (CIN = 32 only): the kernel size, 5 (the reference model) or 3 (hyperparam_scan.py's
+// k = 3 model): K^2 resident tap fragments, K B fragments per input row, output rows
+// r + K/2 - ky; the accumulator ring of 6 rows and the pooling lag are the same.
+template <typename T, int CIN, int COUT, int W, int K = 5>
+__global__ __launch_bounds__((RC<CIN, COUT, W, K>::THREADS))
+__attribute__((amdgpu_waves_per_eu(RC<CIN, COUT, W, K>::WPE)))
 void conv_rows_pool_kernel(CRArgs a) {
-  using C = RC<CIN, COUT, W>;
+  using C = RC<CIN, COUT, W, K>;
   extern __shared__ __attribute__((aligned(16))) unsigned char ring[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -135,11 +140,11 @@ void conv_rows_pool_kernel(CRArgs a) {
     const T* __restrict__ Wg = reinterpret_cast<const T*>(a.w);
     const int co = 16 * nb + m;
     auto tap = [&](int ky, int kx, int c8) {
-      return *reinterpret_cast<const uint4*>(Wg + ((co * 5 + ky) * 5 + kx) * CIN + c8);
+      return *reinterpret_cast<const uint4*>(Wg + ((co * K + ky) * K + kx) * CIN + c8);
     };
     if constexpr (CIN == 32) {
 #pragma unroll
-      for (int t = 0; t < 25; ++t) wf[t] = tap(t / 5, t % 5, 8 * kg);
+      for (int t = 0; t < K * K; ++t) wf[t] = tap(t / K, t % K, 8 * kg);
     } else {
       const int hi = kg >> 1, c8 = 8 * (kg & 1);
 #pragma unroll
@@ -156,13 +161,13 @@ void conv_rows_pool_kernel(CRArgs a) {
                            a.b[16 * nb + 4 * kg + 2], a.b[16 * nb + 4 * kg + 3]};
 
   // ---- this lane's B-fragment byte offsets within a ring row ----
-  int boff[5];
+  int boff[CIN == 32 ? K : 1];
   int foff = 0, foffw = 0, fo0 = 0;  // CIN = 16: F fragment (next row in the next slot /
                                      // wrapped), and its offset within one row
   if constexpr (CIN == 32) {
 #pragma unroll
-    for (int kx = 0; kx < 5; ++kx) {
-      const int ps = x0 + m + kx;  // stored pixel (x + 2)
+    for (int kx = 0; kx < K; ++kx) {
+      const int ps = x0 + m + kx + 2 - K / 2;  // stored pixel (x + 2)
       boff[kx] = ps * 64 + 16 * (kg ^ ((ps >> 1) & 3));
     }
   } else {
@@ -173,24 +178,24 @@ void conv_rows_pool_kernel(CRArgs a) {
     foffw = fo - (kg >> 1) * 7 * C::ROWB;  // row r in slot 7: row r + 1 in slot 0
   }
 
-  // ---- row DMA: waves 0 .. DMA_WAVES - 1, wave w moves half (w & 1) of row w >> 1 ----
+  // ---- row DMA: waves 0 .. DMA_WAVES - 1, wave w moves part w % WPR of row w / WPR ----
   const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
   const bool dma_wave = wv < C::DMA_WAVES;
   int dsrc = 0, ddst = 0;
   if (dma_wave) {
-    const int c = (wv & 1) * 64 + lane;  // chunk of the row
+    const int c = (wv % C::WPR) * 64 + lane;  // chunk of the row
     const int ps = 2 + c / C::CPP, gs = c % C::CPP;
     const int g = CIN == 32 ? (gs ^ ((ps >> 1) & 3)) : gs;
     dsrc = (ps - 2) * CIN + 8 * g;  // element offset within the image row
-    ddst = 2 * C::PIX + (wv & 1) * 1024;
+    ddst = 2 * C::PIX + (wv % C::WPR) * 1024;
   }
   // rows of global step s: image (s / SPI) of this workgroup, rows 2q, 2q + 1 (q = s % SPI)
   // rows of global step s = il SPI + q (the caller keeps (il, q) as scalar counters: a
   // run-time division per use cost ~25 SALU and a VALU reciprocal, three per step)
   auto stage_at = [&](int s, int il, int q) -> bool {  // whether this wave issued an LDS-DMA
     if (!dma_wave) return false;
-    const int r = 2 * q + (wv >> 1);
-    unsigned char* dst = ring + ((2 * s + (wv >> 1)) & 7) * C::ROWB + ddst;
+    const int r = 2 * q + wv / C::WPR;
+    unsigned char* dst = ring + ((2 * s + wv / C::WPR) & 7) * C::ROWB + ddst;
     if (s < S && il < nimg && r < H) {
       const long long n = (long long)blockIdx.x + (long long)il * G;
       lds_dma16(X + ((n * H + r) * W) * CIN + dsrc, dst);
@@ -250,7 +255,7 @@ void conv_rows_pool_kernel(CRArgs a) {
     if (il < nimg && 2 * q < H) {
       // every B fragment of the step first (one LDS latency per step, not one per row or
       // tap column: sched_barrier keeps the compiler from sinking the reads to their MFMAs)
-      constexpr int NB = CIN == 32 ? 5 : 3;
+      constexpr int NB = CIN == 32 ? K : 3;
       uint4 bf[2][NB];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -258,7 +263,7 @@ void conv_rows_pool_kernel(CRArgs a) {
         const unsigned char* rb = ring + rs * C::ROWB;
         if constexpr (CIN == 32) {
 #pragma unroll
-          for (int kx = 0; kx < 5; ++kx) bf[j][kx] = *reinterpret_cast<const uint4*>(rb + boff[kx]);
+          for (int kx = 0; kx < K; ++kx) bf[j][kx] = *reinterpret_cast<const uint4*>(rb + boff[kx]);
         } else {
           bf[j][0] = *reinterpret_cast<const uint4*>(rb + boff[0]);
           bf[j][1] = *reinterpret_cast<const uint4*>(rb + boff[0] + 64);
@@ -279,11 +284,11 @@ void conv_rows_pool_kernel(CRArgs a) {
       for (int j = 0; j < 2; ++j) {
         if constexpr (CIN == 32) {
 #pragma unroll
-          for (int kx = 0; kx < 5; ++kx)
+          for (int kx = 0; kx < K; ++kx)
 #pragma unroll
-            for (int ky = 0; ky < 5; ++ky) {
-              f32x4& ac = acc[slot(j + 2 - ky)];
-              ac = mfma<T>(wf[ky * 5 + kx], bf[j][kx], ac);
+            for (int ky = 0; ky < K; ++ky) {
+              f32x4& ac = acc[slot(j + K / 2 - ky)];
+              ac = mfma<T>(wf[ky * K + kx], bf[j][kx], ac);
             }
         } else {
           // consecutive MFMAs into different accumulators (no back-to-back dependency)
@@ -323,10 +328,10 @@ void conv_rows_pool_kernel(CRArgs a) {
   if (s + 1 < S) step(std::integral_constant<int, 1>{}, s + 1);
 }
 
-template <typename T, int CIN, int COUT, int W>
+template <typename T, int CIN, int COUT, int W, int K = 5>
 hipError_t launch_rows(const CRArgs& a, hipStream_t st) {
-  using C = RC<CIN, COUT, W>;
-  const void* k = reinterpret_cast<const void*>(&conv_rows_pool_kernel<T, CIN, COUT, W>);
+  using C = RC<CIN, COUT, W, K>;
+  const void* k = reinterpret_cast<const void*>(&conv_rows_pool_kernel<T, CIN, COUT, W, K>);
   static int per_cu[64] = {};
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -339,8 +344,8 @@ hipError_t launch_rows(const CRArgs& a, hipStream_t st) {
     per_cu[dev] = std::max(1, pc);
   }
   const long long grid = std::min<long long>(a.N, (long long)per_cu[dev] * device_cus());
-  SPECENH_LAUNCH((conv_rows_pool_kernel<T, CIN, COUT, W>), dim3((unsigned)grid), dim3(C::THREADS),
-                 C::LDS, st, a);
+  SPECENH_LAUNCH((conv_rows_pool_kernel<T, CIN, COUT, W, K>), dim3((unsigned)grid),
+                 dim3(C::THREADS), C::LDS, st, a);
   return hipGetLastError();
 }
 
@@ -1477,7 +1482,7 @@ hipError_t launch_enc2(const E2Args& a, hipStream_t st) {
 // shape is one it is built for; *launched = false otherwise (the caller runs
 // conv_patch_kernel).
 int conv_rows_pool(int dtype, const void* x, int N, int H, int W, int CI, const void* w,
-                   const float* b, int CO, void* out, hipStream_t st, bool* launched) {
+                   const float* b, int CO, int K, void* out, hipStream_t st, bool* launched) {
   *launched = false;
   if (variant(V_CONV_NO_ROWS) != 0 || N <= 0 || H < 2 || (H & 1) || !b) return SPECENH_OK;
   if ((long long)N * H * W * CI >= (1ll << 31)) return SPECENH_OK;
@@ -1486,10 +1491,14 @@ int conv_rows_pool(int dtype, const void* x, int N, int H, int W, int CI, const 
   hipError_t e = hipSuccess;
   const bool f16 = dtype == SPECENH_DTYPE_F16;
   if (dtype != SPECENH_DTYPE_F16 && dtype != SPECENH_DTYPE_BF16) return SPECENH_OK;
-  if (CI == 16 && CO == 32 && W == 64)
+  if (CI == 16 && CO == 32 && W == 64 && K == 5)
     e = f16 ? launch_rows<_Float16, 16, 32, 64>(a, st) : launch_rows<__bf16, 16, 32, 64>(a, st);
-  else if (CI == 32 && CO == 64 && W == 32)
+  else if (CI == 32 && CO == 64 && W == 32 && K == 5)
     e = f16 ? launch_rows<_Float16, 32, 64, 32>(a, st) : launch_rows<__bf16, 32, 64, 32>(a, st);
+  else if (CI == 32 && CO == 32 && W == 64 && K == 5)  // hyperparam_scan.py, 256 x 128 inputs
+    e = f16 ? launch_rows<_Float16, 32, 32, 64>(a, st) : launch_rows<__bf16, 32, 32, 64>(a, st);
+  else if (CI == 32 && CO == 32 && W == 64 && K == 3)
+    e = f16 ? launch_rows<_Float16, 32, 32, 64, 3>(a, st) : launch_rows<__bf16, 32, 32, 64, 3>(a, st);
   else
     return SPECENH_OK;
   if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("conv_rows: ") + hipGetErrorString(e));

@@ -18,58 +18,60 @@ from specenh import _lib
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = [(16, 32, 64), (32, 64, 32)]  # (C, CO, W): the model's conv2 and conv3
+# (C, CO, W, K): the 3-layer model's conv2 and conv3 (manual_scan_3layers.py:189-191), and the
+# 32 -> 32 conv2 of hyperparam_scan.py:157 at its 256 x 128 input, k = 5 and 3 (round 6)
+SHAPES = [(16, 32, 64, 5), (32, 64, 32, 5), (32, 32, 64, 5), (32, 32, 64, 3)]
 
 
-def _run(x, w, bias, CO, pool_out):
+def _run(x, w, bias, CO, pool_out, K=5):
     N, H, W, C = x.shape
-    torch.ops.specenh.conv2d_out(x, w, bias, 5, 5, CO, 1, 2, 2, 1, H, W, 1, None, None, pool_out,
-                                 True, None)
+    torch.ops.specenh.conv2d_out(x, w, bias, K, K, CO, 1, K // 2, K // 2, 1, H, W, 1, None, None,
+                                 pool_out, True, None)
 
 
-def _ref(x, w, bias):
+def _ref(x, w, bias, K=5):
     xd = x.double().cpu().permute(0, 3, 1, 2)
     wd = w.double().cpu().permute(0, 3, 1, 2)
     b = bias.double().cpu().view(1, -1, 1, 1)
-    ref = F.max_pool2d(torch.relu(F.conv2d(xd, wd, padding=2) + b), 2)
-    mag = F.max_pool2d(F.conv2d(xd.abs(), wd.abs(), padding=2) + b.abs(), 2)
+    ref = F.max_pool2d(torch.relu(F.conv2d(xd, wd, padding=K // 2) + b), 2)
+    mag = F.max_pool2d(F.conv2d(xd.abs(), wd.abs(), padding=K // 2) + b.abs(), 2)
     return ref.permute(0, 2, 3, 1), mag.permute(0, 2, 3, 1)
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("C,CO,W", SHAPES)
+@pytest.mark.parametrize("C,CO,W,K", SHAPES)
 @pytest.mark.parametrize("N,H", [(1, 64), (3, 32), (7, 2), (5, 18), (513, 8)])
-def test_rows_vs_float64(gpu_device, dtype, C, CO, W, N, H):
-    rng = np.random.default_rng(C + CO + N + H)
+def test_rows_vs_float64(gpu_device, dtype, C, CO, W, K, N, H):
+    rng = np.random.default_rng(C + CO + N + H + K)
     x = torch.tensor(rng.standard_normal((N, H, W, C)), dtype=dtype, device=gpu_device)
-    w = torch.tensor(rng.standard_normal((CO, 5, 5, C)) * 0.1, dtype=dtype, device=gpu_device)
+    w = torch.tensor(rng.standard_normal((CO, K, K, C)) * 0.1, dtype=dtype, device=gpu_device)
     bias = torch.tensor(rng.standard_normal(CO) * 0.5, dtype=torch.float32, device=gpu_device)
     out = torch.full((N, H // 2, W // 2, CO), float("nan"), dtype=dtype, device=gpu_device)
-    _run(x, w, bias, CO, out)
+    _run(x, w, bias, CO, out, K)
     torch.cuda.synchronize()
     assert "conv_rows_pool_kernel" in _lib.last_kernel_name()
-    ref, mag = _ref(x, w, bias)
+    ref, mag = _ref(x, w, bias, K)
     got = out.double().cpu()
     assert bool(torch.isfinite(got).all())
     eps = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
     assert torch.all((got - ref).abs() <= eps * ref.abs() + 1e-5 * mag + 1e-30)
 
 
-@pytest.mark.parametrize("C,CO,W", SHAPES)
-def test_rows_matches_tile_kernel(gpu_device, kernel_variant, C, CO, W):
+@pytest.mark.parametrize("C,CO,W,K", SHAPES)
+def test_rows_matches_tile_kernel(gpu_device, kernel_variant, C, CO, W, K):
     """The same layer through conv_patch_kernel (16 x 16 tiles): equal up to fp32 summation
     order and one 16-bit rounding (the row sweep starts its sums at the bias)."""
     N, H = 300, 64 if C == 16 else 32
-    rng = np.random.default_rng(5 + C)
+    rng = np.random.default_rng(5 + C + K)
     x = torch.tensor(rng.uniform(0, 1, (N, H, W, C)), dtype=torch.float16, device=gpu_device)
-    w = torch.tensor(rng.standard_normal((CO, 5, 5, C)) * 0.05, dtype=torch.float16,
+    w = torch.tensor(rng.standard_normal((CO, K, K, C)) * 0.05, dtype=torch.float16,
                      device=gpu_device)
     bias = torch.tensor(rng.standard_normal(CO) * 0.1, dtype=torch.float32, device=gpu_device)
     a = torch.empty((N, H // 2, W // 2, CO), dtype=torch.float16, device=gpu_device)
     b = torch.empty_like(a)
-    _run(x, w, bias, CO, a)
+    _run(x, w, bias, CO, a, K)
     kernel_variant("CONV_NO_ROWS", 1)
-    _run(x, w, bias, CO, b)
+    _run(x, w, bias, CO, b, K)
     torch.cuda.synchronize()
     assert "conv_patch_kernel" in _lib.last_kernel_name()
     d = (a.float() - b.float()).abs()

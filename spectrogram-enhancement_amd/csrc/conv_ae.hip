@@ -2541,7 +2541,7 @@ int patch_cc(const ConvArgs& a, int nph) {
 int conv_rows_pool(int dtype, const void* x, int N, int H, int W, int CI, const void* w,
                    const float* b, int CO, int K, void* out, hipStream_t st, bool* launched);
 int convt_rows(int dtype, const void* x, int N, int H, int W, int CI, const void* w,
-               const float* b, int CO, void* out, hipStream_t st, bool* launched);
+               const float* b, int CO, int K, void* out, hipStream_t st, bool* launched);
 int conv1_rows_pool(int dtype, const void* x, int N, int H, int W, const void* w,
                     const float* b, int CO, void* out, hipStream_t st, bool* launched);
 
@@ -2771,12 +2771,14 @@ int specenh_conv2d(int dtype, const void* in, int N, int IH, int IW, int C, cons
   if (a.pool && (nph != 1 || (OH & 1) || (OW & 1) || mask || logits || out_f32))
     return set_error(SPECENH_EUNSUPPORTED, "fused max-pool: plain conv with even output only");
   hipStream_t st = (hipStream_t)stream;
-  // Conv2DTranspose(5, s2, relu, same) on 64 channels: the row sweep (conv_rows.hip)
-  if (dtype != SPECENH_DTYPE_F32 && stride == 1 && in_dil == 2 && KH == 5 && KW == 5 &&
-      pad_t == 3 && pad_l == 3 && OH == 2 * IH && OW == 2 * IW && act == 1 && !mask && !logits &&
-      !out_f32 && !pool2 && bias) {
+  // Conv2DTranspose(K, s2, relu, same) on 64 channels (K = 5) or 32 (K = 3 / 5 / 7): the row
+  // sweeps (conv_rows.hip); pad = K - 1 - (K - 2) / 2 of the dilated-input conv
+  if (dtype != SPECENH_DTYPE_F32 && stride == 1 && in_dil == 2 && KH == KW &&
+      (KH == 3 || KH == 5 || KH == 7) && pad_t == KH - 1 - (KH - 2) / 2 && pad_l == pad_t &&
+      OH == 2 * IH && OW == 2 * IW && act == 1 && !mask && !logits && !out_f32 && !pool2 &&
+      bias) {
     bool launched = false;
-    const int rc = convt_rows(dtype, in, N, IH, IW, C, w_gemm, bias, CO, out, st, &launched);
+    const int rc = convt_rows(dtype, in, N, IH, IW, C, w_gemm, bias, CO, KH, out, st, &launched);
     if (rc != SPECENH_OK || launched) return rc;
   }
   // 1 input channel, pooled inference on 128-wide images: the row sweep (conv_rows.hip)

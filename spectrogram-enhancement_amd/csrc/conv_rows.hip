@@ -932,6 +932,202 @@ hipError_t launch_convt_rows(const CRArgs& a, hipStream_t st) {
                                : launch_convt_rows_lead<T, CO, W, 3>(a, st);
 }
 
+// ============================================================================ convT rows, 32 in
+// convt_rows32_kernel: Conv2DTranspose(CO, K, strides=2, relu, same) on 32-channel inputs as a
+// row sweep, K = 3 / 5 / 7 — the decoders' first Conv2DTranspose of the reference's scan models
+// (VAE/hyperparam_scan.py:160 and manual_scan.py:197: 32 -> 32 at 64 x 32 -> 128 x 64 for their
+// 256 x 128 inputs), which conv_patch_kernel ran at 0.06-0.19 of the MFMA peak. The schedule of
+// convt_rows_kernel with the kernel size generalised: output phase (py, px) of position (s, x)
+// reads input row s + dy with tap ky = 2 dy + PT - py (PT = K - 1 - (K - 2) / 2, the dilated
+// conv's pad), so each neighbourhood offset's ONE B fragment (32 channels: one K step) feeds
+// every phase that has the tap, exactly the K^2 useful taps per (row, 16 positions, 16 output
+// channels). Positions: row r of the workgroup's image il at il SPI + r - DY0, SPI = H +
+// max(DY1, -DY0) (zero rows between images), so step g reads positions g .. g + NDY - 1.
+// Input pixels are 64 B with their 16-byte groups swizzled by (p >> 1) & 3 (conflict-free
+// fragment reads at any offset, tools/lds_banks.py).
+template <int CO, int W, int K>
+struct TC32 {
+  static constexpr int CI = 32;
+  static constexpr int NWIN = W / 16, NNB = CO / 16;
+  static constexpr int WAVES = NWIN * NNB;
+  static constexpr int THREADS = 64 * WAVES;
+  static constexpr int PT = K - 1 - (K - 2) / 2;
+  static constexpr int ky_of(int py, int dy) { return 2 * dy + PT - py; }
+  static constexpr bool tap(int ph, int dy, int dx) {
+    return ky_of(ph >> 1, dy) >= 0 && ky_of(ph >> 1, dy) < K && ky_of(ph & 1, dx) >= 0 &&
+           ky_of(ph & 1, dx) < K;
+  }
+  static constexpr bool any_tap(int dy, int dx) {
+    return tap(0, dy, dx) || tap(1, dy, dx) || tap(2, dy, dx) || tap(3, dy, dx);
+  }
+  static constexpr int DY0 = -(PT / 2), DY1 = (K - PT) / 2;  // neighbourhood rows (and columns)
+  static constexpr int NDY = DY1 - DY0 + 1;
+  static constexpr int GAP = DY1 > -DY0 ? DY1 : -DY0;       // zero rows between images
+  static constexpr int tap_index(int ph, int dy, int dx) {  // phase-major, (dy, dx) row-major
+    int u = 0;
+    for (int p = 0; p < 4; ++p)
+      for (int a = DY0; a <= DY1; ++a)
+        for (int b = DY0; b <= DY1; ++b) {
+          if (p == ph && a == dy && b == dx) return u;
+          if (tap(p, a, b)) ++u;
+        }
+    return -1;
+  }
+  static constexpr int ROWB = (W + NDY - 1) * CI * 2;  // pixels x = DY0 .. W - 1 + DY1
+  static constexpr int RING = 8;
+  static constexpr int LDS = RING * ROWB;
+  static constexpr int DMA_WAVES = W * CI * 2 / 1024;  // one 1-KB DMA per wave and row
+  static_assert(WAVES == 4 && DMA_WAVES <= WAVES && (W * CI * 2) % 1024 == 0, "shape");
+  static_assert(tap(3, DY0, DY0) || tap(0, DY0, DY0) || any_tap(DY0, 0), "neighbourhood");
+};
+
+__device__ __forceinline__ int x32off(int ps, int g) { return ps * 64 + 16 * (g ^ ((ps >> 1) & 3)); }
+
+template <typename T, int CO, int W, int K, int LEAD>
+__global__ __launch_bounds__((TC32<CO, W, K>::THREADS)) __attribute__((amdgpu_waves_per_eu(2)))
+void convt_rows32_kernel(CRArgs a) {
+  using C = TC32<CO, W, K>;
+  constexpr int DY0 = C::DY0, DY1 = C::DY1, NDY = C::NDY;
+  static_assert(LEAD >= 1 && NDY + LEAD + 1 <= C::RING, "ring: positions g .. g + NDY + LEAD live");
+  extern __shared__ __attribute__((aligned(16))) unsigned char ring[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = lane & 15, kg = lane >> 4;
+  const int wx = wv % C::NWIN, nb = wv / C::NWIN;
+  const int H = a.H, SPI = H + C::GAP;
+  const int G = gridDim.x;
+  const int nimg = ((int)a.N - (int)blockIdx.x + G - 1) / G;
+  const int S = nimg * SPI;
+
+  {
+    uint4* z = reinterpret_cast<uint4*>(ring);
+    for (int e = tid; e < C::LDS / 16; e += C::THREADS) z[e] = uint4{0u, 0u, 0u, 0u};
+  }
+  uint4 wf[K * K];  // tap fragments, phase-major
+  {
+    const T* __restrict__ Wg = reinterpret_cast<const T*>(a.w);
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+      for (int dy = DY0; dy <= DY1; ++dy)
+#pragma unroll
+        for (int dx = DY0; dx <= DY1; ++dx)
+          if (C::tap(ph, dy, dx))
+            wf[C::tap_index(ph, dy, dx)] = *reinterpret_cast<const uint4*>(
+                Wg + (((16 * nb + m) * K + C::ky_of(ph >> 1, dy)) * K + C::ky_of(ph & 1, dx)) * 32 +
+                8 * kg);
+  }
+  const f32x4 bias = f32x4{a.b[16 * nb + 4 * kg], a.b[16 * nb + 4 * kg + 1],
+                           a.b[16 * nb + 4 * kg + 2], a.b[16 * nb + 4 * kg + 3]};
+  resident_loads_landed();
+  int xo[NDY];  // byte offset of pixel 16 wx + m + dx (stored x - DY0), group kg, in a ring row
+#pragma unroll
+  for (int dx = DY0; dx <= DY1; ++dx) xo[dx - DY0] = x32off(16 * wx + m + dx - DY0, kg);
+  // ring refill: wave w < DMA_WAVES moves chunks 64 w .. 64 w + 63 (pixels 16 w .. 16 w + 15)
+  const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
+  const bool dma_wave = wv < C::DMA_WAVES;
+  int dsrc = 0;
+  if (dma_wave) {
+    const int c = 64 * wv + lane;
+    const int x = c / 4, gs = c & 3, ps = x - DY0;
+    dsrc = x * 32 + 8 * (gs ^ ((ps >> 1) & 3));
+  }
+  // stream position p = il SPI + r - DY0 -> ring slot p & 7 (a zero row unless 0 <= r < H)
+  auto stage_at = [&](int p, int il, int r) -> bool {
+    if (!dma_wave) return false;
+    unsigned char* dst = ring + (p & 7) * C::ROWB + (-DY0) * 64 + 1024 * wv;
+    if (il < nimg && r >= 0 && r < H) {
+      const long long n = (long long)blockIdx.x + (long long)il * G;
+      lds_dma16(X + ((n * H + r) * W) * 32 + dsrc, dst);
+      return true;
+    }
+    *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
+    return false;
+  };
+  auto stage = [&](int p) -> bool {  // (prologue)
+    const int il = p / SPI;
+    return stage_at(p, il, p - il * SPI + DY0);
+  };
+  __syncthreads();  // ring zeroed
+#pragma unroll
+  for (int p = 0; p < NDY + LEAD; ++p) stage(p);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+
+  T* __restrict__ O = reinterpret_cast<T*>(a.out);
+  const int OW = 2 * W;
+  uint2 pk[4];
+  long long po = -1;  // element offset of the held outputs' (2s, 2x) pixel, -1: none
+  int vmn = 0;        // this wave's vector-memory ops issued in the loop
+  int mk[LEAD + 1];   // vmn right after the DMA of position g + NDY + i (-1: none in flight)
+#pragma unroll
+  for (int i = 0; i <= LEAD; ++i) mk[i] = -1;
+  auto store_held = [&]() {
+    if (po >= 0) {
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph)
+        gstore8(O + po + ((ph >> 1) * OW + (ph & 1)) * CO, pk[ph]);
+      vmn += 4;
+    }
+  };
+  // scalar counters (image, step in image) of step g and of its refill position g + NDY + LEAD
+  int il = 0, s = 0;
+  int ilp = (NDY + LEAD) / SPI, sp = NDY + LEAD - ilp * SPI;
+  for (int g = 0; g < S; ++g) {
+    store_held();
+    po = -1;
+    mk[LEAD] = stage_at(g + NDY + LEAD, ilp, sp + DY0) ? ++vmn : -1;
+    if (s < H) {
+      f32x4 acc[4] = {bias, bias, bias, bias};
+#pragma unroll
+      for (int dy = DY0; dy <= DY1; ++dy) {
+        const unsigned char* src = ring + ((g + dy - DY0) & 7) * C::ROWB;
+#pragma unroll
+        for (int dx = DY0; dx <= DY1; ++dx) {
+          if (!C::any_tap(dy, dx)) continue;
+          const uint4 b = *reinterpret_cast<const uint4*>(src + xo[dx - DY0]);
+#pragma unroll
+          for (int ph = 0; ph < 4; ++ph)
+            if (C::tap(ph, dy, dx)) acc[ph] = mfma<T>(wf[C::tap_index(ph, dy, dx)], b, acc[ph]);
+        }
+      }
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) pk[ph] = relu_pack4<T>(acc[ph]);
+      const long long n = (long long)blockIdx.x + (long long)il * G;
+      po = ((n * 2 * H + 2 * s) * OW + 2 * (16 * wx + m)) * CO + 16 * nb + 4 * kg;
+    }
+    if (mk[0] >= 0) wait_vmcnt(vmn - mk[0]);  // position g + NDY has landed
+    lds_barrier();
+#pragma unroll
+    for (int i = 0; i < LEAD; ++i) mk[i] = mk[i + 1];
+    if (++s == SPI) { s = 0; ++il; }
+    if (++sp == SPI) { sp = 0; ++ilp; }
+  }
+  store_held();
+}
+
+template <typename T, int CO, int W, int K>
+hipError_t launch_convt_rows32(const CRArgs& a, hipStream_t st) {
+  using C = TC32<CO, W, K>;
+  constexpr int LEAD = 8 - C::NDY - 1 < 3 ? 8 - C::NDY - 1 : 3;
+  const void* k = reinterpret_cast<const void*>(&convt_rows32_kernel<T, CO, W, K, LEAD>);
+  static int per_cu[64] = {};
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (per_cu[dev] == 0) {
+    int pc = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k, C::THREADS, C::LDS);
+    if (e != hipSuccess) return e;
+    per_cu[dev] = std::max(1, pc);
+  }
+  const long long grid = std::min<long long>(a.N, (long long)per_cu[dev] * device_cus());
+  SPECENH_LAUNCH((convt_rows32_kernel<T, CO, W, K, LEAD>), dim3((unsigned)grid),
+                 dim3(C::THREADS), C::LDS, st, a);
+  return hipGetLastError();
+}
+
 // ============================================================================ C = 1 rows
 // The first Conv2D(16, 5, relu, same) + MaxPooling2D(2) (VAE/manual_scan_3layers.py:187-188)
 // on W = 128 one-channel images, as a row sweep. As in conv_c1_mfma.hip the MFMA K index is
@@ -1513,15 +1709,26 @@ namespace specenh {
 // The row-sweep kernel for Conv2DTranspose(CO, 5, s2, relu, same) on 64-channel inputs of
 // width 16 (CO 64) or 32 (CO 32), forward (any batch); *launched = false otherwise.
 int convt_rows(int dtype, const void* x, int N, int H, int W, int CI, const void* w,
-               const float* b, int CO, void* out, hipStream_t st, bool* launched) {
+               const float* b, int CO, int K, void* out, hipStream_t st, bool* launched) {
   *launched = false;
-  if (variant(V_CONVT_NO_ROWS) != 0 || N <= 0 || H <= 0 || CI != 64 || !b) return SPECENH_OK;
+  if (variant(V_CONVT_NO_ROWS) != 0 || N <= 0 || H <= 0 || !b) return SPECENH_OK;
   if (dtype != SPECENH_DTYPE_F16 && dtype != SPECENH_DTYPE_BF16) return SPECENH_OK;
   if ((long long)N * 4 * H * W * CO >= (1ll << 31)) return SPECENH_OK;
   CRArgs a{};
   a.x = x; a.w = w; a.b = b; a.out = out; a.N = N; a.H = H;
   const bool f16 = dtype == SPECENH_DTYPE_F16;
   hipError_t e;
+  if (CI == 32) {  // the scan models' first Conv2DTranspose (32 -> 32 on 32-position rows)
+    if (CO != 32 || W != 32) return SPECENH_OK;
+    if (K == 3) e = f16 ? launch_convt_rows32<_Float16, 32, 32, 3>(a, st) : launch_convt_rows32<__bf16, 32, 32, 3>(a, st);
+    else if (K == 5) e = f16 ? launch_convt_rows32<_Float16, 32, 32, 5>(a, st) : launch_convt_rows32<__bf16, 32, 32, 5>(a, st);
+    else if (K == 7) e = f16 ? launch_convt_rows32<_Float16, 32, 32, 7>(a, st) : launch_convt_rows32<__bf16, 32, 32, 7>(a, st);
+    else return SPECENH_OK;
+    if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("convt_rows32: ") + hipGetErrorString(e));
+    *launched = true;
+    return SPECENH_OK;
+  }
+  if (CI != 64 || K != 5) return SPECENH_OK;
   if (CO == 64 && W == 16 && variant(V_CONVT_SHARED_RING) == 0 && variant(V_CONVT_PG) != 0)
     e = f16 ? launch_convt_rows_pg<_Float16>(a, st) : launch_convt_rows_pg<__bf16>(a, st);
   else if (CO == 64 && W == 16 && variant(V_CONVT_SHARED_RING) == 0)

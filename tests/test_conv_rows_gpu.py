@@ -120,6 +120,45 @@ def test_convt_rows_vs_float64(gpu_device, dtype, CO, W, N, H):
     assert torch.all((got - ref).abs() <= eps * ref.abs() + 1e-5 * mag + 1e-30)
 
 
+def _convt32_ref(x, w, bias, K):
+    """Conv2DTranspose(K, s2, same) as the stride-1 conv of the dilated input, pad
+    PT = K - 1 - (K - 2) // 2 before and K - PT after (Keras SAME)."""
+    N, H, W, C = x.shape
+    PT = K - 1 - (K - 2) // 2
+    xd = torch.zeros((N, C, 2 * H - 1, 2 * W - 1), dtype=torch.float64)
+    xd[:, :, ::2, ::2] = x.double().cpu().permute(0, 3, 1, 2)
+    xd = F.pad(xd, (PT, K - PT, PT, K - PT))
+    wd = w.double().cpu().permute(0, 3, 1, 2)
+    b = bias.double().cpu().view(1, -1, 1, 1)
+    ref = torch.relu(F.conv2d(xd, wd) + b)
+    mag = F.conv2d(xd.abs(), wd.abs()) + b.abs()
+    return ref.permute(0, 2, 3, 1), mag.permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("K", [3, 5, 7])
+@pytest.mark.parametrize("N,H", [(1, 16), (3, 1), (5, 7), (300, 4), (2, 64)])
+def test_convt_rows32_vs_float64(gpu_device, dtype, K, N, H):
+    """convt_rows32_kernel (round 6): the scan models' Conv2DTranspose(32, K, s2) on 32-wide
+    32-channel maps (hyperparam_scan.py:160, manual_scan.py:197), NaN-poisoned output."""
+    rng = np.random.default_rng(K + N + H)
+    x = torch.tensor(np.maximum(rng.standard_normal((N, H, 32, 32)), 0), dtype=dtype,
+                     device=gpu_device)
+    w = torch.tensor(rng.standard_normal((32, K, K, 32)) * 0.08, dtype=dtype, device=gpu_device)
+    bias = torch.tensor(rng.standard_normal(32) * 0.3, dtype=torch.float32, device=gpu_device)
+    out = torch.full((N, 2 * H, 64, 32), float("nan"), dtype=dtype, device=gpu_device)
+    PT = K - 1 - (K - 2) // 2
+    torch.ops.specenh.conv2d_out(x, w, bias, K, K, 32, 1, PT, PT, 2, 2 * H, 64, 1, None, None,
+                                 out, False, None)
+    torch.cuda.synchronize()
+    assert "convt_rows32" in _lib.last_kernel_name()
+    ref, mag = _convt32_ref(x, w, bias, K)
+    got = out.double().cpu()
+    assert bool(torch.isfinite(got).all())
+    eps = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
+    assert torch.all((got - ref).abs() <= eps * ref.abs() + 1e-5 * mag + 1e-30)
+
+
 @pytest.mark.parametrize("CO,W", [(64, 16), (32, 32)])
 def test_convt_rows_matches_tile_kernel(gpu_device, kernel_variant, CO, W):
     N, H = 257, W

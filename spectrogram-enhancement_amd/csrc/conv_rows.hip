@@ -198,7 +198,7 @@ void conv_rows_pool_kernel(CRArgs a) {
     unsigned char* dst = ring + ((2 * s + wv / C::WPR) & 7) * C::ROWB + ddst;
     if (s < S && il < nimg && r < H) {
       const long long n = (long long)blockIdx.x + (long long)il * G;
-      lds_dma16(X + ((n * H + r) * W) * CIN + dsrc, dst);
+      lds_dma16_s(X + ((n * H + r) * W) * CIN, 2u * dsrc, dst);
       return true;
     }
     *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
@@ -238,11 +238,10 @@ void conv_rows_pool_kernel(CRArgs a) {
           float v[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[i] = fmaxf(max_pair(fmaxf(r0[i], r1[i])), 0.f);
-          if ((m & 1) == 0) {
-            const long long n = (long long)blockIdx.x + (long long)il * G;
-            const long long o = ((n * PHh + q) * PW + (x0 + m) / 2) * COUT + 16 * nb + 4 * kg;
-            *reinterpret_cast<uint2*>(O + o) = uint2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
-          }
+          // lanes m, m ^ 1 hold the same pooled values: both store them (no exec-mask branch)
+          const long long n = (long long)blockIdx.x + (long long)il * G;
+          const long long o = ((n * PHh + q) * PW + (x0 + m) / 2) * COUT + 16 * nb + 4 * kg;
+          *reinterpret_cast<uint2*>(O + o) = uint2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
         }
       }
       r0 = bias;
@@ -482,7 +481,7 @@ void convt_rows_kernel(CRArgs a) {
     unsigned char* dst = ring + (p & 7) * C::ROWB + 128 + 1024 * wv;
     if (il < nimg && r >= 0) {
       const long long n = (long long)blockIdx.x + (long long)il * G;
-      lds_dma16(X + ((n * H + r) * W) * 64 + dsrc, dst);
+      lds_dma16_s(X + ((n * H + r) * W) * 64, 2u * dsrc, dst);
       return true;
     }
     *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
@@ -629,8 +628,8 @@ void convt_rows_pw_kernel(CRArgs a) {
     if (il < nimg && r >= 0) {
       const long long n = (long long)blockIdx.x + (long long)il * G;
       const T* src = X + ((n * H + r) * W) * 64;
-      lds_dma16(src + dsrc[0], dst);
-      lds_dma16(src + dsrc[1], dst + 1024);
+      lds_dma16_s(src, 2u * dsrc[0], dst);
+      lds_dma16_s(src, 2u * dsrc[1], dst + 1024);
       return 2;
     }
     *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
@@ -756,8 +755,8 @@ void convt_rows_pg_kernel(CRArgs a) {
     if (il < nimg && r >= 0) {
       const long long n = (long long)blockIdx.x + (long long)il * G;
       const T* src = X + ((n * H + r) * W) * 64;
-      lds_dma16(src + dsrc[0], dst);
-      lds_dma16(src + dsrc[1], dst + 1024);
+      lds_dma16_s(src, 2u * dsrc[0], dst);
+      lds_dma16_s(src, 2u * dsrc[1], dst + 1024);
       return 2;
     }
     *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
@@ -1038,7 +1037,7 @@ void convt_rows32_kernel(CRArgs a) {
     unsigned char* dst = ring + (p & 7) * C::ROWB + (-DY0) * 64 + 1024 * wv;
     if (il < nimg && r >= 0 && r < H) {
       const long long n = (long long)blockIdx.x + (long long)il * G;
-      lds_dma16(X + ((n * H + r) * W) * 32 + dsrc, dst);
+      lds_dma16_s(X + ((n * H + r) * W) * 32, 2u * dsrc, dst);
       return true;
     }
     *reinterpret_cast<uint4*>(dst + 16 * lane) = uint4{0u, 0u, 0u, 0u};
@@ -1427,10 +1426,14 @@ void enc2_rows_kernel(E2Args a) {
     uint32_t* dst = ring1 + (pos & (E2R1 - 1)) * E2ROW + 4;
     if (il < nimg && y >= 0 && y < H1) {
       const long long n = (long long)blockIdx.x + (long long)il * G;
-      if (lane < 16) lds_dma16(X + (n * H1 + y) * C1W + 8 * lane, dst);
+      // wave-uniform row base + 16 B per lane (SGPR base, no 64-bit lane address to keep)
+      if (lane < 16) lds_dma16_s(X + (n * H1 + y) * C1W, 16u * lane, dst);
       return 1;
     }
-    if (lane < 16) *reinterpret_cast<uint4*>(dst + 4 * lane) = uint4{0u, 0u, 0u, 0u};
+    // a zero formed at the store: as a loop-invariant uint4 it was hoisted and spilled
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    if (lane < 16) *reinterpret_cast<uint4*>(dst + 4 * lane) = uint4{(uint32_t)z, (uint32_t)z, (uint32_t)z, (uint32_t)z};
     return 0;
   };
   auto stage1 = [&](int pp) -> int {  // (prologue)
@@ -1545,11 +1548,11 @@ void enc2_rows_kernel(E2Args a) {
           float v[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[i] = fmaxf(max_pair(fmaxf(r0[i], r1[i])), 0.f);
-          if ((m & 1) == 0) {
-            const long long n = (long long)blockIdx.x + (long long)il * G;
-            const long long o = ((n * PHh + q) * PW + (x0 + m) / 2) * 32 + 16 * nb + 4 * kg;
-            *reinterpret_cast<uint2*>(O + o) = uint2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
-          }
+          // lanes m and m ^ 1 hold the same pooled values (max_pair) and store them to the same
+          // pixel: no exec-mask branch around the store
+          const long long n = (long long)blockIdx.x + (long long)il * G;
+          const long long o = ((n * PHh + q) * PW + (x0 + m) / 2) * 32 + 16 * nb + 4 * kg;
+          *reinterpret_cast<uint2*>(O + o) = uint2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
         }
       }
       const f32x4 bias = bias2_ld();

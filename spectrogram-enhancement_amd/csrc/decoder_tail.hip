@@ -840,7 +840,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       unsigned char* dst = ddst + (p & (NX1 - 1)) * X1ROW * 2;
       if (il < nimg && row >= 0 && row < H1) {
         const long long n = (long long)blockIdx.x + (long long)il * G;
-        lds_dma16(X + ((n * H1 + row) * W1) * CI1 + dsrc, dst);
+        lds_dma16_s(X + ((n * H1 + row) * W1) * CI1, 2u * dsrc, dst);
         return true;
       }
       // between / after the images: the zero padding rows

@@ -25,6 +25,18 @@ __device__ __forceinline__ void lds_dma16(const void* src, void* dst) {
                : "m0");
 }
 
+// The same DMA from a wave-uniform base address (SGPR pair) + a 32-bit per-lane byte offset
+// (the global instruction's saddr form): no 64-bit per-lane address register to keep live
+// across a loop (enc2_rows_kernel spilled one, and the spill reload's vmcnt(0) then waited for
+// every DMA in flight each step).
+__device__ __forceinline__ void lds_dma16_s(const void* sbase, unsigned voff, void* dst) {
+  const unsigned m0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)dst;
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+               :
+               : "v"(voff), "s"(sbase), "s"(m0)
+               : "m0");
+}
+
 // one 8-byte global store per lane as exactly ONE vector-memory instruction, so a kernel that
 // keeps a ledger of its own vector-memory ops (vmcnt counts stores as well as loads on gfx9)
 // knows how many were issued after a given DMA

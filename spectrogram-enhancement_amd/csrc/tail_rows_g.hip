@@ -306,7 +306,7 @@ __global__ __launch_bounds__((TG<CO, KT, KO>::THREADS)) void tailg_kernel(TGArgs
   auto stage = [&](int row, int slot) -> int {
     T* dst = xr + slot * C::XROW + (16 * wv - DY0) * C::XST;  // wave-uniform, 16-B aligned
     if (row >= 0 && row < H) {
-      lds_dma16(X + ((long long)row * C::QW + sx) * CI + 8 * sg, dst);
+      lds_dma16_s(X + (long long)row * C::QW * CI, 2u * (sx * CI + 8 * sg), dst);
       return 1;
     }
     *reinterpret_cast<uint4*>(dst + 8 * lane) = uint4{0u, 0u, 0u, 0u};

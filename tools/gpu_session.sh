@@ -1,9 +1,16 @@
-# round-6 GPU session: row-sweep pooled conv for K = 3 / 32 -> 32 (tests + variant layers)
+# same-box A/B: working tree vs HEAD (pre) vs round-5 end (r05): per-layer C5 AE times + step
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-bash tools/gpu.sh s8 tests:tests/test_conv_rows_gpu.py,tests/test_ae_gpu.py || exit 1
-for M in hyper_k3 hyper_k5 hyper_k7 manual_scan 3layer; do
-  timeout -k 10 200 python tools/ae_layers.py --model $M > gpurun_out/s8_layers_$M.txt 2>&1 || { tail -5 gpurun_out/s8_layers_$M.txt; exit 1; }
-  grep -v amdgpu.ids gpurun_out/s8_layers_$M.txt | python -c "import sys,json; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d['model'], d['total_ms'], [(l['kernel'][:40], l['ms']) for l in d['launches']])"
-done
+sed -i 's/timeout -k 10 120 python/timeout -k 10 200 python/' tools/lib_ab.sh
+timeout -k 10 600 bash tools/lib_ab.sh tools/layer_ab.py --reps 20 -- main pre r05 > gpurun_out/s11_layer_ab.txt 2>&1 || { tail -20 gpurun_out/s11_layer_ab.txt; exit 1; }
+grep -v amdgpu.ids gpurun_out/s11_layer_ab.txt | tail -40
+timeout -k 10 600 bash tools/lib_ab.sh bench.py --steps 30 --warmup 5 --no-stages --no-cpu-baseline -- main pre r05 > gpurun_out/s11_bench_ab.txt 2>&1 || { tail -20 gpurun_out/s11_bench_ab.txt; exit 1; }
+grep -v amdgpu.ids gpurun_out/s11_bench_ab.txt | python -c "
+import sys, json
+for l in sys.stdin:
+    l=l.strip()
+    if l.startswith('=='): print(l, end=' ')
+    elif l.startswith('{'):
+        d=json.loads(l); print(d['value'], d['ms_per_step'])
+"

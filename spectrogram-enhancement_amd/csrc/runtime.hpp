@@ -48,6 +48,7 @@ enum Variant : int {
   V_PATCH_MIN_WG,     // patch kernels: fewer output-channel tiles per workgroup until this many workgroups
   V_WGRAD_WG,         // weight-gradient MFMA kernels: workgroups per launch aimed at (tile runs)
   V_WGRAD_C1_TILES,   // one-input-channel weight gradient: at least this many tiles per workgroup
+  V_EIG_GRID,         // flagged-matrix fallback: workgroups per launch (<= 0: two per CU)
   V_COUNT
 };
 

@@ -3347,8 +3347,13 @@ int eig_denoise(const float* A, long long batch, int m, int n, long long a_strid
     xv.base = A + b0 * a_stride;
     const int* on = only ? only + b0 : nullptr;
     // fallback (on: the flagged few): a grid of at most two workgroups per CU looping over
-    // the matrices instead of one per matrix (gram64_kernel's comment)
-    const unsigned gm = on ? (unsigned)std::min<long long>(nb, 2LL * device_cus()) : (unsigned)nb;
+    // the matrices instead of one per matrix (gram64_kernel's comment). The merged launch
+    // takes 32 workgroups (SPECENH_EIG_GRID): in the two-stream C5 step its 58 KB-LDS
+    // workgroups wait for CU slots held by the other stream's autoencoder kernels, and 512 of
+    // them that return at once still cost 0.65 % of the step (2.142 -> 2.128 ms at 16, 2.132
+    // at 64, profiles/r06_eig_grid_ab.txt); a batch with many flagged matrices loops 32-wide.
+    const long long gcap = variant(V_EIG_GRID) > 0 ? variant(V_EIG_GRID) : 2LL * device_cus();
+    const unsigned gm = on ? (unsigned)std::min<long long>(nb, gcap) : (unsigned)nb;
     // The merged one-workgroup-per-matrix fallback was A/B'd at C5's size (128 x 128, a few
     // flagged matrices); a large matrix (C3: 513 x 256) puts its whole Gram, tridiagonal
     // solve and reconstruction on one workgroup per CU, which loses to the split launches'

@@ -706,9 +706,6 @@ __device__ __forceinline__ int x2_off(int ps, int g) { return ps * d3::X2ST + 8 
 #ifndef SPECENH_D3_CPRIO
 #define SPECENH_D3_CPRIO 0  // measured +4 % (tools/lib_ab.sh, profiles/r04_d3_ab.txt)
 #endif
-#ifndef SPECENH_D3_READ_AHEAD
-#define SPECENH_D3_READ_AHEAD 1
-#endif
 #ifndef SPECENH_D3_BRANCHFREE
 #define SPECENH_D3_BRANCHFREE 1
 #endif
@@ -765,7 +762,7 @@ struct D3Clock {
 // LEAD: the producer's input-ring refills in flight beyond the one a macro step waits for
 // (step g needs position g + 3 after its barrier and waits for that DMA only, issued LEAD steps
 // earlier; round 3: LEAD 0, the DMA issued by the same step).
-template <typename T, bool MAP, int LEAD>
+template <typename T, bool MAP, int LEAD, bool OUT16 = false>
 __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
   static_assert(LEAD >= 0 && LEAD <= 4, "8-row input ring");
   using namespace d3;
@@ -1026,8 +1023,21 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
 
     f32x4 P0 = f32x4{0.f, 0.f, 0.f, 0.f}, P1 = P0, P2 = P0;
     int il = -1, tl = TPI - 3;  // tail step t = -3
-    auto tstep = [&](auto ic, float* bb, f32x4& E, int& eil, int& etl) -> bool {
+    // the nine B fragments of tail step t (ring slot T8 = t & 7): rows t - 1 .. t + 1, pixel
+    // shifts dx = -1 .. 1
+    auto frags = [&](auto ic, uint4 (&bq)[9]) {
+      constexpr int T8 = decltype(ic)::value;
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx)
+          bq[3 * (dy + 1) + dx + 1] =
+              *reinterpret_cast<const uint4*>(x2r + ((T8 + dy + 8) & 7) * X2ROW + xo[dx + 1]);
+    };
+    auto tstep = [&](auto ic, const uint4 (&bq)[9], float* bb, f32x4& E, int& eil,
+                     int& etl) -> bool {
       constexpr int T8 = decltype(ic)::value;  // t & 7: the tail-input ring slot of row t
+      (void)T8;
       eil = il;
       etl = tl;
       if (++tl == TPI) { tl = 0; ++il; }
@@ -1040,27 +1050,13 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       // the scheduler can interleave their MFMA chains)
       f32x4 acc[4] = {bias, bias, bias, bias};
       int u0[4] = {0, 4, 10, 16};  // first tap register of each phase (4 / 6 / 6 / 9 taps)
-      // all nine B fragments first, then the 25 MFMAs: read in pairs just ahead of their
-      // MFMAs (the compiler's schedule), each pair's LDS latency was exposed
-#if SPECENH_D3_READ_AHEAD
-      uint4 bq[9];
-#pragma unroll
-      for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-        for (int dx = -1; dx <= 1; ++dx)
-          bq[3 * (dy + 1) + dx + 1] =
-              *reinterpret_cast<const uint4*>(x2r + ((T8 + dy + 8) & 7) * X2ROW + xo[dx + 1]);
-      __builtin_amdgcn_sched_barrier(0);
-#endif
+      // all nine B fragments first (frags, by the caller), then the 25 MFMAs: read in pairs
+      // just ahead of their MFMAs (the compiler's schedule), each pair's LDS latency was exposed
 #pragma unroll
       for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
         for (int dx = -1; dx <= 1; ++dx) {
-#if SPECENH_D3_READ_AHEAD
           const uint4 b = bq[3 * (dy + 1) + dx + 1];
-#else
-          const uint4 b = *reinterpret_cast<const uint4*>(x2r + ((T8 + dy + 8) & 7) * X2ROW + xo[dx + 1]);
-#endif
 #pragma unroll
           for (int ph = 0; ph < 4; ++ph) {
             const int ky = ky_of(ph >> 1, dy), kx = ky_of(ph & 1, dx);
@@ -1095,15 +1091,17 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       return true;
 #endif
     };
-    auto emit = [&](const f32x4& E, const float* bb, int eil, int etl) {
+    auto emit = [&](const f32x4& E, float edge, int eil, int etl) {  // edge: bb[bri]
       float s = bo + E[0];
       s += dpp_shift<0x111>(E[1]);  // row_shr:1: lane m reads lane m - 1
       s += dpp_shift<0x101>(E[2]);  // row_shl:1: lane m reads lane m + 1
-      s += bb[bri];
+      s += edge;
       const long long n = (long long)blockIdx.x + (long long)eil * G;
       const long long o = (n * H3 + 2 * (etl - 1) + orow) * rows::MW + ocol;
       const float y = __builtin_amdgcn_rcpf(1.f + __expf(-s));
-      if (a.out_f16)  // (uniform)
+      // (the output dtype as a template argument: a run-time test of out_f16 split the macro
+      // step into blocks, and the LDS waits after the join were conservative; 1.1 % per launch)
+      if constexpr (OUT16)
         reinterpret_cast<_Float16*>(a.out)[o] = (_Float16)y;
       else
         reinterpret_cast<float*>(a.out)[o] = y;
@@ -1114,11 +1112,18 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       float* const b1 = b0 + NBND;
       f32x4 E0, E1;
       int il0, tl0, il1, tl1;
-      const bool e0 = tstep(IC<(2 * I + 5) & 7>{}, b0, E0, il0, tl0);  // (2g - 3) & 7
-      const bool e1 = tstep(IC<(2 * I + 6) & 7>{}, b1, E1, il1, tl1);
+      uint4 bq[9];
+      frags(IC<(2 * I + 5) & 7>{}, bq);  // (2g - 3) & 7
+      __builtin_amdgcn_sched_barrier(0);
+      const bool e0 = tstep(IC<(2 * I + 5) & 7>{}, bq, b0, E0, il0, tl0);
+      frags(IC<(2 * I + 6) & 7>{}, bq);
+      __builtin_amdgcn_sched_barrier(0);
+      const bool e1 = tstep(IC<(2 * I + 6) & 7>{}, bq, b1, E1, il1, tl1);
       D3_BARRIER();
-      if (e0) emit(E0, b0, il0, tl0);
-      if (e1) emit(E1, b1, il1, tl1);
+      // (emitting these in the next macro step, after its first fragment reads, to overlap the
+      // two LDS latencies: measured neutral, profiles/r06_d3_out16_ab.txt)
+      if (e0) emit(E0, b0[bri], il0, tl0);
+      if (e1) emit(E1, b1[bri], il1, tl1);
     };
     int g = 0;
     for (; g + 4 <= S; g += 4) {
@@ -1353,10 +1358,15 @@ extern "C" int specenh_decoder3_ex(int dtype, const void* x, int N, int H, int W
   std::call_once(attr_once, [k16, kb16] {
     (void)hipFuncSetAttribute(k16, hipFuncAttributeMaxDynamicSharedMemorySize, d3::LDS_BYTES);
     (void)hipFuncSetAttribute(kb16, hipFuncAttributeMaxDynamicSharedMemorySize, d3::LDS_BYTES);
-    const void* const nm[4] = {reinterpret_cast<const void*>(&decoder3_kernel<_Float16, false, 3>),
-                               reinterpret_cast<const void*>(&decoder3_kernel<__bf16, false, 3>),
-                               reinterpret_cast<const void*>(&decoder3_kernel<_Float16, false, 0>),
-                               reinterpret_cast<const void*>(&decoder3_kernel<__bf16, false, 0>)};
+    const void* const nm[8] = {
+        reinterpret_cast<const void*>(&decoder3_kernel<_Float16, false, 3>),
+        reinterpret_cast<const void*>(&decoder3_kernel<__bf16, false, 3>),
+        reinterpret_cast<const void*>(&decoder3_kernel<_Float16, false, 0>),
+        reinterpret_cast<const void*>(&decoder3_kernel<__bf16, false, 0>),
+        reinterpret_cast<const void*>(&decoder3_kernel<_Float16, false, 3, true>),
+        reinterpret_cast<const void*>(&decoder3_kernel<__bf16, false, 3, true>),
+        reinterpret_cast<const void*>(&decoder3_kernel<_Float16, false, 0, true>),
+        reinterpret_cast<const void*>(&decoder3_kernel<__bf16, false, 0, true>)};
     for (const void* k : nm)
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, d3::LDS_BYTES_NM);
   });
@@ -1367,20 +1377,31 @@ extern "C" int specenh_decoder3_ex(int dtype, const void* x, int N, int H, int W
   if (map && a.out_f16)
     return set_error(SPECENH_EUNSUPPORTED, "fused decoder: the map consumer stores fp32 only");
   const dim3 gd(grid), bd(512);
+  // the map-free kernels by (input dtype, output dtype) as a compile-time pair
+  auto launch_nm = [&](auto t, auto o16) {
+    using TT = decltype(t);
+    constexpr bool O16 = decltype(o16)::value;
+    if (short_lead)
+      SPECENH_LAUNCH((decoder3_kernel<TT, false, 0, O16>), gd, bd, d3::LDS_BYTES_NM, st, a);
+    else
+      SPECENH_LAUNCH((decoder3_kernel<TT, false, 3, O16>), gd, bd, d3::LDS_BYTES_NM, st, a);
+  };
+  using F16OUT = std::integral_constant<bool, true>;
+  using F32OUT = std::integral_constant<bool, false>;
   if (dtype == SPECENH_DTYPE_F16) {
     if (map)
       SPECENH_LAUNCH((decoder3_kernel<_Float16, true, 0>), gd, bd, d3::LDS_BYTES, st, a);
-    else if (short_lead)
-      SPECENH_LAUNCH((decoder3_kernel<_Float16, false, 0>), gd, bd, d3::LDS_BYTES_NM, st, a);
+    else if (a.out_f16)
+      launch_nm(_Float16{}, F16OUT{});
     else
-      SPECENH_LAUNCH((decoder3_kernel<_Float16, false, 3>), gd, bd, d3::LDS_BYTES_NM, st, a);
+      launch_nm(_Float16{}, F32OUT{});
   } else {
     if (map)
       SPECENH_LAUNCH((decoder3_kernel<__bf16, true, 0>), gd, bd, d3::LDS_BYTES, st, a);
-    else if (short_lead)
-      SPECENH_LAUNCH((decoder3_kernel<__bf16, false, 0>), gd, bd, d3::LDS_BYTES_NM, st, a);
+    else if (a.out_f16)
+      launch_nm(__bf16{}, F16OUT{});
     else
-      SPECENH_LAUNCH((decoder3_kernel<__bf16, false, 3>), gd, bd, d3::LDS_BYTES_NM, st, a);
+      launch_nm(__bf16{}, F32OUT{});
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(SPECENH_EHIP, std::string("decoder3: ") + hipGetErrorString(e));

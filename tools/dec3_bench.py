@@ -1,7 +1,7 @@
 """The C5 decoder's last three layers at the bench's launch shape (2048 x 32 x 32 x 64 fp16):
 decoder3_kernel map-free (default) vs its round-3 map-ring consumer (D3_MAP=1) vs the unfused
 engine path (convT2 conv_patch launch + the row-sweep tail), interleaved rounds in one
-process, HIP events.  python tools/dec3_bench.py [N] [arm,arm...]"""
+process, HIP events.  python tools/dec3_bench.py [N] [arm,arm...]  (D3_OUT16=1: fp16 output)"""
 import os
 import sys
 
@@ -24,6 +24,8 @@ def main():
         _lib.set_variant("DECODER_UNFUSED", v)
         e = ae.AutoencoderEngine(ops_, (32, 32, 64), compute_dtype="float16", device=dev)
         e.set_keras_weights(w)
+        if v == 0 and os.environ.get("D3_OUT16"):  # the bench's fp16 reconstructions
+            e.set_inference_output_dtype(torch.float16)
         engs[v] = e
     _lib.set_variant("DECODER_UNFUSED", 0)
     arms = {"mapfree": (engs[0], 0), "map": (engs[0], 1), "unfused": (engs[1], 0)}

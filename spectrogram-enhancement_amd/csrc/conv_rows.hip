@@ -500,13 +500,14 @@ void convt_rows_kernel(CRArgs a) {
   T* __restrict__ O = reinterpret_cast<T*>(a.out);
   const int OW = 2 * W;
   uint2 pk[4];
-  long long po = -1;  // element offset of the held outputs' (2s, 2x) pixel, -1: none
+  long long po = 0;   // element offset of the held outputs' (2s, 2x) pixel
+  bool held = false;  // (wave-uniform, as convt_rows_pw_kernel's)
   int vmn = 0;        // this wave's vector-memory ops issued in the loop
   int mk[LEAD + 1];   // vmn right after the DMA of position g + 3 + i (-1: none in flight)
 #pragma unroll
   for (int i = 0; i <= LEAD; ++i) mk[i] = -1;
   auto store_held = [&]() {
-    if (po >= 0) {
+    if (held) {
 #pragma unroll
       for (int ph = 0; ph < 4; ++ph)
         gstore8(O + po + ((ph >> 1) * OW + (ph & 1)) * CO, pk[ph]);
@@ -518,7 +519,7 @@ void convt_rows_kernel(CRArgs a) {
   int ilp = (3 + LEAD) / SPI, sp = 3 + LEAD - ilp * SPI;
   for (int g = 0; g < S; ++g) {
     store_held();
-    po = -1;
+    held = false;
     mk[LEAD] = stage_at(g + 3 + LEAD, ilp, sp - 1) ? ++vmn : -1;
     if (s < H) {
       f32x4 acc[4] = {bias, bias, bias, bias};
@@ -546,8 +547,9 @@ void convt_rows_kernel(CRArgs a) {
       for (int ph = 0; ph < 4; ++ph) pk[ph] = relu_pack4<T>(acc[ph]);
       const long long n = (long long)blockIdx.x + (long long)il * G;
       po = ((n * 2 * H + 2 * s) * OW + 2 * (16 * wx + m)) * CO + 16 * nb + 4 * kg;
+      held = true;
     }
-    if (mk[0] >= 0) wait_vmcnt(vmn - mk[0]);  // position g + 3 has landed
+    if (mk[0] >= 0) wait_vmcnt_ss<15>(vmn - mk[0]);  // position g + 3 has landed
     lds_barrier();
 #pragma unroll
     for (int i = 0; i < LEAD; ++i) mk[i] = mk[i + 1];
@@ -646,13 +648,15 @@ void convt_rows_pw_kernel(CRArgs a) {
   T* __restrict__ O = reinterpret_cast<T*>(a.out);
   constexpr int OW = 2 * W;
   uint2 pk[4];
-  long long po = -1;  // element offset of the held outputs' (2s, 2x) pixel, -1: none
-  int vmn = 0;        // this wave's vector-memory ops issued in the loop
-  int mk[LEAD + 1];   // vmn right after the DMAs of position g + 3 + i (-1: none in flight)
+  long long po = 0;    // element offset of the held outputs' (2s, 2x) pixel
+  bool held = false;   // (wave-uniform: a per-lane "po >= 0" test had made the ledger below
+                       // per-lane VGPRs, the stores an exec-masked region and the wait a ladder)
+  int vmn = 0;         // this wave's vector-memory ops issued in the loop
+  int mk[LEAD + 1];    // vmn right after the DMAs of position g + 3 + i (-1: none in flight)
 #pragma unroll
   for (int i = 0; i <= LEAD; ++i) mk[i] = -1;
   auto store_held = [&]() {
-    if (po >= 0) {
+    if (held) {
 #pragma unroll
       for (int ph = 0; ph < 4; ++ph)
         gstore8(O + po + ((ph >> 1) * OW + (ph & 1)) * CO, pk[ph]);
@@ -663,7 +667,7 @@ void convt_rows_pw_kernel(CRArgs a) {
   int ilp = (3 + LEAD) / SPI, sp = 3 + LEAD - ilp * SPI;
   for (int g = 0; g < S; ++g) {
     store_held();
-    po = -1;
+    held = false;
     const int nd = stage_at(g + 3 + LEAD, ilp, sp - 1);
     vmn += nd;
     mk[LEAD] = nd ? vmn : -1;
@@ -692,10 +696,12 @@ void convt_rows_pw_kernel(CRArgs a) {
       for (int ph = 0; ph < 4; ++ph) pk[ph] = relu_pack4<T>(acc[ph]);
       const long long n = (long long)blockIdx.x + (long long)il * G;
       po = ((n * 2 * H + 2 * s) * OW + 2 * m) * CO + 16 * nb + 4 * kg;
+      held = true;
     }
     // this wave's refill of position g + 3 (both DMAs) has landed; LDS reads are in order
-    // within a wave, so the zero-filled rows need no wait
-    if (mk[0] >= 0) wait_vmcnt(vmn - mk[0]);
+    // within a wave, so the zero-filled rows need no wait. Steady state: 3 steps of 4 stores
+    // + 2 DMAs younger than it, i.e. >= 15
+    if (mk[0] >= 0) wait_vmcnt_ss<15>(vmn - mk[0]);
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int i = 0; i < LEAD; ++i) mk[i] = mk[i + 1];
@@ -799,13 +805,14 @@ void convt_rows_pg_kernel(CRArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     uint2 pk[2];
-    long long po = -1;  // element offset of the held outputs' (2s, 2x) pixel, -1: none
+    long long po = 0;   // element offset of the held outputs' (2s, 2x) pixel
+    bool held = false;  // (wave-uniform, as convt_rows_pw_kernel's)
     int vmn = 0;        // this wave's vector-memory ops issued in the loop
     int mk[LEAD + 1];   // vmn right after the DMAs of position g + 3 + i (-1: none in flight)
 #pragma unroll
     for (int i = 0; i <= LEAD; ++i) mk[i] = -1;
     auto store_held = [&]() {
-      if (po >= 0) {
+      if (held) {
 #pragma unroll
         for (int q = 0; q < 2; ++q)
           gstore8(O + po + ((PHS[q] >> 1) * OW + (PHS[q] & 1)) * CO, pk[q]);
@@ -816,7 +823,7 @@ void convt_rows_pg_kernel(CRArgs a) {
     int ilp = (3 + LEAD) / SPI, sp = 3 + LEAD - ilp * SPI;
     for (int g = 0; g < S; ++g) {
       store_held();
-      po = -1;
+      held = false;
       const int nd = stage_at(g + 3 + LEAD, ilp, sp - 1);
       vmn += nd;
       mk[LEAD] = nd ? vmn : -1;
@@ -851,6 +858,7 @@ void convt_rows_pg_kernel(CRArgs a) {
         for (int q = 0; q < 2; ++q) pk[q] = relu_pack4<T>(acc[q]);
         const long long n = (long long)blockIdx.x + (long long)il * G;
         po = ((n * 2 * H + 2 * s) * OW + 2 * m) * CO + 16 * nb + 4 * kg;
+        held = true;
       }
       if (mk[0] >= 0) wait_vmcnt(vmn - mk[0]);
       asm volatile("" ::: "memory");
@@ -1056,13 +1064,14 @@ void convt_rows32_kernel(CRArgs a) {
   T* __restrict__ O = reinterpret_cast<T*>(a.out);
   const int OW = 2 * W;
   uint2 pk[4];
-  long long po = -1;  // element offset of the held outputs' (2s, 2x) pixel, -1: none
+  long long po = 0;   // element offset of the held outputs' (2s, 2x) pixel
+  bool held = false;  // (wave-uniform, as convt_rows_pw_kernel's)
   int vmn = 0;        // this wave's vector-memory ops issued in the loop
   int mk[LEAD + 1];   // vmn right after the DMA of position g + NDY + i (-1: none in flight)
 #pragma unroll
   for (int i = 0; i <= LEAD; ++i) mk[i] = -1;
   auto store_held = [&]() {
-    if (po >= 0) {
+    if (held) {
 #pragma unroll
       for (int ph = 0; ph < 4; ++ph)
         gstore8(O + po + ((ph >> 1) * OW + (ph & 1)) * CO, pk[ph]);
@@ -1074,7 +1083,7 @@ void convt_rows32_kernel(CRArgs a) {
   int ilp = (NDY + LEAD) / SPI, sp = NDY + LEAD - ilp * SPI;
   for (int g = 0; g < S; ++g) {
     store_held();
-    po = -1;
+    held = false;
     mk[LEAD] = stage_at(g + NDY + LEAD, ilp, sp + DY0) ? ++vmn : -1;
     if (s < H) {
       f32x4 acc[4] = {bias, bias, bias, bias};
@@ -1094,8 +1103,9 @@ void convt_rows32_kernel(CRArgs a) {
       for (int ph = 0; ph < 4; ++ph) pk[ph] = relu_pack4<T>(acc[ph]);
       const long long n = (long long)blockIdx.x + (long long)il * G;
       po = ((n * 2 * H + 2 * s) * OW + 2 * (16 * wx + m)) * CO + 16 * nb + 4 * kg;
+      held = true;
     }
-    if (mk[0] >= 0) wait_vmcnt(vmn - mk[0]);  // position g + NDY has landed
+    if (mk[0] >= 0) wait_vmcnt_ss<15>(vmn - mk[0]);  // position g + NDY has landed
     lds_barrier();
 #pragma unroll
     for (int i = 0; i < LEAD; ++i) mk[i] = mk[i + 1];

@@ -912,7 +912,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
         *reinterpret_cast<uint4*>(r0 + x2w16) = uint4{0u, 0u, 0u, 0u};
         *reinterpret_cast<uint4*>(r1 + x2w16) = uint4{0u, 0u, 0u, 0u};
       }
-      if (mk[0] >= 0) wait_vmcnt(vmn - mk[0]);  // input position g + 3 has landed
+      if (mk[0] >= 0) wait_vmcnt_ss<LEAD>(vmn - mk[0]);  // input position g + 3 has landed
       D3_BARRIER();
 #pragma unroll
       for (int i = 0; i < LEAD; ++i) mk[i] = mk[i + 1];

@@ -75,4 +75,16 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
   }
 }
 
+// wait_vmcnt with the loop's steady-state count as a compile-time fast path: n >= STEADY waits
+// with vmcnt(STEADY) (stricter for n > STEADY, never laxer) in two scalar instructions instead
+// of the switch's compare ladder
+template <int STEADY>
+__device__ __forceinline__ void wait_vmcnt_ss(int n) {
+  static_assert(STEADY >= 0 && STEADY <= 15, "vmcnt is 4 bits on gfx9");
+  if (__builtin_amdgcn_readfirstlane(n) >= STEADY)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEADY) : "memory");
+  else
+    wait_vmcnt(n);
+}
+
 }  // namespace specenh

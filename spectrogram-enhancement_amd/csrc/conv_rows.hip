@@ -108,6 +108,7 @@ struct CRArgs {
   const float* b;    // [COUT]
   void* out;         // [N][H/2][W/2][COUT]
   int N, H;
+  int lgb;           // convT row sweeps: log2 of the row bands per image (0: whole images)
 };
 
 // K (CIN = 32 only): the kernel size, 5 (the reference model) or 3 (hyperparam_scan.py's
@@ -429,9 +430,11 @@ void convt_rows_kernel(CRArgs a) {
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int m = lane & 15, kg = lane >> 4;
   const int wx = wv % C::NWIN, nb = wv / C::NWIN;
-  const int H = a.H, SPI = H + 1;
+  // the stream's units: whole images (lgb = 0) or row bands of HB rows (small batches)
+  const int H = a.H, lgb = a.lgb, HB = H >> lgb, bmask = (1 << lgb) - 1;
+  const int SPI = HB + (lgb ? 2 : 1);
   const int G = gridDim.x;
-  const int nimg = ((int)a.N - (int)blockIdx.x + G - 1) / G;
+  const int nimg = (((int)a.N << lgb) - (int)blockIdx.x + G - 1) / G;
   const int S = nimg * SPI;
 
   {
@@ -475,12 +478,16 @@ void convt_rows_kernel(CRArgs a) {
     const int ps = 1 + c / 8, gs = c & 7;
     dsrc = (ps - 1) * 64 + 8 * (gs ^ (ps & 7));
   }
-  // stream position p = il SPI + r + 1 -> ring slot p & 7
-  auto stage_at = [&](int p, int il, int r) -> bool {
+  // stream position p = il SPI + q -> ring slot p & 7: row r0 + q - 1 of the workgroup's unit
+  // il (unit v = blockIdx.x + il G: image v >> lgb, first row r0 = (v & bmask) HB); rows
+  // outside the image are the zero rows (one between whole images, two between bands)
+  auto stage_at = [&](int p, int il, int q) -> bool {
     if (!dma_wave) return false;
     unsigned char* dst = ring + (p & 7) * C::ROWB + 128 + 1024 * wv;
-    if (il < nimg && r >= 0) {
-      const long long n = (long long)blockIdx.x + (long long)il * G;
+    const int v = (int)blockIdx.x + il * G;
+    const int r = (v & bmask) * HB + q - 1;
+    if (il < nimg && r >= 0 && r < H) {
+      const long long n = (long long)(v >> lgb);
       lds_dma16_s(X + ((n * H + r) * W) * 64, 2u * dsrc, dst);
       return true;
     }
@@ -489,7 +496,7 @@ void convt_rows_kernel(CRArgs a) {
   };
   auto stage = [&](int p) -> bool {  // (prologue)
     const int il = p / SPI;
-    return stage_at(p, il, p - il * SPI - 1);
+    return stage_at(p, il, p - il * SPI);
   };
   __syncthreads();  // ring zeroed
 #pragma unroll
@@ -520,8 +527,8 @@ void convt_rows_kernel(CRArgs a) {
   for (int g = 0; g < S; ++g) {
     store_held();
     held = false;
-    mk[LEAD] = stage_at(g + 3 + LEAD, ilp, sp - 1) ? ++vmn : -1;
-    if (s < H) {
+    mk[LEAD] = stage_at(g + 3 + LEAD, ilp, sp) ? ++vmn : -1;
+    if (s < HB) {
       f32x4 acc[4] = {bias, bias, bias, bias};
       int u0[4] = {0, 8, 20, 32};
 #pragma unroll
@@ -545,8 +552,9 @@ void convt_rows_kernel(CRArgs a) {
       }
 #pragma unroll
       for (int ph = 0; ph < 4; ++ph) pk[ph] = relu_pack4<T>(acc[ph]);
-      const long long n = (long long)blockIdx.x + (long long)il * G;
-      po = ((n * 2 * H + 2 * s) * OW + 2 * (16 * wx + m)) * CO + 16 * nb + 4 * kg;
+      const int v = (int)blockIdx.x + il * G;
+      const long long n = (long long)(v >> lgb);
+      po = ((n * 2 * H + 2 * ((v & bmask) * HB + s)) * OW + 2 * (16 * wx + m)) * CO + 16 * nb + 4 * kg;
       held = true;
     }
     if (mk[0] >= 0) wait_vmcnt_ss<15>(vmn - mk[0]);  // position g + 3 has landed
@@ -579,9 +587,11 @@ void convt_rows_pw_kernel(CRArgs a) {
   const int m = lane & 15, kg = lane >> 4;
   const int nb = wv;
   unsigned char* const ring = lds_pw + wv * WR;
-  const int H = a.H, SPI = H + 1;
+  // units: whole images or row bands, as convt_rows_kernel's
+  const int H = a.H, lgb = a.lgb, HB = H >> lgb, bmask = (1 << lgb) - 1;
+  const int SPI = HB + (lgb ? 2 : 1);
   const int G = gridDim.x;
-  const int nimg = ((int)a.N - (int)blockIdx.x + G - 1) / G;
+  const int nimg = (((int)a.N << lgb) - (int)blockIdx.x + G - 1) / G;
   const int S = nimg * SPI;
 
   for (int e = lane; e < WR / 16; e += 64) reinterpret_cast<uint4*>(ring)[e] = uint4{0u, 0u, 0u, 0u};
@@ -624,11 +634,14 @@ void convt_rows_pw_kernel(CRArgs a) {
     const int ps = 1 + c / 8, gs = c & 7;
     dsrc[h] = (ps - 1) * 64 + 8 * (gs ^ (ps & 7));
   }
-  // stream position p = il SPI + r + 1 -> ring slot p & 7; returns the DMAs issued
-  auto stage_at = [&](int p, int il, int r) -> int {
+  // stream position p = il SPI + q -> ring slot p & 7 (row r0 + q - 1 of unit il, as
+  // convt_rows_kernel's); returns the DMAs issued
+  auto stage_at = [&](int p, int il, int q) -> int {
     unsigned char* dst = ring + (p & 7) * C::ROWB + 128;
-    if (il < nimg && r >= 0) {
-      const long long n = (long long)blockIdx.x + (long long)il * G;
+    const int v = (int)blockIdx.x + il * G;
+    const int r = (v & bmask) * HB + q - 1;
+    if (il < nimg && r >= 0 && r < H) {
+      const long long n = (long long)(v >> lgb);
       const T* src = X + ((n * H + r) * W) * 64;
       lds_dma16_s(src, 2u * dsrc[0], dst);
       lds_dma16_s(src, 2u * dsrc[1], dst + 1024);
@@ -641,7 +654,7 @@ void convt_rows_pw_kernel(CRArgs a) {
 #pragma unroll
   for (int p = 0; p < 3 + LEAD; ++p) {
     const int il = p / SPI;
-    stage_at(p, il, p - il * SPI - 1);
+    stage_at(p, il, p - il * SPI);
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 
@@ -668,10 +681,10 @@ void convt_rows_pw_kernel(CRArgs a) {
   for (int g = 0; g < S; ++g) {
     store_held();
     held = false;
-    const int nd = stage_at(g + 3 + LEAD, ilp, sp - 1);
+    const int nd = stage_at(g + 3 + LEAD, ilp, sp);
     vmn += nd;
     mk[LEAD] = nd ? vmn : -1;
-    if (s < H) {
+    if (s < HB) {
       f32x4 acc[4] = {bias, bias, bias, bias};
       int u0[4] = {0, 8, 20, 32};
 #pragma unroll
@@ -694,8 +707,9 @@ void convt_rows_pw_kernel(CRArgs a) {
       }
 #pragma unroll
       for (int ph = 0; ph < 4; ++ph) pk[ph] = relu_pack4<T>(acc[ph]);
-      const long long n = (long long)blockIdx.x + (long long)il * G;
-      po = ((n * 2 * H + 2 * s) * OW + 2 * m) * CO + 16 * nb + 4 * kg;
+      const int v = (int)blockIdx.x + il * G;
+      const long long n = (long long)(v >> lgb);
+      po = ((n * 2 * H + 2 * ((v & bmask) * HB + s)) * OW + 2 * m) * CO + 16 * nb + 4 * kg;
       held = true;
     }
     // this wave's refill of position g + 3 (both DMAs) has landed; LDS reads are in order
@@ -890,8 +904,20 @@ hipError_t launch_convt_rows_pg(const CRArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// log2 of the row bands per image for the convT row sweeps: whole images while the batch
+// fills the resident workgroup slots; a small batch (C4's 128 images: 128 workgroups for 512
+// slots) is cut into up to 8 bands of >= 4 rows (two bubble steps and two halo rows each)
+int convt_row_bands_lg(int N, int H, long long slots) {
+  const int forced = variant(V_ROWS_BANDS);
+  int lg = 0;
+  while (lg < 3 && (H % (2 << lg)) == 0 && (H >> (lg + 1)) >= 4 &&
+         (forced >= 0 ? lg < forced : ((long long)N << (lg + 1)) <= slots))
+    ++lg;
+  return lg;
+}
+
 template <typename T>
-hipError_t launch_convt_rows_pw(const CRArgs& a, hipStream_t st) {
+hipError_t launch_convt_rows_pw(const CRArgs& a0, hipStream_t st) {
   using C = TC<64, 16>;
   constexpr int LDS = 4 * C::RING * C::ROWB;
   const void* k = reinterpret_cast<const void*>(&convt_rows_pw_kernel<T, 3>);
@@ -907,13 +933,16 @@ hipError_t launch_convt_rows_pw(const CRArgs& a, hipStream_t st) {
     if (e != hipSuccess) return e;
     per_cu[dev] = std::max(1, pc);
   }
-  const long long grid = std::min<long long>(a.N, (long long)per_cu[dev] * device_cus());
+  const long long slots = (long long)per_cu[dev] * device_cus();
+  CRArgs a = a0;
+  a.lgb = convt_row_bands_lg(a.N, a.H, slots);
+  const long long grid = std::min<long long>((long long)a.N << a.lgb, slots);
   SPECENH_LAUNCH((convt_rows_pw_kernel<T, 3>), dim3((unsigned)grid), dim3(256), LDS, st, a);
   return hipGetLastError();
 }
 
 template <typename T, int CO, int W, int LEAD>
-hipError_t launch_convt_rows_lead(const CRArgs& a, hipStream_t st) {
+hipError_t launch_convt_rows_lead(const CRArgs& a0, hipStream_t st) {
   using C = TC<CO, W>;
   const void* k = reinterpret_cast<const void*>(&convt_rows_kernel<T, CO, W, LEAD>);
   static int per_cu[64] = {};
@@ -927,7 +956,10 @@ hipError_t launch_convt_rows_lead(const CRArgs& a, hipStream_t st) {
     if (e != hipSuccess) return e;
     per_cu[dev] = std::max(1, pc);
   }
-  const long long grid = std::min<long long>(a.N, (long long)per_cu[dev] * device_cus());
+  const long long slots = (long long)per_cu[dev] * device_cus();
+  CRArgs a = a0;
+  a.lgb = convt_row_bands_lg(a.N, a.H, slots);
+  const long long grid = std::min<long long>((long long)a.N << a.lgb, slots);
   SPECENH_LAUNCH((convt_rows_kernel<T, CO, W, LEAD>), dim3((unsigned)grid), dim3(C::THREADS),
                  C::LDS, st, a);
   return hipGetLastError();

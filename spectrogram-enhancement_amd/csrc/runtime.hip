@@ -30,7 +30,7 @@ constexpr VariantName kVariants[V_COUNT] = {
     {"ROWS_SHORT_LEAD", 0},  {"SVD_GRAM_F32", 0},
     {"SVD_RECON_BLOCKS", 0}, {"CONVT_PG", 0}, {"SVD_GZ_ROWS", 0}, {"EIG_SPLIT", 0}, {"CO1_VALU", 0},
     {"C1_MASK_MFMA", 0}, {"S2_MIN_NT", 2}, {"PATCH_MIN_WG", 512}, {"WGRAD_WG", 4096}, {"WGRAD_C1_TILES", 4},
-    {"EIG_GRID", 32},
+    {"EIG_GRID", 32}, {"ROWS_BANDS", -1},
 };
 
 std::atomic<int> g_variant[V_COUNT];

@@ -49,6 +49,7 @@ enum Variant : int {
   V_WGRAD_WG,         // weight-gradient MFMA kernels: workgroups per launch aimed at (tile runs)
   V_WGRAD_C1_TILES,   // one-input-channel weight gradient: at least this many tiles per workgroup
   V_EIG_GRID,         // flagged-matrix fallback: workgroups per launch (<= 0: two per CU)
+  V_ROWS_BANDS,       // convT row sweeps: log2 row bands per image (-1: auto, small batches)
   V_COUNT
 };
 

@@ -318,3 +318,31 @@ def test_encoder2_engine_path(gpu_device, kernel_variant):
     b = eng2.forward(x)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("CO,W,ring", [(64, 16, "pw"), (64, 16, "shared"), (32, 32, "shared")])
+@pytest.mark.parametrize("N,H", [(1, 16), (3, 32), (128, 16), (200, 8), (5, 12)])
+def test_convt_rows_bands_bitwise(gpu_device, kernel_variant, CO, W, ring, N, H):
+    """Row bands (round 6): a small batch's images cut into 2 / 4 / 8 bands of rows (halo rows
+    read from the neighbouring band, two bubble steps between bands) give the whole-image
+    sweep's outputs bit for bit; N = 128 is the C4 training batch the automatic choice bands."""
+    rng = np.random.default_rng(23 + CO + N + H)
+    x = torch.tensor(rng.uniform(0, 1, (N, H, W, 64)), dtype=torch.float16, device=gpu_device)
+    w = torch.tensor(rng.standard_normal((CO, 5, 5, 64)) * 0.03, dtype=torch.float16,
+                     device=gpu_device)
+    bias = torch.tensor(rng.standard_normal(CO) * 0.1, dtype=torch.float32, device=gpu_device)
+    if ring == "shared":
+        kernel_variant("CONVT_SHARED_RING", 1)
+    kernel_variant("ROWS_BANDS", 0)
+    ref = torch.full((N, 2 * H, 2 * W, CO), float("nan"), dtype=torch.float16, device=gpu_device)
+    _convt_run(x, w, bias, CO, ref)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(ref).all())
+    for lg in (1, 2, 3, -1):
+        kernel_variant("ROWS_BANDS", lg)
+        got = torch.full_like(ref, float("nan"))
+        _convt_run(x, w, bias, CO, got)
+        torch.cuda.synchronize()
+        name = _lib.last_kernel_name()
+        assert ("convt_rows_pw_kernel" if ring == "pw" else "convt_rows_kernel") in name
+        assert torch.equal(got, ref), (lg, float((got.float() - ref.float()).abs().max()))

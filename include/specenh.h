@@ -240,14 +240,27 @@ int specenh_conv2d_wgrad(int dtype, const void* in, int N, int IH, int IW, int C
  * specenh_maxpool2_bwd(dpool, argmax, pooled) would write (the gradient routed to the argmax,
  * zero where pooled <= 0; pooled may be NULL: no ReLU mask), formed while the tiles are staged
  * (the model's first Conv2D in Model.fit, manual_scan_3layers.py:187-188: no full-resolution
- * gradient is written). bf16 / f16, C = 1, stride 1, even OH / OW, CO % 8 == 0, else
- * SPECENH_EUNSUPPORTED. Same workspace as specenh_conv2d_wgrad, but dw and dbias are
- * OVERWRITTEN with the gradient (not accumulated: no zeroing launch before it). */
+ * gradient is written; round 6: also the pooled Conv2Ds after it, :190-193). bf16 / f16,
+ * C = 1 or C % 16 == 0, stride 1, even OH / OW, CO % 8 == 0, else SPECENH_EUNSUPPORTED. Same
+ * workspace as specenh_conv2d_wgrad, but dw and dbias are OVERWRITTEN with the gradient (not
+ * accumulated: no zeroing launch before it). */
 int specenh_conv2d_wgrad_pooled(int dtype, const void* in, int N, int IH, int IW, int C,
                                 const void* dpool, const unsigned char* argmax, const void* pooled,
                                 int KH, int KW, int CO, int stride, int pad_t, int pad_l,
                                 int in_dil, int OH, int OW, float* dw, float* dbias,
                                 void* workspace, void* stream);
+/* specenh_conv2d (stride 1, in_dil 1, no pool2 / logits / out_f32) of an input that is the
+ * full-resolution gradient of a ReLU + MaxPooling2D((2,2)), given as the POOL's output
+ * gradient dpool [N][IH/2][IW/2][C], its argmax and pooled output (pooled may be NULL: no ReLU
+ * mask): in = what specenh_maxpool2_bwd(dpool, argmax, pooled) would write, formed while the
+ * input patches are staged — the input gradient of a pooled Conv2D in Model.fit
+ * (manual_scan_3layers.py:188-193) without the full-resolution gradient tensor or the pool
+ * backward launch. Bitwise the pool backward followed by specenh_conv2d. bf16 / f16, even
+ * IH / IW, C % 16 == 0 (else SPECENH_EUNSUPPORTED); mask, bias and act as specenh_conv2d. */
+int specenh_conv2d_pooled_in(int dtype, const void* dpool, const unsigned char* argmax,
+                             const void* pooled, int N, int IH, int IW, int C, const void* w_gemm,
+                             int KH, int KW, int CO, const float* bias, int pad_t, int pad_l,
+                             int OH, int OW, int act, const void* mask, void* out, void* stream);
 /* MaxPooling2D((2,2), padding="same") on even H, W: out [N][H/2][W/2][C] + argmax (0..3). */
 int specenh_maxpool2_fwd(int dtype, const void* in, int N, int H, int W, int C, void* out,
                          unsigned char* argmax, void* stream);

@@ -287,7 +287,37 @@ struct ConvArgs {
   // conv_patch_kernel<..., WL>: the workgroup's weight rows staged in LDS at byte offset
   // wl_off, row stride wl_rs elements (wl_rs / 2 = 8 mod 64 dwords: conflict-free fragments)
   int wl_off, wl_rs;
+  // conv_patch_kernel (specenh_conv2d_pooled_in): the input is the full-resolution gradient of
+  // a ReLU + MaxPooling2D((2,2)), formed from the pool's gradient rpd [N][IH/2][IW/2][C], its
+  // argmax ram and pooled output rpy (null: no ReLU mask) while the patch is staged
+  const void* rpd;
+  const unsigned char* ram;
+  const void* rpy;
 };
+
+// 8 channels of the full-resolution gradient a MaxPooling2D((2,2)) backward would write at a
+// pixel of parity sel = 2 (y & 1) + (x & 1): the pool's gradient dv where the argmax bytes am
+// name sel and the pooled output yv > 0 (the ReLU mask of the pool's input at its argmax;
+// > 0 as 16-bit bits: sign clear and nonzero), else 0 (specenh_maxpool2_bwd's arithmetic)
+__device__ __forceinline__ uint4 pool_route8(uint4 dv, uint2 am, uint4 yv, uint32_t sel) {
+  const uint32_t d4[4] = {dv.x, dv.y, dv.z, dv.w}, y4[4] = {yv.x, yv.y, yv.z, yv.w};
+  uint32_t o4[4];
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const uint32_t amw = h < 2 ? am.x : am.y;
+    uint32_t r = 0u;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const uint32_t y16 = (y4[h] >> (16 * b)) & 0xffffu;
+      const bool keep = ((amw >> (8 * (2 * (h & 1) + b))) & 0xffu) == sel && !(y16 & 0x8000u) &&
+                        y16 != 0u;
+      r |= keep ? (d4[h] & (0xffffu << (16 * b))) : 0u;
+    }
+    o4[h] = r;
+  }
+  return uint4{o4[0], o4[1], o4[2], o4[3]};
+}
+constexpr uint32_t POOL_ROUTE_POS = 0x3f803f80u;  // two 16-bit values > 0 (no ReLU mask)
 
 // ------------------------------------------------------------------ forward / dgrad
 template <typename T, int MT, int NT>
@@ -581,6 +611,56 @@ void conv_patch_kernel(ConvArgs a) {
       // zeroed, so the loads are unconditional
       constexpr int NB = (SPECENH_PATCH_WPE(PAIR, NT, CC) >= 4 || NT >= 4) ? 4 : 8;  // VGPR budget
       const int total = PH * PW * GP;
+      if constexpr (!S2 && !PAIR) {
+        if (a.rpd) {  // routed from the pool's gradient (specenh_conv2d_pooled_in)
+          // one element per (pooled pixel, 8-channel group) covering the patch: its gradient,
+          // argmax bytes and pooled value are loaded ONCE and give the 2 x 2 full-resolution
+          // pixels (those inside the patch; even IH / IW: all in the image or all out)
+          const int PHl = IHl >> 1, PWl = IWl >> 1;
+          const int qy0 = iy0 >> 1, qx0 = ix0 >> 1;  // (floor: arithmetic shifts)
+          const int QH = ((iy0 + PH - 1) >> 1) - qy0 + 1, QW = ((ix0 + PW - 1) >> 1) - qx0 + 1;
+          const int qwinv = (65536 + QW - 1) / QW;  // exact: qpix * (QW - 1) < 2^16
+          const int pbase = n * PHl * PWl * Cl + c * CC;
+          const T* __restrict__ dpb = reinterpret_cast<const T*>(a.rpd) + pbase;
+          const T* __restrict__ ypb = a.rpy ? reinterpret_cast<const T*>(a.rpy) + pbase : nullptr;
+          const unsigned char* __restrict__ amb = a.ram + pbase;
+          const int qtotal = QH * QW * GP;
+          constexpr int NR = NB / 2;  // three loads per element
+          for (int e0 = tid; e0 < qtotal; e0 += NR * 256) {
+            uint4 dv[NR], yv[NR];
+            uint2 am[NR];
+            int qy[NR], qx[NR], cg[NR];
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+              const int e = min(e0 + 256 * k, qtotal - 1);
+              const int qpix = e / GP;
+              cg[k] = e - qpix * GP;
+              const int r = (qpix * qwinv) >> 16;
+              qy[k] = qy0 + r;
+              qx[k] = qx0 + qpix - r * QW;
+              const bool ok = (unsigned)qy[k] < (unsigned)PHl && (unsigned)qx[k] < (unsigned)PWl;
+              const int po = (ok ? qy[k] * PWl + qx[k] : 0) * Cl + 8 * cg[k];
+              dv[k] = *reinterpret_cast<const uint4*>(dpb + po);
+              am[k] = *reinterpret_cast<const uint2*>(amb + po);
+              yv[k] = ypb ? *reinterpret_cast<const uint4*>(ypb + po)
+                          : uint4{POOL_ROUTE_POS, POOL_ROUTE_POS, POOL_ROUTE_POS, POOL_ROUTE_POS};
+              if (!ok) dv[k] = uint4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+              if (e0 + 256 * k >= qtotal) continue;
+#pragma unroll
+              for (int sub = 0; sub < 4; ++sub) {
+                const int py = 2 * qy[k] + (sub >> 1) - iy0, pxx = 2 * qx[k] + (sub & 1) - ix0;
+                if ((unsigned)py < (unsigned)PH && (unsigned)pxx < (unsigned)PW)
+                  *reinterpret_cast<uint4*>(sP + (py * PW + pxx) * PST + 8 * cg[k]) =
+                      pool_route8(dv[k], am[k], yv[k], (uint32_t)sub);
+              }
+            }
+          }
+          return;
+        }
+      }
       for (int e0 = tid; e0 < total; e0 += NB * 256) {
         uint4 v[NB];
         int dst[NB];
@@ -1309,7 +1389,7 @@ struct WgradTrArgs {
   float* part;       // [Z][CO][Kf]
   float* bpart;      // [nphase][Z][CO] or null
   int upt, upl, PH, PW;  // phase-shared launches (wgrad_trp_kernel): the union patch
-  const void* pd;        // C1 only: dOut from the pool's gradient (WgradArgs::pd), or null
+  const void* pd;        // dOut from the pool's gradient (WgradArgs::pd), or null
   const unsigned char* pam;
   const void* py;
 };
@@ -1428,10 +1508,41 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
     oyt = (int)(trem / (unsigned)ntx) * 16;
     oxt = (int)(trem - (trem / (unsigned)ntx) * (unsigned)ntx) * 16;
   };
+  // dOut element u of this thread: (tile pixel, 8-channel vector). Routed from a pool's
+  // gradient with 4 vectors per pixel, a thread takes ONE pooled (pixel, vector) and its 2 x 2
+  // full-resolution block (u = 2 dy + dx), so each pooled value is loaded once, not 4 times
+  const bool rblk = NDV == 4 && a.pd != nullptr;
+  auto dmap = [&](int u, int& pix, int& v) {
+    if (rblk) {
+      const int qp = tid >> 2;
+      v = tid & 3;
+      pix = ((2 * (qp >> 3) + (u >> 1)) << 4) + 2 * (qp & 7) + (u & 1);
+    } else {
+      const int e = tid + 256 * u;
+      pix = e / NDV;
+      v = e - pix * NDV;
+    }
+  };
   auto fetch = [&](long long tile) {
     int n, oyt, oxt;
     tile_org(tile, n, oyt, oxt);
-    if (co_vec) {
+    if (co_vec && rblk) {
+      const int qp = tid >> 2;
+      const int oy = oyt + 2 * (qp >> 3), ox = oxt + 2 * (qp & 7);  // the block's top left
+      const int co = co0 + 8 * (tid & 3);
+      uint4 dv = uint4{0u, 0u, 0u, 0u};
+      uint4 yv = uint4{POOL_ROUTE_POS, POOL_ROUTE_POS, POOL_ROUTE_POS, POOL_ROUTE_POS};
+      uint2 am = uint2{0u, 0u};
+      const bool ok = oy < g.OH && ox < g.OW && co < g.CO;  // (even OH, OW: whole block)
+      if (ok) {
+        const long long po = (((long long)n * (g.OH >> 1) + (oy >> 1)) * (g.OW >> 1) + (ox >> 1)) * g.CO + co;
+        dv = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.pd) + po);
+        am = *reinterpret_cast<const uint2*>(a.pam + po);
+        if (a.py) yv = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.py) + po);
+      }
+#pragma unroll
+      for (int u = 0; u < NDV; ++u) rd[u] = pool_route8(dv, am, yv, (uint32_t)u);
+    } else if (co_vec) {
 #pragma unroll
       for (int u = 0; u < NDV; ++u) {
         const int e = tid + 256 * u;
@@ -1439,34 +1550,16 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
         const int oy = oyt + (pix >> 4), ox = oxt + (pix & 15);
         const int co = co0 + 8 * v;
         rd[u] = uint4{0u, 0u, 0u, 0u};
-        if constexpr (C1) {
-          if (a.pd) {  // routed from the pool's gradient: argmax select + ReLU mask, 8 channels
-            if (oy < g.OH && ox < g.OW && co < g.CO) {
-              const long long po = (((long long)n * (g.OH >> 1) + (oy >> 1)) * (g.OW >> 1) + (ox >> 1)) * g.CO + co;
-              const uint4 dv = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.pd) + po);
-              const uint2 am = *reinterpret_cast<const uint2*>(a.pam + po);
-              uint4 yv = uint4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};  // > 0
-              if (a.py) yv = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.py) + po);
-              const uint32_t sel = (uint32_t)(((oy & 1) << 1) | (ox & 1));
-              const uint32_t d4[4] = {dv.x, dv.y, dv.z, dv.w}, y4[4] = {yv.x, yv.y, yv.z, yv.w};
-              uint32_t o4[4];
-#pragma unroll
-              for (int h = 0; h < 4; ++h) {
-                const uint32_t amw = h < 2 ? am.x : am.y;
-                uint32_t r = 0u;
-#pragma unroll
-                for (int b = 0; b < 2; ++b) {
-                  const uint32_t y16 = (y4[h] >> (16 * b)) & 0xffffu;  // > 0: sign clear, nonzero
-                  const bool keep = ((amw >> (8 * (2 * (h & 1) + b))) & 0xffu) == sel &&
-                                    !(y16 & 0x8000u) && y16 != 0u;
-                  r |= keep ? (d4[h] & (0xffffu << (16 * b))) : 0u;
-                }
-                o4[h] = r;
-              }
-              rd[u] = uint4{o4[0], o4[1], o4[2], o4[3]};
-            }
-            continue;
+        if (a.pd) {  // routed from the pool's gradient: argmax select + ReLU mask, 8 channels
+          if (oy < g.OH && ox < g.OW && co < g.CO) {
+            const long long po = (((long long)n * (g.OH >> 1) + (oy >> 1)) * (g.OW >> 1) + (ox >> 1)) * g.CO + co;
+            const uint4 dv = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.pd) + po);
+            const uint2 am = *reinterpret_cast<const uint2*>(a.pam + po);
+            uint4 yv = uint4{POOL_ROUTE_POS, POOL_ROUTE_POS, POOL_ROUTE_POS, POOL_ROUTE_POS};
+            if (a.py) yv = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.py) + po);
+            rd[u] = pool_route8(dv, am, yv, (uint32_t)(((oy & 1) << 1) | (ox & 1)));
           }
+          continue;
         }
         if (oy < g.OH && ox < g.OW && co < g.CO)
           rd[u] = *reinterpret_cast<const uint4*>(
@@ -1501,8 +1594,8 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
     if (co_vec) {
 #pragma unroll
       for (int u = 0; u < NDV; ++u) {
-        const int e = tid + 256 * u;
-        const int pix = e / NDV, v = e - (e / NDV) * NDV;
+        int pix, v;
+        dmap(u, pix, v);
         *reinterpret_cast<uint4*>(sD + pix * DST + 16 * dch(pix, v >> 1) + 8 * (v & 1)) = rd[u];
       }
     } else if (co_one) {
@@ -2856,10 +2949,10 @@ int specenh_conv2d_wgrad_pooled(int dtype, const void* in, int N, int IH, int IW
   if (!in || !dpool || !argmax || !dw || !workspace) return set_error(SPECENH_EINVAL, "null pointer");
   if (dtype != SPECENH_DTYPE_BF16 && dtype != SPECENH_DTYPE_F16)
     return set_error(SPECENH_EUNSUPPORTED, "pooled wgrad: bf16 / f16");
-  if (C != 1 || stride != 1 || in_dil != 1 || (OH & 1) || (OW & 1) || (CO & 7) ||
+  if ((C != 1 && C % 16 != 0) || stride != 1 || in_dil != 1 || (OH & 1) || (OW & 1) || (CO & 7) ||
       ((uintptr_t)dpool & 15) || ((uintptr_t)argmax & 7) || ((uintptr_t)pooled & 15))
     return set_error(SPECENH_EUNSUPPORTED,
-                     "pooled wgrad: one input channel, stride 1, even output, CO % 8 == 0");
+                     "pooled wgrad: C = 1 or C % 16 == 0, stride 1, even output, CO % 8 == 0");
   WgradArgs a{};
   int nph = 0;
   if (int e = plan_phases(N, IH, IW, C, CO, KH, KW, stride, pad_t, pad_l, in_dil, OH, OW, a.g, &nph))
@@ -2884,6 +2977,35 @@ int specenh_conv2d_wgrad_pooled(int dtype, const void* in, int N, int IH, int IW
   }
   if (!wgrad_tr_applies<_Float16>(a, nph)) return set_error(SPECENH_EUNSUPPORTED, "pooled wgrad: shape");
   return launch_wgrad_tr<_Float16>(a, nph, dw, dbias, st);
+}
+
+int specenh_conv2d_pooled_in(int dtype, const void* dpool, const unsigned char* argmax,
+                             const void* pooled, int N, int IH, int IW, int C, const void* w_gemm,
+                             int KH, int KW, int CO, const float* bias, int pad_t, int pad_l,
+                             int OH, int OW, int act, const void* mask, void* out, void* stream) {
+  if (int e = check_sizes(N, IH, IW, C, OH, OW, CO)) return e;
+  if (KH <= 0 || KW <= 0) return set_error(SPECENH_EINVAL, "bad convolution geometry");
+  if (!dpool || !argmax || !w_gemm || !out) return set_error(SPECENH_EINVAL, "null pointer");
+  if (act < 0 || act > 2) return set_error(SPECENH_EINVAL, "bad activation");
+  if (dtype != SPECENH_DTYPE_BF16 && dtype != SPECENH_DTYPE_F16)
+    return set_error(SPECENH_EUNSUPPORTED, "pool-routed conv: bf16 / f16");
+  if ((IH & 1) || (IW & 1) || C % 16 != 0 || ((uintptr_t)dpool & 15) || ((uintptr_t)argmax & 7) ||
+      ((uintptr_t)pooled & 15))
+    return set_error(SPECENH_EUNSUPPORTED, "pool-routed conv: even input, C % 16 == 0");
+  ConvArgs a{};
+  int nph = 0;
+  if (int e = plan_phases(N, IH, IW, C, CO, KH, KW, 1, pad_t, pad_l, 1, OH, OW, a.g, &nph)) return e;
+  a.in = dpool; a.w = w_gemm; a.bias = bias; a.out = out; a.mask = mask; a.act = act; a.nph = nph;
+  a.rpd = dpool; a.ram = argmax; a.rpy = pooled;
+  const int cc = variant(V_CONV_NO_PATCH) != 0 ? 0 : patch_cc(a, nph);
+  if (nph != 1 || (cc != 16 && cc != 32 && cc != 64))
+    return set_error(SPECENH_EUNSUPPORTED, "pool-routed conv: a stride-1 conv on the LDS-patch path");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == SPECENH_DTYPE_BF16)
+    return cc == 64 ? launch_patch<__bf16, 64>(a, nph, st)
+                    : (cc == 32 ? launch_patch<__bf16, 32>(a, nph, st) : launch_patch<__bf16, 16>(a, nph, st));
+  return cc == 64 ? launch_patch<_Float16, 64>(a, nph, st)
+                  : (cc == 32 ? launch_patch<_Float16, 32>(a, nph, st) : launch_patch<_Float16, 16>(a, nph, st));
 }
 
 int specenh_maxpool2_fwd(int dtype, const void* in, int N, int H, int W, int C, void* out,

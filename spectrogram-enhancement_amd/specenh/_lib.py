@@ -107,6 +107,11 @@ SIGNATURES = {
                                                _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
                                                _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p,
                                                _c.c_void_p]),
+    "specenh_conv2d_pooled_in": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                            _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_void_p,
+                                            _c.c_int, _c.c_int, _c.c_int, _c.c_void_p, _c.c_int,
+                                            _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_void_p,
+                                            _c.c_void_p, _c.c_void_p]),
     "specenh_convt_conv_out": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
                                           _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int,
                                           _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p,

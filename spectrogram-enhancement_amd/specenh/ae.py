@@ -200,6 +200,22 @@ class AutoencoderEngine:
                              and isinstance(self.ops[1], PoolOp)
                              and self.input_shape[0] % 2 == 0 and self.input_shape[1] % 2 == 0
                              and os.environ.get("SPECENH_NO_WGRAD_POOLED", "0") in ("", "0"))
+        # training (round 6): the other pooled Conv2Ds' weight AND input gradients straight
+        # from their pool's gradient (specenh_conv2d_wgrad_pooled, specenh_conv2d_pooled_in:
+        # argmax select + ReLU mask while the tiles / patches are staged), so the pool backward
+        # launch and its full-resolution gradient are gone from the input-gradient chain.
+        # SPECENH_NO_POOL_ROUTED=1: the pool backward + plain conv launches (bitwise the same)
+        self.pool_routed = set()
+        if self.dt != F32 and os.environ.get("SPECENH_NO_POOL_ROUTED", "0") in ("", "0"):
+            hw = self.input_shape[:2]
+            for i, op in enumerate(self.ops):
+                nxt = self.ops[i + 1] if i + 1 < len(self.ops) else None
+                if (i > 0 and isinstance(op, ConvOp) and op.kind == "conv" and op.stride == 1
+                        and op.padding == "same" and op.cin % 16 == 0 and op.cout % 16 == 0
+                        and op.k <= 7 and op.act in (None, "linear", "relu")
+                        and isinstance(nxt, PoolOp) and hw[0] % 2 == 0 and hw[1] % 2 == 0):
+                    self.pool_routed.add(i)
+                hw = op.out_hw(*hw) if isinstance(op, ConvOp) else (hw[0] // 2, hw[1] // 2)
         self.t = 0  # Adam iterations
         # backward: weight gradients on a second stream, off the input-gradient chain
         # (SPECENH_WGRAD_SERIAL=1: one stream, the round-4 order)
@@ -571,8 +587,8 @@ class AutoencoderEngine:
             prev_relu = isinstance(prev, ConvOp) and prev.act == "relu"
             relu_mask = hin if prev_relu else None
             if isinstance(op, PoolOp):
-                if i == 0 or (i == 1 and self.wgrad_pooled):
-                    continue  # nothing upstream needs it / conv 0's wgrad reads d[2] directly
+                if i == 0 or (i == 1 and self.wgrad_pooled) or (i - 1) in self.pool_routed:
+                    continue  # nothing upstream needs it / the conv reads d[i + 1] directly
                 _, H, W, C = d_out.shape
                 # ReLU mask of the pool's input at its argmax == (pooled output > 0)
                 ops.maxpool2_bwd_out(d_out, b["am"][i], b["h"][i + 1] if prev_relu else None,
@@ -587,8 +603,7 @@ class AutoencoderEngine:
                 if i == 0:
                     self._wgrad0(b, hin, d_out, op, s, pt, pl, dil, b["ws"])
                 else:
-                    ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[i],
-                                         self._gbv[i], b["ws"])
+                    self._wgrad(b, i, hin, d_out, op, s, pt, pl, dil, b["ws"])
                 if on_layer_done is not None:
                     on_layer_done(i)
             elif i == first and zeroed:
@@ -608,11 +623,17 @@ class AutoencoderEngine:
                     if i == 0:
                         self._wgrad0(b, hin, d_out, op, s, pt, pl, dil, b["ws"])
                     else:
-                        ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil,
-                                             self._gwv[i], self._gbv[i], b["ws"])
+                        self._wgrad(b, i, hin, d_out, op, s, pt, pl, dil, b["ws"])
                     if on_layer_done is not None:
                         on_layer_done(i)
             if i == 0:
+                continue
+            if i in self.pool_routed:
+                _, dpt, dpl, _ = op.dgrad_geom()
+                ops.conv2d_pooled_in_out(b["d"][i + 2], b["am"][i + 1],
+                                         b["h"][i + 2] if op.act == "relu" else None,
+                                         self.w_d[i], None, op.k, op.k, op.cin, dpt, dpl, IH, IW,
+                                         0, relu_mask, b["d"][i])
                 continue
             self._conv(i, d_out, b["d"][i], weights=self.w_d[i], geom=op.dgrad_geom(),
                        act=None, mask=relu_mask, bias=False, out_shape=(IH, IW), cout=op.cin)
@@ -631,6 +652,18 @@ class AutoencoderEngine:
         else:
             ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[0],
                                  self._gbv[0], ws)
+
+    def _wgrad(self, b, i, hin, d_out, op, s, pt, pl, dil, ws):
+        """Weight gradient of op i > 0: from its pool's gradient d[i + 2] when i is pool-routed
+        (d_out = d[i + 1] is then never formed), else from d_out. The routed form overwrites
+        the layer's slice, the other accumulates into it (zeroed beforehand): same values."""
+        if i in self.pool_routed:
+            ops.conv2d_wgrad_pooled_out(hin, b["d"][i + 2], b["am"][i + 1],
+                                        b["h"][i + 2] if op.act == "relu" else None, op.k, op.k,
+                                        s, pt, pl, dil, self._gwv[i], self._gbv[i], ws)
+        else:
+            ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[i],
+                                 self._gbv[i], ws)
 
     def _wait(self, waiter, signaler):
         if self.fork_mode == "torch":

@@ -356,6 +356,39 @@ _op(f"conv2d_wgrad_pooled_out(Tensor x, Tensor dpool, Tensor argmax, Tensor? poo
     lambda *a: None)
 
 
+def _conv_pooled_in_out(dpool, argmax, pooled, w, bias, kh, kw, cout, pad_t, pad_l, oh, ow, act,
+                        mask, out):
+    """specenh_conv2d_pooled_in: a stride-1 conv of the full-resolution gradient of a ReLU +
+    MaxPooling2D((2,2)) given as the pool's gradient dpool [N, IH/2, IW/2, C] (+ argmax, pooled
+    output): bitwise maxpool2_bwd followed by conv2d_out, without the full-resolution tensor."""
+    _need(dpool, "dpool")
+    _need(out, "out")
+    N, PH, PW, C = dpool.shape
+    IH, IW = 2 * PH, 2 * PW
+    if argmax.dtype != torch.uint8 or argmax.shape != dpool.shape:
+        raise ValueError("argmax must be uint8 like dpool")
+    if pooled is not None and (pooled.dtype != dpool.dtype or pooled.shape != dpool.shape):
+        raise ValueError("pooled must be like dpool")
+    if w.dtype != dpool.dtype or w.numel() != cout * kh * kw * C:
+        raise ValueError("w must be the [CO][KH][KW][C] GEMM weights in dpool's dtype")
+    _need(w, "w")
+    if tuple(out.shape) != (N, oh, ow, cout) or out.dtype != dpool.dtype:
+        raise ValueError(f"out must be {(N, oh, ow, cout)} in dpool's dtype")
+    if bias is not None and (bias.dtype != torch.float32 or bias.numel() != cout):
+        raise ValueError("bias must be float32 [CO]")
+    if mask is not None and (mask.dtype != dpool.dtype or mask.numel() != N * oh * ow * cout):
+        raise ValueError("mask must match the output (compute dtype)")
+    _lib.check(_lib.lib().specenh_conv2d_pooled_in(
+        _code(dpool), _vp(dpool), _vp(argmax), _vp(pooled), N, IH, IW, C, _vp(w), kh, kw, cout,
+        _vp(bias), pad_t, pad_l, oh, ow, act, _vp(mask), _vp(out), _st(dpool)),
+        "conv2d_pooled_in")
+
+
+_op("conv2d_pooled_in_out(Tensor dpool, Tensor argmax, Tensor? pooled, Tensor w, Tensor? bias, "
+    "int kh, int kw, int cout, int pad_t, int pad_l, int oh, int ow, int act, Tensor? mask, "
+    "Tensor(a!) out) -> ()", _conv_pooled_in_out, lambda *a: None)
+
+
 def _tail_out(x, wt, bt, cout, kt, wo, bo, ko, out):
     _need(x, "x")
     _need(out, "out")

@@ -250,6 +250,81 @@ def test_engine_wgrad_pooled_is_bitwise(gpu_device):
     assert torch.equal(grads[0], grads[1])
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("hw,c,co,k", [((32, 32), 64, 32, 5), ((64, 64), 32, 16, 5),
+                                        ((18, 22), 16, 32, 3), ((10, 6), 32, 48, 7)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_pool_routed_equals_pool_backward(gpu_device, dtype, hw, c, co, k, relu):
+    """Round 6: the pooled Conv2Ds after the first (C = 16 / 32 / 64 in, the C4 model's conv2
+    and conv3 at (64, 64) / (32, 32)) take their input gradient (specenh_conv2d_pooled_in) and
+    weight gradient (specenh_conv2d_wgrad_pooled, now any C % 16 == 0) straight from the
+    pool's gradient: bitwise specenh_maxpool2_bwd followed by specenh_conv2d / _wgrad, incl.
+    the ReLU mask of the layer below, ragged tiles and no pooled-output mask."""
+    from specenh import _lib
+    from specenh.ops import ops, wgrad_workspace
+    dev = torch.device(gpu_device)
+    g = torch.Generator(device=dev).manual_seed(7 + c + k)
+    N, (H, W) = 3, hw
+    p = (k - 1) // 2
+    # the conv's input (its own gradient's ReLU mask) and its pre-pool output's pool
+    x = torch.randn(N, H, W, co, device=dev, generator=g).to(dtype)
+    pre = torch.randn(N, H, W, c, device=dev, generator=g).to(dtype)
+    pooled, am = ops.maxpool2(pre)
+    dpool = torch.randn(N, H // 2, W // 2, c, device=dev, generator=g).to(dtype)
+    wd = (torch.randn(co, k, k, c, device=dev, generator=g) * 0.1).to(dtype)
+    mask = x if relu else None
+    pm = pooled if relu else None
+    # input gradient
+    d = torch.empty_like(pre)
+    ops.maxpool2_bwd_out(dpool, am, pm, d)
+    ref = torch.full((N, H, W, co), float("nan"), device=dev, dtype=dtype)
+    ops.conv2d_out(d, wd, None, k, k, co, 1, p, p, 1, H, W, 0, mask, None, ref, False, None)
+    got = torch.full_like(ref, float("nan"))
+    ops.conv2d_pooled_in_out(dpool, am, pm, wd, None, k, k, co, p, p, H, W, 0, mask, got)
+    torch.cuda.synchronize()
+    assert "conv_patch_kernel" in _lib.last_kernel_name()
+    assert bool(torch.isfinite(ref).all()) and float(ref.float().abs().max()) > 0
+    assert torch.equal(got, ref)
+    # weight gradient of the conv whose input is x (C = co) and output the pre-pool map
+    ws = wgrad_workspace(x, pre, k, k)
+    res = []
+    for fused in (True, False):
+        dw = torch.full((c, k, k, co), 7.0 if fused else 0.0, device=dev)
+        db = torch.full((c,), -3.0 if fused else 0.0, device=dev)
+        if fused:
+            ops.conv2d_wgrad_pooled_out(x, dpool, am, pm, k, k, 1, p, p, 1, dw, db, ws)
+        else:
+            ops.conv2d_wgrad_out(x, d, k, k, 1, p, p, 1, dw, db, ws)
+        res.append((dw, db))
+    torch.cuda.synchronize()
+    assert float(res[1][0].abs().max()) > 0
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("dtype", ["mixed_bfloat16", "mixed_float16"])
+def test_engine_pool_routed_is_bitwise(gpu_device, monkeypatch, dtype):
+    """The engine's pool-routed backward (round 6 default: no pool backward launches for
+    conv2 / conv3) and the pool backward + plain launches (SPECENH_NO_POOL_ROUTED=1):
+    bitwise equal gradients, with the weight gradients on the second stream and serial."""
+    ops_ = ref_model_ops()
+    rng = np.random.default_rng(29)
+    x = rng.uniform(0, 1, (8, 64, 64, 1))
+    y = rng.uniform(0, 1, (8, 64, 64, 1))
+    for serial in ("0", "1"):
+        monkeypatch.setenv("SPECENH_WGRAD_SERIAL", serial)
+        grads = []
+        for off in ("0", "1"):
+            monkeypatch.setenv("SPECENH_NO_POOL_ROUTED", off)
+            eng, _ = make(ops_, (64, 64, 1), dtype=dtype, seed=31)
+            assert eng.pool_routed == ({2, 4} if off == "0" else set())
+            eng.forward(upload(eng, x), train=True)
+            eng.loss_and_grad(upload(eng, y))
+            eng.backward()
+            grads.append(eng.g.clone())
+        assert float(grads[0].abs().max()) > 0
+        assert torch.equal(grads[0], grads[1])
+
+
 # ----------------------------------------------------------------------------- full model
 def test_reference_model_forward_fp32(gpu_device):
     ops = ref_model_ops()

@@ -7,7 +7,7 @@ import torch
 import specenh  # noqa: F401  (registers the operators)
 
 OPS = ["stft_psd", "stft_psd_out", "csd", "svd_denoise", "svd_denoise_out", "svd_denoise_optimal",
-       "conv2d", "conv2d_out", "conv2d_wgrad", "conv2d_wgrad_out", "conv2d_wgrad_pooled_out", "convt_conv_out",
+       "conv2d", "conv2d_out", "conv2d_wgrad", "conv2d_wgrad_out", "conv2d_wgrad_pooled_out", "conv2d_pooled_in_out", "convt_conv_out",
        "convt_conv_out_out", "convt_conv_out_train_out", "decoder3", "decoder3_out", "encoder2", "encoder2_out", "maxpool2",
        "maxpool2_out",
        "maxpool2_bwd", "maxpool2_bwd_out", "bce_logits", "bce_logits_out", "adam_step_", "adam_step_flip_",
@@ -21,6 +21,7 @@ CABI = {"specenh_stft_psd": "stft_psd_out", "specenh_stft_psd_f16": "stft_psd_ou
         "specenh_svd_denoise_optimal": "svd_denoise_optimal_out", "specenh_conv2d": "conv2d_out",
         "specenh_conv2d_wgrad": "conv2d_wgrad_out",
         "specenh_conv2d_wgrad_pooled": "conv2d_wgrad_pooled_out",
+        "specenh_conv2d_pooled_in": "conv2d_pooled_in_out",
         "specenh_convt_conv_out": "convt_conv_out_out",
         "specenh_convt_conv_out_train": "convt_conv_out_train_out", "specenh_decoder3_ex": "decoder3_out",
         "specenh_encoder2": "encoder2_out",

@@ -235,6 +235,13 @@ int specenh_conv2d_wgrad(int dtype, const void* in, int N, int IH, int IW, int C
                          const void* dout, int KH, int KW, int CO, int stride, int pad_t,
                          int pad_l, int in_dil, int OH, int OW, float* dw, float* dbias,
                          void* workspace, void* stream);
+/* specenh_conv2d_wgrad with overwrite != 0: dw and dbias are OVERWRITTEN with the gradient
+ * (same values as accumulating into zeroed buffers; Model.fit's layers each own their slice
+ * of the gradient buffer, so no zeroing launch precedes them). */
+int specenh_conv2d_wgrad_ex(int dtype, const void* in, int N, int IH, int IW, int C,
+                            const void* dout, int KH, int KW, int CO, int stride, int pad_t,
+                            int pad_l, int in_dil, int OH, int OW, float* dw, float* dbias,
+                            int overwrite, void* workspace, void* stream);
 /* specenh_conv2d_wgrad of a convolution followed by ReLU + MaxPooling2D((2,2)), given the
  * POOL's output gradient dpool [N][OH/2][OW/2][CO] instead of dout: dout is what
  * specenh_maxpool2_bwd(dpool, argmax, pooled) would write (the gradient routed to the argmax,

@@ -517,10 +517,15 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 // (row, column) parity sub-patches of 18 x 18, so tap (jy, jx) of output pixel (y, x) is
 // pixel (y + jy/2, x + jx/2) of sub-patch (jy&1, jx&1): the lanes' fragment reads stay
 // unit-stride and the k-step loop is the stride-1 one.
+// RT (round 6, specenh_conv2d_pooled_in): the input patch is routed from a pool's gradient
+// (ConvArgs::rpd / ram / rpy) while it is staged; a template argument, not a run-time test, so
+// the other instantiations' register allocation is untouched (as a run-time branch it cost
+// them 20-40 VGPRs and SGPR spills)
 template <typename T, int NT, int CC, bool POOL, bool PAIR = false, bool S2 = false, bool WS = false,
-          bool WL = false, bool K5 = false>
+          bool WL = false, bool K5 = false, bool RT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WS ? 3 : SPECENH_PATCH_WPE(PAIR, NT, CC))))
 void conv_patch_kernel(ConvArgs a) {
+  static_assert(!RT || (!S2 && !PAIR && !POOL && CC >= 16), "routed input: a plain stride-1 conv");
   static_assert(!S2 || (CC == 16 && !POOL && !PAIR), "stride-2 patches: CC 16, plain epilogue");
   static_assert(!WL || (CC == 16 && !PAIR && !WS), "LDS weights: the 16-channel single-chunk kernel");
   // K5: a plain stride-1 5 x 5 conv of one phase and one channel chunk (host-checked), so
@@ -611,8 +616,8 @@ void conv_patch_kernel(ConvArgs a) {
       // zeroed, so the loads are unconditional
       constexpr int NB = (SPECENH_PATCH_WPE(PAIR, NT, CC) >= 4 || NT >= 4) ? 4 : 8;  // VGPR budget
       const int total = PH * PW * GP;
-      if constexpr (!S2 && !PAIR) {
-        if (a.rpd) {  // routed from the pool's gradient (specenh_conv2d_pooled_in)
+      if constexpr (RT) {
+        {  // routed from the pool's gradient (specenh_conv2d_pooled_in)
           // one element per (pooled pixel, 8-channel group) covering the patch: its gradient,
           // argmax bytes and pooled value are loaded ONCE and give the 2 x 2 full-resolution
           // pixels (those inside the patch; even IH / IW: all in the image or all out)
@@ -1421,7 +1426,10 @@ __device__ __forceinline__ f32x4 mfma_s16(s16x8 a, s16x8 b, f32x4 acc) {
 #ifndef SPECENH_WGRAD_SWZ
 #define SPECENH_WGRAD_SWZ 1
 #endif
-template <typename T, int NTW, bool C1>
+// PD: dOut routed from a pool's gradient (WgradTrArgs::pd) — compiled in for C1 (the model's
+// first Conv2D, run-time test) and the PD instantiations (round 6: the pooled Conv2Ds after it)
+// only, so the other layers' kernels keep their registers
+template <typename T, int NTW, bool C1, bool PD = false>
 __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
   constexpr int CH = 16;             // input channels per workgroup: one k-block per tap
   constexpr int COT = 16 * NTW;      // output channels per workgroup
@@ -1511,7 +1519,7 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
   // dOut element u of this thread: (tile pixel, 8-channel vector). Routed from a pool's
   // gradient with 4 vectors per pixel, a thread takes ONE pooled (pixel, vector) and its 2 x 2
   // full-resolution block (u = 2 dy + dx), so each pooled value is loaded once, not 4 times
-  const bool rblk = NDV == 4 && a.pd != nullptr;
+  const bool rblk = PD && NDV == 4;
   auto dmap = [&](int u, int& pix, int& v) {
     if (rblk) {
       const int qp = tid >> 2;
@@ -1526,7 +1534,7 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
   auto fetch = [&](long long tile) {
     int n, oyt, oxt;
     tile_org(tile, n, oyt, oxt);
-    if (co_vec && rblk) {
+    if (PD && co_vec && rblk) {
       const int qp = tid >> 2;
       const int oy = oyt + 2 * (qp >> 3), ox = oxt + 2 * (qp & 7);  // the block's top left
       const int co = co0 + 8 * (tid & 3);
@@ -1550,7 +1558,7 @@ __global__ __launch_bounds__(256) void wgrad_tr_kernel(WgradTrArgs a) {
         const int oy = oyt + (pix >> 4), ox = oxt + (pix & 15);
         const int co = co0 + 8 * v;
         rd[u] = uint4{0u, 0u, 0u, 0u};
-        if (a.pd) {  // routed from the pool's gradient: argmax select + ReLU mask, 8 channels
+        if ((C1 || PD) && a.pd) {  // routed from the pool's gradient: argmax select + ReLU mask
           if (oy < g.OH && ox < g.OW && co < g.CO) {
             const long long po = (((long long)n * (g.OH >> 1) + (oy >> 1)) * (g.OW >> 1) + (ox >> 1)) * g.CO + co;
             const uint4 dv = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.pd) + po);
@@ -2440,7 +2448,7 @@ inline int patch_nt(int CO, unsigned tiles) {
   return nt;
 }
 
-template <typename T, int CC>
+template <typename T, int CC, bool RT = false>
 int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   // all phases of a dilated conv in one workgroup when they share a tile grid and the
   // input fits one channel chunk: one staged patch serves every phase, and the phases'
@@ -2482,10 +2490,10 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
     pair = g.oys == 2 && g.oxs == 2 && g.oy0 == i / 2 && g.ox0 == i % 2 && g.OHs == 2 * g.OH &&
            g.OWs == 2 * g.OW;
   }
-  if (pair) {
+  if (pair && !RT) {
     const dim3 grid2((tiles + 7) / 8 * 16, 1, 1);
     const size_t lds = patch_lds_bytes<T, CC>(a, nph, nt, true);
-#define SPECENH_PAIR(NT) SPECENH_LAUNCH((conv_patch_kernel<T, NT, CC, false, true>), grid2, dim3(256), lds, st, a)
+#define SPECENH_PAIR(NT) SPECENH_LAUNCH((conv_patch_kernel<T, NT, CC, false, !RT>), grid2, dim3(256), lds, st, a)
     if (nt == 1) SPECENH_PAIR(1);
     else if (nt == 2) SPECENH_PAIR(2);
     else if (nt == 3) SPECENH_PAIR(3);
@@ -2497,7 +2505,7 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   // are staged in LDS next to the patch, so the k-loop issues no global loads. With the
   // weights streamed from L2 into a register ring the compiler drained every in-flight ring
   // load at each k-step (s_waitcnt vmcnt(0)); SPECENH_PATCH_NO_WL=1 restores that path.
-  if constexpr (CC == 16) {
+  if constexpr (CC == 16 && !RT) {
     const int Kf = a.g[0].Kf;
     if (nph == 1 && !a.ph_shared && a.g[0].C == 16 && Kf % 8 == 0 &&
         !(variant(V_PATCH_NO_WL) != 0)) {
@@ -2553,7 +2561,7 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   if (ws_shape && (wsm == 1 || (wsm < 0 && ws_auto))) {
     const dim3 gridw(tiles, (unsigned)(CO / (32 * ntw)), a.ph_shared ? 1 : nph);
     const size_t ldsw = patch_lds_bytes<T, CC>(a, nph, ntw, false);
-#define SPECENH_PATCHW(NT, P) SPECENH_LAUNCH((conv_patch_kernel<T, NT, CC, P, false, false, true>), gridw, dim3(256), ldsw, st, a)
+#define SPECENH_PATCHW(NT, P) SPECENH_LAUNCH((conv_patch_kernel<T, NT, CC, P && !RT, false, false, true, false, false, RT>), gridw, dim3(256), ldsw, st, a)
     if (a.pool) {
       if (ntw == 1) SPECENH_PATCHW(1, true);
       else SPECENH_PATCHW(2, true);
@@ -2566,7 +2574,7 @@ int launch_patch(ConvArgs a, int nph, hipStream_t st) {
   }
   const dim3 grid(tiles, (unsigned)((CO + 16 * nt - 1) / (16 * nt)), a.ph_shared ? 1 : nph);
   const size_t lds = patch_lds_bytes<T, CC>(a, nph, nt, false);
-#define SPECENH_PATCH(NT, P) SPECENH_LAUNCH((conv_patch_kernel<T, NT, CC, P>), grid, dim3(256), lds, st, a)
+#define SPECENH_PATCH(NT, P) SPECENH_LAUNCH((conv_patch_kernel<T, NT, CC, P && !RT, false, false, false, false, false, RT>), grid, dim3(256), lds, st, a)
   if (a.pool) {
     if (nt == 1) SPECENH_PATCH(1, true);
     else if (nt == 2) SPECENH_PATCH(2, true);
@@ -2752,7 +2760,7 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
       !(variant(V_WGRAD_NO_CO1) != 0)) {
     a.Z = (int)std::max(1LL, std::min<long long>({tiles / 2, (long long)wgrad_tr_zmax(1, g0.Kf), wg_target}));
     SPECENH_LAUNCH(wgrad_co1_kernel<T>, dim3((unsigned)a.Z), dim3(64), 0, st, a);
-    launch_ordered_sums(a.part, a.Z, g0.Kf, dw, a.bpart, a.Z, 1, db, st);
+    launch_ordered_sums(a.part, a.Z, g0.Kf, dw, a.bpart, a.Z, 1, db, st, w.overwrite);
     return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
   }
   // Conv2DTranspose stride 2: all four phases per workgroup over one union patch
@@ -2793,7 +2801,8 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
       a.Z = (int)std::max(1LL, std::min<long long>(zp, wgrad_tr_zmax(g0.CO, g0.Kf)));
       SPECENH_LAUNCH(wgrad_trp_kernel<T>, dim3((unsigned)a.Z, (unsigned)(nchunk * a.ncog)), dim3(256), 0,
                          st, a);
-      launch_ordered_sums(a.part, a.Z, (long long)g0.CO * g0.Kf, dw, a.bpart, nph * a.Z, g0.CO, db, st);
+      launch_ordered_sums(a.part, a.Z, (long long)g0.CO * g0.Kf, dw, a.bpart, nph * a.Z, g0.CO, db, st,
+                          w.overwrite);
       return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
     }
   }
@@ -2802,8 +2811,13 @@ int launch_wgrad_tr(const WgradArgs& w, int nph, float* dw, float* db, hipStream
     if (ntw == 1) SPECENH_LAUNCH((wgrad_tr_kernel<T, 1, true>), grid, dim3(256), 0, st, a);
     else SPECENH_LAUNCH((wgrad_tr_kernel<T, 2, true>), grid, dim3(256), 0, st, a);
   } else {
-    if (ntw == 1) SPECENH_LAUNCH((wgrad_tr_kernel<T, 1, false>), grid, dim3(256), 0, st, a);
-    else SPECENH_LAUNCH((wgrad_tr_kernel<T, 2, false>), grid, dim3(256), 0, st, a);
+    if (a.pd) {
+      if (ntw == 1) SPECENH_LAUNCH((wgrad_tr_kernel<T, 1, false, true>), grid, dim3(256), 0, st, a);
+      else SPECENH_LAUNCH((wgrad_tr_kernel<T, 2, false, true>), grid, dim3(256), 0, st, a);
+    } else {
+      if (ntw == 1) SPECENH_LAUNCH((wgrad_tr_kernel<T, 1, false>), grid, dim3(256), 0, st, a);
+      else SPECENH_LAUNCH((wgrad_tr_kernel<T, 2, false>), grid, dim3(256), 0, st, a);
+    }
   }
   launch_ordered_sums(a.part, a.Z, (long long)g0.CO * g0.Kf, dw, a.bpart, nph * a.Z, g0.CO, db, st,
                       w.overwrite);
@@ -2833,7 +2847,8 @@ int launch_wgrad(WgradArgs& a, int nph, float* dw, float* db, hipStream_t st) {
   else if (p.nt == 3) SPECENH_WG(3);
   else SPECENH_WG(4);
 #undef SPECENH_WG
-  launch_ordered_sums(a.part, p.Z, (long long)g0.CO * g0.Kf, dw, a.bpart, nph * p.Z, g0.CO, db, st);
+  launch_ordered_sums(a.part, p.Z, (long long)g0.CO * g0.Kf, dw, a.bpart, nph * p.Z, g0.CO, db, st,
+                      a.overwrite);
   return hipGetLastError() == hipSuccess ? SPECENH_OK : set_error(SPECENH_EHIP, "wgrad launch");
 }
 
@@ -2913,6 +2928,14 @@ size_t specenh_conv2d_wgrad_workspace_bytes(int N, int OH, int OW, int KH, int K
 int specenh_conv2d_wgrad(int dtype, const void* in, int N, int IH, int IW, int C, const void* dout,
                          int KH, int KW, int CO, int stride, int pad_t, int pad_l, int in_dil,
                          int OH, int OW, float* dw, float* dbias, void* workspace, void* stream) {
+  return specenh_conv2d_wgrad_ex(dtype, in, N, IH, IW, C, dout, KH, KW, CO, stride, pad_t, pad_l,
+                                 in_dil, OH, OW, dw, dbias, 0, workspace, stream);
+}
+
+int specenh_conv2d_wgrad_ex(int dtype, const void* in, int N, int IH, int IW, int C,
+                            const void* dout, int KH, int KW, int CO, int stride, int pad_t,
+                            int pad_l, int in_dil, int OH, int OW, float* dw, float* dbias,
+                            int overwrite, void* workspace, void* stream) {
   if (int e = check_sizes(N, IH, IW, C, OH, OW, CO)) return e;
   if (KH <= 0 || KW <= 0 || stride <= 0 || in_dil <= 0)
     return set_error(SPECENH_EINVAL, "bad convolution geometry");
@@ -2927,6 +2950,7 @@ int specenh_conv2d_wgrad(int dtype, const void* in, int N, int IH, int IW, int C
   const WgradPlan p = wgrad_plan(KH * KW * C, CO);
   a.in = in;
   a.dout = dout;
+  a.overwrite = overwrite != 0;
   a.part = (float*)workspace;
   const size_t Zws = (C % 16 == 0 || C == 1)
                          ? std::max<size_t>(p.Z, wgrad_tr_zmax(CO, (long long)KH * KW * C))
@@ -3002,10 +3026,12 @@ int specenh_conv2d_pooled_in(int dtype, const void* dpool, const unsigned char* 
     return set_error(SPECENH_EUNSUPPORTED, "pool-routed conv: a stride-1 conv on the LDS-patch path");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == SPECENH_DTYPE_BF16)
-    return cc == 64 ? launch_patch<__bf16, 64>(a, nph, st)
-                    : (cc == 32 ? launch_patch<__bf16, 32>(a, nph, st) : launch_patch<__bf16, 16>(a, nph, st));
-  return cc == 64 ? launch_patch<_Float16, 64>(a, nph, st)
-                  : (cc == 32 ? launch_patch<_Float16, 32>(a, nph, st) : launch_patch<_Float16, 16>(a, nph, st));
+    return cc == 64 ? launch_patch<__bf16, 64, true>(a, nph, st)
+                    : (cc == 32 ? launch_patch<__bf16, 32, true>(a, nph, st)
+                                : launch_patch<__bf16, 16, true>(a, nph, st));
+  return cc == 64 ? launch_patch<_Float16, 64, true>(a, nph, st)
+                  : (cc == 32 ? launch_patch<_Float16, 32, true>(a, nph, st)
+                              : launch_patch<_Float16, 16, true>(a, nph, st));
 }
 
 int specenh_maxpool2_fwd(int dtype, const void* in, int N, int H, int W, int C, void* out,

@@ -787,7 +787,8 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
   // that separate images; the consumer's tail steps then run on, 2 per macro step, with
   // per-image tail step t = 0 .. 2 H1 + 1 (t >= 2 H1: zero map rows). The input stream has
   // one zero row between images (position i SPI), so producer step g reads positions
-  // g .. g + 2. Ring slots are global (macro step g, tail step 2g - 3 / 2g - 2), so the
+  // g .. g + 2. Ring slots are global (macro step g, tail steps 2g - 4 / 2g - 3; the MAP
+  // consumer 2g - 3 / 2g - 2), so the
   // compile-time slot offsets of the unrolled loops are the single-image ones. Round 2/3
   // launched one workgroup per image: per image the LDS clear, the 50 + 28 fragment loads
   // and the pipeline fill and drain (3 of 35 macro steps) were paid again.
@@ -941,7 +942,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
     clk.flush(wv);
 #endif
   } else if constexpr (!MAP) {
-    // ======================= map-free consumer, tail steps t = 2g - 3, 2g - 2 per macro step g
+    // ======================= map-free consumer, tail steps t = 2g - 4, 2g - 3 per macro step g
     // Tail step t (per-image tl) turns tail-input rows t - 1 .. t + 1 into the Conv2DTranspose
     // accumulators of map rows 2tl, 2tl + 1 (16 positions x 16 channels x 4 phases per wave),
     // packs them after bias + ReLU exactly as the map would hold them, and adds their Conv2D(1)
@@ -1022,7 +1023,10 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
     D3_BARRIER();  // macro step -1
 
     f32x4 P0 = f32x4{0.f, 0.f, 0.f, 0.f}, P1 = P0, P2 = P0;
-    int il = -1, tl = TPI - 3;  // tail step t = -3
+    // tail steps t = 2g - 4, 2g - 3 per macro step g (round 6; round 5: 2g - 3, 2g - 2): the
+    // per-image steps pair as (even, odd), so the two zero-map steps 2 H1, 2 H1 + 1 of an image
+    // share one macro step, which skips their MFMAs (tskip) instead of masking them
+    int il = -1, tl = TPI - 4;  // tail step t = -4
     // the nine B fragments of tail step t (ring slot T8 = t & 7): rows t - 1 .. t + 1, pixel
     // shifts dx = -1 .. 1
     auto frags = [&](auto ic, uint4 (&bq)[9]) {
@@ -1091,6 +1095,19 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       return true;
 #endif
     };
+    // a tail step without MFMAs (zero map rows: the image's steps 2 H1, 2 H1 + 1 and the
+    // pipeline's fill / drain): the pair rotation, exchange store and emit test of tstep
+    auto tskip = [&](float* bb, f32x4& E, int& eil, int& etl) -> bool {
+      eil = il;
+      etl = tl;
+      if (++tl == TPI) { tl = 0; ++il; }
+      E = P0;
+      P0 = P1;
+      P1 = P2;
+      P2 = f32x4{0.f, 0.f, 0.f, 0.f};
+      *(m == 0 || m == 15 ? bb + bwi : dump) = m == 0 ? E[2] : E[1];
+      return eil >= 0 && eil < nimg && etl >= 1 && etl <= H2;
+    };
     auto emit = [&](const f32x4& E, float edge, int eil, int etl) {  // edge: bb[bri]
       float s = bo + E[0];
       s += dpp_shift<0x111>(E[1]);  // row_shr:1: lane m reads lane m - 1
@@ -1112,13 +1129,19 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       float* const b1 = b0 + NBND;
       f32x4 E0, E1;
       int il0, tl0, il1, tl1;
-      uint4 bq[9];
-      frags(IC<(2 * I + 5) & 7>{}, bq);  // (2g - 3) & 7
-      __builtin_amdgcn_sched_barrier(0);
-      const bool e0 = tstep(IC<(2 * I + 5) & 7>{}, bq, b0, E0, il0, tl0);
-      frags(IC<(2 * I + 6) & 7>{}, bq);
-      __builtin_amdgcn_sched_barrier(0);
-      const bool e1 = tstep(IC<(2 * I + 6) & 7>{}, bq, b1, E1, il1, tl1);
+      bool e0, e1;
+      if (il >= 0 && il < nimg && tl < H2) {  // (wave-uniform) both steps inside an image
+        uint4 bq[9];
+        frags(IC<(2 * I + 4) & 7>{}, bq);  // (2g - 4) & 7
+        __builtin_amdgcn_sched_barrier(0);
+        e0 = tstep(IC<(2 * I + 4) & 7>{}, bq, b0, E0, il0, tl0);
+        frags(IC<(2 * I + 5) & 7>{}, bq);
+        __builtin_amdgcn_sched_barrier(0);
+        e1 = tstep(IC<(2 * I + 5) & 7>{}, bq, b1, E1, il1, tl1);
+      } else {
+        e0 = tskip(b0, E0, il0, tl0);
+        e1 = tskip(b1, E1, il1, tl1);
+      }
       D3_BARRIER();
       // (emitting these in the next macro step, after its first fragment reads, to overlap the
       // two LDS latencies: measured neutral, profiles/r06_d3_out16_ab.txt)

@@ -100,6 +100,11 @@ SIGNATURES = {
                                         _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
                                         _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p,
                                         _c.c_void_p]),
+    "specenh_conv2d_wgrad_ex": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                           _c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                           _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
+                                           _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int,
+                                           _c.c_void_p, _c.c_void_p]),
     "specenh_conv2d_wgrad_workspace_bytes": (_c.c_size_t, [_c.c_int] * 7),
     "specenh_conv2d_wgrad_pooled": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int,
                                                _c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p,

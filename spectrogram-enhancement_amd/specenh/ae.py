@@ -220,7 +220,14 @@ class AutoencoderEngine:
         # backward: weight gradients on a second stream, off the input-gradient chain
         # (SPECENH_WGRAD_SERIAL=1: one stream, the round-4 order)
         self.wgrad_overlap = os.environ.get("SPECENH_WGRAD_SERIAL", "0") in ("", "0")
-        self._side = None
+        # round 6: the weight gradients alternate over this many side streams (the side chain
+        # of one stream had become the step's critical path at batch 128), and every layer's
+        # weight gradient OVERWRITES its slice of self.g (no zeroing launches; the slices'
+        # alignment padding is never written and stays zero). SPECENH_WGRAD_STREAMS=1 and
+        # SPECENH_WGRAD_ACCUM=1 restore the round-5 schedule.
+        self.wgrad_streams = max(1, int(os.environ.get("SPECENH_WGRAD_STREAMS", "2") or 2))
+        self.wgrad_overwrite = os.environ.get("SPECENH_WGRAD_ACCUM", "0") in ("", "0")
+        self._sides = None
         # fork / join of the weight-gradient stream: "device" (library events with a
         # device-scope release, the default), "system" (library events, system-scope
         # fence), "torch" (torch.cuda.Stream.wait_stream)
@@ -321,6 +328,9 @@ class AutoencoderEngine:
                     ws = max(ws, int(self.L.specenh_conv2d_wgrad_workspace_bytes(
                         N, OH, OW, op.k, op.k, op.cin, op.cout)))
             b["ws"] = torch.empty(ws, dtype=torch.uint8, device=dev)
+            # one more per extra weight-gradient stream
+            b["wss"] = [b["ws"]] + [torch.empty(ws, dtype=torch.uint8, device=dev)
+                                    for _ in range(self.wgrad_streams - 1)]
             # the first convolution's weight gradient runs on the current stream beside the
             # second stream's last ones (backward): a workspace of its own
             first = next((i for i, op in enumerate(self.ops) if isinstance(op, ConvOp)), None)
@@ -556,22 +566,28 @@ class AutoencoderEngine:
         self.g[ops[i].off_w:] is final in that stream's order.
 
         The input-gradient chain (dgrad, pool backward) stays on the current stream; each
-        layer's weight gradient (wgrad + its ordered partial sum) is enqueued on a second
-        stream as soon as the layer's output gradient exists, so the under-filled wgrad
-        launches of a 128-sample step run beside the chain instead of after each link. The
-        current stream waits for the second one before returning: the same kernels on the
-        same inputs, bitwise the serial result (tests/test_ae_gpu.py)."""
+        layer's weight gradient (wgrad + its ordered partial sum) is enqueued on a side
+        stream (round-robin over self.wgrad_streams of them, each with its own workspace) as
+        soon as the layer's output gradient exists, so the under-filled wgrad launches of a
+        128-sample step run beside the chain and beside each other instead of after each
+        link. The current stream waits for the side streams before returning: the same
+        kernels on the same inputs, bitwise the serial result (tests/test_ae_gpu.py)."""
         N = self._last_train_N
         b = self._buffers(N, True)
         main = torch.cuda.current_stream(self.device)
-        side = None
+        ow = self.wgrad_overwrite
+        sides = []
         if self.wgrad_overlap:
-            if self._side is None:
-                self._side = torch.cuda.Stream(device=self.device)
-            side = self._side
-        else:
+            if self._sides is None or len(self._sides) != self.wgrad_streams:
+                self._sides = [torch.cuda.Stream(device=self.device)
+                               for _ in range(self.wgrad_streams)]
+            sides = self._sides
+        elif not ow:
             self.g.zero_()
-        zeroed = side is None
+        zeroed = not sides or ow
+        while len(b["wss"]) < len(sides):  # (wgrad_streams raised after the buffers were made)
+            b["wss"].append(torch.empty_like(b["ws"]))
+        used = []  # side streams that received work, in issue order
         n_ops = len(self.ops)
         first = next((i for i, op in enumerate(self.ops) if isinstance(op, ConvOp)), -1)
         # the first convolution's gradient slice g[:g0_end] (the layers' slices follow the op
@@ -599,7 +615,7 @@ class AutoencoderEngine:
             _, IH, IW, C = hin.shape
             OH, OW = d_out.shape[1:3]
             s, pt, pl, dil = op.fwd_geom()
-            if side is None:
+            if not sides:
                 if i == 0:
                     self._wgrad0(b, hin, d_out, op, s, pt, pl, dil, b["ws"])
                 else:
@@ -608,24 +624,31 @@ class AutoencoderEngine:
                     on_layer_done(i)
             elif i == first and zeroed:
                 # no input gradient follows: the current stream is idle, so this weight
-                # gradient runs there, beside the second stream's remaining ones
-                if not self.wgrad_pooled:  # (the pooled form overwrites its slice)
+                # gradient runs there, beside the side streams' remaining ones
+                if not (self.wgrad_pooled or ow):  # (overwriting forms need no zeroing)
                     self.g[:g0_end].zero_()
                 self._wgrad0(b, hin, d_out, op, s, pt, pl, dil, b["ws0"])
                 if on_layer_done is not None:
                     on_layer_done(i)
             else:
+                k = len(used) % len(sides)
+                side = sides[k]
                 self._wait(side, main)  # d_out is ready
                 with torch.cuda.stream(side):
                     if not zeroed:  # zeroed off the input-gradient chain (but the first
                         self.g[g0_end:].zero_()  # layer's slice: its wgrad runs on `main`)
                         zeroed = True
                     if i == 0:
-                        self._wgrad0(b, hin, d_out, op, s, pt, pl, dil, b["ws"])
+                        self._wgrad0(b, hin, d_out, op, s, pt, pl, dil, b["wss"][k])
                     else:
-                        self._wgrad(b, i, hin, d_out, op, s, pt, pl, dil, b["ws"])
+                        self._wgrad(b, i, hin, d_out, op, s, pt, pl, dil, b["wss"][k])
                     if on_layer_done is not None:
+                        # every weight gradient enqueued so far is final in this stream's order
+                        for o in sides:
+                            if o is not side and o in used:
+                                self._wait(side, o)
                         on_layer_done(i)
+                used.append(side)
             if i == 0:
                 continue
             if i in self.pool_routed:
@@ -639,8 +662,9 @@ class AutoencoderEngine:
                        act=None, mask=relu_mask, bias=False, out_shape=(IH, IW), cout=op.cin)
         if not zeroed:  # no convolution reported a gradient
             self.g.zero_()
-        if side is not None:
-            self._wait(main, side)
+        for side in sides:
+            if side in used:
+                self._wait(main, side)
 
     def _wgrad0(self, b, hin, d_out, op, s, pt, pl, dil, ws):
         """Weight gradient of op 0: from its pool's gradient d[2] (argmax + ReLU mask of the
@@ -651,7 +675,7 @@ class AutoencoderEngine:
                                         pt, pl, dil, self._gwv[0], self._gbv[0], ws)
         else:
             ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[0],
-                                 self._gbv[0], ws)
+                                 self._gbv[0], ws, self.wgrad_overwrite)
 
     def _wgrad(self, b, i, hin, d_out, op, s, pt, pl, dil, ws):
         """Weight gradient of op i > 0: from its pool's gradient d[i + 2] when i is pool-routed
@@ -663,7 +687,7 @@ class AutoencoderEngine:
                                         s, pt, pl, dil, self._gwv[i], self._gbv[i], ws)
         else:
             ops.conv2d_wgrad_out(hin, d_out, op.k, op.k, s, pt, pl, dil, self._gwv[i],
-                                 self._gbv[i], ws)
+                                 self._gbv[i], ws, self.wgrad_overwrite)
 
     def _wait(self, waiter, signaler):
         if self.fork_mode == "torch":

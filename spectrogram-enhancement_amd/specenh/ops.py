@@ -288,7 +288,8 @@ def wgrad_workspace(x, dout, kh, kw):
     return torch.empty(max(16, n), dtype=torch.uint8, device=x.device)
 
 
-def _wgrad_out(x, dout, kh, kw, stride, pad_t, pad_l, in_dil, dw, dbias, workspace):
+def _wgrad_out(x, dout, kh, kw, stride, pad_t, pad_l, in_dil, dw, dbias, workspace,
+               overwrite=False):
     _need(x, "x")
     _need(dout, "dout")
     N, IH, IW, C = x.shape
@@ -302,6 +303,11 @@ def _wgrad_out(x, dout, kh, kw, stride, pad_t, pad_l, in_dil, dw, dbias, workspa
     need = int(_lib.lib().specenh_conv2d_wgrad_workspace_bytes(N, OH, OW, kh, kw, C, CO))
     if workspace.numel() < need:
         raise ValueError(f"workspace needs {need} bytes")
+    if overwrite:  # dw / dbias = the gradient (no zeroing beforehand)
+        _lib.check(_lib.lib().specenh_conv2d_wgrad_ex(
+            _code(x), _vp(x), N, IH, IW, C, _vp(dout), kh, kw, CO, stride, pad_t, pad_l, in_dil,
+            OH, OW, _vp(dw), _vp(dbias), 1, _vp(workspace), _st(x)), "conv2d_wgrad")
+        return
     _lib.check(_lib.lib().specenh_conv2d_wgrad(
         _code(x), _vp(x), N, IH, IW, C, _vp(dout), kh, kw, CO, stride, pad_t, pad_l, in_dil, OH,
         OW, _vp(dw), _vp(dbias), _vp(workspace), _st(x)), "conv2d_wgrad")
@@ -322,7 +328,7 @@ _op(f"conv2d_wgrad(Tensor x, Tensor dout, {_WG_ARGS}) -> (Tensor, Tensor)", _wgr
     (x.new_empty((dout.shape[3], kh, kw, x.shape[3]), dtype=torch.float32),
      x.new_empty((dout.shape[3],), dtype=torch.float32)))
 _op(f"conv2d_wgrad_out(Tensor x, Tensor dout, {_WG_ARGS}, Tensor(a!) dw, Tensor(b!)? dbias, "
-    "Tensor(c!) workspace) -> ()", _wgrad_out, lambda *a: None)
+    "Tensor(c!) workspace, bool overwrite=False) -> ()", _wgrad_out, lambda *a, **k: None)
 
 
 def _wgrad_pooled_out(x, dpool, argmax, pooled, kh, kw, stride, pad_t, pad_l, in_dil, dw, dbias,

@@ -605,9 +605,14 @@ def test_wgrad_side_stream_is_bitwise_serial(gpu_device, dtype, hw, n):
     xs = [rng.uniform(0, 1, (n, *hw, 1)) for _ in range(3)]
     ys = [rng.uniform(0, 1, (n, *hw, 1)) for _ in range(3)]
     state = []
-    for overlap in (True, False):
+    # (overlap, side streams, overwrite): the round-6 default (two side streams, overwriting
+    # weight gradients), round 5's one accumulating side stream, and the serial orders
+    for overlap, streams, ow in ((True, 2, True), (True, 3, True), (True, 1, False),
+                                 (False, 1, True), (False, 1, False)):
         eng, _ = make(ops, (*hw, 1), dtype=dtype, seed=41)
         eng.wgrad_overlap = overlap
+        eng.wgrad_streams = streams
+        eng.wgrad_overwrite = ow
         seen = []
         for x, y in zip(xs, ys):
             eng.forward(upload(eng, x), train=True)
@@ -617,8 +622,9 @@ def test_wgrad_side_stream_is_bitwise_serial(gpu_device, dtype, hw, n):
         torch.cuda.synchronize()
         assert seen == [i for i in range(len(ops) - 1, -1, -1) if ops[i].__class__.__name__ == "ConvOp"] * 3
         state.append([t.clone() for t in (eng.g, eng.w, eng.m, eng.v)])
-    for a, b in zip(*state):
-        assert torch.equal(a, b)
+    for other in state[1:]:
+        for a, b in zip(state[0], other):
+            assert torch.equal(a, b)
 
 
 def test_reference_model_fp16_relative(gpu_device):

@@ -33,6 +33,9 @@ def _cases(dev):
     xb1 = r(2, 8, 8, 1, dtype=torch.bfloat16)
     pooled_b, am_b = r(2, 4, 4, 8, dtype=torch.bfloat16), torch.zeros(2, 4, 4, 8, dtype=torch.uint8,
                                                                      device=dev)
+    pq_b = r(2, 4, 4, 32, dtype=torch.bfloat16, lo=-1)
+    am_q = torch.randint(0, 4, (2, 4, 4, 32), dtype=torch.uint8, device=dev)
+    wq_b = r(16 * 9 * 32, dtype=torch.bfloat16, lo=-0.1, hi=0.1)
     wt, bc16 = r(16 * 25 * 32, dtype=torch.float16, lo=-0.1, hi=0.1), r(16, lo=-0.1, hi=0.1)
     wo, bo = r(25 * 16, dtype=torch.float16, lo=-0.2, hi=0.2), r(1)
     Sp = r(1, 256, 3845)
@@ -72,6 +75,12 @@ def _cases(dev):
                                        torch.zeros(8, 3, 3, 1, device=dev),
                                        torch.zeros(8, device=dev),
                                        torch.empty(1 << 20, dtype=torch.uint8, device=dev))),
+        (ops.conv2d_pooled_in_out, (pq_b, am_q, pq_b, wq_b, None, 3, 3, 16, 1, 1, 8, 8, 0,
+                                    r(2, 8, 8, 16, dtype=torch.bfloat16, lo=-1),
+                                    torch.empty(2, 8, 8, 16, device=dev, dtype=torch.bfloat16))),
+        (ops.conv2d_wgrad_out, (xc, dout, 3, 3, 1, 1, 1, 1, torch.zeros(8, 3, 3, 4, device=dev),
+                                torch.zeros(8, device=dev),
+                                torch.empty(1 << 20, dtype=torch.uint8, device=dev), True)),
         (ops.convt_conv_out, (xt, wt, bc16, 16, 5, wo, bo, 5)),
         (ops.convt_conv_out_out, (xt, wt, bc16, 16, 5, wo, bo, 5,
                                   torch.empty(2, 40, 24, 1, device=dev))),

@@ -22,6 +22,7 @@ CABI = {"specenh_stft_psd": "stft_psd_out", "specenh_stft_psd_f16": "stft_psd_ou
         "specenh_conv2d_wgrad": "conv2d_wgrad_out",
         "specenh_conv2d_wgrad_pooled": "conv2d_wgrad_pooled_out",
         "specenh_conv2d_pooled_in": "conv2d_pooled_in_out",
+        "specenh_conv2d_wgrad_ex": "conv2d_wgrad_out",
         "specenh_convt_conv_out": "convt_conv_out_out",
         "specenh_convt_conv_out_train": "convt_conv_out_train_out", "specenh_decoder3_ex": "decoder3_out",
         "specenh_encoder2": "encoder2_out",

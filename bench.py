@@ -31,7 +31,7 @@ Rank 0 prints ONE JSON line with, besides the contract fields:
                 A7 MACs x 2) / the unit's peak (MFMA 2.5 PFLOP/s dense fp16 for every layer of
                 the fused forward; an unfused 1-output-channel conv would run on the VALU,
                 v_dot2 314.6 TFLOP/s). traffic = measured HBM
-                bytes of that launch from profiles/pmc_r05.json (rocprofv3 --pmc passes of
+                bytes of that launch from profiles/pmc_r06.json (rocprofv3 --pmc passes of
                 tools/pmc_refresh.sh at the same shapes, keyed by the exact kernel symbol: null
                 with a warning when the timed launch ran a different kernel); stages.ae_layers
                 has every layer.
@@ -177,7 +177,7 @@ def ae_layer_costs(h=HW5, w=HW5, act_bytes=2, out_bytes=4, tail=False, dec3=Fals
     return res
 
 
-PMC_FILE = os.path.join(REPO, "profiles", "pmc_r05.json")
+PMC_FILE = os.path.join(REPO, "profiles", "pmc_r06.json")
 
 
 def load_pmc():

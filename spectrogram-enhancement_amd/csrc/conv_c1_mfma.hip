@@ -1,9 +1,10 @@
 // conv_c1_mfma.hip — one-input-channel convolutions on MFMA (gfx950).
 //
 // The first Conv2D of the reference model (1 -> 16 channels, k 5, relu, then
-// MaxPooling2D((2,2)); VAE/manual_scan_3layers.py:187-188). (The masked epilogue below also
-// serves the input gradient of the last conv, 16 -> 1 through the previous ReLU, :199, but
-// the dispatcher sends that one to the VALU kernel, which measured faster for it.) With
+// MaxPooling2D((2,2)); VAE/manual_scan_3layers.py:187-188). The masked epilogue below also
+// serves the input gradient of the last conv, 16 -> 1 through the previous ReLU, :199 (round 6
+// default: with the C4 weight gradients on two side streams the C4 step is 0.688 -> 0.671 ms
+// against the VALU kernel, which round 5 had kept; SPECENH_C1_MASK_MFMA=0 selects it). With
 // C == 1 the GEMM-K of a pixel is its K x K window. The window
 // rows are contiguous runs of the input row, so the MFMA K index is laid out as (ky, kx)
 // with kx padded to 8: a lane's 8 K-elements are ONE 8-element run of an input row, and
@@ -326,8 +327,8 @@ int launch_conv_c1_mfma(int dtype, const void* in, int N, int IH, int IW, int C,
                         unsigned char* argmax, const void* mask, hipStream_t st) {
   if (C != 1 || (dtype != SPECENH_DTYPE_BF16 && dtype != SPECENH_DTYPE_F16)) return 0;
   if (KH != KW || KH > 8 || out_f32 || logits) return 0;
-  // the masked full-resolution store (the C4 input gradient of the last conv) is faster on
-  // the VALU kernel (tools/c1_bench.py: 630 vs 834 us per 2048 shots, fp16)
+  // the masked full-resolution store (the C4 input gradient of the last conv): here by default
+  // (round 6, see the file comment; SPECENH_C1_MASK_MFMA=0: the VALU kernel)
   if (mask && variant(V_C1_MASK_MFMA) == 0) return 0;
   if (pool && ((OH & 1) || (OW & 1))) return 0;
   if ((IW & 1) || ((uintptr_t)in & 3)) return 0;  // staged as 32-bit words

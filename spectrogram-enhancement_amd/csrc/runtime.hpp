@@ -43,7 +43,7 @@ enum Variant : int {
   V_SVD_GZ_ROWS,      // subspace G Z one row per thread (round 4) instead of four
   V_EIG_SPLIT,        // flagged-matrix fp64 fallback as four launches instead of one
   V_CO1_VALU,         // one-output-channel conv on 32 channels: VALU dot2 kernel instead of MFMA
-  V_C1_MASK_MFMA,     // masked C = 1 conv (C4 input gradient of the last conv) on MFMA
+  V_C1_MASK_MFMA,     // masked C = 1 conv (C4 input gradient of the last conv) on MFMA (1, round 6) or the VALU (0)
   V_S2_MIN_NT,        // stride-2 input-gradient patch kernel: at least this many 16-channel N tiles
   V_PATCH_MIN_WG,     // patch kernels: fewer output-channel tiles per workgroup until this many workgroups
   V_WGRAD_WG,         // weight-gradient MFMA kernels: workgroups per launch aimed at (tile runs)

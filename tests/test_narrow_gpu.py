@@ -59,6 +59,10 @@ def test_c1_masked_dgrad(gpu_device, kernel_variant, dtype, N, H, W, path):
     mask = torch.tensor(rng.standard_normal((N, H, W, co)), dtype=dtype, device=gpu_device)
     mask[0, 0, :4] = 0.0  # exact zeros: masked like negatives
     got = _conv(x, w, bias, k, co, 0, dtype, mask).double().cpu()
+    from specenh import _lib
+    name = _lib.last_kernel_name()
+    assert {"c1mfma": "conv_c1_mfma_kernel", "narrow": "conv_c1_kernel",
+            "generic": "conv_patch_kernel"}[path] in name, name
     ref, mag = _ref(x, w, bias, k)
     keep = (mask.double().cpu() > 0)
     ref = torch.where(keep, ref, torch.zeros_like(ref))

@@ -704,7 +704,10 @@ __device__ __forceinline__ int x2_off(int ps, int g) { return ps * d3::X2ST + 8 
 
 
 #ifndef SPECENH_D3_CPRIO
-#define SPECENH_D3_CPRIO 0  // measured +4 % (tools/lib_ab.sh, profiles/r04_d3_ab.txt)
+// round 4: +4 % (profiles/r04_d3_ab.txt); round 6, with the zero-map steps skipped and the
+// consumer at 0.95 of the macro step vs the producers' 0.66 (tools/d3_stats.py): -1.3 % per
+// launch over 3 interleaved rounds (profiles/r06_d3_cprio_ab.txt)
+#define SPECENH_D3_CPRIO 1
 #endif
 #ifndef SPECENH_D3_BRANCHFREE
 #define SPECENH_D3_BRANCHFREE 1

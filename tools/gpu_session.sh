@@ -2,6 +2,5 @@
 # Per-call GPU script (overwritten per experiment).
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_decoder_tail_gpu.py tests/test_c5_chain_gpu.py tests/test_decoder3_mapping.py -x -q --timeout 120 --timeout-method thread > gpurun_out/s31_pytest.txt 2>&1 || { tail -30 gpurun_out/s31_pytest.txt; exit 1; }
-tail -1 gpurun_out/s31_pytest.txt
-bash tools/gpu.sh r06c bench prof
+timeout -k 10 200 python tools/c4_routed_probe.py > gpurun_out/s32_routed.txt 2>&1 || { tail gpurun_out/s32_routed.txt; exit 1; }
+grep -v amdgpu.ids gpurun_out/s32_routed.txt

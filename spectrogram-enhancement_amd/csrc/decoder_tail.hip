@@ -689,7 +689,8 @@ constexpr int LDS_BYTES = LDS_X1 + LDS_X2 + LDS_M + LDS_S;  // 123,136 B: one wo
 // of the 4 consumer waves, slots 1 .. 4 (0 and 5: the image's zero borders), 2 sides x 4
 // lane groups
 constexpr int NBND = 6 * 2 * 4;
-constexpr int LDS_BYTES_NM = LDS_X1 + LDS_X2 + (4 * NBND + 64) * 4;  // 69,632 B (+ 64 dump words)
+constexpr int BSTR = NBND + 64;  // exchange buffer stride: the slots + one dump word per lane
+constexpr int LDS_BYTES_NM = LDS_X1 + LDS_X2 + 4 * BSTR * 4;  // 70,400 B
 }  // namespace d3
 
 // first Conv2DTranspose input pixel ps (x = ps - 1), 16-byte group g of its 8: group g sits
@@ -1014,9 +1015,9 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
     // every other lane a never-written zero word
     const int orow = kg >> 1, ocol = 32 * w + 2 * m + (kg & 1);
     // every lane stores its word each tail step (no exec-mask branch): lanes other than
-    // m = 0 / 15 into their own word of a dump area past the four exchange buffers
-    float* const dump = bnd + 4 * NBND + lane;
-    const int bwi = ((w + 1) * 2 + (m == 0 ? 1 : 0)) * 4 + kg;
+    // m = 0 / 15 into their own word of the buffer's dump area (one lane-constant index: a
+    // per-buffer pointer select had compiled to exec-mask branches every tail step)
+    const int bwi = (m == 0 || m == 15) ? ((w + 1) * 2 + (m == 0 ? 1 : 0)) * 4 + kg : NBND + lane;
     const int bri = m == 0 ? (w * 2 + 0) * 4 + kg : (m == 15 ? ((w + 2) * 2 + 1) * 4 + kg : 0);
 #if SPECENH_D3_CPRIO
     // the consumer waves are the macro step's critical path (barrier clocks, tools/d3_stats.py:
@@ -1090,7 +1091,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       P1 = P2;
       P2 = f32x4{0.f, 0.f, 0.f, 0.f};
 #if SPECENH_D3_BRANCHFREE
-      *(m == 0 || m == 15 ? bb + bwi : dump) = m == 0 ? E[2] : E[1];
+      bb[bwi] = m == 0 ? E[2] : E[1];
       return img && etl >= 1 && etl <= H2;  // pair tl - 1 is an output row pair
 #else
       if (etl < 1 || etl > H2) return false;  // pair tl - 1 is not an output row pair
@@ -1108,7 +1109,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       P0 = P1;
       P1 = P2;
       P2 = f32x4{0.f, 0.f, 0.f, 0.f};
-      *(m == 0 || m == 15 ? bb + bwi : dump) = m == 0 ? E[2] : E[1];
+      bb[bwi] = m == 0 ? E[2] : E[1];
       return eil >= 0 && eil < nimg && etl >= 1 && etl <= H2;
     };
     auto emit = [&](const f32x4& E, float edge, int eil, int etl) {  // edge: bb[bri]
@@ -1128,8 +1129,8 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
     };
     auto cstep = [&](auto ic) {
       constexpr int I = decltype(ic)::value;  // g & 3
-      float* const b0 = bnd + ((I & 1) * 2) * NBND;
-      float* const b1 = b0 + NBND;
+      float* const b0 = bnd + ((I & 1) * 2) * BSTR;
+      float* const b1 = b0 + BSTR;
       f32x4 E0, E1;
       int il0, tl0, il1, tl1;
       bool e0, e1;

@@ -671,6 +671,15 @@ __global__ __launch_bounds__(256, 2) void tail_rows_kernel(RowsArgs a) {
 //    rows behind the producer.
 // Waves w and w + 4 share a SIMD (MI355X_MICROARCH.md, two waves per SIMD): each SIMD pairs
 // one producer and one consumer. Macro steps are unrolled by 4, the rings' period.
+// the output emission (bias, edge word, sigmoid, store) of each tail step runs on the producer
+// waves (idle 0.34 of a macro step, tools/d3_stats.py) from per-lane partial sums the consumer
+// leaves in LDS; the consumer (0.95 busy) keeps only the two DPP adds and one LDS write.
+// Measured 8 % SLOWER per launch (0.429 vs 0.398 ms per 2048, 3 interleaved rounds,
+// profiles/r06_d3_producer_emit_ab.txt): the producers' added sigmoid, stores and LDS reads
+// take issue slots from the consumer on the shared SIMD. Off; kept for the record.
+#ifndef SPECENH_D3_PEMIT
+#define SPECENH_D3_PEMIT 0
+#endif
 namespace d3 {
 constexpr int CI1 = 64, CO1 = 32;     // the first Conv2DTranspose
 constexpr int W1 = 32;                // its input positions per row
@@ -690,7 +699,10 @@ constexpr int LDS_BYTES = LDS_X1 + LDS_X2 + LDS_M + LDS_S;  // 123,136 B: one wo
 // lane groups
 constexpr int NBND = 6 * 2 * 4;
 constexpr int BSTR = NBND + 64;  // exchange buffer stride: the slots + one dump word per lane
-constexpr int LDS_BYTES_NM = LDS_X1 + LDS_X2 + 4 * BSTR * 4;  // 70,400 B
+// SPECENH_D3_PEMIT: the consumer's per-lane partial sums of a tail step (parity, step, wave,
+// lane) for the producer waves to finish and store
+constexpr int LDS_ES = SPECENH_D3_PEMIT ? 2 * 2 * 4 * 64 * 4 : 0;
+constexpr int LDS_BYTES_NM = LDS_X1 + LDS_X2 + 4 * BSTR * 4 + LDS_ES;  // 70,400 B (+ 4 KB PEMIT)
 }  // namespace d3
 
 // first Conv2DTranspose input pixel ps (x = ps - 1), 16-byte group g of its 8: group g sits
@@ -777,6 +789,7 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
   T* const mr = reinterpret_cast<T*>(lds_raw + LDS_X1 + LDS_X2);
   float* const sc = reinterpret_cast<float*>(lds_raw + LDS_X1 + LDS_X2 + LDS_M);
   float* const bnd = reinterpret_cast<float*>(lds_raw + LDS_X1 + LDS_X2);  // !MAP
+  float* const es = bnd + 4 * BSTR;                                          // !MAP, PEMIT
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -881,6 +894,11 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
 #pragma unroll
     for (int i = 0; i <= LEAD; ++i) mk[i] = -1;
 
+    // the consumer's emission (SPECENH_D3_PEMIT): its lane layout for consumer wave wv, and the
+    // (image, tail step) counters of its tail steps 2g - 4, 2g - 3
+    int eil_p = -1, etl_p = TPI - 4;
+    const int orow_p = kg >> 1, ocol_p = 32 * wv + 2 * m + (kg & 1);
+    const int bri_p = m == 0 ? (wv * 2 + 0) * 4 + kg : (m == 15 ? ((wv + 2) * 2 + 1) * 4 + kg : 0);
     // scalar counters (image, step in image) of macro step g and of its refill position
     int ilg = 0, sg = 0;
     int ilp = (3 + LEAD) / SPI, sp = 3 + LEAD - ilp * SPI;
@@ -923,6 +941,24 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
       for (int i = 0; i < LEAD; ++i) mk[i] = mk[i + 1];
       if (++sg == SPI) { sg = 0; ++ilg; }
       if (++sp == SPI) { sp = 0; ++ilp; }
+      if constexpr (!MAP && SPECENH_D3_PEMIT) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {  // the consumer's tail steps 2g - 4 + k of this macro step
+          const int eil = eil_p, etl = etl_p;
+          if (++etl_p == TPI) { etl_p = 0; ++eil_p; }
+          if (eil >= 0 && eil < nimg && etl >= 1 && etl <= H2) {
+            const float sp_ = es[(((I & 1) * 2 + k) * 4 + wv) * 64 + lane] +
+                              bnd[((I & 1) * 2 + k) * BSTR + bri_p];
+            const long long n = (long long)blockIdx.x + (long long)eil * G;
+            const long long o = (n * H3 + 2 * (etl - 1) + orow_p) * rows::MW + ocol_p;
+            const float y = __builtin_amdgcn_rcpf(1.f + __expf(-sp_));
+            if constexpr (OUT16)
+              reinterpret_cast<_Float16*>(a.out)[o] = (_Float16)y;
+            else
+              reinterpret_cast<float*>(a.out)[o] = y;
+          }
+        }
+      }
     };
     int g = 0;
     for (; g + 8 <= S; g += 8) {
@@ -1146,11 +1182,21 @@ __global__ __launch_bounds__(512, 2) void decoder3_kernel(D3Args a) {
         e0 = tskip(b0, E0, il0, tl0);
         e1 = tskip(b1, E1, il1, tl1);
       }
+#if SPECENH_D3_PEMIT
+      (void)e0;
+      (void)e1;
+      float* const ep = es + ((I & 1) * 2 * 4 + w) * 64 + lane;
+      // (emit's summation order: bo + E[0], the two shifted terms, then the edge word)
+      ep[0] = ((bo + E0[0]) + dpp_shift<0x111>(E0[1])) + dpp_shift<0x101>(E0[2]);
+      ep[4 * 64] = ((bo + E1[0]) + dpp_shift<0x111>(E1[1])) + dpp_shift<0x101>(E1[2]);
+      D3_BARRIER();
+#else
       D3_BARRIER();
       // (emitting these in the next macro step, after its first fragment reads, to overlap the
       // two LDS latencies: measured neutral, profiles/r06_d3_out16_ab.txt)
       if (e0) emit(E0, b0[bri], il0, tl0);
       if (e1) emit(E1, b1[bri], il1, tl1);
+#endif
     };
     int g = 0;
     for (; g + 4 <= S; g += 4) {

@@ -29,7 +29,7 @@ constexpr VariantName kVariants[V_COUNT] = {
     {"ENC2_WPE2", 0},        {"CONVT_SHARED_RING", 0}, {"SVD_RECON_VALU", 0},
     {"ROWS_SHORT_LEAD", 0},  {"SVD_GRAM_F32", 0},
     {"SVD_RECON_BLOCKS", 0}, {"CONVT_PG", 0}, {"SVD_GZ_ROWS", 0}, {"EIG_SPLIT", 0}, {"CO1_VALU", 0},
-    {"C1_MASK_MFMA", 1}, {"S2_MIN_NT", 2}, {"PATCH_MIN_WG", 512}, {"WGRAD_WG", 4096}, {"WGRAD_C1_TILES", 4},
+    {"C1_MASK_MFMA", 1}, {"S2_MIN_NT", 2}, {"PATCH_MIN_WG", 512}, {"WGRAD_WG", 1024}, {"WGRAD_C1_TILES", 4},
     {"EIG_GRID", 32}, {"ROWS_BANDS", -1},
 };
 
